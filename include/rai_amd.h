@@ -1,0 +1,182 @@
+/*
+ * rai_amd.h — C ABI of the MI355X (gfx950) PPO/A2C rollout+update hot path.
+ *
+ * Drop-in boundary for toldo4/rl-algo-impls.  The reference is pure Python; every
+ * entry point below replaces one eager NumPy/PyTorch region of its trainer and is
+ * bound from Python through ctypes.  The signature style is
+ * deliberately FFI-plain: device pointers, sizes, POD structs, and an opaque
+ * `stream` (a hipStream_t; NULL = the null stream).  No allocation happens inside
+ * any call: scratch memory is caller-owned (`workspace`), so every call can be
+ * captured into a hipGraph.
+ *
+ * Return value: 0 on success; a negative RAI_E_* code for argument errors (checked
+ * on the host before anything is launched); a positive hipError_t if a launch
+ * failed.  rai_strerror() maps either to a message.
+ *
+ * All entry points are stream-ordered on `stream` and deterministic: fixed
+ * reduction orders, no floating-point atomics.
+ */
+#ifndef RAI_AMD_H_
+#define RAI_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RAI_ABI_VERSION 1
+#define RAI_MAX_K 8 /* max value columns (multi-critic), reference value_shape (K,) */
+
+enum {
+  RAI_OK = 0,
+  RAI_E_NULLPTR = -1,
+  RAI_E_SHAPE = -2,
+  RAI_E_MODE = -3,
+  RAI_E_TOO_MANY_COLUMNS = -4,
+  RAI_E_WORKSPACE = -5,
+  RAI_E_UNSUPPORTED = -6,
+};
+
+int rai_abi_version(void);
+const char* rai_strerror(int code);
+
+/* --------------------------------------------------------------------------
+ * GAE / returns
+ * Replaces rl_algo_impls/shared/gae.py:97-124 (compute_advantages) and the
+ * fused `returns = advantages + values` of rl_algo_impls/rollout/vec_rollout.py:88.
+ *
+ * Layout: rewards/values/adv/returns are (T, N, K) row-major fp32; episode_starts
+ * (T, N) and next_episode_starts (N) are uint8 booleans; next_values (N, K).
+ * gamma/gae_lambda: host arrays of length K (or 1 when the reference argument is a
+ * Python float).  gamma_is_vector selects the reference's numpy promotion path:
+ *   0: gamma is a Python float -> gamma*V_next computed in fp32 (gae.py:121)
+ *   1: gamma is an ndarray     -> gamma*V_next computed in fp64
+ * mode: 0 = exact (fp64 carry in the reference's operation order; bit-exact),
+ *       1 = fast  (fp32 carry; within 1e-5 relative of exact).
+ * returns_out may be NULL.
+ * ------------------------------------------------------------------------ */
+#define RAI_GAE_EXACT 0
+#define RAI_GAE_FAST 1
+int rai_gae(const float* rewards, const float* values, const uint8_t* episode_starts,
+            const uint8_t* next_episode_starts, const float* next_values, int64_t T, int64_t N,
+            int32_t K, const double* gamma, const double* gae_lambda, int32_t gamma_is_vector,
+            int32_t mode, float* adv_out, float* returns_out, void* stream);
+
+/* --------------------------------------------------------------------------
+ * Device-resident hyperparameters and training state.
+ * These live in HBM so a captured hipGraph replays against values the host
+ * rewrites once per update (schedules: rl_algo_impls/shared/callbacks/
+ * hyperparam_transitions.py:19-31 mutate lr/clip/ent/vf coefficients).
+ * ------------------------------------------------------------------------ */
+typedef struct rai_ppo_hparams {
+  float clip_range;      /* ppo.py:224,328 */
+  float clip_range_vf;   /* ppo.py:233-237; used iff has_clip_range_vf */
+  float ent_coef;        /* ppo.py:359 */
+  float kl_cutoff;       /* ppo.py:354; used iff has_kl_cutoff */
+  float grad_scale;      /* 1/num_minibatches under gradient_accumulation (ppo.py:373-374) */
+  int32_t K;             /* value columns */
+  int32_t has_clip_range_vf;
+  int32_t has_kl_cutoff;
+  int32_t normalize_advantage;       /* ppo.py:313-314 */
+  int32_t standardize_advantage;     /* ppo.py:315-316 */
+  int32_t normalize_after_scaling;   /* ppo.py:307-311 */
+  int32_t ppo2_vf_coef_halving;      /* ppo.py:348-349 */
+  int32_t has_vf_weights;            /* ppo.py:344-345 */
+  int32_t has_multi_reward_weights;  /* ppo.py:308-309,317-318 */
+  int32_t vf_loss_fn;                /* 0 mse_loss, 1 huber_loss(delta=1), 2 smooth_l1_loss(beta=1) */
+  int32_t loss_kind;                 /* 0 PPO clipped surrogate, 1 A2C -(A*logp) (a2c.py:148-158) */
+  float vf_coef[RAI_MAX_K];
+  float vf_weights[RAI_MAX_K];
+  float multi_reward_weights[RAI_MAX_K];
+} rai_ppo_hparams;
+
+typedef struct rai_optim_hparams {
+  float lr;            /* ppo.py:223 update_learning_rate */
+  float beta1;         /* Adam (0.9) */
+  float beta2;         /* Adam (0.999) */
+  float eps;           /* ppo.py:146 eps=1e-7 ; RMSprop a2c.py:46 eps=1e-5 */
+  float alpha;         /* RMSprop smoothing (0.99) */
+  float max_grad_norm; /* ppo.py:442-444; <= 0 disables clipping */
+  int32_t kind;        /* 0 Adam, 1 RMSprop */
+  int32_t pad;
+} rai_optim_hparams;
+
+typedef struct rai_train_state {
+  int64_t opt_step;      /* torch optimizer state['step'] */
+  int32_t stat_index;    /* next per-minibatch stats row */
+  int32_t pi_coef_zero;  /* kl_cutoff latch, reset per update (ppo.py:279,354-355) */
+  int32_t norm_index;    /* next grad-norm slot */
+  int32_t pad;
+} rai_train_state;
+
+/* Per-minibatch stats row layout (floats), stride RAI_STAT_STRIDE:
+ *  [0] loss [1] pi_loss [2] entropy_loss [3] approx_kl [4] clipped_frac
+ *  [5 .. 5+K) v_loss  [5+RAI_MAX_K .. 5+RAI_MAX_K+K) val_clipped_frac       */
+#define RAI_STAT_STRIDE (5 + 2 * RAI_MAX_K)
+
+/* --------------------------------------------------------------------------
+ * Fused policy-gradient loss forward + backward (to the network outputs).
+ * Replaces rl_algo_impls/ppo/ppo.py:307-371,379-396 (advantage normalisation,
+ * clipped surrogate, (clipped) value loss, entropy loss, approx_kl/clip stats)
+ * and rl_algo_impls/a2c/a2c.py:132-158 when hp->loss_kind == 1.
+ *
+ * Inputs (device, fp32): new_logp (B), entropy (n_entropy: B or B*act_dim),
+ * new_values/old_values/advantages/returns (B,K), old_logp (B; unused for A2C).
+ * Outputs: d_logp (B), d_entropy (n_entropy), d_values (B,K) = dLoss/d(output),
+ * and one stats row written at stats[state->stat_index] (then stat_index++).
+ * workspace: >= rai_ppo_loss_workspace_bytes(B, K) bytes of device memory.
+ * ------------------------------------------------------------------------ */
+int64_t rai_ppo_loss_workspace_bytes(int64_t B, int32_t K);
+int rai_ppo_loss(const float* new_logp, const float* entropy, int64_t n_entropy,
+                 const float* new_values, const float* old_logp, const float* old_values,
+                 const float* advantages, const float* returns, int64_t B, int32_t K,
+                 const rai_ppo_hparams* hp, rai_train_state* state, float* d_logp,
+                 float* d_entropy, float* d_values, float* stats, int32_t max_stats,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------------------------------
+ * Fused clip_grad_norm_ + optimizer step over one flat fp32 parameter buffer.
+ * Replaces rl_algo_impls/ppo/ppo.py:441-447 (clip_grad_norm_(...).item(),
+ * Adam(eps=1e-7).step(), zero_grad) and rl_algo_impls/a2c/a2c.py:202-205
+ * (RMSprop).  Grads are zeroed after use (zero_grad equivalent; the flat grad
+ * buffer keeps its storage so parameter .grad views stay valid).
+ * The total grad norm (pre-clip) is written to norms[state->norm_index++].
+ * state->opt_step is incremented on device (bias corrections use it).
+ * ------------------------------------------------------------------------ */
+int64_t rai_optim_workspace_bytes(int64_t P);
+int rai_clip_optim_step(float* params, float* grads, float* state1, float* state2, int64_t P,
+                        const rai_optim_hparams* hp, rai_train_state* state, float* norms,
+                        int32_t max_norms, void* workspace, int64_t workspace_bytes,
+                        void* stream);
+
+/* --------------------------------------------------------------------------
+ * Multi-field row gather: dst_f[i] = src_f[idx[i]] for up to RAI_MAX_FIELDS
+ * fields of arbitrary row size (bytes).  Replaces the minibatch fancy-index
+ * gather of rl_algo_impls/rollout/rollout.py:56-69 / vec_rollout.py:166-175;
+ * the trainer uses it once per epoch to materialise the permuted rollout so
+ * that minibatches become contiguous slices.
+ * ------------------------------------------------------------------------ */
+#define RAI_MAX_FIELDS 8
+int rai_gather_rows(int32_t n_fields, const void* const* src, void* const* dst,
+                    const int64_t* row_bytes, const int64_t* idx, int64_t n_rows, void* stream);
+
+/* --------------------------------------------------------------------------
+ * Rollout post-head: sample actions from the policy head and write the
+ * rollout-buffer slot.  Replaces rl_algo_impls/shared/policy/actor_critic.py:
+ * 306-318 (pi.sample, pi.log_prob, .cpu()) and the slot writes of
+ * rl_algo_impls/rollout/sync_step_rollout.py:193-201.
+ * Random numbers: Philox4x32-10 keyed by (seed), counter (offset, row).
+ * ------------------------------------------------------------------------ */
+int rai_categorical_sample(const float* logits, const uint8_t* mask, int64_t N, int32_t A,
+                           uint64_t seed, uint64_t offset, int64_t* actions_out, float* logp_out,
+                           const float* v_in, float* v_out, int32_t K, void* stream);
+int rai_gaussian_sample(const float* mu, const float* log_std, int64_t N, int32_t A,
+                        const float* low, const float* high, uint64_t seed, uint64_t offset,
+                        float* actions_out, float* clamped_out, float* logp_out,
+                        const float* v_in, float* v_out, int32_t K, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAI_AMD_H_ */

@@ -1,0 +1,150 @@
+"""ctypes binding of the C ABI in include/rai_amd.h (librai_amd.so).
+
+The library is loaded AFTER torch so that its DT_NEEDED libamdhip64.so.7 resolves
+(by SONAME) to the HIP runtime torch already mapped: torch's streams and device
+pointers are then valid arguments.  There is no CPU fallback: if the library is
+missing or cannot be loaded, every product entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import re
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+from .build import lib_path
+
+RAI_MAX_K = 8
+RAI_MAX_FIELDS = 8
+RAI_STAT_STRIDE = 5 + 2 * RAI_MAX_K
+ABI_VERSION = 1
+
+
+class PPOHparams(C.Structure):
+    """Mirror of rai_ppo_hparams (device-resident hyperparameters)."""
+
+    _fields_ = [
+        ("clip_range", C.c_float),
+        ("clip_range_vf", C.c_float),
+        ("ent_coef", C.c_float),
+        ("kl_cutoff", C.c_float),
+        ("grad_scale", C.c_float),
+        ("K", C.c_int32),
+        ("has_clip_range_vf", C.c_int32),
+        ("has_kl_cutoff", C.c_int32),
+        ("normalize_advantage", C.c_int32),
+        ("standardize_advantage", C.c_int32),
+        ("normalize_after_scaling", C.c_int32),
+        ("ppo2_vf_coef_halving", C.c_int32),
+        ("has_vf_weights", C.c_int32),
+        ("has_multi_reward_weights", C.c_int32),
+        ("vf_loss_fn", C.c_int32),
+        ("loss_kind", C.c_int32),
+        ("vf_coef", C.c_float * RAI_MAX_K),
+        ("vf_weights", C.c_float * RAI_MAX_K),
+        ("multi_reward_weights", C.c_float * RAI_MAX_K),
+    ]
+
+
+class OptimHparams(C.Structure):
+    _fields_ = [
+        ("lr", C.c_float),
+        ("beta1", C.c_float),
+        ("beta2", C.c_float),
+        ("eps", C.c_float),
+        ("alpha", C.c_float),
+        ("max_grad_norm", C.c_float),
+        ("kind", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
+class TrainState(C.Structure):
+    _fields_ = [
+        ("opt_step", C.c_int64),
+        ("stat_index", C.c_int32),
+        ("pi_coef_zero", C.c_int32),
+        ("norm_index", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
+_vp, _i32, _i64, _u64, _f64p = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_double)
+
+_SIGNATURES = {
+    "rai_abi_version": (C.c_int, []),
+    "rai_strerror": (C.c_char_p, [C.c_int]),
+    "rai_gae": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _f64p, _f64p, _i32, _i32, _vp, _vp, _vp]),
+    "rai_ppo_loss_workspace_bytes": (_i64, [_i64, _i32]),
+    "rai_ppo_loss": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp,
+                               _vp, _i32, _vp, _i64, _vp]),
+    "rai_optim_workspace_bytes": (_i64, [_i64]),
+    "rai_clip_optim_step": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
+    "rai_gather_rows": (C.c_int, [_i32, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "rai_categorical_sample": (C.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "rai_gaussian_sample": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp,
+                                      _i32, _vp]),
+}
+EXPORTED = tuple(_SIGNATURES)
+
+_lock = threading.Lock()
+_lib = None
+
+
+def hip_runtimes_mapped() -> list[str]:
+    try:
+        maps = open("/proc/self/maps").read()
+    except OSError:
+        return []
+    return sorted(set(re.findall(r"\S*libamdhip64\.so\S*", maps)))
+
+
+def lib() -> C.CDLL:
+    """Load (once) and return the C-ABI library; raises if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if not path.exists():
+            raise RuntimeError(
+                f"rl_algo_impls_amd: HIP library {path} is missing; run __graft_entry__.build() "
+                "(there is no CPU fallback for the product path)"
+            )
+        handle = C.CDLL(str(path))
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.rai_abi_version() != ABI_VERSION:
+            raise RuntimeError("librai_amd ABI version mismatch")
+        runtimes = hip_runtimes_mapped()
+        if len(runtimes) > 1:
+            raise RuntimeError(f"two HIP runtimes mapped in one process: {runtimes}")
+        _lib = handle
+        return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().rai_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(*tensors) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("rl_algo_impls_amd: device kernels require tensors on a HIP device")

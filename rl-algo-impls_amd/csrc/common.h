@@ -1,0 +1,80 @@
+// Shared device helpers for the gfx950 kernels (wave64, CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rai_amd.h"
+
+#define RAI_WAVE 64
+
+#define RAI_LAUNCH_CHECK()                      \
+  do {                                          \
+    hipError_t e__ = hipGetLastError();         \
+    if (e__ != hipSuccess) return (int)e__;     \
+  } while (0)
+
+static inline hipStream_t rai_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- wave64 reductions (fixed order -> deterministic) ----------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum of NV values per thread; every thread receives the totals.
+// scratch: >= NV * (blockDim/64) doubles of LDS.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) scratch[i * nw + w] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < nw; ++j) s += scratch[i * nw + j];
+    v[i] = s;
+  }
+  __syncthreads();
+}
+
+// ---- Philox4x32-10 counter RNG ---------------------------------------------
+struct Philox4 {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ Philox4 philox4x32_10(uint64_t ctr_hi, uint64_t ctr_lo, uint64_t key) {
+  uint32_t c0 = (uint32_t)ctr_lo, c1 = (uint32_t)(ctr_lo >> 32);
+  uint32_t c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return Philox4{c0, c1, c2, c3};
+}
+// uniform in (0, 1]  (never 0 -> safe for log)
+__device__ __forceinline__ float u01_open0(uint32_t x) {
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}

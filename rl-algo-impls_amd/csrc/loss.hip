@@ -1,0 +1,317 @@
+// Fused policy-gradient loss forward + backward for gfx950.
+//
+// Restates, per minibatch:
+//   rl_algo_impls/ppo/ppo.py:307-318  advantage normalisation / standardisation /
+//                                     multi_reward_weights (before or after scaling)
+//   rl_algo_impls/ppo/ppo.py:326-361  ratio, clipped surrogate, (clipped) value loss,
+//                                     vf_weights, ppo2 halving, entropy loss,
+//                                     approx_kl, kl_cutoff latch, total loss
+//   rl_algo_impls/ppo/ppo.py:373-374  gradient_accumulation scaling
+//   rl_algo_impls/ppo/ppo.py:379-396  clipped_frac / val_clipped_frac
+//   rl_algo_impls/a2c/a2c.py:132-158  A2C loss (loss_kind = 1)
+// and emits dLoss/d(new_logp), dLoss/d(entropy), dLoss/d(new_values) with the
+// autograd tie rules of torch.min/torch.max (ties split 1/2-1/2) and clamp
+// (gradient passes on the closed interval), so PyTorch-ROCm backpropagates the
+// network from these three tensors.  Stats are written as one row to a
+// device-resident table (no host sync per minibatch; the reference does ~6
+// `.item()` syncs here).
+//
+// One 1024-thread workgroup owns the whole minibatch (B up to tens of
+// thousands): the advantage moments, approx_kl (needed before the kl_cutoff
+// decision) and every stat are block reductions in a fixed order -> the
+// result is deterministic and needs no inter-workgroup protocol.
+#include "common.h"
+
+namespace {
+
+constexpr int LOSS_THREADS = 1024;
+constexpr int NRED = 4 + 2 * RAI_MAX_K;  // pi_sum, kl_sum, clip_cnt, ent_sum, vloss[K], vclip[K]
+
+struct LossArgs {
+  const float* new_logp;
+  const float* entropy;
+  const float* new_values;
+  const float* old_logp;
+  const float* old_values;
+  const float* adv;
+  const float* ret;
+  const rai_ppo_hparams* hp;
+  rai_train_state* state;
+  float* d_logp;
+  float* d_entropy;
+  float* d_values;
+  float* stats;
+  int64_t B;
+  int64_t n_entropy;
+  int32_t K;
+  int32_t max_stats;
+};
+
+struct AdvNorm {
+  float mean[RAI_MAX_K];
+  float inv_den[RAI_MAX_K];  // unused: keep (x - mean) / den as torch does
+  float den[RAI_MAX_K];
+  float smean, sden;  // scalar (normalize-after-scaling) moments
+};
+
+// The per-row advantage actually used by the surrogate (ppo.py:307-318).
+__device__ __forceinline__ float row_advantage(const LossArgs& a, const rai_ppo_hparams& hp,
+                                               const AdvNorm& nm, int64_t b) {
+  const int K = a.K;
+  if (hp.normalize_after_scaling) {
+    float x;
+    if (hp.has_multi_reward_weights) {
+      x = 0.f;
+      for (int k = 0; k < K; ++k) x += a.adv[b * K + k] * hp.multi_reward_weights[k];
+    } else {
+      x = a.adv[b * K];
+    }
+    return (x - nm.smean) / nm.sden;
+  }
+  if (K == 1 && !hp.has_multi_reward_weights) {
+    const float x = a.adv[b];
+    if (hp.normalize_advantage) return (x - nm.mean[0]) / nm.den[0];
+    if (hp.standardize_advantage) return x / nm.den[0];
+    return x;
+  }
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    float x = a.adv[b * K + k];
+    if (hp.normalize_advantage) x = (x - nm.mean[k]) / nm.den[k];
+    else if (hp.standardize_advantage) x = x / nm.den[k];
+    s += x * (hp.has_multi_reward_weights ? hp.multi_reward_weights[k] : 1.f);
+  }
+  return s;
+}
+
+__device__ __forceinline__ float vf_elem_loss(int fn, float x) {
+  if (fn == 0) return x * x;
+  const float z = fabsf(x);
+  return z < 1.f ? 0.5f * z * z : (z - 0.5f);
+}
+__device__ __forceinline__ float vf_elem_grad(int fn, float x) {  // d loss / d x
+  if (fn == 0) return 2.f * x;
+  return x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x);
+}
+
+__global__ __launch_bounds__(LOSS_THREADS) void pg_loss_kernel(const LossArgs a) {
+  __shared__ double red[NRED * (LOSS_THREADS / 64)];
+  __shared__ AdvNorm nm_s;
+  const rai_ppo_hparams hp = *a.hp;
+  const int K = a.K;
+  const int64_t B = a.B;
+  const int tid = threadIdx.x;
+  const bool ppo = hp.loss_kind == 0;
+
+  // ---- pass 0: advantage moments (two-pass, fp64 accumulation) ----------------
+  const bool need_cols = !hp.normalize_after_scaling &&
+                         (hp.normalize_advantage || hp.standardize_advantage);
+  if (hp.normalize_after_scaling) {
+    double acc[NRED];
+    for (int i = 0; i < NRED; ++i) acc[i] = 0.0;
+    for (int64_t b = tid; b < B; b += LOSS_THREADS) {
+      float x;
+      if (hp.has_multi_reward_weights) {
+        x = 0.f;
+        for (int k = 0; k < K; ++k) x += a.adv[b * K + k] * hp.multi_reward_weights[k];
+      } else {
+        x = a.adv[b * K];
+      }
+      acc[0] += (double)x;
+    }
+    block_sum<NRED>(acc, red);
+    const float mean = (float)(acc[0] / (double)B);
+    for (int i = 0; i < NRED; ++i) acc[i] = 0.0;
+    for (int64_t b = tid; b < B; b += LOSS_THREADS) {
+      float x;
+      if (hp.has_multi_reward_weights) {
+        x = 0.f;
+        for (int k = 0; k < K; ++k) x += a.adv[b * K + k] * hp.multi_reward_weights[k];
+      } else {
+        x = a.adv[b * K];
+      }
+      const double d = (double)x - (double)mean;
+      acc[0] += d * d;
+    }
+    block_sum<NRED>(acc, red);
+    if (tid == 0) {
+      nm_s.smean = mean;
+      nm_s.sden = (float)sqrt(acc[0] / (double)(B - 1)) + 1e-8f;
+    }
+  } else if (need_cols) {
+    double acc[NRED];
+    for (int i = 0; i < NRED; ++i) acc[i] = 0.0;
+    for (int64_t b = tid; b < B; b += LOSS_THREADS)
+      for (int k = 0; k < K; ++k) acc[k] += (double)a.adv[b * K + k];
+    block_sum<NRED>(acc, red);
+    float mean[RAI_MAX_K];
+    for (int k = 0; k < RAI_MAX_K; ++k) mean[k] = (float)(acc[k] / (double)B);
+    for (int i = 0; i < NRED; ++i) acc[i] = 0.0;
+    for (int64_t b = tid; b < B; b += LOSS_THREADS)
+      for (int k = 0; k < K; ++k) {
+        const double d = (double)a.adv[b * K + k] - (double)mean[k];
+        acc[k] += d * d;
+      }
+    block_sum<NRED>(acc, red);
+    if (tid == 0) {
+      for (int k = 0; k < RAI_MAX_K; ++k) {
+        nm_s.mean[k] = mean[k];
+        nm_s.den[k] = (float)sqrt(acc[k] / (double)(B - 1)) + 1e-8f;
+      }
+    }
+  }
+  __syncthreads();
+  const AdvNorm nm = nm_s;
+
+  // ---- pass 1: forward statistics ---------------------------------------------
+  const float lo = 1.f - hp.clip_range, hi = 1.f + hp.clip_range;
+  const float vclip = hp.clip_range_vf;
+  double acc[NRED];
+  for (int i = 0; i < NRED; ++i) acc[i] = 0.0;
+  for (int64_t b = tid; b < B; b += LOSS_THREADS) {
+    const float A = row_advantage(a, hp, nm, b);
+    if (ppo) {
+      const float logratio = a.new_logp[b] - a.old_logp[b];
+      const float ratio = expf(logratio);
+      const float cr = fminf(fmaxf(ratio, lo), hi);
+      acc[0] += (double)fminf(ratio * A, cr * A);
+      acc[1] += (double)((ratio - 1.f) - logratio);
+      acc[2] += (fabsf(ratio - 1.f) > hp.clip_range) ? 1.0 : 0.0;
+    } else {
+      acc[0] += (double)(A * a.new_logp[b]);
+    }
+    for (int k = 0; k < K; ++k) {
+      const float v = a.new_values[b * K + k], R = a.ret[b * K + k];
+      float l = vf_elem_loss(hp.vf_loss_fn, v - R);
+      if (ppo && hp.has_clip_range_vf) {
+        const float vo = a.old_values[b * K + k];
+        const float vc = vo + fminf(fmaxf(v - vo, -vclip), vclip);
+        l = fmaxf(l, vf_elem_loss(hp.vf_loss_fn, vc - R));
+        acc[4 + RAI_MAX_K + k] += (fabsf(v - vo) > vclip) ? 1.0 : 0.0;
+      }
+      acc[4 + k] += (double)l;
+    }
+  }
+  for (int64_t i = tid; i < a.n_entropy; i += LOSS_THREADS) acc[3] += (double)a.entropy[i];
+  block_sum<NRED>(acc, red);
+
+  const float invB = 1.f / (float)B;
+  const float approx_kl = (float)(acc[1] / (double)B);
+  int latched = a.state->pi_coef_zero;
+  if (ppo && hp.has_kl_cutoff && approx_kl > hp.kl_cutoff) latched = 1;
+  const float pi_coef = (ppo && latched) ? 0.f : 1.f;
+  const float halve = hp.ppo2_vf_coef_halving ? 0.5f : 1.f;
+  const float gs = hp.grad_scale;
+
+  // ---- pass 2: gradients to the network outputs ---------------------------------
+  const float g_pi = (-pi_coef * invB) * gs;
+  for (int64_t b = tid; b < B; b += LOSS_THREADS) {
+    const float A = row_advantage(a, hp, nm, b);
+    if (ppo) {
+      const float logratio = a.new_logp[b] - a.old_logp[b];
+      const float ratio = expf(logratio);
+      const float cr = fminf(fmaxf(ratio, lo), hi);
+      const float s1 = ratio * A, s2 = cr * A;
+      float g1, g2;
+      if (s1 < s2) { g1 = g_pi; g2 = 0.f; }
+      else if (s1 > s2) { g1 = 0.f; g2 = g_pi; }
+      else { g1 = g_pi * 0.5f; g2 = g_pi * 0.5f; }
+      const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+      const float d_ratio = g1 * A + (g2 * A) * in_clip;
+      a.d_logp[b] = d_ratio * ratio;
+    } else {
+      a.d_logp[b] = ((-invB) * gs) * A;
+    }
+    for (int k = 0; k < K; ++k) {
+      const float v = a.new_values[b * K + k], R = a.ret[b * K + k];
+      const float gl = ((hp.vf_coef[k] * halve) * invB) * gs;  // d loss / d l_bk
+      float dv;
+      if (ppo && hp.has_clip_range_vf) {
+        const float vo = a.old_values[b * K + k];
+        const float dvo = v - vo;
+        const float vc = vo + fminf(fmaxf(dvo, -vclip), vclip);
+        const float l1 = vf_elem_loss(hp.vf_loss_fn, v - R);
+        const float l2 = vf_elem_loss(hp.vf_loss_fn, vc - R);
+        float w1, w2;
+        if (l1 > l2) { w1 = gl; w2 = 0.f; }
+        else if (l1 < l2) { w1 = 0.f; w2 = gl; }
+        else { w1 = gl * 0.5f; w2 = gl * 0.5f; }
+        const float in_vclip = (dvo >= -vclip && dvo <= vclip) ? 1.f : 0.f;
+        dv = w1 * vf_elem_grad(hp.vf_loss_fn, v - R) +
+             (w2 * vf_elem_grad(hp.vf_loss_fn, vc - R)) * in_vclip;
+      } else {
+        dv = gl * vf_elem_grad(hp.vf_loss_fn, v - R);
+      }
+      a.d_values[b * K + k] = dv;
+    }
+  }
+  const float g_ent = (-hp.ent_coef / (float)a.n_entropy) * gs;
+  for (int64_t i = tid; i < a.n_entropy; i += LOSS_THREADS) a.d_entropy[i] = g_ent;
+
+  // ---- stats row -------------------------------------------------------------------
+  if (tid == 0) {
+    const float pi_loss = ppo ? (float)(-acc[0] / (double)B) : (float)(-acc[0] / (double)B);
+    const float ent_loss = (float)(-acc[3] / (double)a.n_entropy);
+    float vsum = 0.f;
+    const int idx = a.state->stat_index;
+    float* row = (a.stats && idx < a.max_stats) ? a.stats + (int64_t)idx * RAI_STAT_STRIDE : nullptr;
+    for (int k = 0; k < K; ++k) {
+      const float vl = (float)(acc[4 + k] / (double)B) * halve;
+      vsum += hp.vf_coef[k] * vl;
+      if (row) {
+        row[5 + k] = vl;
+        row[5 + RAI_MAX_K + k] =
+            (ppo && hp.has_clip_range_vf) ? (float)(acc[4 + RAI_MAX_K + k] / (double)B) : 0.f;
+      }
+    }
+    const float loss = (pi_coef * pi_loss + hp.ent_coef * ent_loss + vsum) * gs;
+    if (row) {
+      row[0] = loss;
+      row[1] = pi_loss;
+      row[2] = ent_loss;
+      row[3] = ppo ? approx_kl : 0.f;
+      row[4] = ppo ? (float)(acc[2] / (double)B) : 0.f;
+    }
+    a.state->stat_index = idx + 1;
+    a.state->pi_coef_zero = latched;
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t rai_ppo_loss_workspace_bytes(int64_t /*B*/, int32_t /*K*/) { return 0; }
+
+extern "C" int rai_ppo_loss(const float* new_logp, const float* entropy, int64_t n_entropy,
+                            const float* new_values, const float* old_logp,
+                            const float* old_values, const float* advantages,
+                            const float* returns, int64_t B, int32_t K, const rai_ppo_hparams* hp,
+                            rai_train_state* state, float* d_logp, float* d_entropy,
+                            float* d_values, float* stats, int32_t max_stats, void* /*workspace*/,
+                            int64_t /*workspace_bytes*/, void* stream) {
+  if (B < 1 || K < 1 || n_entropy < 1) return RAI_E_SHAPE;
+  if (K > RAI_MAX_K) return RAI_E_TOO_MANY_COLUMNS;
+  if (!new_logp || !entropy || !new_values || !advantages || !returns || !hp || !state ||
+      !d_logp || !d_entropy || !d_values)
+    return RAI_E_NULLPTR;
+  LossArgs a;
+  a.new_logp = new_logp;
+  a.entropy = entropy;
+  a.new_values = new_values;
+  a.old_logp = old_logp ? old_logp : new_logp;
+  a.old_values = old_values ? old_values : new_values;
+  a.adv = advantages;
+  a.ret = returns;
+  a.hp = hp;
+  a.state = state;
+  a.d_logp = d_logp;
+  a.d_entropy = d_entropy;
+  a.d_values = d_values;
+  a.stats = stats;
+  a.B = B;
+  a.n_entropy = n_entropy;
+  a.K = K;
+  a.max_stats = max_stats;
+  hipLaunchKernelGGL(pg_loss_kernel, dim3(1), dim3(LOSS_THREADS), 0, rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

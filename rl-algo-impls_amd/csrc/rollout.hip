@@ -1,0 +1,192 @@
+// Rollout-buffer side kernels for gfx950:
+//  * multi-field row gather (minibatch / epoch permutation),
+//  * categorical and diagonal-Gaussian post-head sampling that writes the
+//    rollout slot (action, log-prob, value) in one pass.
+//
+// Reference regions replaced:
+//   rl_algo_impls/rollout/rollout.py:56-69      Batch.__getitem__ (fancy-index gather)
+//   rl_algo_impls/rollout/vec_rollout.py:166-175 minibatches()
+//   rl_algo_impls/shared/policy/actor_critic.py:306-318  step(): pi.sample(), log_prob
+//   rl_algo_impls/shared/actor/categorical.py:12-54      MaskedCategorical
+//   rl_algo_impls/shared/actor/gaussian.py:11-16         GaussianDistribution
+//   rl_algo_impls/shared/policy/actor_critic.py:62-87    clamp_actions (Box clip)
+//   rl_algo_impls/rollout/sync_step_rollout.py:193-201   slot writes
+#include "common.h"
+
+namespace {
+
+struct GatherField {
+  const uint8_t* src;
+  uint8_t* dst;
+  int64_t units;  // granules per row
+  int32_t gran;   // 16, 4 or 1 bytes
+};
+struct GatherArgs {
+  GatherField f[RAI_MAX_FIELDS];
+  const int64_t* idx;
+  int64_t n_rows;
+};
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
+  const GatherField f = a.f[blockIdx.y];
+  const int64_t total = a.n_rows * f.units;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total; u += stride) {
+    const int64_t r = u / f.units;
+    const int64_t j = u - r * f.units;
+    const int64_t sr = a.idx[r];
+    if (f.gran == 16) {
+      reinterpret_cast<uint4*>(f.dst)[u] = reinterpret_cast<const uint4*>(f.src)[sr * f.units + j];
+    } else if (f.gran == 4) {
+      reinterpret_cast<uint32_t*>(f.dst)[u] =
+          reinterpret_cast<const uint32_t*>(f.src)[sr * f.units + j];
+    } else {
+      f.dst[u] = f.src[sr * f.units + j];
+    }
+  }
+}
+
+// One thread per env row.  Masked logits follow MaskedCategorical
+// (torch.where(mask, logits, finfo.min)); torch.distributions normalises
+// logits by logsumexp; log_prob(a) = logits[a] - logsumexp.
+__global__ __launch_bounds__(256) void categorical_sample_kernel(
+    const float* __restrict__ logits, const uint8_t* __restrict__ mask, int64_t N, int A,
+    uint64_t seed, uint64_t offset, int64_t* __restrict__ actions, float* __restrict__ logp,
+    const float* __restrict__ v_in, float* __restrict__ v_out, int K) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  const float* l = logits + r * A;
+  const uint8_t* mk = mask ? mask + r * A : nullptr;
+  const float NEG = -3.4028234663852886e38f;  // torch.finfo(float32).min
+  float m = -INFINITY;
+  for (int i = 0; i < A; ++i) {
+    const float x = (mk && !mk[i]) ? NEG : l[i];
+    m = fmaxf(m, x);
+  }
+  float s = 0.f;
+  for (int i = 0; i < A; ++i) {
+    const float x = (mk && !mk[i]) ? NEG : l[i];
+    s += expf(x - m);
+  }
+  const float lse = m + logf(s);
+  const Philox4 rnd = philox4x32_10(offset, (uint64_t)r, seed);
+  const float u = u01_open0(rnd.x) * s;  // inverse CDF on unnormalised mass
+  float c = 0.f;
+  int act = -1, last_valid = 0;
+  for (int i = 0; i < A; ++i) {
+    const bool ok = !(mk && !mk[i]);
+    if (!ok) continue;
+    last_valid = i;
+    c += expf(l[i] - m);
+    if (act < 0 && u <= c) act = i;
+  }
+  if (act < 0) act = last_valid;
+  actions[r] = act;
+  logp[r] = l[act] - lse;
+  if (v_in && v_out)
+    for (int k = 0; k < K; ++k) v_out[r * K + k] = v_in[r * K + k];
+}
+
+// a = mu + std*eps (rsample); logp = sum_d Normal.log_prob; clamped = clip(a, low, high)
+__global__ __launch_bounds__(256) void gaussian_sample_kernel(
+    const float* __restrict__ mu, const float* __restrict__ log_std, int64_t N, int A,
+    const float* __restrict__ low, const float* __restrict__ high, uint64_t seed,
+    uint64_t offset, float* __restrict__ actions, float* __restrict__ clamped,
+    float* __restrict__ logp, const float* __restrict__ v_in, float* __restrict__ v_out, int K) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  const float LOG_SQRT_2PI = 0.91893853320467274178f;  // log(sqrt(2*pi))
+  float lp = 0.f;
+  for (int d = 0; d < A; d += 2) {
+    const Philox4 rnd = philox4x32_10(offset, ((uint64_t)r << 16) | (uint64_t)(d >> 1), seed);
+    const float u1 = u01_open0(rnd.x), u2 = u01_open0(rnd.y);
+    const float rad = sqrtf(-2.f * logf(u1));
+    float s, c;
+    sincosf(6.283185307179586f * u2, &s, &c);
+    const float e2[2] = {rad * c, rad * s};
+    for (int q = 0; q < 2 && d + q < A; ++q) {
+      const int dd = d + q;
+      const float ls = log_std[dd];
+      const float sd = expf(ls);
+      const float m = mu[r * A + dd];
+      const float a = m + sd * e2[q];
+      const float var = sd * sd;
+      const float diff = a - m;
+      lp += -(diff * diff) / (2.f * var) - ls - LOG_SQRT_2PI;
+      actions[r * A + dd] = a;
+      if (clamped) {
+        float x = a;
+        if (low) x = fmaxf(x, low[dd]);
+        if (high) x = fminf(x, high[dd]);
+        clamped[r * A + dd] = x;
+      }
+    }
+  }
+  logp[r] = lp;
+  if (v_in && v_out)
+    for (int k = 0; k < K; ++k) v_out[r * K + k] = v_in[r * K + k];
+}
+
+}  // namespace
+
+extern "C" int rai_gather_rows(int32_t n_fields, const void* const* src, void* const* dst,
+                               const int64_t* row_bytes, const int64_t* idx, int64_t n_rows,
+                               void* stream) {
+  if (n_fields < 1 || n_fields > RAI_MAX_FIELDS || n_rows < 0) return RAI_E_SHAPE;
+  if (n_rows == 0) return RAI_OK;
+  if (!src || !dst || !row_bytes || !idx) return RAI_E_NULLPTR;
+  GatherArgs a;
+  int64_t max_units = 0;
+  for (int i = 0; i < n_fields; ++i) {
+    if (!src[i] || !dst[i]) return RAI_E_NULLPTR;
+    if (row_bytes[i] < 1) return RAI_E_SHAPE;
+    const uintptr_t al = (uintptr_t)src[i] | (uintptr_t)dst[i];
+    int gran = 1;
+    if (row_bytes[i] % 16 == 0 && al % 16 == 0) gran = 16;
+    else if (row_bytes[i] % 4 == 0 && al % 4 == 0) gran = 4;
+    a.f[i].src = static_cast<const uint8_t*>(src[i]);
+    a.f[i].dst = static_cast<uint8_t*>(dst[i]);
+    a.f[i].gran = gran;
+    a.f[i].units = row_bytes[i] / gran;
+    if (a.f[i].units > max_units) max_units = a.f[i].units;
+  }
+  a.idx = idx;
+  a.n_rows = n_rows;
+  int64_t blocks = (n_rows * max_units + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks, (unsigned)n_fields), dim3(256), 0,
+                     rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_categorical_sample(const float* logits, const uint8_t* mask, int64_t N,
+                                      int32_t A, uint64_t seed, uint64_t offset,
+                                      int64_t* actions_out, float* logp_out, const float* v_in,
+                                      float* v_out, int32_t K, void* stream) {
+  if (N < 0 || A < 1 || K < 0) return RAI_E_SHAPE;
+  if (N == 0) return RAI_OK;
+  if (!logits || !actions_out || !logp_out) return RAI_E_NULLPTR;
+  const unsigned blocks = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(categorical_sample_kernel, dim3(blocks), dim3(256), 0, rai_stream(stream),
+                     logits, mask, N, A, seed, offset, actions_out, logp_out, v_in, v_out, K);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_gaussian_sample(const float* mu, const float* log_std, int64_t N, int32_t A,
+                                   const float* low, const float* high, uint64_t seed,
+                                   uint64_t offset, float* actions_out, float* clamped_out,
+                                   float* logp_out, const float* v_in, float* v_out, int32_t K,
+                                   void* stream) {
+  if (N < 0 || A < 1 || K < 0) return RAI_E_SHAPE;
+  if (N == 0) return RAI_OK;
+  if (!mu || !log_std || !actions_out || !logp_out) return RAI_E_NULLPTR;
+  const unsigned blocks = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(gaussian_sample_kernel, dim3(blocks), dim3(256), 0, rai_stream(stream), mu,
+                     log_std, N, A, low, high, seed, offset, actions_out, clamped_out, logp_out,
+                     v_in, v_out, K);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

@@ -1,0 +1,395 @@
+"""ActorCritic policy with the reference's module tree (state_dict-compatible).
+
+Mirrors rl_algo_impls/shared/policy/actor_critic.py:110-340 for the configurations
+on the hot path (share_features_extractor=True -> ConnectedTrio network,
+rl_algo_impls/shared/policy/actor_critic_network/connected_trio.py:17-116):
+
+  network._feature_extractor   Encoder: Flatten for 1-D Box obs
+                               (shared/encoder/encoder.py:51-58) or NatureCnn for
+                               3-D Box obs (shared/encoder/nature_cnn.py:10-53,
+                               shared/encoder/cnn.py:24-72; /range_size prescale)
+  network._pi                  CategoricalActorHead._fc (shared/actor/categorical.py:57-87)
+                               or GaussianActorHead.{log_std, mu_net} (shared/actor/gaussian.py:19-61)
+  network._v                   CriticHead._fc = Sequential(mlp) (shared/policy/critic.py:11-41)
+
+Modules are constructed (and layer_init'ed, shared/module/utils.py:7-45) in the
+reference's order, so the same torch seed yields bit-identical initial weights,
+and model.pth checkpoints load in both directions.
+
+The networks' forward/backward run on PyTorch-ROCm (rocBLAS/hipBLASLt GEMMs,
+MIOpen convolutions -> MFMA on gfx950).  Distribution math is written out
+(no torch.distributions validation, which forces host syncs) with the exact
+formulas of torch.distributions.Categorical / Normal.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import NamedTuple, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .envs import is_box, is_discrete
+
+ACTIVATION = {"tanh": nn.Tanh, "relu": nn.ReLU, "identity": nn.Identity, "sigmoid": nn.Sigmoid}
+MODEL_FILENAME = "model.pth"
+F32_MIN = torch.finfo(torch.float32).min
+
+
+class Step(NamedTuple):  # actor_critic.py:42-46
+    a: np.ndarray
+    v: np.ndarray
+    logp_a: np.ndarray
+    clamped_a: np.ndarray
+
+
+class ACForward(NamedTuple):  # actor_critic.py:49-53
+    logp_a: torch.Tensor
+    entropy: torch.Tensor
+    v: torch.Tensor
+
+
+def layer_init(layer: nn.Module, init_layers_orthogonal: bool, std: float = np.sqrt(2)) -> nn.Module:
+    if not init_layers_orthogonal:
+        return layer
+    nn.init.orthogonal_(layer.weight, std)
+    nn.init.constant_(layer.bias, 0.0)
+    return layer
+
+
+def mlp(layer_sizes: Sequence[int], activation, output_activation=nn.Identity,
+        init_layers_orthogonal: bool = False, final_layer_gain: float = np.sqrt(2),
+        hidden_layer_gain: float = np.sqrt(2)) -> nn.Sequential:
+    layers = []
+    for i in range(len(layer_sizes) - 2):
+        layers.append(layer_init(nn.Linear(layer_sizes[i], layer_sizes[i + 1]), init_layers_orthogonal,
+                                 std=hidden_layer_gain))
+        layers.append(activation())
+    layers.append(layer_init(nn.Linear(layer_sizes[-2], layer_sizes[-1]), init_layers_orthogonal,
+                             std=final_layer_gain))
+    layers.append(output_activation())
+    return nn.Sequential(*layers)
+
+
+def default_hidden_sizes(obs_space) -> Sequence[int]:  # actor_critic_network/network.py:73-85
+    if is_box(obs_space):
+        if len(obs_space.shape) == 3:
+            return []
+        if len(obs_space.shape) == 1:
+            return [64, 64]
+        raise ValueError(f"Unsupported observation space: {obs_space}")
+    if is_discrete(obs_space):
+        return [64]
+    raise ValueError(f"Unsupported observation space: {obs_space}")
+
+
+class NatureCnnEncoder(nn.Module):
+    """shared/encoder/nature_cnn.py + cnn.py FlattenedCnnEncoder (keys cnn.{0,2,4}, fc.1)."""
+
+    def __init__(self, obs_space, activation, cnn_init_layers_orthogonal: Optional[bool],
+                 linear_init_layers_orthogonal: bool, cnn_flatten_dim: int):
+        super().__init__()
+        if cnn_init_layers_orthogonal is None:
+            cnn_init_layers_orthogonal = True
+        self.range_size = float(np.max(obs_space.high) - np.min(obs_space.low))
+        in_channels = obs_space.shape[0]
+        self.cnn = nn.Sequential(
+            layer_init(nn.Conv2d(in_channels, 32, kernel_size=8, stride=4), cnn_init_layers_orthogonal),
+            activation(),
+            layer_init(nn.Conv2d(32, 64, kernel_size=4, stride=2), cnn_init_layers_orthogonal),
+            activation(),
+            layer_init(nn.Conv2d(64, 64, kernel_size=3, stride=1), cnn_init_layers_orthogonal),
+            activation(),
+        )
+        with torch.no_grad():
+            dummy = torch.zeros((1,) + tuple(obs_space.shape))
+            n_flat = torch.flatten(self.cnn(dummy), start_dim=1).shape[1]
+        self.fc = nn.Sequential(
+            nn.Flatten(),
+            layer_init(nn.Linear(n_flat, cnn_flatten_dim), linear_init_layers_orthogonal),
+            activation(),
+        )
+        self.out_dim = cnn_flatten_dim
+
+    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+        if obs.dim() == 3:
+            obs = obs.unsqueeze(0)
+        x = obs.float() / self.range_size
+        return self.fc(self.cnn(x))
+
+
+class Encoder(nn.Module):  # shared/encoder/encoder.py:25-73
+    def __init__(self, obs_space, activation, init_layers_orthogonal: bool = False,
+                 cnn_flatten_dim: int = 512, cnn_style: str = "nature",
+                 cnn_layers_init_orthogonal: Optional[bool] = None):
+        super().__init__()
+        if is_box(obs_space) and len(obs_space.shape) == 3:
+            if cnn_style != "nature":
+                raise NotImplementedError(f"cnn_style={cnn_style} is outside the hot-path scope")
+            self.kind = "cnn"
+            self.feature_extractor = NatureCnnEncoder(obs_space, activation, cnn_layers_init_orthogonal,
+                                                      init_layers_orthogonal, cnn_flatten_dim)
+            self.out_dim = self.feature_extractor.out_dim
+        elif is_box(obs_space) and len(obs_space.shape) == 1:
+            self.kind = "flat"
+            self.feature_extractor = nn.Flatten()
+            self.out_dim = int(np.prod(obs_space.shape))
+        elif is_discrete(obs_space):
+            self.kind = "onehot"
+            self.n = obs_space.n
+            self.feature_extractor = nn.Flatten()
+            self.out_dim = obs_space.n
+        else:
+            raise NotImplementedError(f"Unsupported observation space: {obs_space}")
+
+    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+        if self.kind == "flat":
+            if obs.dim() == 1:
+                obs = obs.unsqueeze(0)
+            obs = obs.float()
+        elif self.kind == "onehot":
+            obs = nn.functional.one_hot(obs, self.n).float()
+        return self.feature_extractor(obs)
+
+
+class CategoricalActorHead(nn.Module):
+    def __init__(self, act_dim, in_dim, hidden_sizes=(32,), activation=nn.Tanh, init_layers_orthogonal=True):
+        super().__init__()
+        self.act_dim = act_dim
+        self._fc = mlp((in_dim,) + tuple(hidden_sizes) + (act_dim,), activation,
+                       init_layers_orthogonal=init_layers_orthogonal, final_layer_gain=0.01)
+
+    def params(self, x):
+        return self._fc(x)
+
+    @staticmethod
+    def logp_entropy(logits, actions, action_masks=None):
+        """torch.distributions.Categorical (+ MaskedCategorical, categorical.py:12-54)."""
+        if action_masks is not None:
+            logits = torch.where(action_masks, logits, F32_MIN)
+        norm = logits - logits.logsumexp(dim=-1, keepdim=True)
+        probs = torch.softmax(norm, dim=-1)
+        logp = norm.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)
+        if action_masks is None:
+            ent = -(torch.clamp(norm, min=F32_MIN) * probs).sum(-1)
+        else:
+            ent = -torch.where(action_masks, norm * probs, torch.zeros((), device=norm.device)).sum(-1)
+        return logp, ent
+
+    def mode(self, logits, action_masks=None):
+        if action_masks is not None:
+            logits = torch.where(action_masks, logits, F32_MIN)
+        return logits.argmax(-1)
+
+    @property
+    def action_shape(self):
+        return ()
+
+
+class GaussianActorHead(nn.Module):
+    def __init__(self, act_dim, in_dim, hidden_sizes=(32,), activation=nn.Tanh, init_layers_orthogonal=True,
+                 log_std_init=-0.5):
+        super().__init__()
+        self.act_dim = act_dim
+        self.mu_net = mlp((in_dim,) + tuple(hidden_sizes) + (act_dim,), activation,
+                          init_layers_orthogonal=init_layers_orthogonal, final_layer_gain=0.01)
+        self.log_std = nn.Parameter(torch.ones(act_dim, dtype=torch.float32) * log_std_init)
+
+    def params(self, x):
+        return self.mu_net(x)
+
+    def logp_entropy(self, mu, actions, action_masks=None):
+        """GaussianDistribution (gaussian.py:11-16): log_prob summed over action dims,
+        entropy per dimension (B, act_dim) — the loss averages it (ppo.py:351)."""
+        assert action_masks is None, "GaussianActorHead does not support action_masks"
+        scale = torch.exp(self.log_std)
+        var = scale ** 2
+        log_scale = scale.log()
+        lp = -((actions - mu) ** 2) / (2 * var) - log_scale - math.log(math.sqrt(2 * math.pi))
+        ent = (0.5 + 0.5 * math.log(2 * math.pi) + torch.log(scale)).expand_as(mu)
+        return lp.sum(dim=-1), ent
+
+    def mode(self, mu, action_masks=None):
+        return mu
+
+    @property
+    def action_shape(self):
+        return (self.act_dim,)
+
+
+class CriticHead(nn.Module):
+    def __init__(self, in_dim, hidden_sizes=(), activation=nn.Tanh, init_layers_orthogonal=True):
+        super().__init__()
+        self._fc = nn.Sequential(mlp((in_dim,) + tuple(hidden_sizes) + (1,), activation,
+                                     init_layers_orthogonal=init_layers_orthogonal, final_layer_gain=1.0))
+
+    def forward(self, x):
+        return self._fc(x).squeeze(-1)
+
+
+class ConnectedTrioNetwork(nn.Module):
+    def __init__(self, observation_space, action_space, pi_hidden_sizes=None, v_hidden_sizes=None,
+                 init_layers_orthogonal=True, activation_fn="tanh", log_std_init=-0.5,
+                 cnn_flatten_dim=512, cnn_style="nature", cnn_layers_init_orthogonal=None):
+        super().__init__()
+        pi_hidden_sizes = pi_hidden_sizes if pi_hidden_sizes is not None else default_hidden_sizes(observation_space)
+        v_hidden_sizes = v_hidden_sizes if v_hidden_sizes is not None else default_hidden_sizes(observation_space)
+        activation = ACTIVATION[activation_fn]
+        self.activation_fn = activation_fn
+        self._feature_extractor = Encoder(observation_space, activation, init_layers_orthogonal,
+                                          cnn_flatten_dim, cnn_style, cnn_layers_init_orthogonal)
+        in_dim = self._feature_extractor.out_dim
+        if is_discrete(action_space):
+            self._pi = CategoricalActorHead(action_space.n, in_dim, tuple(pi_hidden_sizes), activation,
+                                            init_layers_orthogonal)
+        elif is_box(action_space):
+            self._pi = GaussianActorHead(action_space.shape[0], in_dim, tuple(pi_hidden_sizes), activation,
+                                         init_layers_orthogonal, log_std_init)
+        else:
+            raise NotImplementedError(f"action space {action_space} is outside the hot-path scope")
+        self._v = CriticHead(in_dim, v_hidden_sizes, activation, init_layers_orthogonal)
+        self.pi_hidden_sizes = tuple(pi_hidden_sizes)
+        self.v_hidden_sizes = tuple(v_hidden_sizes)
+
+    def forward(self, obs, action, action_masks=None):
+        enc = self._feature_extractor(obs)
+        logp, ent = self._pi.logp_entropy(self._pi.params(enc), action, action_masks)
+        return logp, ent, self._v(enc)
+
+    def dist_params_and_value(self, obs):
+        enc = self._feature_extractor(obs)
+        return self._pi.params(enc), self._v(enc)
+
+    def value(self, obs):
+        return self._v(self._feature_extractor(obs))
+
+
+class ActorCritic(nn.Module):
+    """Same constructor kwargs as the reference ActorCritic for the hot-path
+    configurations; unsupported styles raise NotImplementedError loudly."""
+
+    def __init__(self, env, pi_hidden_sizes=None, v_hidden_sizes=None, init_layers_orthogonal=True,
+                 activation_fn="tanh", log_std_init=-0.5, use_sde=False, full_std=True, squash_output=False,
+                 share_features_extractor=True, cnn_flatten_dim=512, cnn_style="nature",
+                 cnn_layers_init_orthogonal=None, actor_head_style="single", **kwargs):
+        super().__init__()
+        if use_sde or squash_output:
+            raise NotImplementedError("gSDE / squash_output are outside the hot-path scope")
+        if not share_features_extractor:
+            raise NotImplementedError("SeparateActorCriticNetwork is outside the hot-path scope")
+        if actor_head_style != "single":
+            raise NotImplementedError(f"actor_head_style={actor_head_style} is outside the hot-path scope")
+        self.env = env
+        self.action_space = env.single_action_space
+        self.observation_space = env.single_observation_space
+        self.squash_output = squash_output
+        self.network = ConnectedTrioNetwork(env.single_observation_space, env.single_action_space,
+                                            pi_hidden_sizes, v_hidden_sizes, init_layers_orthogonal,
+                                            activation_fn, log_std_init, cnn_flatten_dim, cnn_style,
+                                            cnn_layers_init_orthogonal)
+        self._device: Optional[torch.device] = None
+
+    # -- reference API ------------------------------------------------------------
+    def to(self, device=None, *args, **kwargs):
+        super().to(device, *args, **kwargs)
+        if device is not None:
+            self._device = torch.device(device)
+        return self
+
+    @property
+    def device(self) -> torch.device:
+        assert self._device is not None, "Expect device to be set"
+        return self._device
+
+    @property
+    def action_shape(self) -> Tuple[int, ...]:
+        return self.network._pi.action_shape
+
+    @property
+    def value_shape(self) -> Tuple[int, ...]:
+        return ()
+
+    @property
+    def is_discrete(self) -> bool:
+        return isinstance(self.network._pi, CategoricalActorHead)
+
+    def forward(self, obs, action, action_masks=None) -> ACForward:
+        return ACForward(*self.network(obs, action, action_masks))
+
+    def _as_tensor(self, a):
+        return torch.as_tensor(a).to(self.device)
+
+    def value(self, obs: np.ndarray) -> np.ndarray:
+        with torch.no_grad():
+            return self.network.value(self._as_tensor(obs)).cpu().numpy()
+
+    def step(self, obs: np.ndarray, action_masks=None) -> Step:
+        """Numpy step for eval/enjoy parity (actor_critic.py:306-318); the trainer's
+        rollout uses the HBM-resident path in rollout.py instead."""
+        with torch.no_grad():
+            o = self._as_tensor(obs)
+            params, v = self.network.dist_params_and_value(o)
+            if self.is_discrete:
+                m = self._as_tensor(action_masks) if action_masks is not None else None
+                if m is not None:
+                    params = torch.where(m, params, F32_MIN)
+                a = torch.multinomial(torch.softmax(params, -1), 1).squeeze(-1)
+                logp, _ = self.network._pi.logp_entropy(params, a, m)
+            else:
+                a = params + torch.exp(self.network._pi.log_std) * torch.randn_like(params)
+                logp, _ = self.network._pi.logp_entropy(params, a)
+        a_np = a.cpu().numpy()
+        return Step(a_np, v.cpu().numpy(), logp.cpu().numpy(), clamp_actions(a_np, self.action_space, False))
+
+    def act(self, obs: np.ndarray, deterministic: bool = True, action_masks=None) -> np.ndarray:
+        if not deterministic:
+            return self.step(obs, action_masks=action_masks).clamped_a
+        with torch.no_grad():
+            o = self._as_tensor(obs)
+            params, _ = self.network.dist_params_and_value(o)
+            m = self._as_tensor(action_masks) if action_masks is not None else None
+            a = self.network._pi.mode(params, m)
+        return clamp_actions(a.cpu().numpy(), self.action_space, self.squash_output)
+
+    def reset_noise(self, batch_size: Optional[int] = None) -> None:
+        pass
+
+    def save_weights(self, path: str) -> None:
+        torch.save(self.state_dict(), os.path.join(path, MODEL_FILENAME))
+
+    def load_weights(self, path: str) -> None:
+        self.load_state_dict(torch.load(os.path.join(path, MODEL_FILENAME), map_location=self._device,
+                                        weights_only=True))
+
+    def save(self, path: str) -> None:
+        os.makedirs(path, exist_ok=True)
+        self.save_weights(path)
+
+    def load(self, path: str, load_norm_rms_count_override=None) -> None:
+        self.load_weights(path)
+
+    def num_parameters(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def freeze(self, freeze_policy_head: bool, freeze_value_head: bool, freeze_backbone: bool = True) -> None:
+        for p in self.network._pi.parameters():
+            p.requires_grad = not freeze_policy_head
+        for p in self.network._v.parameters():
+            p.requires_grad = not freeze_value_head
+        for p in self.network._feature_extractor.parameters():
+            p.requires_grad = not freeze_backbone
+
+    def unfreeze(self) -> None:
+        self.freeze(False, False, False)
+
+
+def clamp_actions(actions, action_space, squash_output: bool):
+    """actor_critic.py:62-87 (Box: clip, or rescale when squash_output)."""
+    if is_box(action_space):
+        low, high = action_space.low, action_space.high
+        if squash_output:
+            return low + 0.5 * (actions + 1) * (high - low)
+        return np.clip(actions, low, high)
+    return actions

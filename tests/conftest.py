@@ -1,0 +1,60 @@
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+import _pkgload  # noqa: E402
+
+rai = _pkgload.load()
+GOLDEN = ROOT / "tests" / "golden"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) device")
+
+
+def _has_gpu():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if _has_gpu():
+        return
+    skip = pytest.mark.skip(reason="no HIP device in this container")
+    for item in items:
+        if "gpu" in item.keywords:
+            item.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def golden():
+    def load(name):
+        return np.load(GOLDEN / name, allow_pickle=False)
+
+    return load
+
+
+@pytest.fixture(scope="session")
+def gae_cases(golden):
+    z = golden("gae_cases.npz")
+    meta = json.loads(str(z["meta"]))
+    cases = []
+    for i, m in enumerate(meta):
+        p = f"c{i}_"
+        c = {k[len(p):]: z[k] for k in z.files if k.startswith(p)}
+        gamma = c["gamma"] if m["gamma_is_vector"] else float(c["gamma"][0])
+        lam = c["lam"] if m["lam_is_vector"] else float(c["lam"][0])
+        c.update(gamma=gamma, lam=lam, idx=i)
+        cases.append(c)
+    return cases
