@@ -1,0 +1,187 @@
+#!/usr/bin/env python
+"""bench.py — PPO rollout+update throughput on MI355X (BASELINE.json configs[1]).
+
+One "step" = one PPO update (learn_epoch): a rollout of n_steps x num_envs env
+steps on the seeded synthetic CartPole-shaped VecEnv (host), GAE on device, and
+n_epochs x minibatches of fused loss / backward / clip+Adam — exactly the region
+the reference times as train/steps_per_second (rl_algo_impls/ppo/ppo.py:221,422-427).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config cartpole|pong|halfcheetah]
+                    [--batch-policy yaml|scaled]
+
+Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), each rank
+owns its own env group of num_envs envs and its own HBM rollout; gradients are
+all-reduced (RCCL) once per optimizer step.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+CONFIGS = {
+    # BASELINE.json configs[1]: ppo CartPole-v1, num_envs=4096, n_steps=128 (YAML algo hyperparams,
+    # rl_algo_impls/hyperparams/ppo.yml:1-23)
+    "cartpole": dict(env="cartpole", num_envs=4096, n_steps=128, policy=dict(),
+                     algo=dict(batch_size=256, n_epochs=20, gamma=0.98, gae_lambda=0.8, ent_coef=0.0,
+                               learning_rate=1e-3, clip_range=0.2)),
+    # configs[2]: PongNoFrameskip-v4 NatureCNN, num_envs=1024, n_steps=128 (ppo.yml:225-253 _atari)
+    "pong": dict(env="pong", num_envs=1024, n_steps=128, policy=dict(activation_fn="relu"),
+                 algo=dict(batch_size=256, n_epochs=4, learning_rate=2.5e-4, clip_range=0.1, vf_coef=0.5,
+                           ent_coef=0.01)),
+    # configs[3]: HalfCheetah-v4, num_envs=2048 (global; per-rank share under DP), n_steps=512 (ppo.yml:337-359)
+    "halfcheetah": dict(env="halfcheetah", num_envs=2048, n_steps=512,
+                        policy=dict(pi_hidden_sizes=[256, 256], v_hidden_sizes=[256, 256], activation_fn="relu",
+                                    log_std_init=-2, init_layers_orthogonal=False),
+                        algo=dict(batch_size=64, n_epochs=20, gamma=0.98, gae_lambda=0.92, ent_coef=0.000401762,
+                                  max_grad_norm=0.8, vf_coef=0.58096, learning_rate=2.0633e-05, clip_range=0.1)),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default="cartpole", choices=sorted(CONFIGS))
+    p.add_argument("--batch-policy", default="yaml", choices=["yaml", "scaled"],
+                   help="yaml: the YAML batch_size; scaled: batch = T*N/4 (4 minibatches/epoch)")
+    p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--roofline-reps", type=int, default=200)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd import _lib
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.gae import compute_advantages_device
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    _lib.lib()
+
+    cfg = CONFIGS[args.config]
+    N, T = cfg["num_envs"], cfg["n_steps"]
+    if args.config == "halfcheetah" and world > 1:
+        N = N // world  # configs[3] is quoted as a global env count across the node
+    algo_kw = dict(cfg["algo"])
+    if args.batch_policy == "scaled":
+        algo_kw["batch_size"] = T * N // 4
+    torch.manual_seed(1 + rank)
+    env = SyntheticVecEnv(N, cfg["env"], seed=1000 * rank + 1)
+    policy = ActorCritic(env, **cfg["policy"]).to(dev)
+    if world > 1:  # identical initial weights on every rank
+        with torch.no_grad():
+            for p in policy.parameters():
+                torch.distributed.broadcast(p.data, 0)
+    gen = SyncStepRolloutGenerator(policy, env, n_steps=T, seed=1234 + rank)
+    algo = PPO(policy, dev, None, **algo_kw)
+    if world > 1:
+        algo.enable_data_parallel()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        algo.learn_epoch(0, 1, gen, None)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        algo.learn_epoch(0, 1, gen, None)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_steps = args.steps * T * N * world
+    value = total_steps / elapsed
+
+    # ---- roofline of the GAE kernel (named by the BASELINE metric), live HIP events on the
+    # stream the kernel is launched on (torch's current stream = the stream passed to rai_gae)
+    r = gen.rollout(gamma=algo.gamma, gae_lambda=algo.gae_lambda)
+    K = 1
+    gae_bytes = (4 * T * N * K) * 4 + T * N + 4 * N * K + N  # r, V, adv, returns + starts + next V/starts
+    adv = torch.empty_like(r.values)
+    ret = torch.empty_like(r.values)
+    for _ in range(10):
+        compute_advantages_device(r.rewards, r.values, r.episode_starts, r.next_episode_starts, r.next_values,
+                                  algo.gamma, algo.gae_lambda, advantages_out=adv, returns_out=ret)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(args.roofline_reps):
+        compute_advantages_device(r.rewards, r.values, r.episode_starts, r.next_episode_starts, r.next_values,
+                                  algo.gamma, algo.gae_lambda, advantages_out=adv, returns_out=ret)
+    ev1.record()
+    ev1.synchronize()
+    gae_us = ev0.elapsed_time(ev1) * 1e3 / args.roofline_reps
+    achieved = gae_bytes / (gae_us * 1e-6) / 1e9
+    peak = 8000.0
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "cartpole":
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import cpu_trainer  # checker/baseline only
+
+        res = cpu_trainer.time_sampled_update(budget_seconds=args.cpu_baseline_seconds, num_envs=N, n_steps=T,
+                                              batch_size=algo_kw["batch_size"], n_epochs=algo_kw["n_epochs"])
+        cpu = {"value": round(res["env_steps_per_s"], 1), "unit": "env-steps/s", "cores": res["threads"],
+               "kind": "port",
+               "sample": (f"full rollout {T}x{N} + numpy GAE + {res['minibatches_timed']} of "
+                          f"{res['minibatches_total']} minibatch steps timed, update time extrapolated "
+                          f"(oracle/cpu_trainer.py, torch CPU eager like the reference)")}
+
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec (rollout+update) at 1/2/4/8 MI355X; GAE kernel HBM GB/s",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded host VecEnv with the config's obs/action shapes; random-init policy)",
+            "config": {"workload": f"ppo {args.config} num_envs={N}/rank n_steps={T}",
+                       "global_batch": algo_kw["batch_size"] * world, "n_epochs": algo_kw["n_epochs"],
+                       "batch_policy": args.batch_policy, "seq_len": T, "parallelism": f"dp{world}"},
+            "roofline": {"kernel": "gae_kernel<double> (rai_gae exact mode)", "bound": "hbm",
+                         "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "avg_us": round(gae_us, 3), "bytes_per_launch": gae_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

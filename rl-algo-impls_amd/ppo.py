@@ -1,0 +1,189 @@
+"""PPO on MI355X — drop-in for rl_algo_impls/ppo/ppo.py:106-447.
+
+Same constructor kwargs, same mutable attributes (learning_rate, clip_range,
+ent_coef, gamma, gae_lambda, vf_coef, ... — what HyperparamTransitions and
+LearningRateByKLDivergence set), same learn()/learn_epoch() contract, same
+TrainStats and tensorboard tags, same `train/steps_per_second` definition
+(wall time of learn_epoch before callbacks, ppo.py:221,422-427).
+
+Per minibatch the work is: PyTorch-ROCm forward of the policy on a contiguous
+slice of the permuted HBM rollout -> ONE fused HIP loss kernel (advantage
+normalisation, clipped surrogate, value/entropy loss, gradients w.r.t. the
+network outputs, stats row) -> PyTorch-ROCm backward seeded with those
+gradients -> ONE fused clip_grad_norm_ + Adam step (two HIP launches) over the
+flat parameter buffer.  No host synchronisation until the update ends.
+"""
+from __future__ import annotations
+
+import gc
+import logging
+from time import perf_counter
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .optim import FlatOptimizer, FlatParams
+from .pg_common import (DeviceBlocks, TrainStats, launch_loss, load_optimizer, log_scalars, make_hparams,
+                        num_or_array, save_optimizer, unsupported, value_columns)
+
+
+class PPO:
+    def __init__(self, policy, device: torch.device, tb_writer, learning_rate: float = 3e-4,
+                 batch_size: int = 64, n_epochs: int = 10, gamma=0.99, gae_lambda=0.95, clip_range: float = 0.2,
+                 clip_range_vf: Optional[float] = None, normalize_advantage: bool = True,
+                 standardize_advantage: bool = False, ent_coef: float = 0.0, vf_coef=0.5,
+                 ppo2_vf_coef_halving: bool = False, max_grad_norm: float = 0.5,
+                 multi_reward_weights: Optional[List[float]] = None, gradient_accumulation: bool = False,
+                 kl_cutoff: Optional[float] = None, freeze_policy_head: bool = False,
+                 freeze_value_head: bool = False, freeze_backbone: bool = False, switch_range=None,
+                 guide_probability=None, normalize_advantages_after_scaling: bool = False,
+                 autocast_loss: bool = False, vf_loss_fn: str = "mse_loss", vf_weights=None,
+                 teacher_kl_loss_coef=None, teacher_kl_loss_fn=None, teacher_loss_importance_sampling=True):
+        unsupported(freeze_policy_head=freeze_policy_head, freeze_value_head=freeze_value_head,
+                    freeze_backbone=freeze_backbone, switch_range=switch_range is not None,
+                    guide_probability=guide_probability is not None, autocast_loss=autocast_loss,
+                    teacher_kl_loss_coef=teacher_kl_loss_coef is not None)
+        assert not (normalize_advantage and standardize_advantage), "Cannot both normalize and standardize advantage"
+        self.policy = policy
+        self.device = torch.device(device)
+        self.tb_writer = tb_writer
+        self.learning_rate = learning_rate
+        self.flat = FlatParams(policy, self.device)
+        self.optimizer = FlatOptimizer(self.flat, FlatOptimizer.ADAM, lr=learning_rate, eps=1e-7,
+                                       max_grad_norm=max_grad_norm)
+        self.gamma = num_or_array(gamma)
+        self.gae_lambda = num_or_array(gae_lambda)
+        self.max_grad_norm = max_grad_norm
+        self.clip_range = clip_range
+        self.clip_range_vf = clip_range_vf
+        self.normalize_advantage = normalize_advantage
+        self.standardize_advantage = standardize_advantage
+        self.ent_coef = ent_coef
+        self.vf_coef = num_or_array(vf_coef)
+        self.vf_weights = np.array(vf_weights) if vf_weights is not None else None
+        self.ppo2_vf_coef_halving = ppo2_vf_coef_halving
+        self.batch_size = batch_size
+        self.n_epochs = n_epochs
+        self.multi_reward_weights = np.array(multi_reward_weights) if multi_reward_weights else None
+        self.gradient_accumulation = gradient_accumulation
+        self.kl_cutoff = kl_cutoff
+        self.normalize_advantages_after_scaling = normalize_advantages_after_scaling
+        self.vf_loss_fn = vf_loss_fn
+        self.blocks = DeviceBlocks(self.device)
+        self.last_update_seconds: Optional[float] = None
+
+    # -- reference API -------------------------------------------------------------------
+    def learn(self, train_timesteps: int, rollout_generator, callbacks=None, total_timesteps=None,
+              start_timesteps: int = 0) -> "PPO":
+        if total_timesteps is None:
+            total_timesteps = train_timesteps
+        assert start_timesteps + train_timesteps <= total_timesteps
+        timesteps_elapsed = start_timesteps
+        while timesteps_elapsed < start_timesteps + train_timesteps:
+            timesteps_elapsed, should_continue = self.learn_epoch(timesteps_elapsed, total_timesteps,
+                                                                  rollout_generator, callbacks)
+            gc.collect()
+            if not should_continue:
+                break
+        return self
+
+    def _hparams(self, K: int, num_minibatches: int):
+        return make_hparams(
+            loss_kind=0, K=K, clip_range=self.clip_range, clip_range_vf=self.clip_range_vf,
+            ent_coef=self.ent_coef, vf_coef=self.vf_coef, vf_weights=self.vf_weights,
+            multi_reward_weights=self.multi_reward_weights, normalize_advantage=self.normalize_advantage,
+            standardize_advantage=self.standardize_advantage,
+            normalize_after_scaling=self.normalize_advantages_after_scaling,
+            ppo2_vf_coef_halving=self.ppo2_vf_coef_halving, kl_cutoff=self.kl_cutoff, vf_loss_fn=self.vf_loss_fn,
+            grad_scale=(1.0 / num_minibatches) if self.gradient_accumulation else 1.0)
+
+    def learn_epoch(self, timesteps_elapsed: int, total_timesteps: int, rollout_generator,
+                    callbacks=None) -> Tuple[int, bool]:
+        start_time = perf_counter()
+        self.optimizer.param_groups[0]["lr"] = self.learning_rate  # update_learning_rate (schedule.py:64-66)
+        self.optimizer.max_grad_norm = self.max_grad_norm
+        self.optimizer.sync_hparams()
+        chart = {"learning_rate": self.learning_rate, "ent_coef": self.ent_coef, "pi_clip": self.clip_range,
+                 "gamma": self.gamma, "gae_lambda": self.gae_lambda, "vf_coef": self.vf_coef}
+        if self.clip_range_vf is not None:
+            chart["v_clip"] = self.clip_range_vf
+        if self.multi_reward_weights is not None:
+            chart["reward_weights"] = self.multi_reward_weights
+        if self.vf_weights is not None:
+            chart["vf_weights"] = self.vf_weights
+        log_scalars(self.tb_writer, "charts", chart, timesteps_elapsed)
+
+        r = rollout_generator.rollout(gamma=self.gamma, gae_lambda=self.gae_lambda)
+        timesteps_elapsed += r.total_steps
+        stats, norms, K = self.update(r)
+        explained_var = r.explained_variance()
+        train_stats = self._train_stats(stats, norms, K, r.num_minibatches(self.batch_size), explained_var)
+        train_stats.write_to_tensorboard(self.tb_writer)
+        end_time = perf_counter()
+        self.last_update_seconds = end_time - start_time
+        if self.tb_writer is not None:
+            self.tb_writer.add_scalar("train/steps_per_second", r.total_steps / (end_time - start_time))
+            if hasattr(self.tb_writer, "on_steps"):
+                self.tb_writer.on_steps(r.total_steps)
+        self.last_train_stats = train_stats
+        if callbacks:
+            if not all(c.on_step(timesteps_elapsed=r.total_steps, train_stats=train_stats) for c in callbacks):
+                logging.info(f"Callback terminated training at {timesteps_elapsed} timesteps")
+                return timesteps_elapsed, False
+        return timesteps_elapsed, True
+
+    def update(self, r) -> Tuple[np.ndarray, np.ndarray, int]:
+        """All epochs x minibatches of one update, enqueued without host syncs;
+        returns the per-minibatch stats rows and grad norms (one D2H copy)."""
+        nmb = r.num_minibatches(self.batch_size)
+        n_steps = self.n_epochs * nmb
+        n_norms = self.n_epochs if self.gradient_accumulation else n_steps
+        blocks = self.blocks
+        blocks.ensure_tables(n_steps, n_norms)
+        K = None
+        self.flat.check_views()
+        for _ in range(self.n_epochs):
+            for mb in r.minibatches(self.batch_size, shuffle=not self.gradient_accumulation):
+                logp, ent, v = self.policy(mb.obs, mb.actions, action_masks=mb.action_masks)
+                if K is None:
+                    K = value_columns(v)
+                    blocks.upload(self._hparams(K, nmb), self.optimizer.step_count)
+                if mb.logprobs is None:
+                    raise ValueError("PPO needs rollout logprobs (include_logp=True)")
+                d_logp, d_ent, d_v = launch_loss(blocks, logp, ent, v, mb.logprobs, mb.values, mb.advantages,
+                                                 mb.returns, K)
+                torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
+                if not self.gradient_accumulation:
+                    self.optimizer.step(blocks.state, blocks.norms)
+            if self.gradient_accumulation:
+                self.optimizer.step(blocks.state, blocks.norms)
+        host = torch.cat([blocks.stats[:n_steps].reshape(-1), blocks.norms[:n_norms]]).cpu().numpy()
+        stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE)
+        return stats, host[n_steps * _lib.RAI_STAT_STRIDE:], K or 1
+
+    def _train_stats(self, stats: np.ndarray, norms: np.ndarray, K: int, nmb: int, explained_var: float):
+        last = stats[-nmb:].astype(np.float64)  # only the last epoch's stats are kept (ppo.py:288-289)
+        vl = last[:, 5:5 + K]
+        vc = last[:, 5 + _lib.RAI_MAX_K:5 + _lib.RAI_MAX_K + K]
+        if self.vf_weights is not None:
+            w = np.asarray(self.vf_weights, np.float64)
+            v_loss = float(np.mean(vl @ w))
+        else:
+            v_loss = np.mean(vl, axis=0)
+            v_loss = float(v_loss[0]) if K == 1 else v_loss
+        val_clipped = np.mean(vc, axis=0)
+        last_norms = norms[-1:] if self.gradient_accumulation else norms[-nmb:]
+        return TrainStats(
+            loss=float(last[:, 0].mean()), pi_loss=float(last[:, 1].mean()), v_loss=v_loss,
+            entropy_loss=float(last[:, 2].mean()), approx_kl=float(last[:, 3].mean()),
+            clipped_frac=float(last[:, 4].mean()),
+            val_clipped_frac=float(val_clipped[0]) if K == 1 else val_clipped, additional_losses={},
+            explained_var=explained_var, grad_norm=float(np.mean(last_norms)))
+
+    def save(self, path: str) -> None:
+        save_optimizer(self.optimizer, path)
+
+    def load(self, path: str) -> None:
+        load_optimizer(self.optimizer, path, self.device)

@@ -1,0 +1,12 @@
+"""Plugin registries under the reference's names (rl_algo_impls/runner/running_utils.py:38-55),
+so `--algo ppo|a2c` hyperparameters resolve to the MI355X implementations."""
+from __future__ import annotations
+
+from .a2c import A2C
+from .policy import ActorCritic
+from .ppo import PPO
+from .rollout import SyncStepRolloutGenerator
+
+ALGOS = {"ppo": PPO, "a2c": A2C}
+POLICIES = {"ppo": ActorCritic, "a2c": ActorCritic}
+DEFAULT_ROLLOUT_GENERATORS = {"ppo": SyncStepRolloutGenerator, "a2c": SyncStepRolloutGenerator}

@@ -1,0 +1,348 @@
+"""HBM-resident rollout buffer, GAE and minibatching behind the reference's
+Rollout / RolloutGenerator / Batch contract.
+
+Reference interfaces mirrored:
+  Batch (field order, consumed positionally via astuple)   rl_algo_impls/rollout/rollout.py:23-72
+  Rollout ABC (y_true, y_pred, total_steps, num_minibatches, minibatches, add_to_batch)
+                                                            rl_algo_impls/rollout/rollout.py:78-103
+  RolloutGenerator ABC (__init__(policy, vec_env, **kw), prepare, rollout)
+                                                            rl_algo_impls/rollout/rollout.py:106-117
+  SyncStepRolloutGenerator kwargs / loop                    rl_algo_impls/rollout/sync_step_rollout.py:14-216
+  VecRollout (GAE, returns, minibatches)                    rl_algo_impls/rollout/vec_rollout.py:38-175
+
+Design (MI355X-first): the (T, N, ...) buffers live in HBM for the whole update
+(288 GB/GPU: the 3.7 GB Pong buffer fits with room for its permuted copy).  Per
+env step the host obs go H2D into slot s, the policy head runs on the slot and a
+fused HIP kernel samples the action and writes action / log-prob / value into the
+slot; only the actions return to the host (the env steps there).  GAE and returns
+run as one HIP reverse-scan over the resident buffers.  Each epoch's shuffle is a
+single multi-field gather kernel into a permuted copy, after which every
+minibatch is a contiguous slice (zero-copy views) instead of a fancy-index
+gather per minibatch.
+"""
+from __future__ import annotations
+
+import dataclasses
+from abc import ABC, abstractmethod
+from dataclasses import dataclass
+from typing import Callable, Dict, Iterator, List, Optional
+
+import ctypes as C
+import numpy as np
+import torch
+
+from . import _lib
+from .envs import is_box, is_discrete
+from .gae import EXACT, compute_advantages_device
+
+
+@dataclass
+class Batch:  # rollout.py:23-36 — field ORDER is part of the contract
+    obs: torch.Tensor
+    logprobs: Optional[torch.Tensor]
+    actions: torch.Tensor
+    action_masks: Optional[torch.Tensor]
+    num_actions: Optional[torch.Tensor]
+    values: torch.Tensor
+    advantages: torch.Tensor
+    returns: torch.Tensor
+    additional: Dict[str, torch.Tensor] = dataclasses.field(default_factory=dict)
+
+    @property
+    def device(self) -> torch.device:
+        return self.obs.device
+
+    def to(self, device: torch.device) -> "Batch":
+        if self.device == torch.device(device):
+            return self
+        mv = lambda t: None if t is None else t.to(device)
+        return Batch(*(mv(getattr(self, f.name)) for f in dataclasses.fields(self)[:-1]),
+                     {k: v.to(device) for k, v in self.additional.items()})
+
+    def __getitem__(self, indices: torch.Tensor) -> "Batch":
+        g = lambda t: None if t is None else t[indices]
+        return Batch(self.obs[indices], g(self.logprobs), self.actions[indices], g(self.action_masks),
+                     g(self.num_actions), self.values[indices], self.advantages[indices],
+                     self.returns[indices], {k: v[indices] for k, v in self.additional.items()})
+
+    def __len__(self) -> int:
+        return self.obs.shape[0]
+
+
+BatchMapFn = Callable[[Batch], Dict[str, torch.Tensor]]
+
+
+class Rollout(ABC):
+    @property
+    @abstractmethod
+    def y_true(self) -> np.ndarray: ...
+
+    @property
+    @abstractmethod
+    def y_pred(self) -> np.ndarray: ...
+
+    @property
+    @abstractmethod
+    def total_steps(self) -> int: ...
+
+    @abstractmethod
+    def num_minibatches(self, batch_size: int) -> int: ...
+
+    @abstractmethod
+    def minibatches(self, batch_size: int, shuffle: bool = True) -> Iterator[Batch]: ...
+
+    def add_to_batch(self, map_fn: BatchMapFn, batch_size: int) -> None: ...
+
+
+class RolloutGenerator(ABC):
+    def __init__(self, policy, vec_env, **kwargs) -> None:
+        super().__init__()
+        self.policy = policy
+        self.vec_env = vec_env
+
+    def prepare(self) -> None:
+        pass
+
+    @abstractmethod
+    def rollout(self, **kwargs) -> Rollout: ...
+
+
+def gather_rows(srcs: List[torch.Tensor], dsts: List[torch.Tensor], idx: torch.Tensor) -> None:
+    """dst_f[i] = src_f[idx[i]] for every field, one kernel launch (rai_gather_rows)."""
+    n = len(srcs)
+    assert 0 < n <= _lib.RAI_MAX_FIELDS and len(dsts) == n
+    idx = idx.to(torch.int64).contiguous()
+    rows = idx.shape[0]
+    src_p = (C.c_void_p * n)(*[s.data_ptr() for s in srcs])
+    dst_p = (C.c_void_p * n)(*[d.data_ptr() for d in dsts])
+    rb = (C.c_int64 * n)(*[s[0].numel() * s.element_size() if s.shape[0] else 1 for s in srcs])
+    for s, d in zip(srcs, dsts):
+        assert s.is_contiguous() and d.is_contiguous() and s.dtype == d.dtype
+        assert d.shape[0] >= rows and s.shape[1:] == d.shape[1:]
+    rc = _lib.lib().rai_gather_rows(n, C.cast(src_p, C.c_void_p), C.cast(dst_p, C.c_void_p),
+                                    C.cast(rb, C.c_void_p), idx.data_ptr(), rows,
+                                    _lib.stream_handle(idx.device))
+    _lib.check(rc, "rai_gather_rows")
+
+
+class DeviceRollout(Rollout):
+    """VecRollout equivalent over HBM-resident (T, N, ...) tensors."""
+
+    def __init__(self, device: torch.device, next_episode_starts: torch.Tensor, next_values: torch.Tensor,
+                 obs: torch.Tensor, actions: torch.Tensor, rewards: torch.Tensor,
+                 episode_starts: torch.Tensor, values: torch.Tensor, logprobs: Optional[torch.Tensor],
+                 action_masks: Optional[torch.Tensor], gamma, gae_lambda,
+                 scale_advantage_by_values_accuracy: bool = False, gae_mode: int = EXACT,
+                 perm_source: Optional[Callable[[int], torch.Tensor]] = None,
+                 generator: Optional[torch.Generator] = None) -> None:
+        super().__init__()
+        self.device = device
+        self.obs, self.actions, self.rewards = obs, actions, rewards
+        self.episode_starts, self.values, self.logprobs = episode_starts, values, logprobs
+        self.action_masks = action_masks
+        self.next_episode_starts, self.next_values = next_episode_starts, next_values
+        self.num_actions = None
+        if action_masks is not None:  # rollout.py:130-180 (no subaction masks on the hot path)
+            self.num_actions = action_masks.any(-1).sum(-1) if action_masks.dim() > 3 else None
+        self.advantages, self.returns = compute_advantages_device(
+            rewards, values, episode_starts, next_episode_starts, next_values, gamma, gae_lambda,
+            mode=gae_mode, want_returns=True)
+        if scale_advantage_by_values_accuracy:  # vec_rollout.py:91-94
+            ptp = self.returns.max() - self.returns.min()
+            self.advantages *= torch.exp(-torch.abs(self.values - self.returns) / ptp)
+        self._perm_source = perm_source
+        self._generator = generator
+        self._flat: Optional[List[torch.Tensor]] = None
+        self._perm_buf: Optional[List[torch.Tensor]] = None
+
+    # -- Rollout API ---------------------------------------------------------------------
+    @property
+    def y_true(self) -> np.ndarray:
+        return self.returns.reshape((-1,) + tuple(self.returns.shape[2:])).cpu().numpy()
+
+    @property
+    def y_pred(self) -> np.ndarray:
+        return self.values.reshape((-1,) + tuple(self.values.shape[2:])).cpu().numpy()
+
+    @property
+    def total_steps(self) -> int:
+        return int(self.rewards.shape[0] * self.rewards.shape[1])
+
+    def num_minibatches(self, batch_size: int) -> int:
+        return self.total_steps // batch_size + (1 if self.total_steps % batch_size else 0)
+
+    def explained_variance(self) -> float:
+        """1 - var(R - V)/var(R) (ppo.py:415-418), reduced on device, one host read."""
+        y = self.returns.reshape(-1).double()
+        p = self.values.reshape(-1).double()
+        var_y = torch.var(y, unbiased=False)
+        ev = 1 - torch.var(y - p, unbiased=False) / var_y
+        var_y, ev = (float(x) for x in torch.stack([var_y, ev]).cpu())
+        return float("nan") if var_y == 0 else ev
+
+    def _flat_fields(self) -> List[torch.Tensor]:
+        if self._flat is None:
+            fl = lambda t: t.reshape((-1,) + tuple(t.shape[2:]))
+            fields = [fl(self.obs), fl(self.actions), fl(self.values), fl(self.advantages), fl(self.returns)]
+            if self.logprobs is not None:
+                fields.append(fl(self.logprobs))
+            if self.action_masks is not None:
+                fields.append(fl(self.action_masks))
+            self._flat = fields
+        return self._flat
+
+    def _batch_from(self, fields: List[torch.Tensor], sl: slice) -> Batch:
+        obs, actions, values, adv, ret = (f[sl] for f in fields[:5])
+        i = 5
+        logprobs = None
+        if self.logprobs is not None:
+            logprobs = fields[i][sl]
+            i += 1
+        masks = fields[i][sl] if self.action_masks is not None else None
+        return Batch(obs, logprobs, actions, masks, None, values, adv, ret)
+
+    def permutation(self) -> torch.Tensor:
+        if self._perm_source is not None:
+            return self._perm_source(self.total_steps).to(self.device)
+        return torch.randperm(self.total_steps, device=self.device, generator=self._generator)
+
+    def minibatches(self, batch_size: int, shuffle: bool = True) -> Iterator[Batch]:
+        flat = self._flat_fields()
+        if shuffle:
+            if self._perm_buf is None:
+                self._perm_buf = [torch.empty_like(f) for f in flat]
+            gather_rows(flat, self._perm_buf, self.permutation())
+            src = self._perm_buf
+        else:
+            src = flat
+        for i in range(0, self.total_steps, batch_size):
+            yield self._batch_from(src, slice(i, i + batch_size))
+
+    def add_to_batch(self, map_fn: BatchMapFn, batch_size: int) -> None:
+        raise NotImplementedError("teacher-KL additional batch fields are outside the hot-path scope")
+
+
+_UNSUPPORTED_GEN_KW = ("sde_sample_freq", "num_envs_reset_every_rollout", "rolling_num_envs_reset_every_rollout",
+                       "random_num_envs_reset_every_rollout", "prepare_steps",
+                       "rolling_num_envs_reset_every_prepare_step")
+
+
+class SyncStepRolloutGenerator(RolloutGenerator):
+    """Device-resident SyncStepRolloutGenerator (sync_step_rollout.py:14-216)."""
+
+    def __init__(self, policy, vec_env, n_steps: int = 2048, sde_sample_freq: int = -1,
+                 scale_advantage_by_values_accuracy: bool = False, full_batch_off_accelerator: bool = False,
+                 include_logp: bool = True, subaction_mask=None, num_envs_reset_every_rollout: int = 0,
+                 rolling_num_envs_reset_every_rollout: int = 0, random_num_envs_reset_every_rollout: int = 0,
+                 prepare_steps: int = 0, rolling_num_envs_reset_every_prepare_step: int = 0,
+                 gae_mode: int = EXACT, seed: Optional[int] = None) -> None:
+        super().__init__(policy, vec_env)
+        bad = [k for k, v, d in [("sde_sample_freq", sde_sample_freq, -1),
+                                 ("num_envs_reset_every_rollout", num_envs_reset_every_rollout, 0),
+                                 ("rolling_num_envs_reset_every_rollout", rolling_num_envs_reset_every_rollout, 0),
+                                 ("random_num_envs_reset_every_rollout", random_num_envs_reset_every_rollout, 0),
+                                 ("prepare_steps", prepare_steps, 0),
+                                 ("rolling_num_envs_reset_every_prepare_step",
+                                  rolling_num_envs_reset_every_prepare_step, 0)] if v != d]
+        if bad or subaction_mask or full_batch_off_accelerator:
+            raise NotImplementedError(f"rollout options outside the hot-path scope: {bad or 'subaction_mask/full_batch_off_accelerator'}")
+        if getattr(vec_env, "get_action_mask", None) is not None:
+            raise NotImplementedError("action-masked envs (MicroRTS/Lux) are outside the hot-path scope")
+        self.n_steps = n_steps
+        self.include_logp = include_logp
+        self.scale_advantage_by_values_accuracy = scale_advantage_by_values_accuracy
+        self.gae_mode = gae_mode
+        self.device = policy.device
+        self.seed = int(torch.initial_seed() if seed is None else seed) & 0xFFFFFFFFFFFF
+        self.rng_offset = 0
+        self.perm_source: Optional[Callable[[int], torch.Tensor]] = None
+        self.generator = torch.Generator(device=self.device)
+        self.generator.manual_seed(self.seed)
+
+        N = vec_env.num_envs
+        T = n_steps
+        obs_space, act_space = vec_env.single_observation_space, vec_env.single_action_space
+        self.num_envs = N
+        dev = self.device
+        tdt = lambda d: torch.from_numpy(np.zeros((), dtype=d)).dtype
+        self.obs_dtype = tdt(obs_space.dtype)
+        self.discrete = is_discrete(act_space)
+        if not (self.discrete or is_box(act_space)):
+            raise NotImplementedError(f"action space {act_space} is outside the hot-path scope")
+        self.act_shape = () if self.discrete else tuple(act_space.shape)
+        act_dtype = torch.int64 if self.discrete else torch.float32
+        self.obs = torch.zeros((T, N) + tuple(obs_space.shape), dtype=self.obs_dtype, device=dev)
+        self.rewards = torch.zeros((T, N), dtype=torch.float32, device=dev)
+        self.episode_starts = torch.zeros((T, N), dtype=torch.bool, device=dev)
+        self.values = torch.zeros((T, N), dtype=torch.float32, device=dev)
+        self.logprobs = torch.zeros((T, N), dtype=torch.float32, device=dev)
+        self.actions = torch.zeros((T, N) + self.act_shape, dtype=act_dtype, device=dev)
+        self.clamped = torch.zeros((N,) + self.act_shape, dtype=act_dtype, device=dev)
+        if not self.discrete:
+            self.act_low = torch.as_tensor(np.asarray(act_space.low, np.float32), device=dev)
+            self.act_high = torch.as_tensor(np.asarray(act_space.high, np.float32), device=dev)
+        # pinned host staging (H2D obs/rewards/dones, D2H actions)
+        self.h_obs = torch.zeros((N,) + tuple(obs_space.shape), dtype=self.obs_dtype).pin_memory()
+        self.h_rew = torch.zeros((N,), dtype=torch.float32).pin_memory()
+        self.h_done = torch.zeros((N,), dtype=torch.bool).pin_memory()
+        self.h_act = torch.zeros((N,) + self.act_shape, dtype=act_dtype).pin_memory()
+        self.next_obs_dev = torch.zeros((N,) + tuple(obs_space.shape), dtype=self.obs_dtype, device=dev)
+        self.next_episode_starts = torch.ones((N,), dtype=torch.bool, device=dev)
+        self._act_ready = torch.cuda.Event()
+        obs, _ = vec_env.reset()
+        self._stage_obs(obs)
+
+    def _stage_obs(self, obs: np.ndarray) -> None:
+        np.copyto(self.h_obs.numpy(), obs, casting="same_kind")
+        self.next_obs_dev.copy_(self.h_obs, non_blocking=True)
+
+    def _sample(self, params: torch.Tensor, v: torch.Tensor, s: int) -> None:
+        L = _lib.lib()
+        st = _lib.stream_handle(self.device)
+        N = self.num_envs
+        params = params.contiguous().float()
+        v = v.contiguous().float()
+        if self.discrete:
+            rc = L.rai_categorical_sample(params.data_ptr(), None, N, params.shape[-1], self.seed,
+                                          self.rng_offset, self.actions[s].data_ptr(), self.logprobs[s].data_ptr(),
+                                          v.data_ptr(), self.values[s].data_ptr(), 1, st)
+            _lib.check(rc, "rai_categorical_sample")
+        else:
+            log_std = self.policy.network._pi.log_std.detach().contiguous()
+            rc = L.rai_gaussian_sample(params.data_ptr(), log_std.data_ptr(), N, params.shape[-1],
+                                       self.act_low.data_ptr(), self.act_high.data_ptr(), self.seed,
+                                       self.rng_offset, self.actions[s].data_ptr(), self.clamped.data_ptr(),
+                                       self.logprobs[s].data_ptr(), v.data_ptr(), self.values[s].data_ptr(), 1, st)
+            _lib.check(rc, "rai_gaussian_sample")
+        self.rng_offset += 1
+
+    @torch.no_grad()
+    def _rollout(self, output_next_values: bool) -> Optional[torch.Tensor]:
+        self.policy.eval()
+        net = self.policy.network
+        for s in range(self.n_steps):
+            self.obs[s].copy_(self.next_obs_dev)
+            self.episode_starts[s].copy_(self.next_episode_starts)
+            params, v = net.dist_params_and_value(self.obs[s])
+            self._sample(params, v, s)
+            src = self.actions[s] if self.discrete else self.clamped
+            self.h_act.copy_(src, non_blocking=True)
+            self._act_ready.record()
+            self._act_ready.synchronize()
+            obs, rew, term, trunc, _ = self.vec_env.step(self.h_act.numpy())
+            np.copyto(self.h_rew.numpy(), rew, casting="same_kind")
+            np.logical_or(term, trunc, out=self.h_done.numpy())
+            self.rewards[s].copy_(self.h_rew, non_blocking=True)
+            self.next_episode_starts.copy_(self.h_done, non_blocking=True)
+            self._stage_obs(obs)
+        next_values = net.value(self.next_obs_dev).float() if output_next_values else None
+        self.policy.train()
+        return next_values
+
+    def rollout(self, gamma, gae_lambda) -> DeviceRollout:
+        next_values = self._rollout(output_next_values=True)
+        return DeviceRollout(
+            self.device, self.next_episode_starts.clone(), next_values, self.obs, self.actions, self.rewards,
+            self.episode_starts, self.values, self.logprobs if self.include_logp else None, None, gamma,
+            gae_lambda, self.scale_advantage_by_values_accuracy, self.gae_mode, self.perm_source,
+            self.generator)

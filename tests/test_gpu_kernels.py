@@ -1,0 +1,324 @@
+"""Parity of the gfx950 kernels against the oracle and the reference's golden vectors.
+Every test calls through the C ABI (librai_amd.so)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from rl_algo_impls_amd import _lib
+from rl_algo_impls_amd.gae import EXACT, FAST, compute_advantages, compute_advantages_device
+from rl_algo_impls_amd.pg_common import DeviceBlocks, launch_loss, make_hparams
+from rl_algo_impls_amd.rollout import gather_rows
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+# ---------------------------------------------------------------- GAE ----------------
+def test_gae_golden_bit_exact_numpy_dropin(gae_cases):
+    for c in gae_cases:
+        adv = compute_advantages(c["rewards"], c["values"], c["episode_starts"], c["next_episode_starts"],
+                                 c["next_values"], c["gamma"], c["lam"])
+        assert adv.dtype == np.float32
+        np.testing.assert_array_equal(adv, c["adv"], err_msg=f"case {c['idx']}")
+
+
+def test_gae_golden_returns_fused(gae_cases):
+    for c in gae_cases:
+        adv, ret = compute_advantages_device(dev(c["rewards"]), dev(c["values"]), dev(c["episode_starts"]),
+                                             dev(c["next_episode_starts"]), dev(c["next_values"]),
+                                             c["gamma"], c["lam"], want_returns=True)
+        np.testing.assert_array_equal(adv.cpu().numpy(), c["adv"])
+        np.testing.assert_array_equal(ret.cpu().numpy(), c["returns"])
+
+
+@pytest.mark.parametrize("T,N,K,dens", [(128, 4096, 1, 0.005), (512, 2048, 1, 0.001), (37, 999, 3, 0.05),
+                                        (128, 65536, 1, 0.005)])
+def test_gae_full_size_exact_vs_c_oracle(T, N, K, dens):
+    rng = np.random.default_rng(T * N + K)
+    shp = (T, N) if K == 1 else (T, N, K)
+    r = rng.standard_normal(shp, dtype=np.float32)
+    v = rng.standard_normal(shp, dtype=np.float32) * 5
+    es = rng.random((T, N)) < dens
+    nes = rng.random(N) < dens
+    nv = rng.standard_normal(shp[1:], dtype=np.float32)
+    gamma = 0.99 if K == 1 else np.array([0.99, 0.995, 0.9][:K])
+    adv_ref, ret_ref = oracle.gae_c(r, v, es, nes, nv, gamma, 0.95)
+    adv, ret = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), gamma, 0.95,
+                                         want_returns=True)
+    np.testing.assert_array_equal(adv.cpu().numpy(), adv_ref)
+    np.testing.assert_array_equal(ret.cpu().numpy(), ret_ref)
+
+
+def test_gae_fast_mode_tolerance():
+    rng = np.random.default_rng(3)
+    T, N = 256, 1000
+    r = rng.standard_normal((T, N), dtype=np.float32)
+    v = rng.standard_normal((T, N), dtype=np.float32)
+    es = rng.random((T, N)) < 0.01
+    nes = rng.random(N) < 0.01
+    nv = rng.standard_normal(N, dtype=np.float32)
+    ref, _ = oracle.gae_c(r, v, es, nes, nv, 0.99, 0.95)
+    adv, _ = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), 0.99, 0.95, mode=FAST)
+    np.testing.assert_allclose(adv.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_gae_edge_cases():
+    # T=1, N=1; all starts; no starts; ragged column count (not a multiple of 64)
+    for T, N in [(1, 1), (1, 65), (33, 63), (64, 129)]:
+        for dens in (0.0, 1.0):
+            rng = np.random.default_rng(T + N)
+            r = rng.standard_normal((T, N), dtype=np.float32)
+            v = rng.standard_normal((T, N), dtype=np.float32)
+            es = np.full((T, N), dens > 0)
+            nes = np.full(N, dens > 0)
+            nv = rng.standard_normal(N, dtype=np.float32)
+            ref = oracle.compute_advantages(r, v, es, nes, nv, 0.98, 0.8)
+            np.testing.assert_array_equal(compute_advantages(r, v, es, nes, nv, 0.98, 0.8), ref)
+
+
+def test_gae_shape_errors_match_reference():
+    r = np.zeros((4, 3), np.float32)
+    with pytest.raises(AssertionError):
+        compute_advantages(r, r, np.zeros((4, 3), bool), np.zeros(2, bool), np.zeros(3, np.float32), 0.9, 0.9)
+
+
+def test_gae_linearity_property_full_size():
+    """Size-independent property at the BASELINE size: GAE is linear in (r, V) for fixed
+    episode boundaries, so adv(r1+r2) ~= adv(r1) + adv(r2) (fp tolerance)."""
+    T, N = 128, 4096
+    rng = np.random.default_rng(9)
+    es = dev(rng.random((T, N)) < 0.005)
+    nes = dev(rng.random(N) < 0.005)
+    z = torch.zeros((T, N), device=DEV)
+    zn = torch.zeros(N, device=DEV)
+    r1 = torch.randn((T, N), device=DEV)
+    r2 = torch.randn((T, N), device=DEV)
+    a1, _ = compute_advantages_device(r1, z, es, nes, zn, 0.99, 0.95)
+    a2, _ = compute_advantages_device(r2, z, es, nes, zn, 0.99, 0.95)
+    a12, _ = compute_advantages_device(r1 + r2, z, es, nes, zn, 0.99, 0.95)
+    torch.testing.assert_close(a12, a1 + a2, rtol=1e-5, atol=1e-5)
+
+
+# ---------------------------------------------------------------- loss ---------------
+def _golden_loss_inputs(z, name, meta, i=0):
+    import make_golden_networks as nets
+
+    policy = nets.build(meta["policy"])
+    nets.load_flat(policy, z[f"{name}/init"])
+    p = f"{name}/b{i}_"
+    with torch.no_grad():
+        lp, ent, v = policy(torch.from_numpy(z[p + "obs"]), torch.from_numpy(z[p + "actions"]))
+    return lp.numpy(), ent.numpy(), v.numpy(), z[p + "logprobs"], z[p + "values"], z[p + "advantages"], z[p + "returns"]
+
+
+def _kw_to_hparams(kw, K, algo="ppo", grad_scale=1.0):
+    return make_hparams(
+        loss_kind=0 if algo == "ppo" else 1, K=K, clip_range=kw.get("clip_range", 0.2),
+        clip_range_vf=kw.get("clip_range_vf"), ent_coef=kw.get("ent_coef", 0.0), vf_coef=kw.get("vf_coef", 0.5),
+        vf_weights=kw.get("vf_weights"), multi_reward_weights=kw.get("multi_reward_weights"),
+        normalize_advantage=kw.get("normalize_advantage", True),
+        standardize_advantage=kw.get("standardize_advantage", False),
+        normalize_after_scaling=kw.get("normalize_advantages_after_scaling", False),
+        ppo2_vf_coef_halving=kw.get("ppo2_vf_coef_halving", False), kl_cutoff=kw.get("kl_cutoff"),
+        vf_loss_fn=kw.get("vf_loss_fn", "mse_loss"), grad_scale=grad_scale)
+
+
+def test_loss_kernel_matches_oracle_on_golden_batches(golden):
+    z = golden("ppo_steps.npz")
+    index = json.loads(str(z["index"]))
+    for name, meta in index.items():
+        lp, ent, v, olp, ov, adv, ret = _golden_loss_inputs(z, name, meta)
+        K = meta["K"]
+        gs = 1.0 / meta["n"] if meta["kw"].get("gradient_accumulation") else 1.0
+        blocks = DeviceBlocks(DEV)
+        blocks.ensure_tables(4, 4)
+        blocks.upload(_kw_to_hparams(meta["kw"], K, grad_scale=gs), 0)
+        d_lp, d_ent, d_v = launch_loss(blocks, dev(lp), dev(ent), dev(v), dev(olp), dev(ov), dev(adv), dev(ret), K)
+        hp = dict(meta["kw"], algo="ppo", grad_scale=gs)
+        r_lp, r_ent, r_v, st = oracle.pg_loss_grads(lp, ent, v, olp, ov, adv, ret, hp)
+        np.testing.assert_allclose(d_lp.cpu().numpy(), r_lp, rtol=2e-5, atol=1e-8, err_msg=name)
+        np.testing.assert_allclose(d_ent.cpu().numpy(), r_ent, rtol=1e-6, atol=0, err_msg=name)
+        np.testing.assert_allclose(d_v.cpu().numpy(), r_v, rtol=2e-5, atol=1e-8, err_msg=name)
+        row = blocks.stats[0].cpu().numpy()
+        np.testing.assert_allclose(row[0], st["loss"], rtol=2e-5, atol=1e-7, err_msg=name)
+        np.testing.assert_allclose(row[1], st["pi_loss"], rtol=2e-5, atol=1e-7, err_msg=name)
+        np.testing.assert_allclose(row[2], st["entropy_loss"], rtol=2e-5, atol=1e-7, err_msg=name)
+        np.testing.assert_allclose(row[3], st["approx_kl"], rtol=1e-4, atol=1e-8, err_msg=name)
+        np.testing.assert_allclose(row[4], st["clipped_frac"], rtol=1e-6, err_msg=name)
+        # reference step stats (PPO.learn_epoch's TrainStepStats) agree as well
+        ref_row = z[f"{name}/stats"][0]
+        np.testing.assert_allclose(row[:5], ref_row[:5], rtol=1e-4, atol=1e-6, err_msg=name)
+
+
+def test_loss_kernel_a2c_and_large_batch():
+    rng = np.random.default_rng(4)
+    for B in (1000, 70000):
+        lp = rng.standard_normal(B, dtype=np.float32)
+        ent = rng.random(B, dtype=np.float32)
+        v = rng.standard_normal(B, dtype=np.float32)
+        adv = rng.standard_normal(B, dtype=np.float32) * 3
+        ret = rng.standard_normal(B, dtype=np.float32)
+        for algo in ("ppo", "a2c"):
+            kw = dict(ent_coef=0.01, normalize_advantage=(algo == "ppo"))
+            blocks = DeviceBlocks(DEV)
+            blocks.upload(_kw_to_hparams(kw, 1, algo=algo), 0)
+            olp = lp + rng.standard_normal(B, dtype=np.float32) * 0.1
+            d_lp, d_ent, d_v = launch_loss(blocks, dev(lp), dev(ent), dev(v), dev(olp), dev(v), dev(adv),
+                                           dev(ret), 1)
+            r_lp, r_ent, r_v, st = oracle.pg_loss_grads(lp, ent, v, olp, v, adv, ret, dict(kw, algo=algo, clip_range=0.2))
+            np.testing.assert_allclose(d_lp.cpu().numpy(), r_lp, rtol=3e-5, atol=1e-10)
+            np.testing.assert_allclose(d_v.cpu().numpy(), r_v, rtol=3e-5, atol=1e-10)
+            np.testing.assert_allclose(d_ent.cpu().numpy(), r_ent, rtol=1e-6)
+
+
+def test_loss_kernel_tie_semantics():
+    """ratio exactly 1 (ties in min) and ratio on the clip boundary follow autograd."""
+    B = 8
+    lp = np.zeros(B, np.float32)
+    adv = np.array([1, -1, 2, -2, 0.5, -0.5, 3, -3], np.float32)
+    kw = dict(normalize_advantage=False)
+    blocks = DeviceBlocks(DEV)
+    blocks.upload(_kw_to_hparams(kw, 1), 0)
+    zeros = np.zeros(B, np.float32)
+    d_lp, _, _ = launch_loss(blocks, dev(lp), dev(zeros), dev(zeros), dev(lp), dev(zeros), dev(adv), dev(zeros), 1)
+    # autograd reference
+    t = torch.zeros(B, requires_grad=True)
+    ratio = torch.exp(t - torch.from_numpy(lp))
+    A = torch.from_numpy(adv)
+    loss = -torch.min(ratio * A, torch.clamp(ratio, 0.8, 1.2) * A).mean()
+    loss.backward()
+    np.testing.assert_allclose(d_lp.cpu().numpy(), t.grad.numpy(), rtol=1e-6)
+
+
+# ---------------------------------------------------------------- optimizer -----------
+def test_clip_adam_matches_torch_over_steps():
+    from rl_algo_impls_amd.optim import FlatOptimizer, FlatParams
+
+    torch.manual_seed(0)
+    for P_sizes in ([9155 - 130, 130], [3, 5, 7], [1 << 20, 37]):
+        ref_params = [torch.nn.Parameter(torch.randn(n, dtype=torch.float64)) for n in P_sizes]
+        mod = torch.nn.ParameterList([torch.nn.Parameter(p.detach().float().clone()) for p in ref_params]).to(DEV)
+        flat = FlatParams(mod, DEV)
+        opt = FlatOptimizer(flat, FlatOptimizer.ADAM, lr=1e-3, eps=1e-7, max_grad_norm=0.5)
+        blocks = DeviceBlocks(DEV)
+        blocks.ensure_tables(1, 8)
+        blocks.upload(make_hparams(loss_kind=0, K=1), 0)
+        p64 = [p.detach().double().clone() for p in ref_params]
+        m = [torch.zeros_like(p) for p in p64]
+        v = [torch.zeros_like(p) for p in p64]
+        for step in range(1, 6):
+            grads = [torch.randn(n, dtype=torch.float64) * (0.01 if step % 2 else 3) for n in P_sizes]
+            for pp, g in zip(mod, grads):
+                pp.grad.copy_(g.float())
+            opt.step(blocks.state, blocks.norms)
+            tot = torch.sqrt(sum((g.double() ** 2).sum() for g in grads))
+            coef = min(0.5 / (tot + 1e-6), 1.0)
+            for i, g in enumerate(grads):
+                g = g * coef
+                m[i] = m[i] + 0.1 * (g - m[i])
+                v[i] = v[i] * 0.999 + 0.001 * g * g
+                bc1, bc2 = 1 - 0.9 ** step, 1 - 0.999 ** step
+                p64[i] = p64[i] - (1e-3 / bc1) * m[i] / (torch.sqrt(v[i]) / np.sqrt(bc2) + 1e-7)
+            norms = blocks.norms[:step].cpu().numpy()
+            np.testing.assert_allclose(norms[-1], float(tot), rtol=1e-5)
+            for pp, ref in zip(mod, p64):
+                np.testing.assert_allclose(pp.detach().cpu().numpy(), ref.numpy(), rtol=1e-4, atol=2e-6)
+            assert float(flat.grad.abs().max()) == 0.0  # zero_grad
+        sd = opt.state_dict()
+        assert sd["state"][0]["step"].item() == 5.0
+
+
+def test_optimizer_state_dict_loads_into_torch_adam():
+    from rl_algo_impls_amd.optim import FlatOptimizer, FlatParams
+
+    mod = torch.nn.Linear(5, 3).to(DEV)
+    flat = FlatParams(mod, DEV)
+    opt = FlatOptimizer(flat, FlatOptimizer.ADAM, lr=3e-4, eps=1e-7)
+    blocks = DeviceBlocks(DEV)
+    blocks.upload(make_hparams(loss_kind=0, K=1), 0)
+    flat.grad.normal_()
+    opt.step(blocks.state, None)
+    sd = opt.state_dict()
+    t = torch.optim.Adam(mod.parameters(), lr=3e-4, eps=1e-7)
+    t.load_state_dict(sd)
+    assert t.state_dict()["state"][1]["exp_avg"].shape == (3,)
+    opt2 = FlatOptimizer(flat, FlatOptimizer.ADAM, lr=1.0, eps=1e-7)
+    opt2.load_state_dict(t.state_dict())
+    torch.testing.assert_close(opt2.state1, opt.state1)
+    assert opt2.step_count == 1 and opt2.lr == 3e-4
+
+
+# ---------------------------------------------------------------- gather / sample -----
+def test_gather_rows_multi_field():
+    rng = np.random.default_rng(0)
+    n = 5000
+    fields = [rng.integers(0, 255, (n, 4, 84, 84), dtype=np.uint8)[:, :, :, :1],  # 336-B rows
+              rng.standard_normal((n, 4), dtype=np.float32),
+              rng.integers(0, 6, n).astype(np.int64),
+              rng.standard_normal((n, 17), dtype=np.float32),  # 68-B rows
+              rng.integers(0, 2, (n, 3)).astype(np.bool_)]   # 3-B rows
+    srcs = [dev(np.ascontiguousarray(f)) for f in fields]
+    idx = rng.permutation(n)[:3000]
+    dsts = [torch.empty((3000,) + tuple(s.shape[1:]), dtype=s.dtype, device=DEV) for s in srcs]
+    gather_rows(srcs, dsts, dev(idx))
+    for f, d in zip(fields, dsts):
+        np.testing.assert_array_equal(d.cpu().numpy(), np.ascontiguousarray(f)[idx])
+
+
+def test_categorical_sample_distribution_and_logp():
+    L = _lib.lib()
+    N, A = 200000, 6
+    logits = torch.randn(8, A, device=DEV).repeat(N // 8, 1).contiguous()
+    acts = torch.empty(N, dtype=torch.int64, device=DEV)
+    logp = torch.empty(N, dtype=torch.float32, device=DEV)
+    v = torch.randn(N, device=DEV)
+    vo = torch.empty(N, device=DEV)
+    rc = L.rai_categorical_sample(logits.data_ptr(), None, N, A, 1234, 7, acts.data_ptr(), logp.data_ptr(),
+                                  v.data_ptr(), vo.data_ptr(), 1, _lib.stream_handle())
+    _lib.check(rc, "sample")
+    a = acts.cpu().numpy()
+    assert a.min() >= 0 and a.max() < A
+    np.testing.assert_allclose(logp.cpu().numpy(), oracle.categorical_logp(logits.cpu().numpy(), a), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(vo, v)
+    probs = torch.softmax(logits[:8], -1).cpu().numpy()
+    for row in range(8):
+        freq = np.bincount(a[row::8], minlength=A) / (N // 8)
+        np.testing.assert_allclose(freq, probs[row], atol=0.015)
+    # masked: never picks a masked action
+    mask = torch.zeros(N, A, dtype=torch.uint8, device=DEV)
+    mask[:, 2] = 1
+    mask[::2, 4] = 1
+    rc = L.rai_categorical_sample(logits.data_ptr(), mask.data_ptr(), N, A, 99, 0, acts.data_ptr(), logp.data_ptr(),
+                                  None, None, 0, _lib.stream_handle())
+    _lib.check(rc, "sample")
+    a = acts.cpu().numpy()
+    assert set(np.unique(a)) <= {2, 4}
+    assert (a[1::2] == 2).all()
+
+
+def test_gaussian_sample_moments_logp_clamp():
+    L = _lib.lib()
+    N, A = 100000, 6
+    mu = (torch.arange(A, device=DEV, dtype=torch.float32) * 0.3 - 0.8).repeat(N, 1).contiguous()
+    log_std = torch.full((A,), -0.5, device=DEV)
+    low = torch.full((A,), -1.0, device=DEV)
+    high = torch.full((A,), 1.0, device=DEV)
+    acts = torch.empty(N, A, device=DEV)
+    cl = torch.empty(N, A, device=DEV)
+    lp = torch.empty(N, device=DEV)
+    rc = L.rai_gaussian_sample(mu.data_ptr(), log_std.data_ptr(), N, A, low.data_ptr(), high.data_ptr(), 5, 0,
+                               acts.data_ptr(), cl.data_ptr(), lp.data_ptr(), None, None, 0, _lib.stream_handle())
+    _lib.check(rc, "gaussian")
+    a = acts.cpu().numpy()
+    np.testing.assert_allclose(a.mean(0), mu[0].cpu().numpy(), atol=0.01)
+    np.testing.assert_allclose(a.std(0), np.exp(-0.5), rtol=0.01)
+    np.testing.assert_allclose(lp.cpu().numpy(), oracle.gaussian_logp(a, mu.cpu().numpy(), log_std.cpu().numpy()),
+                               rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(cl.cpu().numpy(), np.clip(a, -1, 1))
