@@ -107,7 +107,7 @@ typedef struct rai_train_state {
   int32_t stat_index;    /* next per-minibatch stats row */
   int32_t pi_coef_zero;  /* kl_cutoff latch, reset per update (ppo.py:279,354-355) */
   int32_t norm_index;    /* next grad-norm slot */
-  int32_t pad;
+  int32_t err;           /* sticky device-side error flag (e.g. a bounded spin gave up) */
 } rai_train_state;
 
 /* Per-minibatch stats row layout (floats), stride RAI_STAT_STRIDE:
@@ -175,6 +175,29 @@ int rai_gaussian_sample(const float* mu, const float* log_std, int64_t N, int32_
                         const float* low, const float* high, uint64_t seed, uint64_t offset,
                         float* actions_out, float* clamped_out, float* logp_out,
                         const float* v_in, float* v_out, int32_t K, void* stream);
+
+/* --------------------------------------------------------------------------
+ * Fused PPO epoch for MLP actor-critics (Flatten encoder, separate
+ * [in_dim -> 64 -> 64 -> out] actor and critic MLPs, Categorical head; the
+ * CartPole-class policies of rl_algo_impls/shared/policy/actor_critic_network/
+ * connected_trio.py).  One call = every minibatch of one epoch of
+ * rl_algo_impls/ppo/ppo.py:290-411 (forward, loss, backward, clip_grad_norm_,
+ * Adam) over rows [0, n_rows) of the (already permuted) rollout, minibatch i =
+ * rows [i*batch_size, (i+1)*batch_size).  params / exp_avg / exp_avg_sq are the
+ * flat buffers in torch parameters() order.  Requires hidden == 64,
+ * in_dim <= 8, n_actions <= 8, batch_size <= 256, activation 0 tanh / 1 relu,
+ * K == 1, no kl_cutoff and no gradient accumulation.
+ * Stats rows: [0] holds the policy+entropy part of the loss; the caller adds
+ * vf_coef * v_loss ([5]).
+ * ------------------------------------------------------------------------ */
+int64_t rai_mlp_ppo_workspace_bytes(void);
+int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
+                      const int64_t* actions, const float* old_logp, const float* old_values,
+                      const float* advantages, const float* returns, int64_t n_rows,
+                      int32_t batch_size, int32_t in_dim, int32_t hidden, int32_t n_actions,
+                      int32_t activation, const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
+                      rai_train_state* state, float* stats, int32_t max_stats, float* norms,
+                      int32_t max_norms, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -66,7 +66,7 @@ class TrainState(C.Structure):
         ("stat_index", C.c_int32),
         ("pi_coef_zero", C.c_int32),
         ("norm_index", C.c_int32),
-        ("pad", C.c_int32),
+        ("err", C.c_int32),
     ]
 
 
@@ -82,6 +82,9 @@ _SIGNATURES = {
     "rai_optim_workspace_bytes": (_i64, [_i64]),
     "rai_clip_optim_step": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_gather_rows": (C.c_int, [_i32, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "rai_mlp_ppo_workspace_bytes": (_i64, []),
+    "rai_mlp_ppo_epoch": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
+                                    _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
     "rai_categorical_sample": (C.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp, _vp, _vp, _i32, _vp]),
     "rai_gaussian_sample": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp,
                                       _i32, _vp]),

@@ -73,6 +73,8 @@ class PPO:
         self.vf_loss_fn = vf_loss_fn
         self.blocks = DeviceBlocks(self.device)
         self.last_update_seconds: Optional[float] = None
+        self.force_generic = False  # True: always use the per-minibatch (PyTorch network) path
+        self._mlp_ws: Optional[torch.Tensor] = None
 
     # -- reference API -------------------------------------------------------------------
     def learn(self, train_timesteps: int, rollout_generator, callbacks=None, total_timesteps=None,
@@ -134,9 +136,82 @@ class PPO:
                 return timesteps_elapsed, False
         return timesteps_elapsed, True
 
+    # -- fused MLP path ---------------------------------------------------------------------
+    def fused_mlp_spec(self) -> Optional[dict]:
+        """Shape descriptor if the policy/options fit rai_mlp_ppo_epoch (CartPole-class MLP
+        actor-critic: Flatten encoder, [in -> 64 -> 64 -> out] actor and critic, Categorical
+        head); None otherwise (the generic per-minibatch path then runs)."""
+        from .policy import ActorCritic, CategoricalActorHead
+
+        pol = self.policy
+        if self.force_generic or not isinstance(pol, ActorCritic):
+            return None
+        net = pol.network
+        if net._feature_extractor.kind != "flat" or not isinstance(net._pi, CategoricalActorHead):
+            return None
+        if net.pi_hidden_sizes != (64, 64) or net.v_hidden_sizes != (64, 64):
+            return None
+        if net.activation_fn not in ("tanh", "relu"):
+            return None
+        in_dim, n_act = net._feature_extractor.out_dim, net._pi.act_dim
+        if not (1 <= in_dim <= 8 and 1 <= n_act <= 8 and 2 <= self.batch_size <= 256):
+            return None
+        if (self.gradient_accumulation or self.kl_cutoff is not None or self.multi_reward_weights is not None
+                or self.vf_weights is not None or self.normalize_advantages_after_scaling
+                or np.ndim(self.vf_coef) > 0):
+            return None
+        shapes = [tuple(p.shape) for p in pol.parameters()]
+        want = []
+        for out in (n_act, 1):
+            want += [(64, in_dim), (64,), (64, 64), (64,), (out, 64), (out,)]
+        if shapes != want:
+            return None
+        return dict(in_dim=in_dim, n_act=n_act, activation=0 if net.activation_fn == "tanh" else 1)
+
+    def _update_fused(self, r, spec) -> Tuple[np.ndarray, np.ndarray, int]:
+        nmb = r.num_minibatches(self.batch_size)
+        if r.total_steps % self.batch_size == 1:
+            raise ValueError("a 1-row minibatch has no unbiased std (reference would produce NaN)")
+        n_steps = self.n_epochs * nmb
+        blocks = self.blocks
+        blocks.ensure_tables(n_steps, n_steps)
+        blocks.upload(self._hparams(1, nmb), self.optimizer.step_count)
+        if self._mlp_ws is None:
+            self._mlp_ws = torch.zeros(int(_lib.lib().rai_mlp_ppo_workspace_bytes()), dtype=torch.uint8,
+                                       device=self.device)
+        opt = self.optimizer
+        L = _lib.lib()
+        st = _lib.stream_handle(self.device)
+        for _ in range(self.n_epochs):
+            b = r.epoch_batch(shuffle=True)
+            assert b.logprobs is not None, "PPO needs rollout logprobs (include_logp=True)"
+            obs = b.obs if b.obs.dtype == torch.float32 else b.obs.float()
+            rc = L.rai_mlp_ppo_epoch(
+                self.flat.flat.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), obs.contiguous().data_ptr(),
+                b.actions.contiguous().data_ptr(), b.logprobs.data_ptr(), b.values.data_ptr(),
+                b.advantages.data_ptr(), b.returns.data_ptr(), r.total_steps, self.batch_size, spec["in_dim"], 64,
+                spec["n_act"], spec["activation"], blocks.hp.data_ptr(), opt.hp_dev.data_ptr(),
+                blocks.state.data_ptr(), blocks.stats.data_ptr(), int(blocks.stats.shape[0]),
+                blocks.norms.data_ptr(), int(blocks.norms.shape[0]), self._mlp_ws.data_ptr(), self._mlp_ws.numel(),
+                st)
+            _lib.check(rc, "rai_mlp_ppo_epoch")
+            opt.step_count += nmb
+        host = torch.cat([blocks.stats[:n_steps].reshape(-1), blocks.norms[:n_steps],
+                          blocks.state.view(torch.float32)]).cpu().numpy()
+        stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE).copy()
+        norms = host[n_steps * _lib.RAI_STAT_STRIDE: n_steps * _lib.RAI_STAT_STRIDE + n_steps]
+        state = host[n_steps * _lib.RAI_STAT_STRIDE + n_steps:].view(np.int32)
+        if state[5] != 0:
+            raise RuntimeError("rai_mlp_ppo_epoch: device-side exchange timed out (err flag set)")
+        stats[:, 0] += float(self.vf_coef) * stats[:, 5]  # value term of the loss
+        return stats, norms, 1
+
     def update(self, r) -> Tuple[np.ndarray, np.ndarray, int]:
         """All epochs x minibatches of one update, enqueued without host syncs;
         returns the per-minibatch stats rows and grad norms (one D2H copy)."""
+        spec = self.fused_mlp_spec() if hasattr(r, "epoch_batch") else None
+        if spec is not None:
+            return self._update_fused(r, spec)
         nmb = r.num_minibatches(self.batch_size)
         n_steps = self.n_epochs * nmb
         n_norms = self.n_epochs if self.gradient_accumulation else n_steps

@@ -206,7 +206,9 @@ class DeviceRollout(Rollout):
             return self._perm_source(self.total_steps).to(self.device)
         return torch.randperm(self.total_steps, device=self.device, generator=self._generator)
 
-    def minibatches(self, batch_size: int, shuffle: bool = True) -> Iterator[Batch]:
+    def epoch_batch(self, shuffle: bool = True) -> Batch:
+        """The whole rollout as one flat Batch, permuted for this epoch (one gather
+        kernel); minibatch i is rows [i*batch_size, (i+1)*batch_size)."""
         flat = self._flat_fields()
         if shuffle:
             if self._perm_buf is None:
@@ -215,8 +217,15 @@ class DeviceRollout(Rollout):
             src = self._perm_buf
         else:
             src = flat
+        return self._batch_from(src, slice(0, self.total_steps))
+
+    def minibatches(self, batch_size: int, shuffle: bool = True) -> Iterator[Batch]:
+        full = self.epoch_batch(shuffle)
         for i in range(0, self.total_steps, batch_size):
-            yield self._batch_from(src, slice(i, i + batch_size))
+            sl = slice(i, i + batch_size)
+            g = lambda t: None if t is None else t[sl]
+            yield Batch(full.obs[sl], g(full.logprobs), full.actions[sl], g(full.action_masks), None,
+                        full.values[sl], full.advantages[sl], full.returns[sl])
 
     def add_to_batch(self, map_fn: BatchMapFn, batch_size: int) -> None:
         raise NotImplementedError("teacher-KL additional batch fields are outside the hot-path scope")

@@ -85,7 +85,8 @@ def test_ppo_minibatch_steps_match_reference(golden, name):
     np.testing.assert_allclose(s1, z[f"{name}/opt_state1"], rtol=2e-3, atol=2e-7, err_msg=name)
 
 
-def test_learn_epoch_matches_reference_with_injected_rollout(golden):
+@pytest.mark.parametrize("generic", [False, True], ids=["fused_mlp_kernel", "generic_path"])
+def test_learn_epoch_matches_reference_with_injected_rollout(golden, generic):
     z = golden("learn_epoch_cartpole.npz")
     kw = json.loads(str(z["kw"]))
     policy = nets.build("cartpole")
@@ -93,6 +94,8 @@ def test_learn_epoch_matches_reference_with_injected_rollout(golden):
     policy = policy.to(DEV)
     rec = Recorder()
     algo = PPO(policy, DEV, rec, **kw)
+    algo.force_generic = generic
+    assert (algo.fused_mlp_spec() is None) == generic
     perms = list(z["perms"])
     t = lambda k: torch.from_numpy(z[k]).to(DEV)
     r = DeviceRollout(DEV, t("next_episode_starts"), t("next_values"), t("obs"), t("actions"), t("rewards"),
@@ -112,6 +115,60 @@ def test_learn_epoch_matches_reference_with_injected_rollout(golden):
     got = np.array([rec.scalars[f"losses/{k}"] for k in names])
     np.testing.assert_allclose(got, z["losses"], rtol=2e-4, atol=2e-6)
     assert rec.scalars["train/steps_per_second"] > 0
+
+
+class FixedEpochRollout(FixedDeviceRollout):
+    """Exposes epoch_batch() so PPO takes the fused rai_mlp_ppo_epoch path."""
+
+    def epoch_batch(self, shuffle=True):
+        cat = lambda f: torch.cat([getattr(b, f) for b in self.batches])
+        return Batch(cat("obs"), cat("logprobs"), cat("actions"), None, None, cat("values"), cat("advantages"),
+                     cat("returns"))
+
+
+@pytest.mark.parametrize("name", ["cp_default", "cp_vclip_ent"])
+def test_fused_mlp_kernel_matches_reference_steps(golden, name):
+    z = golden("ppo_steps.npz")
+    meta = json.loads(str(z["index"]))[name]
+    policy = nets.build(meta["policy"])
+    nets.load_flat(policy, z[f"{name}/init"])
+    policy = policy.to(DEV)
+    algo = PPO(policy, DEV, Recorder(), n_epochs=1, **meta["kw"])
+    assert algo.fused_mlp_spec() is not None
+    r = FixedEpochRollout(_device_batches(z, name, meta["n"]))
+    stats, norms, K = algo.update(r)
+    np.testing.assert_allclose(algo.flat.flat.cpu().numpy(), z[f"{name}/params"][-1], rtol=1e-4,
+                               atol=float(meta["kw"]["learning_rate"]) * 2e-3)
+    np.testing.assert_allclose(norms, z[f"{name}/norms"], rtol=1e-4)
+    np.testing.assert_allclose(stats[:, :6], z[f"{name}/stats"][:, :6], rtol=2e-4, atol=2e-6)
+    np.testing.assert_allclose(algo.optimizer.state1.cpu().numpy(), z[f"{name}/opt_state1"], rtol=2e-3, atol=2e-7)
+    assert algo.optimizer.step_count == meta["opt_step"]
+
+
+def test_fused_matches_generic_on_large_rollout():
+    """Same permutations, same rollout: fused single-launch epoch vs the per-minibatch
+    PyTorch path, 4096 envs x 16 steps, batch 256 (256 optimizer steps)."""
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    results = []
+    for generic in (False, True):
+        torch.manual_seed(3)
+        env = SyntheticVecEnv(4096, "cartpole", seed=5)
+        policy = ActorCritic(env).to(DEV)
+        gen = SyncStepRolloutGenerator(policy, env, n_steps=16, seed=11)
+        algo = PPO(policy, DEV, None, batch_size=256, n_epochs=1, learning_rate=1e-4, gamma=0.98, gae_lambda=0.8)
+        algo.force_generic = generic
+        r = gen.rollout(gamma=0.98, gae_lambda=0.8)
+        g = torch.Generator(device=DEV)
+        g.manual_seed(123)
+        r._perm_source = lambda n: torch.randperm(n, device=DEV, generator=g)
+        stats, norms, _ = algo.update(r)
+        results.append((algo.flat.flat.cpu().numpy(), stats, norms))
+    (pf, sf, nf), (pg, sg, ng) = results
+    np.testing.assert_allclose(nf, ng, rtol=1e-3)
+    np.testing.assert_allclose(sf[:, :6], sg[:, :6], rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(pf, pg, rtol=2e-3, atol=2e-5)
 
 
 def test_a2c_step_matches_reference(golden):
