@@ -38,17 +38,25 @@ def sources() -> list[Path]:
     return sorted(CSRC.glob("*.hip"))
 
 
-def lib_path() -> Path:
-    return LIBDIR / LIBNAME
+def lib_path(variant: str = "") -> Path:
+    if variant:
+        return LIBDIR / LIBNAME.replace(".so", f"_{variant}.so")
+    override = os.environ.get("RAI_AMD_LIB")
+    return Path(override) if override else LIBDIR / LIBNAME
 
 
-def _compile(src: Path) -> Path:
-    obj = OBJDIR / (src.stem + ".o")
+VARIANT_FLAGS = {"": [], "stamps": ["-DRAI_STAMPS"]}
+
+
+def _compile(src: Path, variant: str = "") -> Path:
+    objdir = OBJDIR if not variant else OBJDIR.parent / f"obj_{variant}"
+    objdir.mkdir(parents=True, exist_ok=True)
+    obj = objdir / (src.stem + ".o")
     deps = [src, CSRC / "common.h", PKG.parent / "include" / "rai_amd.h"]
     deps += list(CSRC.glob("*.h"))
     if obj.exists() and obj.stat().st_mtime >= max(d.stat().st_mtime for d in deps if d.exists()):
         return obj
-    flags = list(COMMON_FLAGS)
+    flags = list(COMMON_FLAGS) + VARIANT_FLAGS[variant]
     if src.name in NO_CONTRACT:
         flags.append("-ffp-contract=off")
     cmd = [HIPCC, *flags, "-c", str(src), "-o", str(obj)]
@@ -60,13 +68,15 @@ def _compile(src: Path) -> Path:
     return obj
 
 
-def build(verbose: bool = False) -> Path:
+def build(verbose: bool = False, variant: str = "") -> Path:
+    """Build librai_amd.so (variant "" = the shipped library; "stamps" = the per-phase
+    cycle-stamp diagnostic build, lib/librai_amd_stamps.so, never loaded by the product)."""
     OBJDIR.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
     srcs = sources()
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    out = lib_path()
+        objs = list(ex.map(lambda s: _compile(s, variant), srcs))
+    out = lib_path(variant) if variant else LIBDIR / LIBNAME
     if out.exists() and out.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
         return out
     tmp = out.with_suffix(".so.tmp")
@@ -82,4 +92,4 @@ def build(verbose: bool = False) -> Path:
 
 
 if __name__ == "__main__":
-    print(build(verbose=True))
+    print(build(verbose=True, variant=sys.argv[1] if len(sys.argv) > 1 else ""))

@@ -15,6 +15,14 @@
 
 static inline hipStream_t rai_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Workgroup barrier for LDS hand-offs only: drains this wave's LDS traffic and meets
+// the other waves, but does NOT wait for outstanding global loads/stores
+// (__syncthreads() adds s_waitcnt vmcnt(0), which exposes prefetch and store latency).
+// Register results of global loads are still waited for by the compiler at first use.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ---- wave64 reductions (fixed order -> deterministic) ----------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

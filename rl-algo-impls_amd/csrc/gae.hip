@@ -4,15 +4,16 @@
 // rl_algo_impls/rollout/vec_rollout.py:88 (returns = advantages + values).
 //
 // Layout in HBM: rewards/values/adv/returns (T, C) fp32 with C = N*K columns,
-// episode_starts (T, N) u8.  A block owns 64 consecutive columns (one wave-wide,
-// so every row load/store is a coalesced 256-B segment) and walks T backwards
-// in 32-row tiles:
-//   * all four waves load a tile's rows (8 rows each) and compute the
-//     carry-independent part delta_t and next_nonterminal into LDS
-//     (double-buffered), and
-//   * wave 0 runs the serial carry recurrence over the previous tile from LDS,
-//     writing adv and returns, while the other waves' loads for the next tile
-//     are in flight.
+// episode_starts (T, N) u8.  A 512-thread block owns 64 consecutive columns (one
+// wave-wide, so every row load/store is a coalesced 256-B segment) and walks T
+// backwards in 64-row tiles:
+//   (1) all 8 waves hold 8 rows each in registers and write the carry-independent
+//       part delta_t (+ next_nonterminal) to LDS,
+//   (2) wave 0 runs the serial carry recurrence (two dependent FP64 ops per row,
+//       operands batched out of LDS 16 rows at a time) while the other waves'
+//       loads of the NEXT tile are already in flight,
+//   (3) every wave stores its rows of adv and returns (= adv + V, from registers).
+// So per tile the exposed latency is one HBM round trip shared by all 64 rows.
 // Exact mode keeps the reference's numpy precision sequence bit for bit:
 //   t1    = fp32(fp32(gamma) * V_next)          (gamma Python float; fp64 if ndarray)
 //   delta = (f64(r_t) + f64(t1) * nn) - f64(V_t)
@@ -26,10 +27,21 @@
 
 namespace {
 
-constexpr int GAE_COLS = 64;
-constexpr int GAE_WAVES = 4;
-constexpr int GAE_TT = 32;
-constexpr int ROWS_PER_WAVE = GAE_TT / GAE_WAVES;
+#ifndef GAE_DIAG
+#define GAE_DIAG 0  // diagnostic builds only (tools/gae_diag.hip): 1 no chain, 2 no stores, 4 no prefetch,
+                    // 8 phase stamps of block 0 wave 0 into gae_stamps[]
+#endif
+#if GAE_DIAG & 8
+__device__ long long gae_stamps[8];
+#define GSTAMP(i) do { if (blockIdx.x == 0 && threadIdx.x == 0) { long long t_ = clock64(); gae_stamps[i] += t_ - t_last; t_last = t_; } } while (0)
+#else
+#define GSTAMP(i) do { } while (0)
+#endif
+
+constexpr int GAE_COLS = 64;   // columns per block (one wave-wide row segment = 256 B)
+constexpr int GAE_WAVES = 8;   // 512 threads
+constexpr int GAE_TT = 64;     // rows per tile
+constexpr int RPW = GAE_TT / GAE_WAVES;  // rows per wave per tile
 
 struct GaeArgs {
   const float* rewards;
@@ -50,12 +62,11 @@ struct GaeArgs {
 
 template <typename Acc>
 __device__ __forceinline__ Acc gae_delta(float r, float v, float vn, uint8_t esn, bool gvec,
-                                         float g32, double g64, Acc& nn_out);
+                                         float g32, double g64);
 
 template <>
 __device__ __forceinline__ double gae_delta<double>(float r, float v, float vn, uint8_t esn,
-                                                    bool gvec, float g32, double g64,
-                                                    double& nn_out) {
+                                                    bool gvec, float g32, double g64) {
   const double nn = 1.0 - (double)(esn != 0);
   double t1;
   if (gvec) {
@@ -64,27 +75,30 @@ __device__ __forceinline__ double gae_delta<double>(float r, float v, float vn, 
     const float t1f = g32 * vn;
     t1 = (double)t1f;
   }
-  nn_out = nn;
   return ((double)r + t1 * nn) - (double)v;
 }
 
 template <>
 __device__ __forceinline__ float gae_delta<float>(float r, float v, float vn, uint8_t esn,
-                                                  bool /*gvec*/, float g32, double /*g64*/,
-                                                  float& nn_out) {
+                                                  bool /*gvec*/, float g32, double /*g64*/) {
   const float nn = esn ? 0.0f : 1.0f;
-  nn_out = nn;
   return (r + (g32 * vn) * nn) - v;
 }
 
+struct Rows {
+  float r[RPW], v[RPW], vn[RPW];
+  uint8_t e[RPW];
+};
+
 template <typename Acc>
-__global__ __launch_bounds__(256) void gae_kernel(const GaeArgs a) {
-  __shared__ Acc delta_s[2][GAE_TT][GAE_COLS];
-  __shared__ uint8_t nn_s[2][GAE_TT][GAE_COLS];
-  __shared__ float v_s[2][GAE_TT][GAE_COLS];
+__global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
+  __shared__ Acc delta_s[GAE_TT][GAE_COLS];  // delta_t, overwritten in place by the carry
+  __shared__ Acc coef_s[GAE_TT][GAE_COLS];   // (gamma*lambda) * next_nonterminal
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave index made provably wave-uniform: row indices/addresses then live in SGPRs
+  // (scalar base + per-lane column offset) instead of one 64-bit VGPR pair per row.
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t c = (int64_t)blockIdx.x * GAE_COLS + lane;
   const bool valid = c < a.C;
   const int64_t cc = valid ? c : 0;
@@ -97,70 +111,112 @@ __global__ __launch_bounds__(256) void gae_kernel(const GaeArgs a) {
   const int64_t T = a.T;
   const int ntiles = (int)((T + GAE_TT - 1) / GAE_TT);
 
-  float r_reg[ROWS_PER_WAVE], v_reg[ROWS_PER_WAVE], vn_reg[ROWS_PER_WAVE];
-  uint8_t e_reg[ROWS_PER_WAVE];
-
-  // Issue this wave's loads for tile `tile` into registers.
-  auto issue_loads = [&](int tile) {
+  // Kernel arguments copied to locals once (they live in SGPRs; re-reading the large
+  // by-value struct from the kernarg segment in every row branch cost a scalar-load wait
+  // per row).  Loads are branch-free: clamped row index + pointer select, masked after.
+  const float* __restrict__ rewards = a.rewards;
+  const float* __restrict__ values = a.values;
+  const uint8_t* __restrict__ es = a.es;
+  const uint8_t* __restrict__ next_es = a.next_es;
+  const float* __restrict__ next_values = a.next_values;
+  const int64_t C = a.C, N = a.N;
+  auto load = [&](Rows& R, int tile) {
     const int64_t lo = T - (int64_t)(tile + 1) * GAE_TT;
 #pragma unroll
-    for (int j = 0; j < ROWS_PER_WAVE; ++j) {
-      const int lr = wave + j * GAE_WAVES;
-      const int64_t t = lo + lr;
-      r_reg[j] = 0.f; v_reg[j] = 0.f; vn_reg[j] = 0.f; e_reg[j] = 0;
-      if (t >= 0 && valid) {
-        r_reg[j] = a.rewards[t * a.C + c];
-        v_reg[j] = a.values[t * a.C + c];
-        if (t == T - 1) {
-          vn_reg[j] = a.next_values[c];
-          e_reg[j] = a.next_es[n];
-        } else {
-          vn_reg[j] = a.values[(t + 1) * a.C + c];
-          e_reg[j] = a.es[(t + 1) * a.N + n];
-        }
-      }
-    }
-  };
-  // Carry-independent part -> LDS buffer `buf`.
-  auto stage = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < ROWS_PER_WAVE; ++j) {
-      const int lr = wave + j * GAE_WAVES;
-      Acc nn;
-      const Acc d = gae_delta<Acc>(r_reg[j], v_reg[j], vn_reg[j], e_reg[j], gvec, g32, g64, nn);
-      delta_s[buf][lr][lane] = d;
-      nn_s[buf][lr][lane] = (nn != (Acc)0) ? 1 : 0;
-      v_s[buf][lr][lane] = v_reg[j];
+    for (int j = 0; j < RPW; ++j) {
+      const int64_t t = lo + wave * RPW + j;
+      const int64_t tc = t < 0 ? 0 : t;
+      const bool last = tc == T - 1;
+      const float* vn_p = last ? next_values + cc : values + (tc + 1) * C + cc;
+      const uint8_t* e_p = last ? next_es + n : es + (tc + 1) * N + n;
+      const bool ok = t >= 0;
+      const float r = rewards[tc * C + cc];
+      const float v = values[tc * C + cc];
+      const float vn = *vn_p;
+      const uint8_t e = *e_p;
+      R.r[j] = ok ? r : 0.f;
+      R.v[j] = ok ? v : 0.f;
+      R.vn[j] = ok ? vn : 0.f;
+      R.e[j] = ok ? e : 0;
     }
   };
 
-  issue_loads(0);
-  stage(0);
-  __syncthreads();
-
+  float* __restrict__ adv_out = a.adv;
+  float* __restrict__ ret_out = a.ret;
+  Rows cur, nxt;
+#if GAE_DIAG & 8
+  long long t_last = clock64();
+#endif
+  load(cur, 0);
   Acc carry = (Acc)0;
   for (int tile = 0; tile < ntiles; ++tile) {
-    const int buf = tile & 1;
-    const bool more = tile + 1 < ntiles;
-    if (more) issue_loads(tile + 1);
-    if (wave == 0) {
-      const int64_t lo = T - (int64_t)(tile + 1) * GAE_TT;
-      for (int lr = GAE_TT - 1; lr >= 0; --lr) {
-        const int64_t t = lo + lr;
-        if (t < 0) break;
-        const Acc d = delta_s[buf][lr][lane];
-        const Acc nn = nn_s[buf][lr][lane] ? (Acc)1 : (Acc)0;
-        const Acc coef = gl * nn;
-        carry = d + coef * carry;
-        if (valid) {
-          const float adv = (float)carry;
-          a.adv[t * a.C + c] = adv;
-          if (a.ret) a.ret[t * a.C + c] = adv + v_s[buf][lr][lane];
+    const int64_t lo = T - (int64_t)(tile + 1) * GAE_TT;
+    // (1) carry-independent part of every row -> LDS
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int lr = wave * RPW + j;
+      delta_s[lr][lane] = gae_delta<Acc>(cur.r[j], cur.v[j], cur.vn[j], cur.e[j], gvec, g32, g64);
+      // gl * nn with nn in {0, 1} is exactly gl or +0.0 (gl > 0): a select, no multiply
+      coef_s[lr][lane] = cur.e[j] ? (Acc)0 : gl;
+    }
+    GSTAMP(0);
+    lds_barrier();
+    GSTAMP(1);
+    // (2) next tile's loads go out while wave 0 runs the serial recurrence
+    if (!(GAE_DIAG & 4) && tile + 1 < ntiles) load(nxt, tile + 1);
+    if (!(GAE_DIAG & 1) && wave == 0) {
+      // The only serial work: carry = delta + coef*carry (two dependent FP64 ops per row),
+      // operands batched out of LDS, carries written back in place.  Rows with t < 0 (only in
+      // the last-processed partial tile) lie below every valid row and are never stored.
+      constexpr int QB = 4;  // rows per LDS batch; batch h-1 is read while batch h is chained
+      Acc d[QB], cf[QB], dn[QB], cfn[QB];
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        d[q] = delta_s[GAE_TT - QB + q][lane];
+        cf[q] = coef_s[GAE_TT - QB + q][lane];
+      }
+#pragma unroll
+      for (int h = GAE_TT / QB - 1; h >= 0; --h) {
+        if (h > 0) {
+#pragma unroll
+          for (int q = 0; q < QB; ++q) {
+            dn[q] = delta_s[(h - 1) * QB + q][lane];
+            cfn[q] = coef_s[(h - 1) * QB + q][lane];
+          }
+        }
+#pragma unroll
+        for (int q = QB - 1; q >= 0; --q) {
+          carry = d[q] + cf[q] * carry;
+          d[q] = carry;
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) delta_s[h * QB + q][lane] = d[q];
+        if (h > 0) {
+#pragma unroll
+          for (int q = 0; q < QB; ++q) {
+            d[q] = dn[q];
+            cf[q] = cfn[q];
+          }
         }
       }
     }
-    if (more) stage(buf ^ 1);
-    __syncthreads();
+    GSTAMP(2);
+    lds_barrier();
+    GSTAMP(3);
+    // (3) every wave stores its rows: adv and returns = adv + V (fp32), coalesced 256-B rows
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int lr = wave * RPW + j;
+      const int64_t t = lo + lr;
+      if (!(GAE_DIAG & 2) && t >= 0 && valid) {
+        const float adv = (float)delta_s[lr][lane];
+        adv_out[t * C + c] = adv;
+        if (ret_out) ret_out[t * C + c] = adv + cur.v[j];
+      }
+    }
+    GSTAMP(4);
+    if (!(GAE_DIAG & 4) && tile + 1 < ntiles) cur = nxt;
+    GSTAMP(5);
   }
 }
 
@@ -200,9 +256,11 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
   }
   const int64_t blocks = (a.C + GAE_COLS - 1) / GAE_COLS;
   if (mode == RAI_GAE_EXACT)
-    hipLaunchKernelGGL(gae_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, rai_stream(stream), a);
+    hipLaunchKernelGGL(gae_kernel<double>, dim3((unsigned)blocks), dim3(GAE_WAVES * 64), 0,
+                       rai_stream(stream), a);
   else
-    hipLaunchKernelGGL(gae_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, rai_stream(stream), a);
+    hipLaunchKernelGGL(gae_kernel<float>, dim3((unsigned)blocks), dim3(GAE_WAVES * 64), 0,
+                       rai_stream(stream), a);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

@@ -69,7 +69,30 @@ struct MlpArgs {
   int32_t* err;
 };
 
+#ifdef RAI_STAMPS
+// Diagnostic build only (never the shipped library): per-phase cycle totals of wave 0 of
+// each workgroup, accumulated over the launch and copied out by rai_mlp_debug_stamps().
+__device__ unsigned long long g_stamps[2][32];
+#define STAMP(i)                                                        \
+  do {                                                                  \
+    if (threadIdx.x == 0) {                                             \
+      unsigned long long t_;                                            \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      S.stamps[i] += t_ - S.t_last;                                     \
+      S.t_last = t_;                                                    \
+    }                                                                   \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
 struct Smem {
+#ifdef RAI_STAMPS
+  unsigned long long stamps[32];
+  unsigned long long t_last;
+#endif
   float W1[HID][MAXIN];
   float b1[HID];
   float W2[HID][LD];   // [out j][in k]
@@ -101,13 +124,6 @@ __device__ __forceinline__ float vf_loss(int fn, float x) {
 __device__ __forceinline__ float vf_grad(int fn, float x) {
   if (fn == 0) return 2.f * x;
   return x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x);
-}
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic but NOT for
-// outstanding global loads (__syncthreads() would add s_waitcnt vmcnt(0) and expose the
-// latency of the next minibatch's register prefetch).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <int NV>
@@ -237,6 +253,10 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
     r_x1 = tid + NT < nx ? a.obs[row0 * IN + tid + NT] : 0.f;
   };
   prefetch(0);
+#ifdef RAI_STAMPS
+  if (tid < 32) S.stamps[tid] = 0;
+  if (tid == 0) S.t_last = __builtin_amdgcn_s_memtime();
+#endif
   lds_barrier();
 
   for (int mb = 0; mb < nmb; ++mb) {
@@ -276,6 +296,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       // P0: minibatch X elements of this chunk -> LDS
       for (int e = tid; e < CH * MAXIN; e += NT) S.X[e / MAXIN][e % MAXIN] = 0.f;
       lds_barrier();
+      STAMP(1);
       {
         const int e0 = tid, e1 = tid + NT;
         const int s0 = e0 / IN - c * CH, s1 = e1 / IN - c * CH;
@@ -283,6 +304,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         if (s1 >= 0 && s1 < crows) S.X[s1][e1 % IN] = c_x1;
       }
       lds_barrier();
+      STAMP(2);
       asm volatile("" : "+v"(tid));
       // P1: layer 1 (VALU; K = in_dim <= 8)
       {
@@ -301,6 +323,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         }
       }
       lds_barrier();
+      STAMP(3);
       asm volatile("" : "+v"(tid));
       // P2: layer 2 forward on MFMA: Z2[s][j] = sum_k H1[s][k] W2[j][k]
       {
@@ -327,6 +350,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         }
       }
       lds_barrier();
+      STAMP(4);
       asm volatile("" : "+v"(tid));
       // P3: output layer (VALU)
       {
@@ -342,6 +366,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         }
       }
       lds_barrier();
+      STAMP(5);
       asm volatile("" : "+v"(tid));
       // P4: per-sample loss gradient (tid >> 6).r.t. the head outputs (ppo.py:307-361 semantics;
       //     autograd tie rules of min/max and closed-interval clamp, as loss.hip)
@@ -418,6 +443,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         }
       }
       lds_barrier();
+      STAMP(6);
       asm volatile("" : "+v"(tid));
       // P5: output-layer weight/bias grads (slot A owners)
       if (tid < OUT * HID) {
@@ -432,6 +458,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         ga += acc;
       }
       lds_barrier();
+      STAMP(7);
       asm volatile("" : "+v"(tid));
       // P6: dZ2 = (dout . W3) * act'(H2), in place over H2
       {
@@ -449,6 +476,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         }
       }
       lds_barrier();
+      STAMP(8);
       asm volatile("" : "+v"(tid));
       // P7: dW2 += dZ2^T H1 (accumulators persist over chunks), dH1 = dZ2 W2 (held), db2
       f4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = {0.f, 0.f, 0.f, 0.f};
@@ -478,6 +506,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         }
       }
       lds_barrier();
+      STAMP(9);
       asm volatile("" : "+v"(tid));
       // P8: dZ1 = dH1 * act'(H1), in place over H1
       {
@@ -490,6 +519,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         }
       }
       lds_barrier();
+      STAMP(10);
       asm volatile("" : "+v"(tid));
       // P9: layer-1 weight (slot B) and bias (slot A) grads
       if (tid < HID * IN) {
@@ -505,6 +535,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
         ga += acc;
       }
       lds_barrier();
+      STAMP(11);
     }
 
     // ---- global grad norm (both networks), clip coefficient ---------------------------------
@@ -541,6 +572,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       S.bcast[3] = (float)(-((double)lr / bc1));
     }
     lds_barrier();
+      STAMP(12);
     const float total_norm = (float)sqrt((double)S.bcast[0] + (double)S.bcast[1]);
     float coef = 1.f;
     if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
@@ -593,6 +625,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       if (net == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;
     }
     lds_barrier();
+      STAMP(13);
   }
 
   // ---- write back parameters and optimizer moments (torch parameter order) -----------------------
@@ -628,6 +661,9 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       a.exp_avg_sq[oW1 + t2] = b_v;
     }
   }
+#ifdef RAI_STAMPS
+  if (tid < 32) g_stamps[net][tid] = S.stamps[tid];
+#endif
   if (net == 0 && tid == 0) {
     a.state->opt_step = step0 + nmb;
     a.state->stat_index = stat0 + nmb;
@@ -638,6 +674,12 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
 }  // namespace
 
 extern "C" int64_t rai_mlp_ppo_workspace_bytes(void) { return 64; }
+
+#ifdef RAI_STAMPS
+extern "C" int rai_mlp_debug_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
+}
+#endif
 
 extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
                                  const int64_t* actions, const float* old_logp, const float* old_values,

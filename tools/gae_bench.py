@@ -1,0 +1,39 @@
+"""GAE kernel microbenchmark: algorithmic GB/s at the BASELINE shapes and in the
+bandwidth regime (HIP events on the launch stream)."""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import torch  # noqa: E402
+
+import _pkgload  # noqa: E402
+
+_pkgload.load()
+from rl_algo_impls_amd.gae import EXACT, FAST, compute_advantages_device  # noqa: E402
+
+dev = torch.device("cuda", 0)
+for (T, N, K) in [(128, 4096, 1), (512, 2048, 1), (128, 1024, 1), (512, 512, 3), (128, 1 << 20, 1), (512, 1 << 18, 3)]:
+    shp = (T, N) if K == 1 else (T, N, K)
+    r = torch.randn(shp, device=dev)
+    v = torch.randn(shp, device=dev)
+    es = torch.rand((T, N), device=dev) < 0.01
+    nes = torch.rand(N, device=dev) < 0.01
+    nv = torch.randn(shp[1:], device=dev)
+    adv = torch.empty_like(v)
+    ret = torch.empty_like(v)
+    g = 0.99 if K == 1 else __import__("numpy").array([0.99, 0.995, 0.999])
+    byts = 16 * T * N * K + T * N + 4 * N * K + N
+    for mode, name in ((EXACT, "exact"), (FAST, "fast")):
+        for _ in range(5):
+            compute_advantages_device(r, v, es, nes, nv, g, 0.95, mode=mode, advantages_out=adv, returns_out=ret)
+        reps = 50
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            compute_advantages_device(r, v, es, nes, nv, g, 0.95, mode=mode, advantages_out=adv, returns_out=ret)
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        print(f"T={T:4d} N={N:8d} K={K} {name:5s}: {us:9.2f} us  {byts / us / 1e3:8.1f} GB/s  "
+              f"({100 * byts / us / 1e3 / 8000:.1f}% of 8 TB/s)", flush=True)

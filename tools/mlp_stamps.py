@@ -1,0 +1,50 @@
+"""Diagnostic: per-phase cycle breakdown of the fused MLP PPO epoch kernel.
+Loads the stamps build (lib/librai_amd_stamps.so, -DRAI_STAMPS) and runs one epoch of
+the CartPole 4096x128 / batch 256 workload.  Not part of the product or the tests."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+os.environ["RAI_AMD_LIB"] = str(ROOT / "rl-algo-impls_amd" / "lib" / "librai_amd_stamps.so")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import _pkgload  # noqa: E402
+
+_pkgload.load()
+from rl_algo_impls_amd import _lib  # noqa: E402
+from rl_algo_impls_amd.envs import SyntheticVecEnv  # noqa: E402
+from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
+from rl_algo_impls_amd.ppo import PPO  # noqa: E402
+from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
+
+NAMES = ["P0 zero X", "P0 X write (+adv moments)", "P1 layer1", "P2 fwd MFMA", "P3 out layer", "P4 loss",
+         "P5 dW3", "P6 dZ2", "P7 dW2+dH1 MFMA", "P8 dZ1", "P9 dW1", "norm+exchange", "adam"]
+dev = torch.device("cuda", 0)
+torch.manual_seed(1)
+env = SyntheticVecEnv(4096, "cartpole", seed=1)
+policy = ActorCritic(env).to(dev)
+gen = SyncStepRolloutGenerator(policy, env, n_steps=int(os.environ.get("T", "128")))
+algo = PPO(policy, dev, None, batch_size=256, n_epochs=1, learning_rate=1e-3, gamma=0.98, gae_lambda=0.8)
+r = gen.rollout(gamma=0.98, gae_lambda=0.8)
+algo.update(r)  # warm
+torch.cuda.synchronize()
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+algo.update(r)
+ev1.record()
+ev1.synchronize()
+out = (C.c_ulonglong * 64)()
+rc = _lib.lib().rai_mlp_debug_stamps(out)
+assert rc == 0, rc
+st = np.array(out, dtype=np.float64).reshape(2, 32)
+nmb = r.total_steps // 256
+print(f"epoch {ev0.elapsed_time(ev1):.2f} ms for {nmb} minibatches -> {ev0.elapsed_time(ev1) * 1e3 / nmb:.2f} us/mb")
+for net in range(2):
+    tot = st[net, 1:14].sum()
+    print(f"--- workgroup {net} ({'actor' if net == 0 else 'critic'}): {tot / nmb:.0f} stamp-ticks/mb")
+    for i, n in enumerate(NAMES):
+        print(f"  {n:28s} {st[net, i + 1] / nmb:10.1f} ticks/mb  {100 * st[net, i + 1] / tot:5.1f}%")
