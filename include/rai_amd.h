@@ -100,6 +100,8 @@ typedef struct rai_optim_hparams {
   float max_grad_norm; /* ppo.py:442-444; <= 0 disables clipping */
   int32_t kind;        /* 0 Adam, 1 RMSprop */
   int32_t pad;
+  double beta1_d;      /* betas as the Python floats torch uses for its bias corrections */
+  double beta2_d;
 } rai_optim_hparams;
 
 typedef struct rai_train_state {
@@ -198,6 +200,22 @@ int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const fl
                       int32_t activation, const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
                       rai_train_state* state, float* stats, int32_t max_stats, float* norms,
                       int32_t max_norms, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Data-parallel variant: processes minibatches [mb_begin, mb_begin+mb_count) of the
+ * permuted rollout with the current parameters, normalising advantages with the given
+ * global per-minibatch (mean, den) pairs (moments[2*mb], moments[2*mb+1]; den already
+ * includes +1e-8 and the normalize/standardize choice) and averaging the loss over
+ * rows*world samples, and writes the raw (pre-clip) gradients to grad_out in flat
+ * parameter order.  The caller all-reduces grad_out across ranks (RCCL) and then runs
+ * rai_clip_optim_step.  One stats row per minibatch holds this rank's share. */
+int rai_mlp_ppo_grads(const float* params, const float* obs, const int64_t* actions,
+                      const float* old_logp, const float* old_values, const float* advantages,
+                      const float* returns, int64_t n_rows, int32_t batch_size, int32_t mb_begin,
+                      int32_t mb_count, const float* moments, int32_t world, int32_t in_dim,
+                      int32_t hidden, int32_t n_actions, int32_t activation,
+                      const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
+                      rai_train_state* state, float* grad_out, float* stats, int32_t max_stats,
+                      void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

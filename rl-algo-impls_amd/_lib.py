@@ -57,6 +57,8 @@ class OptimHparams(C.Structure):
         ("max_grad_norm", C.c_float),
         ("kind", C.c_int32),
         ("pad", C.c_int32),
+        ("beta1_d", C.c_double),
+        ("beta2_d", C.c_double),
     ]
 
 
@@ -83,6 +85,8 @@ _SIGNATURES = {
     "rai_clip_optim_step": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_gather_rows": (C.c_int, [_i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, []),
+    "rai_mlp_ppo_grads": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _i32,
+                                    _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_mlp_ppo_epoch": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
                                     _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
     "rai_categorical_sample": (C.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp, _vp, _vp, _i32, _vp]),

@@ -67,6 +67,16 @@ struct MlpArgs {
   int32_t max_norms;
   unsigned long long* xchg;  // [2 nets][2 parities], zeroed before every launch
   int32_t* err;
+  // data-parallel "grads" mode (grad_out != nullptr): process minibatches
+  // [mb_begin, mb_begin + mb_count), normalise advantages with the given global
+  // per-minibatch (mean, den) pairs, scale the loss means by 1/(rows*world), write the
+  // raw gradients to grad_out and stop (the caller all-reduces them and runs
+  // rai_clip_optim_step).
+  float* grad_out;
+  const float* moments;
+  int32_t mb_begin;
+  int32_t mb_count;
+  int32_t world;
 };
 
 #ifdef RAI_STAMPS
@@ -106,6 +116,7 @@ struct Smem {
   float out[CH][MAXOUT];
   float dout[CH][MAXOUT];
   double red[8 * NW];
+  double pw[2];
   float bcast[8];
 };
 
@@ -169,7 +180,9 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   const int has_vclip = a.hp->has_clip_range_vf, vf_fn = a.hp->vf_loss_fn;
   const int norm_adv = a.hp->normalize_advantage, std_adv = a.hp->standardize_advantage;
   const float halve = a.hp->ppo2_vf_coef_halving ? 0.5f : 1.f;
-  const float beta1 = a.ohp->beta1, beta2 = a.ohp->beta2, adam_eps = a.ohp->eps, lr = a.ohp->lr;
+  const float beta2 = a.ohp->beta2, adam_eps = a.ohp->eps, lr = a.ohp->lr;
+  const double beta1_d = a.ohp->beta1_d, beta2_d = a.ohp->beta2_d;
+  const bool grads_mode = a.grad_out != nullptr;
   const float max_grad_norm = a.ohp->max_grad_norm;
 
   // ---- flat parameter offsets (torch parameters() order: actor block, critic block) -------
@@ -223,7 +236,10 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
 
   const int B = a.batch;
   const int64_t n_rows = a.n_rows;
-  const int nmb = (int)((n_rows + B - 1) / B);
+  const int nmb_total = (int)((n_rows + B - 1) / B);
+  const int mb_begin = a.mb_begin;
+  const int mb_end = min(nmb_total, a.mb_begin + a.mb_count);
+  const int nmb = mb_end - mb_begin;
   const int64_t step0 = a.state->opt_step;
   const int stat0 = a.state->stat_index;
   const int norm0 = a.state->norm_index;
@@ -252,24 +268,31 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
     r_x0 = tid < nx ? a.obs[row0 * IN + tid] : 0.f;
     r_x1 = tid + NT < nx ? a.obs[row0 * IN + tid + NT] : 0.f;
   };
-  prefetch(0);
+  prefetch(mb_begin);
+  if (tid == 0) {  // running powers beta^step (bias corrections), advanced once per minibatch
+    S.pw[0] = pow(beta1_d, (double)step0);
+    S.pw[1] = pow(beta2_d, (double)step0);
+  }
 #ifdef RAI_STAMPS
   if (tid < 32) S.stamps[tid] = 0;
   if (tid == 0) S.t_last = __builtin_amdgcn_s_memtime();
 #endif
   lds_barrier();
 
-  for (int mb = 0; mb < nmb; ++mb) {
+  for (int mb = mb_begin; mb < mb_end; ++mb) {
     const int64_t row0 = (int64_t)mb * B;
     const int rows = (int)min((int64_t)B, n_rows - row0);
     // take this minibatch's inputs out of the prefetch registers
     const int64_t c_act = r_act;
     const float c_olp = r_olp, c_ov = r_ov, c_adv = r_adv, c_ret = r_ret, c_x0 = r_x0, c_x1 = r_x1;
-    if (mb + 1 < nmb) prefetch(mb + 1);
+    if (mb + 1 < mb_end) prefetch(mb + 1);
 
     // advantage normalisation moments over the minibatch (ppo.py:313-316), actor only
     float amean = 0.f, aden = 1.f;
-    if (net == 0 && (norm_adv || std_adv)) {
+    if (net == 0 && a.moments) {
+      amean = a.moments[2 * mb];
+      aden = a.moments[2 * mb + 1];
+    } else if (net == 0 && (norm_adv || std_adv)) {
       double v1[1] = {tid < rows ? (double)c_adv : 0.0};
       bsum<1>(v1, S.red);
       const float mean = (float)(v1[0] / (double)rows);
@@ -280,7 +303,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       if (norm_adv) { amean = mean; aden = den; }
       else { aden = den; }
     }
-    const float invB = 1.f / (float)rows;
+    const float invB = 1.f / (float)(rows * a.world);
 
     f4 gw2 = {0.f, 0.f, 0.f, 0.f};
     float ga = 0.f, gb = 0.f;
@@ -548,6 +571,36 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       red[0] = ss; red[1] = (double)st[0]; red[2] = (double)st[1]; red[3] = (double)st[2]; red[4] = (double)st[3];
     }
     bsum<5>(red, S.red);
+    if (grads_mode) {
+      // raw gradients out (same flat indices as the parameters), stats row, next minibatch
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a.grad_out[oW2 + w2_idx[r]] = gw2[r];
+      if (a_flat >= 0) a.grad_out[a_flat] = ga;
+      if (b_flat >= 0) a.grad_out[b_flat] = gb;
+    }
+    if (tid == 0) {
+      const int srow = stat0 + (mb - mb_begin);
+      if (a.stats && srow < a.max_stats) {
+        float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
+        const double Bd = (double)rows * (double)a.world;
+        if (net == 0) {
+          const float pi_loss = (float)(-red[1] / Bd);
+          const float ent_loss = (float)(-red[4] / Bd);
+          row[0] = pi_coef * pi_loss + ent_coef * ent_loss;  // host adds the value term
+          row[1] = pi_loss;
+          row[2] = ent_loss;
+          row[3] = (float)(red[2] / Bd);
+          row[4] = (float)(red[3] / Bd);
+        } else {
+          row[5] = (float)(red[1] / Bd) * halve;
+          row[5 + RAI_MAX_K] = has_vclip ? (float)(red[2] / Bd) : 0.f;
+        }
+      }
+    }
+    if (grads_mode) {
+      lds_barrier();
+      continue;
+    }
     if (tid == 0) {
       const float mine = (float)red[0];
       const unsigned tag = (unsigned)(mb + 1);
@@ -565,9 +618,10 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       }
       S.bcast[0] = net == 0 ? mine : other;
       S.bcast[1] = net == 0 ? other : mine;
-      const int64_t step = step0 + mb + 1;
-      const double bc1 = 1.0 - pow((double)beta1, (double)step);
-      const double bc2 = 1.0 - pow((double)beta2, (double)step);
+      S.pw[0] *= beta1_d;
+      S.pw[1] *= beta2_d;
+      const double bc1 = 1.0 - S.pw[0];
+      const double bc2 = 1.0 - S.pw[1];
       S.bcast[2] = (float)sqrt(bc2);
       S.bcast[3] = (float)(-((double)lr / bc1));
     }
@@ -577,7 +631,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
     float coef = 1.f;
     if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
     const float bc2_sqrt = S.bcast[2], neg_step = S.bcast[3];
-    const float w1 = (float)(1.0 - (double)beta1), w2 = (float)(1.0 - (double)beta2);
+    const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
 
     // ---- Adam on owned parameters; refresh the LDS copies ----------------------------------------
 #pragma unroll
@@ -605,24 +659,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       S.W1[j][k] = p;
     }
     if (tid == 0) {
-      const int srow = stat0 + mb;
-      if (a.stats && srow < a.max_stats) {
-        float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
-        const double Bd = (double)rows;
-        if (net == 0) {
-          const float pi_loss = (float)(-red[1] / Bd);
-          const float ent_loss = (float)(-red[4] / Bd);
-          row[0] = pi_coef * pi_loss + ent_coef * ent_loss;  // host adds the value term
-          row[1] = pi_loss;
-          row[2] = ent_loss;
-          row[3] = (float)(red[2] / Bd);
-          row[4] = (float)(red[3] / Bd);
-        } else {
-          row[5] = (float)(red[1] / Bd) * halve;
-          row[5 + RAI_MAX_K] = has_vclip ? (float)(red[2] / Bd) : 0.f;
-        }
-      }
-      if (net == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;
+      if (net == 0 && a.norms && norm0 + (mb - mb_begin) < a.max_norms) a.norms[norm0 + (mb - mb_begin)] = total_norm;
     }
     lds_barrier();
       STAMP(13);
@@ -631,7 +668,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   // ---- write back parameters and optimizer moments (torch parameter order) -----------------------
   // Indices are recomputed from a laundered copy of tid so the compiler does not keep the
   // prologue's 64-bit addresses alive (in VGPRs) across the whole minibatch loop.
-  {
+  if (!grads_mode) {
     int t2 = tid;
     asm volatile("" : "+v"(t2));
     const int lane2 = t2 & 63, w_2 = t2 >> 6, g2 = lane2 >> 4, li2 = lane2 & 15;
@@ -665,9 +702,11 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   if (tid < 32) g_stamps[net][tid] = S.stamps[tid];
 #endif
   if (net == 0 && tid == 0) {
-    a.state->opt_step = step0 + nmb;
     a.state->stat_index = stat0 + nmb;
-    a.state->norm_index = norm0 + nmb;
+    if (!grads_mode) {
+      a.state->opt_step = step0 + nmb;
+      a.state->norm_index = norm0 + nmb;
+    }
   }
 }
 
@@ -681,6 +720,31 @@ extern "C" int rai_mlp_debug_stamps(unsigned long long* host_out) {
 }
 #endif
 
+namespace {
+int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, void* workspace,
+               int64_t workspace_bytes, void* stream) {
+  if (hidden != HID || a.in_dim < 1 || a.in_dim > MAXIN || a.n_act < 1 || a.n_act > MAXOUT ||
+      batch_size < 2 || batch_size > MAXB || n_rows < 1 || (a.act_fn != 0 && a.act_fn != 1) ||
+      a.world < 1)
+    return RAI_E_SHAPE;
+  if (!a.params || !a.obs || !a.actions || !a.old_logp || !a.old_values || !a.adv || !a.ret ||
+      !a.hp || !a.ohp || !a.state || !workspace)
+    return RAI_E_NULLPTR;
+  if (!a.grad_out && (!a.exp_avg || !a.exp_avg_sq)) return RAI_E_NULLPTR;
+  if (workspace_bytes < rai_mlp_ppo_workspace_bytes()) return RAI_E_WORKSPACE;
+  if (n_rows % batch_size == 1 && !a.moments) return RAI_E_SHAPE;  // 1-row minibatch: no std
+  a.n_rows = n_rows;
+  a.batch = batch_size;
+  a.xchg = reinterpret_cast<unsigned long long*>(workspace);
+  a.err = &a.state->err;
+  hipError_t e = hipMemsetAsync(workspace, 0, 64, rai_stream(stream));
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(mlp_ppo_epoch_kernel, dim3(2), dim3(NT), 0, rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+}  // namespace
+
 extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
                                  const int64_t* actions, const float* old_logp, const float* old_values,
                                  const float* advantages, const float* returns, int64_t n_rows,
@@ -689,41 +753,37 @@ extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_s
                                  rai_train_state* state, float* stats, int32_t max_stats, float* norms,
                                  int32_t max_norms, void* workspace, int64_t workspace_bytes,
                                  void* stream) {
-  if (hidden != HID || in_dim < 1 || in_dim > MAXIN || n_actions < 1 || n_actions > MAXOUT ||
-      batch_size < 2 || batch_size > MAXB || n_rows < 1 || (activation != 0 && activation != 1))
-    return RAI_E_SHAPE;
-  if (!params || !exp_avg || !exp_avg_sq || !obs || !actions || !old_logp || !old_values ||
-      !advantages || !returns || !hp || !ohp || !state || !workspace)
-    return RAI_E_NULLPTR;
-  if (workspace_bytes < rai_mlp_ppo_workspace_bytes()) return RAI_E_WORKSPACE;
-  if (n_rows % batch_size == 1) return RAI_E_SHAPE;  // a 1-row minibatch has no unbiased std
-  MlpArgs a;
-  a.params = params;
-  a.exp_avg = exp_avg;
-  a.exp_avg_sq = exp_avg_sq;
-  a.obs = obs;
-  a.actions = actions;
-  a.old_logp = old_logp;
-  a.old_values = old_values;
-  a.adv = advantages;
-  a.ret = returns;
-  a.n_rows = n_rows;
-  a.batch = batch_size;
-  a.in_dim = in_dim;
-  a.n_act = n_actions;
-  a.act_fn = activation;
-  a.hp = hp;
-  a.ohp = ohp;
-  a.state = state;
-  a.stats = stats;
-  a.max_stats = max_stats;
-  a.norms = norms;
-  a.max_norms = max_norms;
-  a.xchg = reinterpret_cast<unsigned long long*>(workspace);
-  a.err = &state->err;
-  hipError_t e = hipMemsetAsync(workspace, 0, 64, rai_stream(stream));
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(mlp_ppo_epoch_kernel, dim3(2), dim3(NT), 0, rai_stream(stream), a);
-  RAI_LAUNCH_CHECK();
-  return RAI_OK;
+  MlpArgs a = {};
+  a.params = params; a.exp_avg = exp_avg; a.exp_avg_sq = exp_avg_sq;
+  a.obs = obs; a.actions = actions; a.old_logp = old_logp; a.old_values = old_values;
+  a.adv = advantages; a.ret = returns;
+  a.in_dim = in_dim; a.n_act = n_actions; a.act_fn = activation;
+  a.hp = hp; a.ohp = ohp; a.state = state;
+  a.stats = stats; a.max_stats = max_stats; a.norms = norms; a.max_norms = max_norms;
+  a.grad_out = nullptr; a.moments = nullptr;
+  a.mb_begin = 0; a.mb_count = 1 << 30; a.world = 1;
+  return mlp_launch(a, hidden, batch_size, n_rows, workspace, workspace_bytes, stream);
+}
+
+extern "C" int rai_mlp_ppo_grads(const float* params, const float* obs, const int64_t* actions,
+                                 const float* old_logp, const float* old_values,
+                                 const float* advantages, const float* returns, int64_t n_rows,
+                                 int32_t batch_size, int32_t mb_begin, int32_t mb_count,
+                                 const float* moments, int32_t world, int32_t in_dim, int32_t hidden,
+                                 int32_t n_actions, int32_t activation, const rai_ppo_hparams* hp,
+                                 const rai_optim_hparams* ohp, rai_train_state* state, float* grad_out,
+                                 float* stats, int32_t max_stats, void* workspace,
+                                 int64_t workspace_bytes, void* stream) {
+  if (!grad_out) return RAI_E_NULLPTR;
+  if (mb_begin < 0 || mb_count < 1) return RAI_E_SHAPE;
+  MlpArgs a = {};
+  a.params = const_cast<float*>(params);
+  a.obs = obs; a.actions = actions; a.old_logp = old_logp; a.old_values = old_values;
+  a.adv = advantages; a.ret = returns;
+  a.in_dim = in_dim; a.n_act = n_actions; a.act_fn = activation;
+  a.hp = hp; a.ohp = ohp; a.state = state;
+  a.stats = stats; a.max_stats = max_stats; a.norms = nullptr; a.max_norms = 0;
+  a.grad_out = grad_out; a.moments = moments;
+  a.mb_begin = mb_begin; a.mb_count = mb_count; a.world = world;
+  return mlp_launch(a, hidden, batch_size, n_rows, workspace, workspace_bytes, stream);
 }

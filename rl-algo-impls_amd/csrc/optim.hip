@@ -75,10 +75,10 @@ __global__ __launch_bounds__(OPT_THREADS) void clip_optim_kernel(
   }
   const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
   if (hp.kind == 0) {
-    const double bc1 = 1.0 - pow((double)hp.beta1, (double)step);
-    const double bc2 = 1.0 - pow((double)hp.beta2, (double)step);
-    const float w1 = (float)(1.0 - (double)hp.beta1);   // lerp weight
-    const float w2 = (float)(1.0 - (double)hp.beta2);   // addcmul value
+    const double bc1 = 1.0 - pow(hp.beta1_d, (double)step);
+    const double bc2 = 1.0 - pow(hp.beta2_d, (double)step);
+    const float w1 = (float)(1.0 - hp.beta1_d);   // lerp weight (torch: 1 - beta1 in Python)
+    const float w2 = (float)(1.0 - hp.beta2_d);   // addcmul value
     const float bc2_sqrt = (float)sqrt(bc2);
     const float neg_step = (float)(-((double)hp.lr / bc1));
     for (int64_t i = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x; i < P; i += stride) {
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(OPT_THREADS) void clip_optim_kernel(
       s2[i] = vv;
     }
   } else {
-    const float w = (float)(1.0 - (double)hp.alpha);
+    const float w = (float)(1.0 - hp.beta1_d);  // RMSprop: beta1_d carries alpha as a Python float
     const float neg_lr = -hp.lr;
     for (int64_t i = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x; i < P; i += stride) {
       const float gi = g[i] * coef;

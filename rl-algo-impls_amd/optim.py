@@ -88,7 +88,9 @@ class FlatOptimizer:
 
     def sync_hparams(self) -> None:
         hp = _lib.OptimHparams(lr=float(self.lr), beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
-                               alpha=self.alpha, max_grad_norm=float(self.max_grad_norm or 0.0), kind=self.kind)
+                               alpha=self.alpha, max_grad_norm=float(self.max_grad_norm or 0.0), kind=self.kind,
+                               beta1_d=float(self.betas[0] if self.kind == self.ADAM else self.alpha),
+                               beta2_d=float(self.betas[1]))
         struct_to_device(hp, self.device, self.hp_dev)
 
     def step(self, state_dev: torch.Tensor, norms: Optional[torch.Tensor]) -> None:

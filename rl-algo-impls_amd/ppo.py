@@ -75,6 +75,107 @@ class PPO:
         self.last_update_seconds: Optional[float] = None
         self.force_generic = False  # True: always use the per-minibatch (PyTorch network) path
         self._mlp_ws: Optional[torch.Tensor] = None
+        self.dp_group = None
+        self.world = 1
+
+    # -- data parallel (one process per GPU) ------------------------------------------------
+    def enable_data_parallel(self, group=None) -> None:
+        """Weak-scaling data parallelism: every rank owns its own env group and HBM rollout;
+        a global minibatch is the union of the ranks' minibatch slices, gradients are summed
+        over ranks with one RCCL all-reduce per optimizer step (rccl/xGMI via
+        torch.distributed), and every rank applies the identical clip+Adam step.  On the
+        fused MLP path the advantage normalisation uses global per-minibatch moments (one
+        small all-reduce per epoch), reproducing the reference's normalisation over the whole
+        (global) minibatch; the generic path normalises per rank."""
+        import torch.distributed as dist
+
+        self.dp_group = group
+        self.world = dist.get_world_size(group)
+        with torch.no_grad():  # identical starting weights everywhere
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            if self.flat.flat.is_cuda and dist.get_backend(group) == "gloo":
+                h = self.flat.flat.cpu()
+                dist.broadcast(h, src=src, group=group)
+                self.flat.flat.copy_(h)
+            else:
+                dist.broadcast(self.flat.flat, src=src, group=group)
+
+    def _all_reduce(self, t: torch.Tensor, average: bool = False) -> None:
+        import torch.distributed as dist
+
+        if t.is_cuda and dist.get_backend(self.dp_group) == "gloo":  # test/rehearsal backend
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.dp_group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.dp_group)  # RCCL over xGMI
+        if average:
+            t.mul_(1.0 / self.world)
+
+    def _global_adv_moments(self, adv: torch.Tensor, nmb: int) -> torch.Tensor:
+        """(mean, den) of every global minibatch of this epoch: local per-minibatch
+        (count, sum, sum of squares) in fp64, one all-reduce, unbiased std (ppo.py:313-316)."""
+        B = self.batch_size
+        a = adv.reshape(-1).double()
+        n_full = a.numel() // B
+        parts = [torch.stack([torch.full((n_full,), float(B), dtype=torch.float64, device=a.device),
+                              a[:n_full * B].view(n_full, B).sum(1), (a[:n_full * B].view(n_full, B) ** 2).sum(1)], 1)]
+        if n_full < nmb:
+            tail = a[n_full * B:]
+            parts.append(torch.stack([torch.tensor(float(tail.numel()), dtype=torch.float64, device=a.device),
+                                      tail.sum(), (tail ** 2).sum()]).view(1, 3))
+        m = torch.cat(parts, 0)
+        self._all_reduce(m)
+        n, s1, s2 = m[:, 0], m[:, 1], m[:, 2]
+        mean = s1 / n
+        std = torch.sqrt(torch.clamp(s2 - n * mean * mean, min=0.0) / (n - 1)).float()
+        out = torch.empty((nmb, 2), dtype=torch.float32, device=a.device)
+        if self.normalize_advantage:
+            out[:, 0] = mean.float()
+            out[:, 1] = std + 1e-8
+        elif self.standardize_advantage:
+            out[:, 0] = 0.0
+            out[:, 1] = std + 1e-8
+        else:
+            out[:, 0] = 0.0
+            out[:, 1] = 1.0
+        return out.contiguous()
+
+    def _update_fused_dp(self, r, spec) -> Tuple[np.ndarray, np.ndarray, int]:
+        nmb = r.num_minibatches(self.batch_size)
+        n_steps = self.n_epochs * nmb
+        blocks = self.blocks
+        blocks.ensure_tables(n_steps, n_steps)
+        blocks.upload(self._hparams(1, nmb), self.optimizer.step_count)
+        if self._mlp_ws is None:
+            self._mlp_ws = torch.zeros(int(_lib.lib().rai_mlp_ppo_workspace_bytes()), dtype=torch.uint8,
+                                       device=self.device)
+        opt = self.optimizer
+        L = _lib.lib()
+        st = _lib.stream_handle(self.device)
+        for _ in range(self.n_epochs):
+            b = r.epoch_batch(shuffle=True)
+            moments = self._global_adv_moments(b.advantages, nmb)
+            obs = (b.obs if b.obs.dtype == torch.float32 else b.obs.float()).contiguous()
+            acts = b.actions.contiguous()
+            for i in range(nmb):
+                rc = L.rai_mlp_ppo_grads(
+                    self.flat.flat.data_ptr(), obs.data_ptr(), acts.data_ptr(), b.logprobs.data_ptr(),
+                    b.values.data_ptr(), b.advantages.data_ptr(), b.returns.data_ptr(), r.total_steps,
+                    self.batch_size, i, 1, moments.data_ptr(), self.world, spec["in_dim"], 64, spec["n_act"],
+                    spec["activation"], blocks.hp.data_ptr(), opt.hp_dev.data_ptr(), blocks.state.data_ptr(),
+                    self.flat.grad.data_ptr(), blocks.stats.data_ptr(), int(blocks.stats.shape[0]),
+                    self._mlp_ws.data_ptr(), self._mlp_ws.numel(), st)
+                _lib.check(rc, "rai_mlp_ppo_grads")
+                self._all_reduce(self.flat.grad)
+                opt.step(blocks.state, blocks.norms)
+        stats_t = blocks.stats[:n_steps].clone()
+        self._all_reduce(stats_t)  # every rank holds its share of the global means
+        host = torch.cat([stats_t.reshape(-1), blocks.norms[:n_steps]]).cpu().numpy()
+        stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE).copy()
+        norms = host[n_steps * _lib.RAI_STAT_STRIDE:]
+        stats[:, 0] += float(self.vf_coef) * stats[:, 5]
+        return stats, norms, 1
 
     # -- reference API -------------------------------------------------------------------
     def learn(self, train_timesteps: int, rollout_generator, callbacks=None, total_timesteps=None,
@@ -211,7 +312,7 @@ class PPO:
         returns the per-minibatch stats rows and grad norms (one D2H copy)."""
         spec = self.fused_mlp_spec() if hasattr(r, "epoch_batch") else None
         if spec is not None:
-            return self._update_fused(r, spec)
+            return self._update_fused_dp(r, spec) if self.world > 1 else self._update_fused(r, spec)
         nmb = r.num_minibatches(self.batch_size)
         n_steps = self.n_epochs * nmb
         n_norms = self.n_epochs if self.gradient_accumulation else n_steps
@@ -231,10 +332,18 @@ class PPO:
                                                  mb.returns, K)
                 torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
                 if not self.gradient_accumulation:
+                    if self.world > 1:
+                        self._all_reduce(self.flat.grad, average=True)
                     self.optimizer.step(blocks.state, blocks.norms)
             if self.gradient_accumulation:
+                if self.world > 1:
+                    self._all_reduce(self.flat.grad, average=True)
                 self.optimizer.step(blocks.state, blocks.norms)
-        host = torch.cat([blocks.stats[:n_steps].reshape(-1), blocks.norms[:n_norms]]).cpu().numpy()
+        stats_t = blocks.stats[:n_steps]
+        if self.world > 1:
+            stats_t = stats_t.clone()
+            self._all_reduce(stats_t, average=True)
+        host = torch.cat([stats_t.reshape(-1), blocks.norms[:n_norms]]).cpu().numpy()
         stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE)
         return stats, host[n_steps * _lib.RAI_STAT_STRIDE:], K or 1
 

@@ -1,0 +1,31 @@
+"""Data-parallel host logic on CPU with the gloo backend, world_size=2."""
+import multiprocessing as mp
+import socket
+
+import numpy as np
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_global_advantage_moments_world2():
+    import dp_worker
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.moments_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs = {r: (np.array(o), np.array(ref)) for r, o, ref in res}
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])  # identical on every rank
+    np.testing.assert_allclose(outs[0][0], outs[0][1], rtol=1e-5, atol=1e-6)
