@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--roofline-reps", type=int, default=200)
+    p.add_argument("--num-envs", type=int, default=None, help="override (rehearsal/debug only; not a bench line)")
     return p.parse_args()
 
 
@@ -76,14 +77,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("RAI_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI; gloo only to rehearse
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % max(ndev, 1))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
     _lib.lib()
 
     cfg = CONFIGS[args.config]
-    N, T = cfg["num_envs"], cfg["n_steps"]
+    N, T = (args.num_envs or cfg["num_envs"]), cfg["n_steps"]
     if args.config == "halfcheetah" and world > 1:
         N = N // world  # configs[3] is quoted as a global env count across the node
     algo_kw = dict(cfg["algo"])

@@ -216,11 +216,14 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   int w2_idx[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) w2_idx[r] = (jt * 16 + g * 4 + r) * HID + kt * 16 + li;
-  float w2_m[4], w2_v[4];
+  // grads mode carries no optimizer state (exp_avg/exp_avg_sq are null there)
+  float w2_m[4] = {0.f, 0.f, 0.f, 0.f}, w2_v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (!grads_mode) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    w2_m[r] = a.exp_avg[oW2 + w2_idx[r]];
-    w2_v[r] = a.exp_avg_sq[oW2 + w2_idx[r]];
+    for (int r = 0; r < 4; ++r) {
+      w2_m[r] = a.exp_avg[oW2 + w2_idx[r]];
+      w2_v[r] = a.exp_avg_sq[oW2 + w2_idx[r]];
+    }
   }
   // slot A: W3 (tid < OUT*64) | b3 (512..512+OUT) | b2 (576..639) | b1 (640..703)
   int a_flat = -1;
@@ -231,8 +234,8 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   // slot B: W1 (tid < 64*IN)
   const int b_flat = tid < HID * IN ? oW1 + tid : -1;
   float a_m = 0.f, a_v = 0.f, b_m = 0.f, b_v = 0.f;
-  if (a_flat >= 0) { a_m = a.exp_avg[a_flat]; a_v = a.exp_avg_sq[a_flat]; }
-  if (b_flat >= 0) { b_m = a.exp_avg[b_flat]; b_v = a.exp_avg_sq[b_flat]; }
+  if (!grads_mode && a_flat >= 0) { a_m = a.exp_avg[a_flat]; a_v = a.exp_avg_sq[a_flat]; }
+  if (!grads_mode && b_flat >= 0) { b_m = a.exp_avg[b_flat]; b_v = a.exp_avg_sq[b_flat]; }
 
   const int B = a.batch;
   const int64_t n_rows = a.n_rows;
@@ -701,6 +704,19 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
 #ifdef RAI_STAMPS
   if (tid < 32) g_stamps[net][tid] = S.stamps[tid];
 #endif
+  // grads mode has no per-minibatch exchange, so the actor must not advance the shared
+  // stat_index before the critic has read it: the critic posts a done flag, the actor waits.
+  if (grads_mode && tid == 0) {
+    if (net == 1) {
+      __hip_atomic_store(&a.xchg[4], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned long long spins = 0;
+      while (__hip_atomic_load(&a.xchg[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0ull) {
+        if (++spins > (1ull << 26)) { atomicExch(a.err, 1); break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
   if (net == 0 && tid == 0) {
     a.state->stat_index = stat0 + nmb;
     if (!grads_mode) {
@@ -733,6 +749,7 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
   if (!a.grad_out && (!a.exp_avg || !a.exp_avg_sq)) return RAI_E_NULLPTR;
   if (workspace_bytes < rai_mlp_ppo_workspace_bytes()) return RAI_E_WORKSPACE;
   if (n_rows % batch_size == 1 && !a.moments) return RAI_E_SHAPE;  // 1-row minibatch: no std
+  if (a.grad_out && (int64_t)a.mb_begin * batch_size >= n_rows) return RAI_E_SHAPE;
   a.n_rows = n_rows;
   a.batch = batch_size;
   a.xchg = reinterpret_cast<unsigned long long*>(workspace);

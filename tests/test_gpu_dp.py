@@ -30,7 +30,19 @@ def test_fused_dp_world2_matches_single_process_global_minibatches():
     procs = [ctx.Process(target=dp_worker.fused_dp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
+    res = []
+    import queue
+    import time
+
+    deadline = time.time() + 240
+    while len(res) < len(procs):  # fail fast when a rank dies instead of waiting out the timeout
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"rank exited with {dead}"
+            assert time.time() < deadline, "ranks did not report in time"
+    res.sort(key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
