@@ -115,11 +115,14 @@ def main():
     for _ in range(args.warmup):
         algo.learn_epoch(0, 1, gen, None)
     barrier()
+    algo.kernel_events = []  # HIP events around every fused epoch launch (same stream as the kernel)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         algo.learn_epoch(0, 1, gen, None)
     barrier()
     elapsed = time.perf_counter() - t0
+    epoch_ms = [e0.elapsed_time(e1) for e0, e1 in algo.kernel_events]
+    algo.kernel_events = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -127,26 +130,57 @@ def main():
     total_steps = args.steps * T * N * world
     value = total_steps / elapsed
 
-    # ---- roofline of the GAE kernel (named by the BASELINE metric), live HIP events on the
-    # stream the kernel is launched on (torch's current stream = the stream passed to rai_gae)
+    # ---- roofline of the GAE kernel (named by the BASELINE metric): each launch bracketed by its
+    # own HIP event pair on the stream it is launched on (torch's current stream = the stream passed
+    # to rai_gae), so host launch overhead between launches is not counted as kernel time
     r = gen.rollout(gamma=algo.gamma, gae_lambda=algo.gae_lambda)
     K = 1
     gae_bytes = (4 * T * N * K) * 4 + T * N + 4 * N * K + N  # r, V, adv, returns + starts + next V/starts
     adv = torch.empty_like(r.values)
     ret = torch.empty_like(r.values)
+
+    def gae():
+        compute_advantages_device(r.rewards, r.values, r.episode_starts, r.next_episode_starts, r.next_values,
+                                  algo.gamma, algo.gae_lambda, advantages_out=adv, returns_out=ret)
+
     for _ in range(10):
-        compute_advantages_device(r.rewards, r.values, r.episode_starts, r.next_episode_starts, r.next_values,
-                                  algo.gamma, algo.gae_lambda, advantages_out=adv, returns_out=ret)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    for _ in range(args.roofline_reps):
-        compute_advantages_device(r.rewards, r.values, r.episode_starts, r.next_episode_starts, r.next_values,
-                                  algo.gamma, algo.gae_lambda, advantages_out=adv, returns_out=ret)
-    ev1.record()
-    ev1.synchronize()
-    gae_us = ev0.elapsed_time(ev1) * 1e3 / args.roofline_reps
-    achieved = gae_bytes / (gae_us * 1e-6) / 1e9
-    peak = 8000.0
+        gae()
+    torch.cuda.synchronize()
+    # park the stream behind a ~20 ms spin so every (event, launch, event) triple below is queued
+    # before the GPU reaches it: the pairs then time the kernel, not the Python launch gap
+    torch.cuda._sleep(50_000_000)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.roofline_reps)]
+    for e0, e1 in evs:
+        e0.record()
+        gae()
+        e1.record()
+    torch.cuda.synchronize()
+    gae_us = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs])) * 1e3
+    workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
+    pmc = {}
+    pmc_path = ROOT / "profiles" / "r1_pmc.json"
+    if pmc_path.exists():
+        pmc = json.loads(pmc_path.read_text()).get(workload, {})
+
+    def traffic(kernel):
+        return pmc.get(kernel, {}).get("traffic_bytes_per_launch")
+
+    roof_gae = {"kernel": "gae_kernel<double>", "bound": "hbm", "achieved": round(gae_bytes / (gae_us * 1e-6) / 1e9, 1),
+                "peak": 8000.0, "unit": "GB/s", "frac": round(gae_bytes / (gae_us * 1e-6) / 1e9 / 8000.0, 4),
+                "traffic": traffic("gae_kernel<double>"), "avg_us": round(gae_us, 3), "bytes_per_launch": gae_bytes}
+    if epoch_ms:
+        # dominant kernel: one fused PPO epoch per launch = T*N samples of forward+backward at
+        # SURVEY.md 8(d)'s 52,352 FLOP/sample (CartPole MLP, torch.utils.flop_counter), f32 MFMA peak
+        flops = 52352.0 * T * N
+        ms = float(np.mean(epoch_ms))
+        tf = flops / (ms * 1e-3) / 1e12
+        roofline = {"kernel": "mlp_ppo_epoch_kernel (rai_mlp_ppo_epoch)", "bound": "mfma", "achieved": round(tf, 4),
+                    "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
+                    "traffic": traffic("mlp_ppo_epoch_kernel"), "avg_ms": round(ms, 3),
+                    "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
+    else:
+        roofline = roof_gae
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "cartpole":
@@ -175,13 +209,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded host VecEnv with the config's obs/action shapes; random-init policy)",
-            "config": {"workload": f"ppo {args.config} num_envs={N}/rank n_steps={T}",
+            "config": {"workload": workload,
                        "global_batch": algo_kw["batch_size"] * world, "n_epochs": algo_kw["n_epochs"],
                        "batch_policy": args.batch_policy, "seq_len": T, "parallelism": f"dp{world}"},
-            "roofline": {"kernel": "gae_kernel<double> (rai_gae exact mode)", "bound": "hbm",
-                         "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
-                         "avg_us": round(gae_us, 3), "bytes_per_launch": gae_bytes},
+            "roofline": roofline,
+            "roofline_gae": roof_gae,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

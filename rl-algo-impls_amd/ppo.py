@@ -74,6 +74,8 @@ class PPO:
         self.blocks = DeviceBlocks(self.device)
         self.last_update_seconds: Optional[float] = None
         self.force_generic = False  # True: always use the per-minibatch (PyTorch network) path
+        # bench/profiling hook: when a list, (start, end) HIP events bracket every fused epoch launch
+        self.kernel_events: Optional[list] = None
         self._mlp_ws: Optional[torch.Tensor] = None
         self.dp_group = None
         self.world = 1
@@ -287,6 +289,10 @@ class PPO:
             b = r.epoch_batch(shuffle=True)
             assert b.logprobs is not None, "PPO needs rollout logprobs (include_logp=True)"
             obs = b.obs if b.obs.dtype == torch.float32 else b.obs.float()
+            ev = None
+            if self.kernel_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             rc = L.rai_mlp_ppo_epoch(
                 self.flat.flat.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), obs.contiguous().data_ptr(),
                 b.actions.contiguous().data_ptr(), b.logprobs.data_ptr(), b.values.data_ptr(),
@@ -296,6 +302,9 @@ class PPO:
                 blocks.norms.data_ptr(), int(blocks.norms.shape[0]), self._mlp_ws.data_ptr(), self._mlp_ws.numel(),
                 st)
             _lib.check(rc, "rai_mlp_ppo_epoch")
+            if ev is not None:
+                ev[1].record()
+                self.kernel_events.append(ev)
             opt.step_count += nmb
         host = torch.cat([blocks.stats[:n_steps].reshape(-1), blocks.norms[:n_steps],
                           blocks.state.view(torch.float32)]).cpu().numpy()

@@ -1,4 +1,5 @@
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests/test_gpu_dp.py -q -x > gpurun_out/pytest_dp.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_dp.log; [ $rc -eq 0 ] || exit $rc
-RAI_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 1 --warmup 0 --num-envs 256 --no-cpu-baseline > gpurun_out/bench2_gloo.log 2>&1; rc=$?; tail -1 gpurun_out/bench2_gloo.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; exit $rc
+R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out && cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 $R/tools/_diag/xchg_diag > $R/gpurun_out/xchg_diag.log 2>&1; rc=$?; cat $R/gpurun_out/xchg_diag.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python $R/bench.py --steps 2 --warmup 1 > $R/gpurun_out/bench_r1b.log 2>&1; rc=$?; grep '^{' $R/gpurun_out/bench_r1b.log | cut -c1-1500; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex mlp_ppo_epoch --output-format csv -d $R/gpurun_out/pmc_fetch_mlp -o fetch -- python $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 > $R/gpurun_out/pmc_fetch_mlp.log 2>&1; rc=$?; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex mlp_ppo_epoch --output-format csv -d $R/gpurun_out/pmc_write_mlp -o write -- python $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 > $R/gpurun_out/pmc_write_mlp.log 2>&1; rc=$?; exit $rc
