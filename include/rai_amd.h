@@ -192,7 +192,8 @@ int rai_gaussian_sample(const float* mu, const float* log_std, int64_t N, int32_
  * Stats rows: [0] holds the policy+entropy part of the loss; the caller adds
  * vf_coef * v_loss ([5]).
  * ------------------------------------------------------------------------ */
-int64_t rai_mlp_ppo_workspace_bytes(void);
+/* Workspace: the inter-workgroup exchange words plus one (mean, den) pair per minibatch. */
+int64_t rai_mlp_ppo_workspace_bytes(int64_t n_rows, int32_t batch_size);
 int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
                       const int64_t* actions, const float* old_logp, const float* old_values,
                       const float* advantages, const float* returns, int64_t n_rows,

@@ -7,23 +7,28 @@
 //   forward, categorical logp/entropy, clipped-surrogate + value loss gradients,
 //   backward, clip_grad_norm_ and Adam(eps) — without leaving the chip.
 //
-// Layout: workgroup 0 owns the actor, workgroup 1 the critic (the two networks
-// share no parameters; the only coupling is the global grad norm of
-// clip_grad_norm_, exchanged once per minibatch as an 8-byte {tag,value} granule
-// with agent-scope relaxed atomics, double-buffered by minibatch parity).  Each
-// 1024-thread workgroup keeps its network's weights in LDS (W2 also transposed
-// for the backward), processes the minibatch in 128-row chunks, and runs the
-// three 64x64 contractions (forward, dW2, dH1) on v_mfma_f32_16x16x4_f32 — exact
-// fp32 (a k-ordered fmaf chain), at the CU's full fp32 rate.  Gradients of W2
-// stay in the MFMA accumulators of the wave that owns the tile, and the Adam
-// moments of every parameter live in the registers of its owning lane for the
-// whole launch; only the next minibatch's inputs are fetched from HBM
-// (prefetched into registers one minibatch ahead).
+// Why one launch: at the CartPole config an update is 40,960 *dependent* Adam steps
+// of ~13 MFLOP each; per-step launches cost more than the arithmetic.  The floor of
+// this design is the f32 MFMA work of one CU per network (3 x 64x64 contractions
+// over the minibatch rows), so everything else is arranged to stay off that path:
 //
-// LDS banking: activations/weights use a 66-float row stride with the K index
-// permuted per lane group (kmap / smap below) so the b64 A/B-operand reads of
-// the forward/dH1 products and the b32 reads of the dW2 product are
-// conflict-free.
+//  * workgroup 0 = actor, workgroup 1 = critic (no shared parameters; the only
+//    coupling is clip_grad_norm_'s global norm, exchanged once per minibatch as an
+//    8-byte {tag,value} granule — ~0.5 us one way, measured by tools/xchg_diag.hip);
+//  * weights live in LDS (W2 also transposed for the backward), Adam moments in the
+//    registers of each parameter's owning lane, W2's gradient in MFMA accumulators;
+//  * the three 64-wide contractions and layer 1 run on v_mfma_f32_16x16x4_f32
+//    (exact f32); the output layer is folded into layer 2's epilogue (two column-
+//    half partial sums, DPP row reductions);
+//  * every sum over minibatch rows (dW3, db3, db2, db1, dW1) is a per-thread partial
+//    over a row slice, reduced once per minibatch through LDS (no serial row loops);
+//  * the next minibatch's rows are prefetched into registers, already in the MFMA
+//    A-operand layout for layer 1;
+//  * advantage normalisation moments (ppo.py:313-316) are computed for all the
+//    epoch's minibatches by a small pre-kernel, off the dependent chain.
+//
+// The kernel is instantiated for padded (in_dim, n_actions) of (4, 2) — CartPole —
+// and (8, 8); padded rows/columns carry zeros.
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -65,15 +70,15 @@ struct MlpArgs {
   int32_t max_stats;
   float* norms;
   int32_t max_norms;
-  unsigned long long* xchg;  // [2 nets][2 parities], zeroed before every launch
+  unsigned long long* xchg;  // [0..3]: [2 nets][2 parities]; [4]: critic-done flag; zeroed per launch
   int32_t* err;
+  // per-minibatch (mean, den) of the advantage normalisation: moments[2*mb], moments[2*mb+1]
+  const float* moments;
   // data-parallel "grads" mode (grad_out != nullptr): process minibatches
-  // [mb_begin, mb_begin + mb_count), normalise advantages with the given global
-  // per-minibatch (mean, den) pairs, scale the loss means by 1/(rows*world), write the
+  // [mb_begin, mb_begin + mb_count), scale the loss means by 1/(rows*world), write the
   // raw gradients to grad_out and stop (the caller all-reduces them and runs
   // rai_clip_optim_step).
   float* grad_out;
-  const float* moments;
   int32_t mb_begin;
   int32_t mb_count;
   int32_t world;
@@ -83,14 +88,14 @@ struct MlpArgs {
 // Diagnostic build only (never the shipped library): per-phase cycle totals of wave 0 of
 // each workgroup, accumulated over the launch and copied out by rai_mlp_debug_stamps().
 __device__ unsigned long long g_stamps[2][32];
-#define STAMP(i)                                                        \
-  do {                                                                  \
-    if (threadIdx.x == 0) {                                             \
-      unsigned long long t_;                                            \
+#define STAMP(i)                                                                 \
+  do {                                                                           \
+    if (threadIdx.x == 0) {                                                      \
+      unsigned long long t_;                                                     \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-      S.stamps[i] += t_ - S.t_last;                                     \
-      S.t_last = t_;                                                    \
-    }                                                                   \
+      S.stamps[i] += t_ - S.t_last;                                              \
+      S.t_last = t_;                                                             \
+    }                                                                            \
   } while (0)
 #else
 #define STAMP(i) \
@@ -98,26 +103,40 @@ __device__ unsigned long long g_stamps[2][32];
   } while (0)
 #endif
 
+// Re-derive the lane coordinates inside each phase from an opaque copy of threadIdx.x (and of
+// the wave index) so the compiler recomputes per-phase LDS addresses where they are used
+// instead of hoisting them all out of the minibatch loop (which overflows 128 VGPRs).
+#define RELANE()                                                                     \
+  int tid_l_ = threadIdx.x;                                                          \
+  asm volatile("" : "+v"(tid_l_));                                                   \
+  int w_l_ = w;                                                                      \
+  asm volatile("" : "+s"(w_l_));                                                     \
+  const int tid = tid_l_, lane = tid & 63, g = lane >> 4, li = lane & 15, w = w_l_;  \
+  (void)tid; (void)lane; (void)g; (void)li; (void)w
+
+template <int INP, int OUTP>
 struct Smem {
 #ifdef RAI_STAMPS
   unsigned long long stamps[32];
   unsigned long long t_last;
 #endif
-  float W1[HID][MAXIN];
+  double red[NW];
+  double pw[2];
+  double st[16];  // loss statistics: [4 row waves][4]
+  float bcast[8];
+  float W1[HID][INP];  // [out j][in k]
   float b1[HID];
+  float b2[HID];
+  float b3[MAXOUT];
   float W2[HID][LD];   // [out j][in k]
   float W2T[HID][LD];  // [in k][out j]
-  float b2[HID];
-  float W3[MAXOUT][LD];
-  float b3[MAXOUT];
-  float X[CH][MAXIN];
-  float H1[CH][LD];    // act(z1), later dZ1
-  float H2[CH][LD];    // act(z2), later dZ2
-  float out[CH][MAXOUT];
-  float dout[CH][MAXOUT];
-  double red[8 * NW];
-  double pw[2];
-  float bcast[8];
+  float W3[OUTP][LD];  // [out o][in k]
+  float X[CH][INP];
+  float H1[CH][LD];    // act(z1), later dZ1, at minibatch end: partial-gradient scratch
+  float H2[CH][LD];    // act(z2), later dZ2, at minibatch end: partial-gradient scratch
+  float outp[2][CH][OUTP];  // output-layer partial sums of the two column halves of H2
+  float dout[CH][OUTP];
+  float db3p[4][OUTP];
 };
 
 __device__ __forceinline__ int kmap(int g, int kk) { return (g & 1) * 32 + (g >> 1) * 16 + kk; }
@@ -137,24 +156,17 @@ __device__ __forceinline__ float vf_grad(int fn, float x) {
   return x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x);
 }
 
-template <int NV>
-__device__ __forceinline__ void bsum(double (&v)[NV], double* red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
-  lds_barrier();
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) red[i * NW + w] = v[i];
-  }
-  lds_barrier();
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    double t = 0.0;
-    for (int j = 0; j < NW; ++j) t += red[i * NW + j];
-    v[i] = t;
-  }
-  lds_barrier();
+// Sum over the 16 lanes of a DPP row; every lane of the row receives the same bits.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return v;
 }
 
 __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float g, float w1, float w2,
@@ -166,19 +178,46 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
   p = p + neg_step * (m / denom);
 }
 
-__global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
-  __shared__ Smem S;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  const int net = blockIdx.x;  // 0 actor, 1 critic
+// Advantage-normalisation moments of every minibatch (one workgroup per minibatch), in the
+// operation order of the loss kernel: fp64 sums, mean rounded to f32, unbiased std
+// (ppo.py:313-316: (A - A.mean()) / (A.std() + 1e-8); standardize: A / (A.std() + 1e-8)).
+__global__ __launch_bounds__(256) void adv_moments_kernel(const float* __restrict__ adv, int64_t n_rows, int B,
+                                                          const rai_ppo_hparams* hp, float* moments) {
+  __shared__ double scratch[4];
+  const int mb = blockIdx.x;
+  const int64_t row0 = (int64_t)mb * B;
+  const int rows = (int)min((int64_t)B, n_rows - row0);
+  const int tid = threadIdx.x;
+  const float x = tid < rows ? adv[row0 + tid] : 0.f;
+  double v1[1] = {tid < rows ? (double)x : 0.0};
+  block_sum<1>(v1, scratch);
+  const float mean = (float)(v1[0] / (double)rows);
+  const double d = tid < rows ? (double)x - (double)mean : 0.0;
+  double v2[1] = {d * d};
+  block_sum<1>(v2, scratch);
+  if (tid == 0) {
+    const float den = (float)sqrt(v2[0] / (double)(rows - 1)) + 1e-8f;
+    float m0 = 0.f, m1 = 1.f;
+    if (hp->normalize_advantage) { m0 = mean; m1 = den; }
+    else if (hp->standardize_advantage) { m1 = den; }
+    moments[2 * mb] = m0;
+    moments[2 * mb + 1] = m1;
+  }
+}
+
+// One network (ACTOR: the policy head; else the value head) of the fused epoch.
+template <int INP, int OUTP, bool ACTOR>
+__device__ __forceinline__ void mlp_net(const MlpArgs& a, Smem<INP, OUTP>& S) {
+  constexpr int net = ACTOR ? 0 : 1;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int IN = a.in_dim;
   const int NA = a.n_act;
-  const int OUT = net == 0 ? NA : 1;
+  const int OUT = ACTOR ? NA : 1;
   const int relu = a.act_fn;
-  // only the hyperparameters this path uses (kept uniform / scalar)
   const float clip_range = a.hp->clip_range, ent_coef = a.hp->ent_coef, vf_coef0 = a.hp->vf_coef[0];
   const float clip_range_vf = a.hp->clip_range_vf;
   const int has_vclip = a.hp->has_clip_range_vf, vf_fn = a.hp->vf_loss_fn;
-  const int norm_adv = a.hp->normalize_advantage, std_adv = a.hp->standardize_advantage;
   const float halve = a.hp->ppo2_vf_coef_halving ? 0.5f : 1.f;
   const float beta2 = a.ohp->beta2, adam_eps = a.ohp->eps, lr = a.ohp->lr;
   const double beta1_d = a.ohp->beta1_d, beta2_d = a.ohp->beta2_d;
@@ -191,13 +230,13 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   const int oW1 = base, ob1 = oW1 + HID * IN, oW2 = ob1 + HID, ob2 = oW2 + HID * HID, oW3 = ob2 + HID,
             ob3 = oW3 + OUT * HID;
 
-  for (int e = tid; e < HID * MAXIN; e += NT) {
-    const int j = e / MAXIN, k = e % MAXIN;
+  for (int e = tid; e < HID * INP; e += NT) {
+    const int j = e / INP, k = e % INP;
     S.W1[j][k] = k < IN ? a.params[oW1 + j * IN + k] : 0.f;
   }
-  for (int e = tid; e < HID; e += NT) {
-    S.b1[e] = a.params[ob1 + e];
-    S.b2[e] = a.params[ob2 + e];
+  if (tid < HID) {
+    S.b1[tid] = a.params[ob1 + tid];
+    S.b2[tid] = a.params[ob2 + tid];
   }
   for (int e = tid; e < HID * HID; e += NT) {
     const int j = e >> 6, k = e & 63;
@@ -205,7 +244,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
     S.W2[j][k] = x;
     S.W2T[k][j] = x;
   }
-  for (int e = tid; e < MAXOUT * HID; e += NT) {
+  for (int e = tid; e < OUTP * HID; e += NT) {
     const int o = e >> 6, k = e & 63;
     S.W3[o][k] = o < OUT ? a.params[oW3 + o * HID + k] : 0.f;
   }
@@ -250,26 +289,39 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   const float pi_coef = latched ? 0.f : 1.f;
 
   // ---- per-minibatch inputs, prefetched into registers one minibatch ahead ------------------
-  // thread t < B: row t's (action, old logp, old value, adv, return); X elements t and t+NT
-  int64_t r_act = 0;
-  float r_olp = 0.f, r_ov = 0.f, r_adv = 0.f, r_ret = 0.f, r_x0 = 0.f, r_x1 = 0.f;
+  // thread t < rows: row t's (action, old logp, adv | old value, return);
+  // px[c][q]: X[c*CH + (w>>1)*16 + li][4q + g] = the layer-1 MFMA A operand of chunk c
+  constexpr int NQ = INP / 4;
+  int r_act = 0;
+  float r_a = 0.f, r_b = 0.f, r_c = 0.f, r_d = 1.f;
+  float px[2][NQ];
   auto prefetch = [&](int mb) {
     const int64_t row0 = (int64_t)mb * B;
     const int rows = (int)min((int64_t)B, n_rows - row0);
     if (tid < rows) {
       const int64_t r = row0 + tid;
-      if (net == 0) {
-        r_act = a.actions[r];
-        r_olp = a.old_logp[r];
-        r_adv = a.adv[r];
+      if (ACTOR) {
+        r_act = (int)a.actions[r];
+        r_a = a.old_logp[r];
+        r_b = a.adv[r];
       } else {
-        r_ov = a.old_values[r];
-        r_ret = a.ret[r];
+        r_a = a.old_values[r];
+        r_b = a.ret[r];
       }
     }
-    const int nx = rows * IN;
-    r_x0 = tid < nx ? a.obs[row0 * IN + tid] : 0.f;
-    r_x1 = tid + NT < nx ? a.obs[row0 * IN + tid + NT] : 0.f;
+    if (ACTOR) {
+      r_c = a.moments[2 * mb];
+      r_d = a.moments[2 * mb + 1];
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int s = c * CH + (w >> 1) * 16 + li;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int k = 4 * q + g;
+        px[c][q] = (s < rows && k < IN) ? a.obs[(row0 + s) * IN + k] : 0.f;
+      }
+    }
   };
   prefetch(mb_begin);
   if (tid == 0) {  // running powers beta^step (bias corrections), advanced once per minibatch
@@ -286,135 +338,133 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
     const int64_t row0 = (int64_t)mb * B;
     const int rows = (int)min((int64_t)B, n_rows - row0);
     // take this minibatch's inputs out of the prefetch registers
-    const int64_t c_act = r_act;
-    const float c_olp = r_olp, c_ov = r_ov, c_adv = r_adv, c_ret = r_ret, c_x0 = r_x0, c_x1 = r_x1;
+    const int c_act = r_act;
+    const float c_a = r_a, c_b = r_b;
+    float cx[2][NQ];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) cx[c][q] = px[c][q];
+    const float amean = r_c, aden = r_d;
     if (mb + 1 < mb_end) prefetch(mb + 1);
-
-    // advantage normalisation moments over the minibatch (ppo.py:313-316), actor only
-    float amean = 0.f, aden = 1.f;
-    if (net == 0 && a.moments) {
-      amean = a.moments[2 * mb];
-      aden = a.moments[2 * mb + 1];
-    } else if (net == 0 && (norm_adv || std_adv)) {
-      double v1[1] = {tid < rows ? (double)c_adv : 0.0};
-      bsum<1>(v1, S.red);
-      const float mean = (float)(v1[0] / (double)rows);
-      const double d = tid < rows ? (double)c_adv - (double)mean : 0.0;
-      double v2[1] = {d * d};
-      bsum<1>(v2, S.red);
-      const float den = (float)sqrt(v2[0] / (double)(rows - 1)) + 1e-8f;
-      if (norm_adv) { amean = mean; aden = den; }
-      else { aden = den; }
-    }
     const float invB = 1.f / (float)(rows * a.world);
 
-    f4 gw2 = {0.f, 0.f, 0.f, 0.f};
-    float ga = 0.f, gb = 0.f;
+    // per-thread partial gradients over this minibatch's rows
+    f4 gw2 = {0.f, 0.f, 0.f, 0.f};   // dW2 tile (MFMA accumulator)
+    float p_w3[OUTP], p_b2 = 0.f;    // B1 layout: column k = lane, rows w + 16 i
+    float p_b1[2] = {0.f, 0.f};      // B3 layout: columns k0, k0 + 16, rows of tile (w>>1)
+    float p_w1 = 0.f;                // B4 layout: (j = lane, k, row slice)
+    float my_dout[OUTP];             // this thread's row (L layout), for db3
     float st[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int o = 0; o < OUTP; ++o) { p_w3[o] = 0.f; my_dout[o] = 0.f; }
 
-    for (int c = 0; c * CH < rows; ++c) {
-      // Re-derive the (tid & 63) coordinates from a laundered tid every chunk so per-(tid & 63) LDS
-      // addresses are computed where they are used instead of being hoisted out of the
-      // loops and kept alive (that hoisting alone overflowed the 128-VGPR budget).
-      int tid = threadIdx.x;
+    const int nch = (rows + CH - 1) / CH;
+    for (int c = 0; c < nch; ++c) {
       const int crows = min(CH, rows - c * CH);
-      asm volatile("" : "+v"(tid));
-      // P0: minibatch X elements of this chunk -> LDS
-      for (int e = tid; e < CH * MAXIN; e += NT) S.X[e / MAXIN][e % MAXIN] = 0.f;
-      lds_barrier();
-      STAMP(1);
+      // ---- F1: layer 1 on MFMA (K = in_dim padded to 4/8), act -> H1; X -> LDS for dW1 ----------
       {
-        const int e0 = tid, e1 = tid + NT;
-        const int s0 = e0 / IN - c * CH, s1 = e1 / IN - c * CH;
-        if (s0 >= 0 && s0 < crows) S.X[s0][e0 % IN] = c_x0;
-        if (s1 >= 0 && s1 < crows) S.X[s1][e1 % IN] = c_x1;
-      }
-      lds_barrier();
-      STAMP(2);
-      asm volatile("" : "+v"(tid));
-      // P1: layer 1 (VALU; K = in_dim <= 8)
-      {
-        const int j = tid & 63;
-        float wv[MAXIN];
+        RELANE();
+        const int mt = w >> 1, ntb = (w & 1) * 2;
+        f4 z0 = {0.f, 0.f, 0.f, 0.f}, z1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < MAXIN; ++k) wv[k] = S.W1[j][k];
-        const float bj = S.b1[j];
+        for (int q = 0; q < NQ; ++q) {
+          const float av = c == 0 ? cx[0][q] : cx[1][q];
+          const float b0 = S.W1[ntb * 16 + li][4 * q + g];
+          const float b1 = S.W1[(ntb + 1) * 16 + li][4 * q + g];
+          z0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, z0, 0, 0, 0);
+          z1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, z1, 0, 0, 0);
+          if ((w & 1) == 0) S.X[mt * 16 + li][4 * q + g] = av;
+        }
+        const int j0 = ntb * 16 + li;
+        const float bb0 = S.b1[j0], bb1 = S.b1[j0 + 16];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int s = (tid >> 6) * 8 + i;
-          float z = 0.f;
-#pragma unroll
-          for (int k = 0; k < MAXIN; ++k) z = fmaf(S.X[s][k], wv[k], z);
-          S.H1[s][j] = act_f(relu, z + bj);
+        for (int r = 0; r < 4; ++r) {
+          const int s = mt * 16 + g * 4 + r;
+          S.H1[s][j0] = act_f(relu, z0[r] + bb0);
+          S.H1[s][j0 + 16] = act_f(relu, z1[r] + bb1);
         }
       }
       lds_barrier();
-      STAMP(3);
-      asm volatile("" : "+v"(tid));
-      // P2: layer 2 forward on MFMA: Z2[s][j] = sum_k H1[s][k] W2[j][k]
+      STAMP(1);
+      // ---- F2: layer 2 on MFMA, act -> H2; output layer folded into the epilogue -----------------
       {
-        const int mt = (tid >> 6) >> 1, nt0 = ((tid >> 6) & 1) * 2;
+        RELANE();
+        const int mt = w >> 1, nt0 = (w & 1) * 2;
         f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < 16; kk += 2) {
-          const int kq = kmap(((tid >> 4) & 3), kk);
-          const f2 av = *reinterpret_cast<const f2*>(&S.H1[mt * 16 + (tid & 15)][kq]);
-          const f2 b0 = *reinterpret_cast<const f2*>(&S.W2[nt0 * 16 + (tid & 15)][kq]);
-          const f2 b1 = *reinterpret_cast<const f2*>(&S.W2[(nt0 + 1) * 16 + (tid & 15)][kq]);
+          const int kq = kmap(g, kk);
+          const f2 av = *reinterpret_cast<const f2*>(&S.H1[mt * 16 + li][kq]);
+          const f2 b0 = *reinterpret_cast<const f2*>(&S.W2[nt0 * 16 + li][kq]);
+          const f2 b1 = *reinterpret_cast<const f2*>(&S.W2[(nt0 + 1) * 16 + li][kq]);
           acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b0.x, acc0, 0, 0, 0);
           acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b1.x, acc1, 0, 0, 0);
           acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b0.y, acc0, 0, 0, 0);
           acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b1.y, acc1, 0, 0, 0);
         }
-        const int j0 = nt0 * 16 + (tid & 15);
+        const int j0 = nt0 * 16 + li;
         const float bb0 = S.b2[j0], bb1 = S.b2[j0 + 16];
+        float w3a[OUTP], w3b[OUTP];
+#pragma unroll
+        for (int o = 0; o < OUTP; ++o) {
+          w3a[o] = S.W3[o][j0];
+          w3b[o] = S.W3[o][j0 + 16];
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int s = mt * 16 + ((tid >> 4) & 3) * 4 + r;
-          S.H2[s][j0] = act_f(relu, acc0[r] + bb0);
-          S.H2[s][j0 + 16] = act_f(relu, acc1[r] + bb1);
-        }
-      }
-      lds_barrier();
-      STAMP(4);
-      asm volatile("" : "+v"(tid));
-      // P3: output layer (VALU)
-      {
-        const int s = tid >> 3, o = tid & 7;
-        if (o < OUT) {
-          float z = 0.f;
-          for (int k = 0; k < HID; k += 2) {
-            const f2 h = *reinterpret_cast<const f2*>(&S.H2[s][k]);
-            z = fmaf(h.x, S.W3[o][k], z);
-            z = fmaf(h.y, S.W3[o][k + 1], z);
+          const int s = mt * 16 + g * 4 + r;
+          const float h0 = act_f(relu, acc0[r] + bb0);
+          const float h1 = act_f(relu, acc1[r] + bb1);
+          S.H2[s][j0] = h0;
+          S.H2[s][j0 + 16] = h1;
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o) {
+            const float part = row_sum16(fmaf(h1, w3b[o], h0 * w3a[o]));
+            if (li == ((r * OUTP + o) & 15)) S.outp[w & 1][s][o] = part;
           }
-          S.out[s][o] = z + S.b3[o];
         }
       }
       lds_barrier();
-      STAMP(5);
-      asm volatile("" : "+v"(tid));
-      // P4: per-sample loss gradient (tid >> 6).r.t. the head outputs (ppo.py:307-361 semantics;
-      //     autograd tie rules of min/max and closed-interval clamp, as loss.hip)
+      STAMP(2);
+      // ---- L: per-row loss gradient w.r.t. the head outputs (ppo.py:326-371 semantics; autograd
+      //      tie rules of min/max and closed-interval clamp, as loss.hip) ---------------------------
       {
+        RELANE();
         const int s = tid - c * CH;
         if (s >= 0 && s < CH) {
+          float d[OUTP];
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o) d[o] = 0.f;
           if (s < crows) {
-            if (net == 0) {
+            float z[OUTP];
+#pragma unroll
+            for (int o = 0; o < OUTP; ++o) z[o] = (S.outp[0][s][o] + S.outp[1][s][o]) + S.b3[o];
+            if (ACTOR) {
               float m = F32_MIN;
-              for (int o = 0; o < NA; ++o) m = fmaxf(m, S.out[s][o]);
+#pragma unroll
+              for (int o = 0; o < OUTP; ++o)
+                if (o < NA) m = fmaxf(m, z[o]);
               float se = 0.f;
-              for (int o = 0; o < NA; ++o) se += expf(S.out[s][o] - m);
+#pragma unroll
+              for (int o = 0; o < OUTP; ++o)
+                if (o < NA) se += expf(z[o] - m);
               const float lse = m + logf(se);
               float H = 0.f;
-              for (int o = 0; o < NA; ++o) {
-                const float n = S.out[s][o] - lse;
-                H -= fmaxf(n, F32_MIN) * expf(n);
-              }
-              const int act = min(max((int)c_act, 0), NA - 1);
-              const float logp = S.out[s][act] - lse;
-              const float A = (c_adv - amean) / aden;
-              const float logratio = logp - c_olp;
+#pragma unroll
+              for (int o = 0; o < OUTP; ++o)
+                if (o < NA) {
+                  const float n = z[o] - lse;
+                  H -= fmaxf(n, F32_MIN) * expf(n);
+                }
+              const int act = min(max(c_act, 0), NA - 1);
+              float zact = z[0];
+#pragma unroll
+              for (int o = 1; o < OUTP; ++o)
+                if (o == act) zact = z[o];
+              const float logp = zact - lse;
+              const float A = (c_b - amean) / aden;
+              const float logratio = logp - c_a;
               const float ratio = expf(logratio);
               const float lo = 1.f - clip_range, hi = 1.f + clip_range;
               const float cr = fminf(fmaxf(ratio, lo), hi);
@@ -427,27 +477,25 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
               const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
               const float dlogp = (g1 * A + (g2 * A) * in_clip) * ratio;
               const float dent = -ent_coef * invB;
-              for (int o = 0; o < MAXOUT; ++o) {
-                float d = 0.f;
+#pragma unroll
+              for (int o = 0; o < OUTP; ++o)
                 if (o < NA) {
-                  const float n = S.out[s][o] - lse;
+                  const float n = z[o] - lse;
                   const float p = expf(n);
-                  d = dlogp * ((o == act ? 1.f : 0.f) - p) + dent * (-p * (n + H));
+                  d[o] = dlogp * ((o == act ? 1.f : 0.f) - p) + dent * (-p * (n + H));
                 }
-                S.dout[s][o] = d;
-              }
               st[0] += fminf(s1, s2);
               st[1] += (ratio - 1.f) - logratio;
               st[2] += (fabsf(ratio - 1.f) > clip_range) ? 1.f : 0.f;
               st[3] += H;
             } else {
-              const float v = S.out[s][0], R = c_ret;
+              const float v = z[0], R = c_b;
               const float gl = (vf_coef0 * halve) * invB;
               float l = vf_loss(vf_fn, v - R), dv;
               if (has_vclip) {
                 const float vc_ = clip_range_vf;
-                const float dvo = v - c_ov;
-                const float vcl = c_ov + fminf(fmaxf(dvo, -vc_), vc_);
+                const float dvo = v - c_a;
+                const float vcl = c_a + fminf(fmaxf(dvo, -vc_), vc_);
                 const float l2 = vf_loss(vf_fn, vcl - R);
                 float w1, w2;
                 if (l > l2) { w1 = gl; w2 = 0.f; }
@@ -455,188 +503,251 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
                 else { w1 = gl * 0.5f; w2 = gl * 0.5f; }
                 const float inv = (dvo >= -vc_ && dvo <= vc_) ? 1.f : 0.f;
                 dv = w1 * vf_grad(vf_fn, v - R) + (w2 * vf_grad(vf_fn, vcl - R)) * inv;
-                st[1] += (fabsf(v - c_ov) > vc_) ? 1.f : 0.f;
+                st[1] += (fabsf(v - c_a) > vc_) ? 1.f : 0.f;
                 l = fmaxf(l, l2);
               } else {
                 dv = gl * vf_grad(vf_fn, v - R);
               }
               st[0] += l;
-              for (int o = 0; o < MAXOUT; ++o) S.dout[s][o] = o == 0 ? dv : 0.f;
+              d[0] = dv;
             }
-          } else {
-            for (int o = 0; o < MAXOUT; ++o) S.dout[s][o] = 0.f;
+          }
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o) {
+            S.dout[s][o] = d[o];
+            my_dout[o] = d[o];
           }
         }
       }
       lds_barrier();
-      STAMP(6);
-      asm volatile("" : "+v"(tid));
-      // P5: output-layer weight/bias grads (slot A owners)
-      if (tid < OUT * HID) {
-        const int o = tid >> 6, k = tid & 63;
-        float acc = 0.f;
-        for (int s = 0; s < CH; ++s) acc = fmaf(S.dout[s][o], S.H2[s][k], acc);
-        ga += acc;
-      } else if (tid >= 512 && tid < 512 + OUT) {
-        const int o = tid - 512;
-        float acc = 0.f;
-        for (int s = 0; s < CH; ++s) acc += S.dout[s][o];
-        ga += acc;
-      }
-      lds_barrier();
-      STAMP(7);
-      asm volatile("" : "+v"(tid));
-      // P6: dZ2 = (dout . W3) * act'(H2), in place over H2
+      STAMP(3);
+      // ---- B1: dZ2 = (dout . W3) * act'(H2) in place over H2; dW3, db2 partials (column k) ------
       {
-        const int k = tid & 63;
-        float w3[MAXOUT];
+        RELANE();
+        const int k = lane;
+        float w3[OUTP];
 #pragma unroll
-        for (int o = 0; o < MAXOUT; ++o) w3[o] = S.W3[o][k];
+        for (int o = 0; o < OUTP; ++o) w3[o] = S.W3[o][k];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int s = (tid >> 6) + 16 * i;
+        for (int i = 0; i < CH / NW; ++i) {
+          const int s = w + NW * i;
+          const float h = S.H2[s][k];
           float dh = 0.f;
 #pragma unroll
-          for (int o = 0; o < MAXOUT; ++o) dh = fmaf(S.dout[s][o], w3[o], dh);
-          S.H2[s][k] = dh * act_d(relu, S.H2[s][k]);
+          for (int o = 0; o < OUTP; ++o) {
+            const float dv = S.dout[s][o];
+            dh = fmaf(dv, w3[o], dh);
+            p_w3[o] = fmaf(dv, h, p_w3[o]);
+          }
+          const float dz = dh * act_d(relu, h);
+          p_b2 += dz;
+          S.H2[s][k] = dz;
         }
       }
       lds_barrier();
-      STAMP(8);
-      asm volatile("" : "+v"(tid));
-      // P7: dW2 += dZ2^T H1 (accumulators persist over chunks), dH1 = dZ2 W2 (held), db2
+      STAMP(4);
+      // ---- B2: dW2 += dZ2^T H1 (accumulators persist over chunks), dH1 = dZ2 W2 (held) ---------
       f4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = {0.f, 0.f, 0.f, 0.f};
       {
+        RELANE();
 #pragma unroll 8
         for (int kk = 0; kk < 32; ++kk) {
-          const int s = smap(((tid >> 4) & 3), kk);
-          gw2 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.H2[s][(tid >> 8) * 16 + (tid & 15)], S.H1[s][((tid >> 6) & 3) * 16 + (tid & 15)], gw2, 0, 0, 0);
+          const int s = smap(g, kk);
+          const int jt = w >> 2, kt = w & 3;
+          gw2 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.H2[s][jt * 16 + li], S.H1[s][kt * 16 + li], gw2, 0, 0, 0);
         }
-        const int mt = (tid >> 6) >> 1, nt0 = ((tid >> 6) & 1) * 2;
+        const int mt = w >> 1, nt0 = (w & 1) * 2;
 #pragma unroll
         for (int kk = 0; kk < 16; kk += 2) {
-          const int kq = kmap(((tid >> 4) & 3), kk);
-          const f2 av = *reinterpret_cast<const f2*>(&S.H2[mt * 16 + (tid & 15)][kq]);
-          const f2 b0 = *reinterpret_cast<const f2*>(&S.W2T[nt0 * 16 + (tid & 15)][kq]);
-          const f2 b1 = *reinterpret_cast<const f2*>(&S.W2T[(nt0 + 1) * 16 + (tid & 15)][kq]);
+          const int kq = kmap(g, kk);
+          const f2 av = *reinterpret_cast<const f2*>(&S.H2[mt * 16 + li][kq]);
+          const f2 b0 = *reinterpret_cast<const f2*>(&S.W2T[nt0 * 16 + li][kq]);
+          const f2 b1 = *reinterpret_cast<const f2*>(&S.W2T[(nt0 + 1) * 16 + li][kq]);
           h0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b0.x, h0, 0, 0, 0);
           h1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b1.x, h1, 0, 0, 0);
           h0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b0.y, h0, 0, 0, 0);
           h1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b1.y, h1, 0, 0, 0);
         }
-        if (tid >= 576 && tid < 640) {
-          const int j = tid - 576;
-          float acc = 0.f;
-          for (int s = 0; s < CH; ++s) acc += S.H2[s][j];
-          ga += acc;
-        }
       }
       lds_barrier();
-      STAMP(9);
-      asm volatile("" : "+v"(tid));
-      // P8: dZ1 = dH1 * act'(H1), in place over H1
+      STAMP(5);
+      // ---- B3: dZ1 = dH1 * act'(H1) in place over H1; db1 partials -------------------------------
       {
-        const int mt = (tid >> 6) >> 1, k0 = ((tid >> 6) & 1) * 32 + (tid & 15);
+        RELANE();
+        const int mt = w >> 1, k0 = (w & 1) * 32 + li;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int s = mt * 16 + ((tid >> 4) & 3) * 4 + r;
-          S.H1[s][k0] = h0[r] * act_d(relu, S.H1[s][k0]);
-          S.H1[s][k0 + 16] = h1[r] * act_d(relu, S.H1[s][k0 + 16]);
+          const int s = mt * 16 + g * 4 + r;
+          const float da = h0[r] * act_d(relu, S.H1[s][k0]);
+          const float db = h1[r] * act_d(relu, S.H1[s][k0 + 16]);
+          S.H1[s][k0] = da;
+          S.H1[s][k0 + 16] = db;
+          p_b1[0] += da;
+          p_b1[1] += db;
         }
       }
       lds_barrier();
-      STAMP(10);
-      asm volatile("" : "+v"(tid));
-      // P9: layer-1 weight (slot B) and bias (slot A) grads
-      if (tid < HID * IN) {
-        const int j = tid / IN, k = tid % IN;
+      STAMP(6);
+      // ---- B4: dW1 partial over a row slice (j = lane, k = w % INP, slice = w / INP) -------------
+      {
+        RELANE();
+        constexpr int NSL = NW / INP, RS = CH / NSL;
+        const int k = w % INP, sl = w / INP;
         float acc = 0.f;
-        for (int s = 0; s < CH; ++s) acc = fmaf(S.H1[s][j], S.X[s][k], acc);
-        gb += acc;
-      }
-      if (tid >= 640 && tid < 704) {
-        const int j = tid - 640;
-        float acc = 0.f;
-        for (int s = 0; s < CH; ++s) acc += S.H1[s][j];
-        ga += acc;
+#pragma unroll 8
+        for (int i = 0; i < RS; ++i) {
+          const int s = sl * RS + i;
+          acc = fmaf(S.H1[s][lane], S.X[s][k], acc);
+        }
+        p_w1 += acc;
       }
       lds_barrier();
-      STAMP(11);
+      STAMP(7);
     }
 
-    // ---- global grad norm (both networks), clip coefficient ---------------------------------
-    double red[5];
+    // ---- E1: per-thread partials -> LDS (H1/H2 are free now) -------------------------------------
+    float* R3 = &S.H2[0][0];           // [NW][OUTP][64]
+    float* Rb2 = &S.H1[0][0];          // [NW][64]
+    float* Rb1 = Rb2 + NW * HID;       // [8 row tiles][64]
+    float* RW1 = Rb1 + 8 * HID;        // [NW / INP slices][INP][64]
     {
-      double ss = (double)gw2.x * gw2.x + (double)gw2.y * gw2.y + (double)gw2.z * gw2.z +
-                  (double)gw2.w * gw2.w;
+      RELANE();
+#pragma unroll
+      for (int o = 0; o < OUTP; ++o) R3[(w * OUTP + o) * HID + lane] = p_w3[o];
+      Rb2[w * HID + lane] = p_b2;
+      float b1a = p_b1[0] + __shfl_xor(p_b1[0], 16, 64);
+      float b1b = p_b1[1] + __shfl_xor(p_b1[1], 16, 64);
+      b1a += __shfl_xor(b1a, 32, 64);
+      b1b += __shfl_xor(b1b, 32, 64);
+      if (g == 0) {
+        const int mt = w >> 1, k0 = (w & 1) * 32 + li;
+        Rb1[mt * HID + k0] = b1a;
+        Rb1[mt * HID + k0 + 16] = b1b;
+      }
+      RW1[((w / INP) * INP + (w % INP)) * HID + lane] = p_w1;
+      if (w < 4) {  // rows live in threads 0..255: db3 and the loss statistics
+#pragma unroll
+        for (int o = 0; o < OUTP; ++o) {
+          const float t = wave_sum(my_dout[o]);
+          if (lane == 0) S.db3p[w][o] = t;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double t = wave_sum((double)st[i]);
+          if (lane == 0) S.st[w * 4 + i] = t;
+        }
+      }
+    }
+    lds_barrier();
+    STAMP(8);
+    // ---- E2: owners sum partials in fixed order; squared norm of this network's gradient ----------
+    float ga = 0.f, gb = 0.f;
+    {
+      RELANE();
+      if (tid < OUT * HID) {
+        const int o = tid >> 6, k = tid & 63;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) t += R3[(q * OUTP + o) * HID + k];
+        ga = t;
+      } else if (tid >= 512 && tid < 512 + OUT) {
+        const int o = tid - 512;
+        ga = ((S.db3p[0][o] + S.db3p[1][o]) + S.db3p[2][o]) + S.db3p[3][o];
+      } else if (tid >= 576 && tid < 640) {
+        const int j = tid - 576;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) t += Rb2[q * HID + j];
+        ga = t;
+      } else if (tid >= 640 && tid < 704) {
+        const int j = tid - 640;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t += Rb1[q * HID + j];
+        ga = t;
+      }
+      if (b_flat >= 0) {
+        const int j = tid / IN, k = tid % IN;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW / INP; ++q) t += RW1[(q * INP + k) * HID + j];
+        gb = t;
+      }
+      double ss = (double)gw2.x * gw2.x + (double)gw2.y * gw2.y + (double)gw2.z * gw2.z + (double)gw2.w * gw2.w;
       if (a_flat >= 0) ss += (double)ga * ga;
       if (b_flat >= 0) ss += (double)gb * gb;
-      red[0] = ss; red[1] = (double)st[0]; red[2] = (double)st[1]; red[3] = (double)st[2]; red[4] = (double)st[3];
-    }
-    bsum<5>(red, S.red);
-    if (grads_mode) {
-      // raw gradients out (same flat indices as the parameters), stats row, next minibatch
+      ss = wave_sum(ss);
+      if (lane == 0) S.red[w] = ss;
+      if (grads_mode) {
+        // raw gradients out (same flat indices as the parameters)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a.grad_out[oW2 + w2_idx[r]] = gw2[r];
-      if (a_flat >= 0) a.grad_out[a_flat] = ga;
-      if (b_flat >= 0) a.grad_out[b_flat] = gb;
+        for (int r = 0; r < 4; ++r) a.grad_out[oW2 + w2_idx[r]] = gw2[r];
+        if (a_flat >= 0) a.grad_out[a_flat] = ga;
+        if (b_flat >= 0) a.grad_out[b_flat] = gb;
+      }
     }
+    lds_barrier();
+    STAMP(9);
+    // ---- E3: stats row, grad-norm exchange with the other network, bias corrections ---------------
     if (tid == 0) {
+      double ssum = 0.0;
+      for (int q = 0; q < NW; ++q) ssum += S.red[q];
+      const double* stp = S.st;
+      double sv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sv[i] = ((stp[0 * 4 + i] + stp[1 * 4 + i]) + stp[2 * 4 + i]) + stp[3 * 4 + i];
       const int srow = stat0 + (mb - mb_begin);
       if (a.stats && srow < a.max_stats) {
         float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
         const double Bd = (double)rows * (double)a.world;
-        if (net == 0) {
-          const float pi_loss = (float)(-red[1] / Bd);
-          const float ent_loss = (float)(-red[4] / Bd);
+        if (ACTOR) {
+          const float pi_loss = (float)(-sv[0] / Bd);
+          const float ent_loss = (float)(-sv[3] / Bd);
           row[0] = pi_coef * pi_loss + ent_coef * ent_loss;  // host adds the value term
           row[1] = pi_loss;
           row[2] = ent_loss;
-          row[3] = (float)(red[2] / Bd);
-          row[4] = (float)(red[3] / Bd);
+          row[3] = (float)(sv[1] / Bd);
+          row[4] = (float)(sv[2] / Bd);
         } else {
-          row[5] = (float)(red[1] / Bd) * halve;
-          row[5 + RAI_MAX_K] = has_vclip ? (float)(red[2] / Bd) : 0.f;
+          row[5] = (float)(sv[0] / Bd) * halve;
+          row[5 + RAI_MAX_K] = has_vclip ? (float)(sv[1] / Bd) : 0.f;
         }
       }
-    }
-    if (grads_mode) {
-      lds_barrier();
-      continue;
-    }
-    if (tid == 0) {
-      const float mine = (float)red[0];
-      const unsigned tag = (unsigned)(mb + 1);
-      const int par = mb & 1;
-      const unsigned long long gr = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(mine);
-      __hip_atomic_store(&a.xchg[net * 2 + par], gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      float other = 0.f;
-      unsigned long long spins = 0;
-      for (;;) {
-        const unsigned long long x =
-            __hip_atomic_load(&a.xchg[(1 - net) * 2 + par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((unsigned)(x >> 32) == tag) { other = __uint_as_float((unsigned)x); break; }
-        if (++spins > (1ull << 26)) { atomicExch(a.err, 1); break; }  // bounded: never hangs
-        __builtin_amdgcn_s_sleep(1);
+      if (!grads_mode) {
+        const float mine = (float)ssum;
+        const unsigned tag = (unsigned)(mb + 1);
+        const int par = mb & 1;
+        const unsigned long long gr = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(mine);
+        __hip_atomic_store(&a.xchg[net * 2 + par], gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float other = 0.f;
+        unsigned long long spins = 0;
+        for (;;) {
+          const unsigned long long x =
+              __hip_atomic_load(&a.xchg[(1 - net) * 2 + par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(x >> 32) == tag) { other = __uint_as_float((unsigned)x); break; }
+          if (++spins > (1ull << 26)) { atomicExch(a.err, 1); break; }  // bounded: never hangs
+          __builtin_amdgcn_s_sleep(1);
+        }
+        S.bcast[0] = net == 0 ? mine : other;
+        S.bcast[1] = net == 0 ? other : mine;
+        S.pw[0] *= beta1_d;
+        S.pw[1] *= beta2_d;
+        const double bc1 = 1.0 - S.pw[0];
+        const double bc2 = 1.0 - S.pw[1];
+        S.bcast[2] = (float)sqrt(bc2);
+        S.bcast[3] = (float)(-((double)lr / bc1));
       }
-      S.bcast[0] = net == 0 ? mine : other;
-      S.bcast[1] = net == 0 ? other : mine;
-      S.pw[0] *= beta1_d;
-      S.pw[1] *= beta2_d;
-      const double bc1 = 1.0 - S.pw[0];
-      const double bc2 = 1.0 - S.pw[1];
-      S.bcast[2] = (float)sqrt(bc2);
-      S.bcast[3] = (float)(-((double)lr / bc1));
     }
     lds_barrier();
-      STAMP(12);
+    STAMP(10);
+    if (grads_mode) continue;
     const float total_norm = (float)sqrt((double)S.bcast[0] + (double)S.bcast[1]);
     float coef = 1.f;
     if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
     const float bc2_sqrt = S.bcast[2], neg_step = S.bcast[3];
     const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
 
-    // ---- Adam on owned parameters; refresh the LDS copies ----------------------------------------
+    // ---- E4: Adam on owned parameters; refresh the LDS copies --------------------------------------
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = w2_idx[r] >> 6, k = w2_idx[r] & 63;
@@ -662,15 +773,13 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       S.W1[j][k] = p;
     }
     if (tid == 0) {
-      if (net == 0 && a.norms && norm0 + (mb - mb_begin) < a.max_norms) a.norms[norm0 + (mb - mb_begin)] = total_norm;
+      if (ACTOR && a.norms && norm0 + (mb - mb_begin) < a.max_norms) a.norms[norm0 + (mb - mb_begin)] = total_norm;
     }
     lds_barrier();
-      STAMP(13);
+    STAMP(11);
   }
 
   // ---- write back parameters and optimizer moments (torch parameter order) -----------------------
-  // Indices are recomputed from a laundered copy of tid so the compiler does not keep the
-  // prologue's 64-bit addresses alive (in VGPRs) across the whole minibatch loop.
   if (!grads_mode) {
     int t2 = tid;
     asm volatile("" : "+v"(t2));
@@ -707,7 +816,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   // grads mode has no per-minibatch exchange, so the actor must not advance the shared
   // stat_index before the critic has read it: the critic posts a done flag, the actor waits.
   if (grads_mode && tid == 0) {
-    if (net == 1) {
+    if (!ACTOR) {
       __hip_atomic_store(&a.xchg[4], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       unsigned long long spins = 0;
@@ -717,7 +826,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
       }
     }
   }
-  if (net == 0 && tid == 0) {
+  if (ACTOR && tid == 0) {
     a.state->stat_index = stat0 + nmb;
     if (!grads_mode) {
       a.state->opt_step = step0 + nmb;
@@ -726,9 +835,15 @@ __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   }
 }
 
-}  // namespace
+template <int INP, int NAP>
+__global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
+  static_assert(sizeof(Smem<INP, NAP>) <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[sizeof(Smem<INP, NAP>)];
+  if (blockIdx.x == 0) mlp_net<INP, NAP, true>(a, *reinterpret_cast<Smem<INP, NAP>*>(smem_raw));
+  else mlp_net<INP, 1, false>(a, *reinterpret_cast<Smem<INP, 1>*>(smem_raw));
+}
 
-extern "C" int64_t rai_mlp_ppo_workspace_bytes(void) { return 64; }
+}  // namespace
 
 #ifdef RAI_STAMPS
 extern "C" int rai_mlp_debug_stamps(unsigned long long* host_out) {
@@ -737,6 +852,12 @@ extern "C" int rai_mlp_debug_stamps(unsigned long long* host_out) {
 #endif
 
 namespace {
+constexpr int64_t XCHG_BYTES = 64;
+
+int64_t num_minibatches(int64_t n_rows, int32_t batch_size) {
+  return batch_size > 0 ? (n_rows + batch_size - 1) / batch_size : 0;
+}
+
 int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, void* workspace,
                int64_t workspace_bytes, void* stream) {
   if (hidden != HID || a.in_dim < 1 || a.in_dim > MAXIN || a.n_act < 1 || a.n_act > MAXOUT ||
@@ -747,20 +868,37 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
       !a.hp || !a.ohp || !a.state || !workspace)
     return RAI_E_NULLPTR;
   if (!a.grad_out && (!a.exp_avg || !a.exp_avg_sq)) return RAI_E_NULLPTR;
-  if (workspace_bytes < rai_mlp_ppo_workspace_bytes()) return RAI_E_WORKSPACE;
+  if (workspace_bytes < rai_mlp_ppo_workspace_bytes(n_rows, batch_size)) return RAI_E_WORKSPACE;
   if (n_rows % batch_size == 1 && !a.moments) return RAI_E_SHAPE;  // 1-row minibatch: no std
   if (a.grad_out && (int64_t)a.mb_begin * batch_size >= n_rows) return RAI_E_SHAPE;
   a.n_rows = n_rows;
   a.batch = batch_size;
   a.xchg = reinterpret_cast<unsigned long long*>(workspace);
   a.err = &a.state->err;
-  hipError_t e = hipMemsetAsync(workspace, 0, 64, rai_stream(stream));
+  hipStream_t s = rai_stream(stream);
+  hipError_t e = hipMemsetAsync(workspace, 0, XCHG_BYTES, s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(mlp_ppo_epoch_kernel, dim3(2), dim3(NT), 0, rai_stream(stream), a);
+  if (!a.moments) {
+    float* mom = reinterpret_cast<float*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES);
+    const int64_t nmb = num_minibatches(n_rows, batch_size);
+    hipLaunchKernelGGL(adv_moments_kernel, dim3((unsigned)nmb), dim3(256), 0, s, a.adv, n_rows, batch_size, a.hp,
+                       mom);
+    RAI_LAUNCH_CHECK();
+    a.moments = mom;
+  }
+  if (a.in_dim <= 4 && a.n_act <= 2)
+    hipLaunchKernelGGL((mlp_ppo_epoch_kernel<4, 2>), dim3(2), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((mlp_ppo_epoch_kernel<8, 8>), dim3(2), dim3(NT), 0, s, a);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }
 }  // namespace
+
+extern "C" int64_t rai_mlp_ppo_workspace_bytes(int64_t n_rows, int32_t batch_size) {
+  const int64_t mom = 8 * num_minibatches(n_rows, batch_size);
+  return XCHG_BYTES + ((mom + 255) / 256) * 256;
+}
 
 extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
                                  const int64_t* actions, const float* old_logp, const float* old_values,

@@ -149,9 +149,7 @@ class PPO:
         blocks = self.blocks
         blocks.ensure_tables(n_steps, n_steps)
         blocks.upload(self._hparams(1, nmb), self.optimizer.step_count)
-        if self._mlp_ws is None:
-            self._mlp_ws = torch.zeros(int(_lib.lib().rai_mlp_ppo_workspace_bytes()), dtype=torch.uint8,
-                                       device=self.device)
+        self._ensure_mlp_workspace(r.total_steps)
         opt = self.optimizer
         L = _lib.lib()
         st = _lib.stream_handle(self.device)
@@ -271,6 +269,11 @@ class PPO:
             return None
         return dict(in_dim=in_dim, n_act=n_act, activation=0 if net.activation_fn == "tanh" else 1)
 
+    def _ensure_mlp_workspace(self, n_rows: int) -> None:
+        need = int(_lib.lib().rai_mlp_ppo_workspace_bytes(n_rows, self.batch_size))
+        if self._mlp_ws is None or self._mlp_ws.numel() < need:
+            self._mlp_ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
+
     def _update_fused(self, r, spec) -> Tuple[np.ndarray, np.ndarray, int]:
         nmb = r.num_minibatches(self.batch_size)
         if r.total_steps % self.batch_size == 1:
@@ -279,9 +282,7 @@ class PPO:
         blocks = self.blocks
         blocks.ensure_tables(n_steps, n_steps)
         blocks.upload(self._hparams(1, nmb), self.optimizer.step_count)
-        if self._mlp_ws is None:
-            self._mlp_ws = torch.zeros(int(_lib.lib().rai_mlp_ppo_workspace_bytes()), dtype=torch.uint8,
-                                       device=self.device)
+        self._ensure_mlp_workspace(r.total_steps)
         opt = self.optimizer
         L = _lib.lib()
         st = _lib.stream_handle(self.device)

@@ -21,8 +21,9 @@ from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
 from rl_algo_impls_amd.ppo import PPO  # noqa: E402
 from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 
-NAMES = ["P0 zero X", "P0 X write (+adv moments)", "P1 layer1", "P2 fwd MFMA", "P3 out layer", "P4 loss",
-         "P5 dW3", "P6 dZ2", "P7 dW2+dH1 MFMA", "P8 dZ1", "P9 dW1", "norm+exchange", "adam"]
+NAMES = ["F1 layer1 MFMA", "F2 layer2 MFMA + out", "L loss grads", "B1 dZ2 + dW3/db2", "B2 dW2+dH1 MFMA",
+         "B3 dZ1 + db1", "B4 dW1", "E1 partials->LDS", "E2 owner sums + norm", "E3 stats + exchange",
+         "E4 adam"]
 dev = torch.device("cuda", 0)
 torch.manual_seed(1)
 env = SyntheticVecEnv(4096, "cartpole", seed=1)
@@ -44,7 +45,7 @@ st = np.array(out, dtype=np.float64).reshape(2, 32)
 nmb = r.total_steps // 256
 print(f"epoch {ev0.elapsed_time(ev1):.2f} ms for {nmb} minibatches -> {ev0.elapsed_time(ev1) * 1e3 / nmb:.2f} us/mb")
 for net in range(2):
-    tot = st[net, 1:14].sum()
+    tot = st[net, 1:1 + len(NAMES)].sum()
     print(f"--- workgroup {net} ({'actor' if net == 0 else 'critic'}): {tot / nmb:.0f} stamp-ticks/mb")
     for i, n in enumerate(NAMES):
         print(f"  {n:28s} {st[net, i + 1] / nmb:10.1f} ticks/mb  {100 * st[net, i + 1] / tot:5.1f}%")
