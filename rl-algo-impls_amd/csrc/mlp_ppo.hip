@@ -74,6 +74,8 @@ struct MlpArgs {
   int32_t* err;
   // per-minibatch (mean, den) of the advantage normalisation: moments[2*mb], moments[2*mb+1]
   const float* moments;
+  // row-tile layout only: per-wave partial gradients [2 nets][NW][parts][64] (workspace)
+  float* scratch;
   // data-parallel "grads" mode (grad_out != nullptr): process minibatches
   // [mb_begin, mb_begin + mb_count), scale the loss means by 1/(rows*world), write the
   // raw gradients to grad_out and stop (the caller all-reduces them and runs
@@ -103,11 +105,12 @@ __device__ unsigned long long g_stamps[2][32];
   } while (0)
 #endif
 
-// Re-derive the lane coordinates inside each phase from an opaque copy of threadIdx.x (and of
-// the wave index) so the compiler recomputes per-phase LDS addresses where they are used
-// instead of hoisting them all out of the minibatch loop (which overflows 128 VGPRs).
+// Re-derive the lane coordinates inside each phase from a freshly computed lane id (mbcnt, so
+// threadIdx.x's register need not stay live) and an opaque copy of the wave index, so the
+// compiler recomputes per-phase LDS addresses where they are used instead of hoisting them all
+// out of the minibatch loop (which overflows 128 VGPRs and spills).
 #define RELANE()                                                                     \
-  int tid_l_ = threadIdx.x;                                                          \
+  int tid_l_ = (w << 6) | (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); \
   asm volatile("" : "+v"(tid_l_));                                                   \
   int w_l_ = w;                                                                      \
   asm volatile("" : "+s"(w_l_));                                                     \
@@ -143,7 +146,21 @@ __device__ __forceinline__ int kmap(int g, int kk) { return (g & 1) * 32 + (g >>
 __device__ __forceinline__ int smap(int g, int kk) {
   return (kk >> 3) * 32 + (g >> 1) * 16 + (g & 1) * 8 + (kk & 7);
 }
-__device__ __forceinline__ float act_f(int relu, float z) { return relu ? fmaxf(z, 0.f) : tanhf(z); }
+// Branch-free tanh (libm's tanhf branches on |x| ranges, which diverges across a wave):
+// |x| < 0.3: odd Taylor series to x^9 (truncation < 1e-7 relative); otherwise
+// 1 - 2 / (exp(2|x|) + 1) with the sign restored (absolute error ~1 ulp of 1).
+__device__ __forceinline__ float tanh_bf(float x) {
+  const float ax = fabsf(x);
+  const float x2 = x * x;
+  float p = fmaf(x2, 62.f / 2835.f, -17.f / 315.f);
+  p = fmaf(x2, p, 2.f / 15.f);
+  p = fmaf(x2, p, -1.f / 3.f);
+  const float small = fmaf(x * x2, p, x);
+  const float e = __builtin_amdgcn_exp2f(ax * 2.885390081777927f);  // exp(2|x|)
+  const float big = fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+  return ax < 0.3f ? small : copysignf(big, x);
+}
+__device__ __forceinline__ float act_f(const int relu, float z) { return relu ? fmaxf(z, 0.f) : tanh_bf(z); }
 __device__ __forceinline__ float act_d(int relu, float h) { return relu ? (h > 0.f ? 1.f : 0.f) : 1.f - h * h; }
 
 __device__ __forceinline__ float vf_loss(int fn, float x) {
@@ -206,7 +223,7 @@ __global__ __launch_bounds__(256) void adv_moments_kernel(const float* __restric
 }
 
 // One network (ACTOR: the policy head; else the value head) of the fused epoch.
-template <int INP, int OUTP, bool ACTOR>
+template <int INP, int OUTP, bool ACTOR, int RELU>
 __device__ __forceinline__ void mlp_net(const MlpArgs& a, Smem<INP, OUTP>& S) {
   constexpr int net = ACTOR ? 0 : 1;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
@@ -214,7 +231,7 @@ __device__ __forceinline__ void mlp_net(const MlpArgs& a, Smem<INP, OUTP>& S) {
   const int IN = a.in_dim;
   const int NA = a.n_act;
   const int OUT = ACTOR ? NA : 1;
-  const int relu = a.act_fn;
+  constexpr int relu = RELU;  // compile-time: keeps the activation epilogues in one basic block
   const float clip_range = a.hp->clip_range, ent_coef = a.hp->ent_coef, vf_coef0 = a.hp->vf_coef[0];
   const float clip_range_vf = a.hp->clip_range_vf;
   const int has_vclip = a.hp->has_clip_range_vf, vf_fn = a.hp->vf_loss_fn;
@@ -835,12 +852,662 @@ __device__ __forceinline__ void mlp_net(const MlpArgs& a, Smem<INP, OUTP>& S) {
   }
 }
 
-template <int INP, int NAP>
+// ================================================================================================
+// Row-tile layout for in_dim <= 4, n_actions <= 2 (the CartPole class; the bench configuration).
+// The whole minibatch (<= 256 rows) is one pass: wave w owns rows [16w, 16w + 16) end to end —
+// layer 1, layer 2 (all 64 columns: 4 MFMA tiles), the output layer and the loss, dZ2, dH1 and
+// dZ1 — so the forward, the loss and most of the backward need no workgroup barrier at all
+// (every LDS hand-off in that stretch is wave-local).  The only cross-wave steps per minibatch are
+// dW2 = dZ2^T H1 over all rows (one MFMA tile of dW2 per wave) and the owner reductions of the
+// per-wave partial gradients (staged in a global scratch slab: LDS holds H1 and dZ2 for 256 rows).
+// 4 barriers per minibatch instead of 18.
+// ================================================================================================
+constexpr int RB = 256;  // rows per pass = NW waves x 16
+
+template <int OUTP>
+struct SmemR {
+#ifdef RAI_STAMPS
+  unsigned long long stamps[32];
+  unsigned long long t_last;
+#endif
+  double red[NW];
+  double pw[2];
+  double st[NW][4];
+  float bcast[8];
+  float db3p[NW][OUTP];
+  float W1[HID][4];    // [out j][in k]
+  float b1[HID];
+  float b2[HID];
+  float b3[MAXOUT];
+  float W2[HID][LD];   // [out j][in k]
+  float W3[OUTP][LD];  // [out o][in k]
+  float X[RB][4];
+  float H1[RB][LD];    // act(z1) of every row
+  float Z2[RB][LD];    // dZ2 of every row
+};
+
+template <int OUTP>
+struct RowParts {
+  static constexpr int N = OUTP + 2 + 4;  // dW3[o], db2, db1, dW1[k] per column
+};
+
+template <int OUTP, bool ACTOR, int RELU>
+__device__ __forceinline__ void mlp_rows(const MlpArgs& a, SmemR<OUTP>& S) {
+  constexpr int net = ACTOR ? 0 : 1;
+  constexpr int relu = RELU;
+  constexpr int NPART = RowParts<OUTP>::N;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int IN = a.in_dim;
+  const int NA = a.n_act;
+  const int OUT = ACTOR ? NA : 1;
+  const float clip_range = a.hp->clip_range, ent_coef = a.hp->ent_coef, vf_coef0 = a.hp->vf_coef[0];
+  const float clip_range_vf = a.hp->clip_range_vf;
+  const int has_vclip = a.hp->has_clip_range_vf, vf_fn = a.hp->vf_loss_fn;
+  const float halve = a.hp->ppo2_vf_coef_halving ? 0.5f : 1.f;
+  const float beta2 = a.ohp->beta2, adam_eps = a.ohp->eps, lr = a.ohp->lr;
+  const double beta1_d = a.ohp->beta1_d, beta2_d = a.ohp->beta2_d;
+  const bool grads_mode = a.grad_out != nullptr;
+  const float max_grad_norm = a.ohp->max_grad_norm;
+  float* const scr = a.scratch + (size_t)net * NW * (MAXOUT + 6) * HID;  // fixed per-net stride
+
+  // ---- flat parameter offsets (torch parameters() order: actor block, critic block) -------
+  const int szA = HID * IN + HID + HID * HID + HID + NA * HID + NA;
+  const int base = net == 0 ? 0 : szA;
+  const int oW1 = base, ob1 = oW1 + HID * IN, oW2 = ob1 + HID, ob2 = oW2 + HID * HID, oW3 = ob2 + HID,
+            ob3 = oW3 + OUT * HID;
+
+  if (tid < HID * 4) {
+    const int j = tid >> 2, k = tid & 3;
+    S.W1[j][k] = k < IN ? a.params[oW1 + j * IN + k] : 0.f;
+  }
+  if (tid < HID) {
+    S.b1[tid] = a.params[ob1 + tid];
+    S.b2[tid] = a.params[ob2 + tid];
+  }
+  for (int e = tid; e < HID * HID; e += NT) S.W2[e >> 6][e & 63] = a.params[oW2 + e];
+  if (tid < OUTP * HID) S.W3[tid >> 6][tid & 63] = (tid >> 6) < OUT ? a.params[oW3 + tid] : 0.f;
+  if (tid < MAXOUT) S.b3[tid] = tid < OUT ? a.params[ob3 + tid] : 0.f;
+
+  // ---- ownership (as the chunked layout): W2 tile element of the dW2 MFMA; slot A; slot B ----
+  const int jt = w >> 2, kt = w & 3;
+  int w2_idx[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) w2_idx[r] = (jt * 16 + g * 4 + r) * HID + kt * 16 + li;
+  float w2_m[4] = {0.f, 0.f, 0.f, 0.f}, w2_v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (!grads_mode) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      w2_m[r] = a.exp_avg[oW2 + w2_idx[r]];
+      w2_v[r] = a.exp_avg_sq[oW2 + w2_idx[r]];
+    }
+  }
+  int a_flat = -1;
+  if (tid < OUT * HID) a_flat = oW3 + tid;
+  else if (tid >= 512 && tid < 512 + OUT) a_flat = ob3 + (tid - 512);
+  else if (tid >= 576 && tid < 640) a_flat = ob2 + (tid - 576);
+  else if (tid >= 640 && tid < 704) a_flat = ob1 + (tid - 640);
+  const int b_flat = tid < HID * IN ? oW1 + tid : -1;
+  float a_m = 0.f, a_v = 0.f, b_m = 0.f, b_v = 0.f;
+  if (!grads_mode && a_flat >= 0) { a_m = a.exp_avg[a_flat]; a_v = a.exp_avg_sq[a_flat]; }
+  if (!grads_mode && b_flat >= 0) { b_m = a.exp_avg[b_flat]; b_v = a.exp_avg_sq[b_flat]; }
+
+  const int B = a.batch;
+  const int64_t n_rows = a.n_rows;
+  const int nmb_total = (int)((n_rows + B - 1) / B);
+  const int mb_begin = a.mb_begin;
+  const int mb_end = min(nmb_total, a.mb_begin + a.mb_count);
+  const int nmb = mb_end - mb_begin;
+  const int64_t step0 = a.state->opt_step;
+  const int stat0 = a.state->stat_index;
+  const int norm0 = a.state->norm_index;
+  const int latched = a.state->pi_coef_zero;
+  const float pi_coef = latched ? 0.f : 1.f;
+
+  // ---- per-minibatch inputs, prefetched into registers one minibatch ahead ------------------
+  // lane (g, li) of wave w: the loss inputs of row 16w + 4g + (li & 3) and the layer-1 MFMA
+  // A operand X[16w + li][g]
+  int r_act = 0;
+  float r_a = 0.f, r_b = 0.f, r_c = 0.f, r_d = 1.f, r_x = 0.f;
+  auto prefetch = [&](int mb) {
+    const int64_t row0 = (int64_t)mb * B;
+    const int rows = (int)min((int64_t)B, n_rows - row0);
+    // lane coordinates recomputed here (mbcnt) and made opaque: keeps per-lane addresses from
+    // being hoisted out of the minibatch loop — kept live they spill, and a spill reload's
+    // vmcnt(0) would then wait for these very prefetch loads
+    int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(ln));
+    const int xr = w * 16 + (ln & 15), xg = ln >> 4;
+    r_x = (xr < rows && xg < IN) ? a.obs[(row0 + xr) * IN + xg] : 0.f;
+    const int rr = w * 16 + (ln >> 4) * 4 + (ln & 3);
+    if (rr < rows) {
+      const int64_t r = row0 + rr;
+      if (ACTOR) {
+        r_act = (int)a.actions[r];
+        r_a = a.old_logp[r];
+        r_b = a.adv[r];
+      } else {
+        r_a = a.old_values[r];
+        r_b = a.ret[r];
+      }
+    }
+    if (ACTOR) {
+      r_c = a.moments[2 * mb];
+      r_d = a.moments[2 * mb + 1];
+    }
+  };
+  prefetch(mb_begin);
+  if (tid == 0) {
+    S.pw[0] = pow(beta1_d, (double)step0);
+    S.pw[1] = pow(beta2_d, (double)step0);
+  }
+#ifdef RAI_STAMPS
+  if (tid < 32) S.stamps[tid] = 0;
+  if (tid == 0) S.t_last = __builtin_amdgcn_s_memtime();
+#endif
+  lds_barrier();
+
+  for (int mb = mb_begin; mb < mb_end; ++mb) {
+    const int64_t row0 = (int64_t)mb * B;
+    const int rows = (int)min((int64_t)B, n_rows - row0);
+    const int c_act = r_act;
+    const float c_a = r_a, c_b = r_b, amean = r_c, aden = r_d, c_x = r_x;
+    if (mb + 1 < mb_end) prefetch(mb + 1);
+    const float invB = 1.f / (float)(rows * a.world);
+    const int R = w * 16;  // first row of this wave's tile
+
+    // ============ P_A: wave-local forward, loss and backward of rows [R, R + 16) ============
+    float h2[4][4];  // [col tile t][row r] = act(z2) at row R + 4g + r, column 16t + li
+    {
+      RELANE();
+      // layer 1 (K = in_dim padded to 4): one MFMA per column tile
+      f4 z[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f4 zero = {0.f, 0.f, 0.f, 0.f};
+        z[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(c_x, S.W1[16 * t + li][g], zero, 0, 0, 0);
+      }
+      S.X[R + li][g] = c_x;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float bj = S.b1[16 * t + li];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S.H1[R + g * 4 + r][16 * t + li] = act_f(relu, z[t][r] + bj);
+      }
+      STAMP(1);
+      // layer 2 over all 64 columns (A = this wave's H1 rows, written just above)
+      f4 acc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 16; kk += 2) {
+        const int kq = kmap(g, kk);
+        const f2 av = *reinterpret_cast<const f2*>(&S.H1[R + li][kq]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f2 bv = *reinterpret_cast<const f2*>(&S.W2[16 * t + li][kq]);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc[t], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float bb = S.b2[16 * t + li];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h2[t][r] = act_f(relu, acc[t][r] + bb);
+      }
+      STAMP(2);
+    }
+    float pw3[4][OUTP], pb2[4];  // per-lane partials over this lane's 4 rows (column 16t + li)
+    float dq[OUTP];              // dL/d(out) of this lane's loss row (li & 3)
+    float st[4] = {0.f, 0.f, 0.f, 0.f};
+    {
+      RELANE();
+      float w3[4][OUTP];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int o = 0; o < OUTP; ++o) w3[t][o] = S.W3[o][16 * t + li];
+      // output layer: logits of rows R + 4g + r, summed over the 16 lanes of the DPP row
+      // per-row loss gradient (ppo.py:326-371; tie rules as loss.hip) for row q = li & 3
+      const int q = li & 3;
+      const bool valid = R + g * 4 + q < rows;
+      float z[OUTP];
+#pragma unroll
+      for (int o = 0; o < OUTP; ++o) {
+        // logit o of rows R + 4g + r (r = 0..3), each summed over the 16 lanes of the DPP row;
+        // this lane keeps row q's (scalar selects: no indexable array, which would go to scratch)
+        float sel = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = h2[0][r] * w3[0][o];
+          p = fmaf(h2[1][r], w3[1][o], p);
+          p = fmaf(h2[2][r], w3[2][o], p);
+          p = fmaf(h2[3][r], w3[3][o], p);
+          const float lgr = row_sum16(p);
+          sel = q == r ? lgr : sel;
+        }
+        z[o] = sel + S.b3[o];
+        dq[o] = 0.f;
+      }
+      if (valid) {
+        if (ACTOR) {
+          float m = F32_MIN;
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o)
+            if (o < NA) m = fmaxf(m, z[o]);
+          float se = 0.f;
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o)
+            if (o < NA) se += expf(z[o] - m);
+          const float lse = m + logf(se);
+          float H = 0.f;
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o)
+            if (o < NA) {
+              const float n = z[o] - lse;
+              H -= fmaxf(n, F32_MIN) * expf(n);
+            }
+          const int act = min(max(c_act, 0), NA - 1);
+          float zact = z[0];
+#pragma unroll
+          for (int o = 1; o < OUTP; ++o)
+            if (o == act) zact = z[o];
+          const float logp = zact - lse;
+          const float A = (c_b - amean) / aden;
+          const float logratio = logp - c_a;
+          const float ratio = expf(logratio);
+          const float lo = 1.f - clip_range, hi = 1.f + clip_range;
+          const float cr = fminf(fmaxf(ratio, lo), hi);
+          const float s1 = ratio * A, s2 = cr * A;
+          const float gpi = -pi_coef * invB;
+          float g1, g2;
+          if (s1 < s2) { g1 = gpi; g2 = 0.f; }
+          else if (s1 > s2) { g1 = 0.f; g2 = gpi; }
+          else { g1 = gpi * 0.5f; g2 = gpi * 0.5f; }
+          const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+          const float dlogp = (g1 * A + (g2 * A) * in_clip) * ratio;
+          const float dent = -ent_coef * invB;
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o)
+            if (o < NA) {
+              const float n = z[o] - lse;
+              const float p = expf(n);
+              dq[o] = dlogp * ((o == act ? 1.f : 0.f) - p) + dent * (-p * (n + H));
+            }
+          if (li < 4) {
+            st[0] = fminf(s1, s2);
+            st[1] = (ratio - 1.f) - logratio;
+            st[2] = (fabsf(ratio - 1.f) > clip_range) ? 1.f : 0.f;
+            st[3] = H;
+          }
+        } else {
+          const float v = z[0], Rt = c_b;
+          const float gl = (vf_coef0 * halve) * invB;
+          float l = vf_loss(vf_fn, v - Rt), dv;
+          float vcf = 0.f;
+          if (has_vclip) {
+            const float vc_ = clip_range_vf;
+            const float dvo = v - c_a;
+            const float vcl = c_a + fminf(fmaxf(dvo, -vc_), vc_);
+            const float l2 = vf_loss(vf_fn, vcl - Rt);
+            float w1, w2;
+            if (l > l2) { w1 = gl; w2 = 0.f; }
+            else if (l < l2) { w1 = 0.f; w2 = gl; }
+            else { w1 = gl * 0.5f; w2 = gl * 0.5f; }
+            const float inv = (dvo >= -vc_ && dvo <= vc_) ? 1.f : 0.f;
+            dv = w1 * vf_grad(vf_fn, v - Rt) + (w2 * vf_grad(vf_fn, vcl - Rt)) * inv;
+            vcf = (fabsf(v - c_a) > vc_) ? 1.f : 0.f;
+            l = fmaxf(l, l2);
+          } else {
+            dv = gl * vf_grad(vf_fn, v - Rt);
+          }
+          dq[0] = dv;
+          if (li < 4) {
+            st[0] = l;
+            st[1] = vcf;
+          }
+        }
+      }
+      // dL/d(out) of the 4 rows of this lane's D-layout: quad broadcast from lane r of each quad
+      float dr[4][OUTP];
+#pragma unroll
+      for (int o = 0; o < OUTP; ++o) {
+        dr[0][o] = dpp<0x00>(dq[o]);
+        dr[1][o] = dpp<0x55>(dq[o]);
+        dr[2][o] = dpp<0xAA>(dq[o]);
+        dr[3][o] = dpp<0xFF>(dq[o]);
+      }
+      // dZ2 = (dout . W3) * act'(H2) -> LDS (wave-local rows); dW3 / db2 partials
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        pb2[t] = 0.f;
+#pragma unroll
+        for (int o = 0; o < OUTP; ++o) pw3[t][o] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < OUTP; ++o) {
+            dh = fmaf(dr[r][o], w3[t][o], dh);
+            pw3[t][o] = fmaf(dr[r][o], h2[t][r], pw3[t][o]);
+          }
+          const float dz = dh * act_d(relu, h2[t][r]);
+          pb2[t] += dz;
+          S.Z2[R + g * 4 + r][16 * t + li] = dz;
+        }
+      }
+      STAMP(3);
+    }
+    float pb1[4], pw1[4][4];  // db1 / dW1 partials (column 16t + li; dW1 also per input k)
+    {
+      RELANE();
+      // dH1 = dZ2 W2 for this wave's rows (A = dZ2 rows written above; B = W2[j][16t + li])
+      f4 dh1[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dh1[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 16; kk += 2) {
+        const int kq = kmap(g, kk);
+        const f2 av = *reinterpret_cast<const f2*>(&S.Z2[R + li][kq]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float bx = S.W2[kq][16 * t + li], by = S.W2[kq + 1][16 * t + li];
+          dh1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bx, dh1[t], 0, 0, 0);
+          dh1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, by, dh1[t], 0, 0, 0);
+        }
+      }
+      STAMP(4);
+      // dZ1 = dH1 * act'(H1); db1 and dW1 partials over this lane's 4 rows
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        pb1[t] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pw1[t][k] = 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f4 xr = *reinterpret_cast<const f4*>(&S.X[R + g * 4 + r][0]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float dz1 = dh1[t][r] * act_d(relu, S.H1[R + g * 4 + r][16 * t + li]);
+          pb1[t] += dz1;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) pw1[t][k] = fmaf(dz1, xr[k], pw1[t][k]);
+        }
+      }
+    }
+    // ---- partials: reduce over the 4 lane groups, lane group g stores column tile t == g ---------
+    {
+      RELANE();
+      auto red4 = [&](float v) {
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        return v;
+      };
+      float* sp = scr + (size_t)w * NPART * HID + 16 * g + li;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float v[NPART];
+#pragma unroll
+        for (int o = 0; o < OUTP; ++o) v[o] = red4(pw3[t][o]);
+        v[OUTP] = red4(pb2[t]);
+        v[OUTP + 1] = red4(pb1[t]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[OUTP + 2 + k] = red4(pw1[t][k]);
+        if (t == g) {
+#pragma unroll
+          for (int p = 0; p < NPART; ++p) sp[p * HID] = v[p];
+        }
+      }
+      // db3 and the loss statistics: lanes li < 4 hold the wave's 16 distinct rows
+#pragma unroll
+      for (int o = 0; o < OUTP; ++o) {
+        const float t3 = wave_sum(li < 4 ? dq[o] : 0.f);
+        if (lane == 0) S.db3p[w][o] = t3;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double t = wave_sum((double)st[i]);
+        if (lane == 0) S.st[w][i] = t;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // partial-gradient stores are out
+    lds_barrier();
+    STAMP(5);
+    // ============ P_B: dW2 = dZ2^T H1 over all rows (wave w: tile jt, kt) ============
+    f4 gw2;
+    {
+      RELANE();
+      const int jt = w >> 2, kt = w & 3;
+      f4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int kk = 0; kk < RB / 4; kk += 2) {
+        const int s0 = smap(g, kk), s1 = smap(g, kk + 1);
+        g0 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Z2[s0][jt * 16 + li], S.H1[s0][kt * 16 + li], g0, 0, 0, 0);
+        g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Z2[s1][jt * 16 + li], S.H1[s1][kt * 16 + li], g1, 0, 0, 0);
+      }
+      gw2 = g0 + g1;
+    }
+    STAMP(6);
+    // ============ E2: owners sum the per-wave partials (fixed order); this network's |g|^2 ============
+    float ga = 0.f, gb = 0.f;
+    {
+      RELANE();
+      auto ld = [&](int wv, int p, int col) {
+        return __hip_atomic_load(scr + ((size_t)wv * NPART + p) * HID + col, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      };
+      if (tid < OUT * HID) {
+        const int o = tid >> 6, k = tid & 63;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) t += ld(q, o, k);
+        ga = t;
+      } else if (tid >= 512 && tid < 512 + OUT) {
+        const int o = tid - 512;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) t += S.db3p[q][o];
+        ga = t;
+      } else if (tid >= 576 && tid < 640) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) t += ld(q, OUTP, tid - 576);
+        ga = t;
+      } else if (tid >= 640 && tid < 704) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) t += ld(q, OUTP + 1, tid - 640);
+        ga = t;
+      }
+      if (tid < HID * IN) {
+        const int j = tid / IN, k = tid % IN;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) t += ld(q, OUTP + 2 + k, j);
+        gb = t;
+      }
+      double ss = (double)gw2.x * gw2.x + (double)gw2.y * gw2.y + (double)gw2.z * gw2.z + (double)gw2.w * gw2.w;
+      if (a_flat >= 0) ss += (double)ga * ga;
+      if (b_flat >= 0) ss += (double)gb * gb;
+      ss = wave_sum(ss);
+      if (lane == 0) S.red[w] = ss;
+      if (grads_mode) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.grad_out[oW2 + w2_idx[r]] = gw2[r];
+        if (a_flat >= 0) a.grad_out[a_flat] = ga;
+        if (b_flat >= 0) a.grad_out[b_flat] = gb;
+      }
+    }
+    lds_barrier();
+    STAMP(7);
+    // ============ E3: stats row, grad-norm exchange, bias corrections (thread 0) ============
+    if (tid == 0) {
+      double ssum = 0.0;
+      for (int q = 0; q < NW; ++q) ssum += S.red[q];
+      double sv[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int q = 0; q < NW; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sv[i] += S.st[q][i];
+      const int srow = stat0 + (mb - mb_begin);
+      if (a.stats && srow < a.max_stats) {
+        float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
+        const double Bd = (double)rows * (double)a.world;
+        if (ACTOR) {
+          const float pi_loss = (float)(-sv[0] / Bd);
+          const float ent_loss = (float)(-sv[3] / Bd);
+          row[0] = pi_coef * pi_loss + ent_coef * ent_loss;  // host adds the value term
+          row[1] = pi_loss;
+          row[2] = ent_loss;
+          row[3] = (float)(sv[1] / Bd);
+          row[4] = (float)(sv[2] / Bd);
+        } else {
+          row[5] = (float)(sv[0] / Bd) * halve;
+          row[5 + RAI_MAX_K] = has_vclip ? (float)(sv[1] / Bd) : 0.f;
+        }
+      }
+      if (!grads_mode) {
+        const float mine = (float)ssum;
+        const unsigned tag = (unsigned)(mb + 1);
+        const int par = mb & 1;
+        const unsigned long long gr = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(mine);
+        __hip_atomic_store(&a.xchg[net * 2 + par], gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float other = 0.f;
+        unsigned long long spins = 0;
+        for (;;) {
+          const unsigned long long x =
+              __hip_atomic_load(&a.xchg[(1 - net) * 2 + par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(x >> 32) == tag) { other = __uint_as_float((unsigned)x); break; }
+          if (++spins > (1ull << 26)) { atomicExch(a.err, 1); break; }  // bounded: never hangs
+          __builtin_amdgcn_s_sleep(1);
+        }
+        S.bcast[0] = net == 0 ? mine : other;
+        S.bcast[1] = net == 0 ? other : mine;
+        S.pw[0] *= beta1_d;
+        S.pw[1] *= beta2_d;
+        const double bc1 = 1.0 - S.pw[0];
+        const double bc2 = 1.0 - S.pw[1];
+        S.bcast[2] = (float)sqrt(bc2);
+        S.bcast[3] = (float)(-((double)lr / bc1));
+      }
+    }
+    lds_barrier();
+    STAMP(8);
+    if (grads_mode) continue;
+    const float total_norm = (float)sqrt((double)S.bcast[0] + (double)S.bcast[1]);
+    float coef = 1.f;
+    if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
+    const float bc2_sqrt = S.bcast[2], neg_step = S.bcast[3];
+    const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
+    // ============ E4: Adam on owned parameters; refresh the LDS copies ============
+    {
+      RELANE();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = (w >> 2) * 16 + g * 4 + r, k = (w & 3) * 16 + li;
+        float p = S.W2[j][k];
+        adam_update(p, w2_m[r], w2_v[r], gw2[r] * coef, w1, w2, beta2, bc2_sqrt, neg_step, adam_eps);
+        S.W2[j][k] = p;
+      }
+      if (a_flat >= 0) {
+        float* slot;
+        if (tid < OUT * HID) slot = &S.W3[tid >> 6][tid & 63];
+        else if (tid < 576) slot = &S.b3[tid - 512];
+        else if (tid < 640) slot = &S.b2[tid - 576];
+        else slot = &S.b1[tid - 640];
+        float p = *slot;
+        adam_update(p, a_m, a_v, ga * coef, w1, w2, beta2, bc2_sqrt, neg_step, adam_eps);
+        *slot = p;
+      }
+      if (b_flat >= 0) {
+        const int j = tid / IN, k = tid % IN;
+        float p = S.W1[j][k];
+        adam_update(p, b_m, b_v, gb * coef, w1, w2, beta2, bc2_sqrt, neg_step, adam_eps);
+        S.W1[j][k] = p;
+      }
+      if (tid == 0) {
+        if (ACTOR && a.norms && norm0 + (mb - mb_begin) < a.max_norms) a.norms[norm0 + (mb - mb_begin)] = total_norm;
+      }
+    }
+    lds_barrier();
+    STAMP(9);
+  }
+
+  // ---- write back parameters and optimizer moments (torch parameter order) -----------------------
+  if (!grads_mode) {
+    int t2 = tid;
+    asm volatile("" : "+v"(t2));
+    const int lane2 = t2 & 63, w_2 = t2 >> 6, g2 = lane2 >> 4, li2 = lane2 & 15;
+    const int jt2 = w_2 >> 2, kt2 = w_2 & 3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jt2 * 16 + g2 * 4 + r, k = kt2 * 16 + li2;
+      const int idx = oW2 + j * HID + k;
+      a.params[idx] = S.W2[j][k];
+      a.exp_avg[idx] = w2_m[r];
+      a.exp_avg_sq[idx] = w2_v[r];
+    }
+    int af = -1;
+    float p = 0.f;
+    if (t2 < OUT * HID) { af = oW3 + t2; p = S.W3[t2 >> 6][t2 & 63]; }
+    else if (t2 >= 512 && t2 < 512 + OUT) { af = ob3 + (t2 - 512); p = S.b3[t2 - 512]; }
+    else if (t2 >= 576 && t2 < 640) { af = ob2 + (t2 - 576); p = S.b2[t2 - 576]; }
+    else if (t2 >= 640 && t2 < 704) { af = ob1 + (t2 - 640); p = S.b1[t2 - 640]; }
+    if (af >= 0) {
+      a.params[af] = p;
+      a.exp_avg[af] = a_m;
+      a.exp_avg_sq[af] = a_v;
+    }
+    if (t2 < HID * IN) {
+      a.params[oW1 + t2] = S.W1[t2 / IN][t2 % IN];
+      a.exp_avg[oW1 + t2] = b_m;
+      a.exp_avg_sq[oW1 + t2] = b_v;
+    }
+  }
+#ifdef RAI_STAMPS
+  if (tid < 32) g_stamps[net][tid] = S.stamps[tid];
+#endif
+  if (grads_mode && tid == 0) {
+    if (!ACTOR) {
+      __hip_atomic_store(&a.xchg[4], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned long long spins = 0;
+      while (__hip_atomic_load(&a.xchg[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0ull) {
+        if (++spins > (1ull << 26)) { atomicExch(a.err, 1); break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+  if (ACTOR && tid == 0) {
+    a.state->stat_index = stat0 + nmb;
+    if (!grads_mode) {
+      a.state->opt_step = step0 + nmb;
+      a.state->norm_index = norm0 + nmb;
+    }
+  }
+}
+
+template <int RELU>
+__global__ __launch_bounds__(NT) void mlp_ppo_rows_kernel(const MlpArgs a) {
+  static_assert(sizeof(SmemR<2>) <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[sizeof(SmemR<2>)];
+  if (blockIdx.x == 0) mlp_rows<2, true, RELU>(a, *reinterpret_cast<SmemR<2>*>(smem_raw));
+  else mlp_rows<1, false, RELU>(a, *reinterpret_cast<SmemR<1>*>(smem_raw));
+}
+
+template <int INP, int NAP, int RELU>
 __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   static_assert(sizeof(Smem<INP, NAP>) <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[sizeof(Smem<INP, NAP>)];
-  if (blockIdx.x == 0) mlp_net<INP, NAP, true>(a, *reinterpret_cast<Smem<INP, NAP>*>(smem_raw));
-  else mlp_net<INP, 1, false>(a, *reinterpret_cast<Smem<INP, 1>*>(smem_raw));
+  if (blockIdx.x == 0) mlp_net<INP, NAP, true, RELU>(a, *reinterpret_cast<Smem<INP, NAP>*>(smem_raw));
+  else mlp_net<INP, 1, false, RELU>(a, *reinterpret_cast<Smem<INP, 1>*>(smem_raw));
+}
+
+template <int INP, int NAP>
+void launch_epoch(const MlpArgs& a, hipStream_t s) {
+  if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_epoch_kernel<INP, NAP, 1>), dim3(2), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((mlp_ppo_epoch_kernel<INP, NAP, 0>), dim3(2), dim3(NT), 0, s, a);
 }
 
 }  // namespace
@@ -852,7 +1519,8 @@ extern "C" int rai_mlp_debug_stamps(unsigned long long* host_out) {
 #endif
 
 namespace {
-constexpr int64_t XCHG_BYTES = 64;
+constexpr int64_t XCHG_BYTES = 256;  // exchange words (first 64 B zeroed per launch), padded
+constexpr int64_t SCRATCH_BYTES = 2LL * NW * (MAXOUT + 2 + 4) * HID * sizeof(float);
 
 int64_t num_minibatches(int64_t n_rows, int32_t batch_size) {
   return batch_size > 0 ? (n_rows + batch_size - 1) / batch_size : 0;
@@ -876,20 +1544,24 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
   a.xchg = reinterpret_cast<unsigned long long*>(workspace);
   a.err = &a.state->err;
   hipStream_t s = rai_stream(stream);
-  hipError_t e = hipMemsetAsync(workspace, 0, XCHG_BYTES, s);
+  hipError_t e = hipMemsetAsync(workspace, 0, 64, s);
+  a.scratch = reinterpret_cast<float*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES);
   if (e != hipSuccess) return (int)e;
   if (!a.moments) {
-    float* mom = reinterpret_cast<float*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES);
+    float* mom = reinterpret_cast<float*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES + SCRATCH_BYTES);
     const int64_t nmb = num_minibatches(n_rows, batch_size);
     hipLaunchKernelGGL(adv_moments_kernel, dim3((unsigned)nmb), dim3(256), 0, s, a.adv, n_rows, batch_size, a.hp,
                        mom);
     RAI_LAUNCH_CHECK();
     a.moments = mom;
   }
-  if (a.in_dim <= 4 && a.n_act <= 2)
-    hipLaunchKernelGGL((mlp_ppo_epoch_kernel<4, 2>), dim3(2), dim3(NT), 0, s, a);
-  else
-    hipLaunchKernelGGL((mlp_ppo_epoch_kernel<8, 8>), dim3(2), dim3(NT), 0, s, a);
+  if (a.in_dim <= 4 && a.n_act <= 2) {
+    // row-tile layout (one pass over <= 256 rows)
+    if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_rows_kernel<1>), dim3(2), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((mlp_ppo_rows_kernel<0>), dim3(2), dim3(NT), 0, s, a);
+  } else {
+    launch_epoch<8, 8>(a, s);
+  }
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }
@@ -897,7 +1569,7 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
 
 extern "C" int64_t rai_mlp_ppo_workspace_bytes(int64_t n_rows, int32_t batch_size) {
   const int64_t mom = 8 * num_minibatches(n_rows, batch_size);
-  return XCHG_BYTES + ((mom + 255) / 256) * 256;
+  return XCHG_BYTES + SCRATCH_BYTES + ((mom + 255) / 256) * 256;
 }
 
 extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,

@@ -21,9 +21,9 @@ from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
 from rl_algo_impls_amd.ppo import PPO  # noqa: E402
 from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 
-NAMES = ["F1 layer1 MFMA", "F2 layer2 MFMA + out", "L loss grads", "B1 dZ2 + dW3/db2", "B2 dW2+dH1 MFMA",
-         "B3 dZ1 + db1", "B4 dW1", "E1 partials->LDS", "E2 owner sums + norm", "E3 stats + exchange",
-         "E4 adam"]
+NAMES = ["F1 layer1 (wave-local)", "F2 layer2 + epilogue", "out layer + loss + dZ2", "dH1 MFMA",
+         "dZ1/partials + barrier", "P_B dW2 MFMA", "E2 owner sums + norm", "E3 stats + exchange",
+         "E4 adam"]  # row-tile layout (in_dim <= 4, n_actions <= 2)
 dev = torch.device("cuda", 0)
 torch.manual_seed(1)
 env = SyntheticVecEnv(4096, "cartpole", seed=1)
