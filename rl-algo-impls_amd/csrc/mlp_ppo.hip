@@ -31,6 +31,9 @@
 // and (8, 8); padded rows/columns carry zeros.
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 #pragma clang fp contract(off)
 
 namespace {
@@ -1496,6 +1499,8 @@ __global__ __launch_bounds__(NT) void mlp_ppo_rows_kernel(const MlpArgs a) {
   else mlp_rows<1, false, RELU>(a, *reinterpret_cast<SmemR<1>*>(smem_raw));
 }
 
+#include "mlp_mc.h"
+
 template <int INP, int NAP, int RELU>
 __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
   static_assert(sizeof(Smem<INP, NAP>) <= 160 * 1024, "LDS budget");
@@ -1520,7 +1525,17 @@ extern "C" int rai_mlp_debug_stamps(unsigned long long* host_out) {
 
 namespace {
 constexpr int64_t XCHG_BYTES = 256;  // exchange words (first 64 B zeroed per launch), padded
-constexpr int64_t SCRATCH_BYTES = 2LL * NW * (MAXOUT + 2 + 4) * HID * sizeof(float);
+constexpr int64_t SCRATCH_ROWS = 2LL * NW * (MAXOUT + 2 + 4) * HID * sizeof(float);
+constexpr int64_t SCRATCH_MC = 2LL * 2 * MC_G * MC_SLOT * sizeof(float);
+constexpr int64_t SCRATCH_BYTES = SCRATCH_ROWS > SCRATCH_MC ? SCRATCH_ROWS : SCRATCH_MC;
+
+// Kernel layout for the CartPole class (diagnostics / A-B only: RAI_MLP_LAYOUT=rows|chunk|mc)
+int mlp_layout() {
+  const char* e = getenv("RAI_MLP_LAYOUT");
+  if (e && !strcmp(e, "rows")) return 1;
+  if (e && !strcmp(e, "chunk")) return 2;
+  return 0;  // multi-CU
+}
 
 int64_t num_minibatches(int64_t n_rows, int32_t batch_size) {
   return batch_size > 0 ? (n_rows + batch_size - 1) / batch_size : 0;
@@ -1544,7 +1559,7 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
   a.xchg = reinterpret_cast<unsigned long long*>(workspace);
   a.err = &a.state->err;
   hipStream_t s = rai_stream(stream);
-  hipError_t e = hipMemsetAsync(workspace, 0, 64, s);
+  hipError_t e = hipMemsetAsync(workspace, 0, XCHG_BYTES, s);
   a.scratch = reinterpret_cast<float*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES);
   if (e != hipSuccess) return (int)e;
   if (!a.moments) {
@@ -1555,10 +1570,17 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
     RAI_LAUNCH_CHECK();
     a.moments = mom;
   }
-  if (a.in_dim <= 4 && a.n_act <= 2) {
-    // row-tile layout (one pass over <= 256 rows)
+  const int layout = mlp_layout();
+  if (a.in_dim <= 4 && a.n_act <= 2 && layout == 0) {
+    // multi-CU layout: MC_G CUs per network, partial-gradient all-reduce per minibatch
+    if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_mc_kernel<1>), dim3(MC_GRID), dim3(MC_NT), 0, s, a);
+    else hipLaunchKernelGGL((mlp_ppo_mc_kernel<0>), dim3(MC_GRID), dim3(MC_NT), 0, s, a);
+  } else if (a.in_dim <= 4 && a.n_act <= 2 && layout == 1) {
+    // row-tile layout on one CU per network (one pass over <= 256 rows)
     if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_rows_kernel<1>), dim3(2), dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((mlp_ppo_rows_kernel<0>), dim3(2), dim3(NT), 0, s, a);
+  } else if (a.in_dim <= 4 && a.n_act <= 2) {
+    launch_epoch<4, 2>(a, s);
   } else {
     launch_epoch<8, 8>(a, s);
   }

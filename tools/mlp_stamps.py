@@ -21,9 +21,14 @@ from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
 from rl_algo_impls_amd.ppo import PPO  # noqa: E402
 from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 
-NAMES = ["F1 layer1 (wave-local)", "F2 layer2 + epilogue", "out layer + loss + dZ2", "dH1 MFMA",
-         "dZ1/partials + barrier", "P_B dW2 MFMA", "E2 owner sums + norm", "E3 stats + exchange",
-         "E4 adam"]  # row-tile layout (in_dim <= 4, n_actions <= 2)
+LAYOUT = os.environ.get("RAI_MLP_LAYOUT", "mc")
+NAMES = {
+    "mc": ["F1+F2 forward", "out layer + loss + dZ2", "dH1 + partials + barrier", "P_B dW2 + sums",
+           "publish + counter wait", "reduce G slots + |g|^2", "stats + norm exchange", "adam"],
+    "rows": ["F1 layer1 (wave-local)", "F2 layer2 + epilogue", "out layer + loss + dZ2", "dH1 MFMA",
+             "dZ1/partials + barrier", "P_B dW2 MFMA", "E2 owner sums + norm", "E3 stats + exchange",
+             "E4 adam"],
+}[LAYOUT]
 dev = torch.device("cuda", 0)
 torch.manual_seed(1)
 env = SyntheticVecEnv(4096, "cartpole", seed=1)
