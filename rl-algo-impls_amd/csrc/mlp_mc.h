@@ -102,6 +102,18 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4 as_f4(u4v v) { return __builtin_bit_cast(f4, v); }
 __device__ __forceinline__ u4v as_u4(f4 v) { return __builtin_bit_cast(u4v, v); }
 
+// torch Adam step (m, v, denom = sqrt(v)/sqrt(bc2) + eps, p -= lr/bc1 * m/denom) with the
+// hardware sqrt / reciprocal (1 ulp each) instead of the IEEE-exact sequences: ~1e-7 relative
+// on the update, inside the fp32 tolerance the parity tests state.
+__device__ __forceinline__ void adam_update_fast(float& p, float& m, float& v, float g, float w1, float w2,
+                                                 float beta2, float inv_bc2_sqrt, float neg_step, float eps) {
+  m = m + w1 * (g - m);
+  v = v * beta2;
+  v = v + (w2 * g) * g;
+  const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2_sqrt + eps;
+  p = p + neg_step * (m * __builtin_amdgcn_rcpf(denom));
+}
+
 template <int OUTP, bool ACTOR, int RELU>
 __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const int c) {
   constexpr int net = ACTOR ? 0 : 1;
@@ -429,10 +441,12 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     }
     {
       RELANE();
+      // sum over the 4 lane groups (lanes l, l^16, l^32, l^48) with VALU lane swaps
       auto red4 = [&](float v) {
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        return v;
+        const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(a16[0]) + __uint_as_float(a16[1]);
+        const auto a32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(a32[0]) + __uint_as_float(a32[1]);
       };
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -658,7 +672,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       const float total_norm = (float)sqrt((double)S.bcast[0] + (double)S.bcast[1]);
       float coef = 1.f;
       if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
-      const float bc2_sqrt = S.bcast[2], neg_step = S.bcast[3];
+      const float inv_bc2_sqrt = 1.f / S.bcast[2], neg_step = S.bcast[3];
       const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
       RELANE();
 #pragma unroll
@@ -669,7 +683,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float pq = p[q], mq = mreg[i][q], vq = vreg[i][q];
-            adam_update(pq, mq, vq, gr[i][q] * coef, w1, w2, beta2, bc2_sqrt, neg_step, adam_eps);
+            adam_update_fast(pq, mq, vq, gr[i][q] * coef, w1, w2, beta2, inv_bc2_sqrt, neg_step, adam_eps);
             p[q] = pq;
             mreg[i][q] = mq;
             vreg[i][q] = vq;
