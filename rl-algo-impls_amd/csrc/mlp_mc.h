@@ -38,7 +38,7 @@ constexpr int WL_W3 = WL_B2 + HID;         // [OUTP][LD]
 constexpr int WL_N = 4752;                 // >= WL_W3 + 2 * LD + 8, multiple of 16
 constexpr int WL_CH = WL_N / 4;            // float4 chunks
 constexpr int MC_CPT = (WL_CH + MC_NT - 1) / MC_NT;  // chunks owned per thread
-constexpr int MC_SLOT = WL_N + 16;         // + 4 doubles of loss statistics (+ pad)
+constexpr int MC_SLOT = WL_N;
 static_assert(WL_W3 + 2 * LD + 8 <= WL_N, "weight layout");
 
 // sync words (u64) at the start of the workspace, zeroed before every launch
@@ -102,6 +102,47 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4 as_f4(u4v v) { return __builtin_bit_cast(f4, v); }
 __device__ __forceinline__ u4v as_u4(f4 v) { return __builtin_bit_cast(u4v, v); }
 
+// Wave-wide sums on the VALU (DPP row butterflies + lane swaps) instead of ds_bpermute shuffles:
+// a fixed combination order in which every lane ends with the same bits.
+__device__ __forceinline__ float wave_sum_v(float v) {
+  v = row_sum16(v);
+  const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a16[0]) + __uint_as_float(a16[1]);
+  const auto a32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a32[0]) + __uint_as_float(a32[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double swap_d16(double v, bool s32) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  unsigned lo0, lo1, hi0, hi1;
+  if (s32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    lo0 = l[0]; lo1 = l[1]; hi0 = h[0]; hi1 = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    lo0 = l[0]; lo1 = l[1]; hi0 = h[0]; hi1 = h[1];
+  }
+  return __builtin_bit_cast(double, ((unsigned long long)hi0 << 32) | lo0) +
+         __builtin_bit_cast(double, ((unsigned long long)hi1 << 32) | lo1);
+}
+__device__ __forceinline__ double wave_sum_v(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  v = swap_d16(v, false);
+  return swap_d16(v, true);
+}
+
 // torch Adam step (m, v, denom = sqrt(v)/sqrt(bc2) + eps, p -= lr/bc1 * m/denom) with the
 // hardware sqrt / reciprocal (1 ulp each) instead of the IEEE-exact sequences: ~1e-7 relative
 // on the update, inside the fp32 tolerance the parity tests state.
@@ -137,6 +178,8 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
   float* const slots = a.scratch;  // [2 nets][2 parities][MC_G][MC_SLOT]
   const int slot_bytes = 2 * 2 * MC_G * MC_SLOT * (int)sizeof(float);
   const __amdgpu_buffer_rsrc_t srs = mc_rsrc(slots, slot_bytes);
+  const int nmb_all = (int)((a.n_rows + a.batch - 1) / a.batch);
+  const __amdgpu_buffer_rsrc_t str = mc_rsrc(a.statp, 2 * nmb_all * MC_G * 32);
 
   const int szA = HID * IN + HID + HID * HID + HID + NA * HID + NA;
   const int base = net == 0 ? 0 : szA;
@@ -464,12 +507,12 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       }
 #pragma unroll
       for (int o = 0; o < OUTP; ++o) {
-        const float t3 = wave_sum(li < 4 ? dq[o] : 0.f);
+        const float t3 = wave_sum_v(li < 4 ? dq[o] : 0.f);
         if (lane == 0) S.db3p[w][o] = t3;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const double t = wave_sum((double)st[i]);
+        const double t = wave_sum_v((double)st[i]);
         if (lane == 0) S.st[w][i] = t;
       }
     }
@@ -540,15 +583,16 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
           __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), srs, sbase + 16 * ch, 0, 16);
         }
       }
-      if (tid == 0) {  // this CU's loss statistics (4 doubles) in the slot tail
+      if (tid == 0) {  // this CU's loss statistics (4 doubles); CU 0 turns them into rows at the end
         double sv[4] = {0.0, 0.0, 0.0, 0.0};
         for (int q = 0; q < MC_NW; ++q)
 #pragma unroll
           for (int i = 0; i < 4; ++i) sv[i] += S.st[q][i];
         const u4v p0 = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){sv[0], sv[1]});
         const u4v p1 = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){sv[2], sv[3]});
-        __builtin_amdgcn_raw_buffer_store_b128(p0, srs, sbase + 4 * WL_N, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(p1, srs, sbase + 4 * WL_N + 16, 0, 16);
+        const int so = ((net * nmb + kk_mb) * MC_G + c) * 32;
+        __builtin_amdgcn_raw_buffer_store_b128(p0, str, so, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(p1, str, so + 16, 0, 16);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
     }
@@ -589,7 +633,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
           for (int q = 0; q < 4; ++q) ss += (double)sum[q] * sum[q];
         }
       }
-      ss = wave_sum(ss);
+      ss = wave_sum_v(ss);
       if (lane == 0) S.red[w] = ss;
       if (grads_mode && c == 0) {  // raw gradients out in flat order (one CU per network)
 #pragma unroll
@@ -611,35 +655,6 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     if (tid == 0) {
       double ssum = 0.0;
       for (int q = 0; q < MC_NW; ++q) ssum += S.red[q];
-      const int srow = stat0 + kk_mb;
-      if (c == 0 && a.stats && srow < a.max_stats) {
-        const int pbase = (net * 2 + par) * MC_G * MC_SLOT * (int)sizeof(float);
-        double sv[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int cc = 0; cc < MC_G; ++cc) {
-          const u4v p0 = __builtin_amdgcn_raw_buffer_load_b128(srs, pbase + cc * MC_SLOT * 4 + 4 * WL_N, 0, 16);
-          const u4v p1 = __builtin_amdgcn_raw_buffer_load_b128(srs, pbase + cc * MC_SLOT * 4 + 4 * WL_N + 16, 0, 16);
-          const auto d0 = __builtin_bit_cast(double __attribute__((ext_vector_type(2))), p0);
-          const auto d1 = __builtin_bit_cast(double __attribute__((ext_vector_type(2))), p1);
-          sv[0] += d0[0];
-          sv[1] += d0[1];
-          sv[2] += d1[0];
-          sv[3] += d1[1];
-        }
-        float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
-        const double Bd = (double)rows * (double)a.world;
-        if (ACTOR) {
-          const float pi_loss = (float)(-sv[0] / Bd);
-          const float ent_loss = (float)(-sv[3] / Bd);
-          row[0] = pi_coef * pi_loss + ent_coef * ent_loss;  // host adds the value term
-          row[1] = pi_loss;
-          row[2] = ent_loss;
-          row[3] = (float)(sv[1] / Bd);
-          row[4] = (float)(sv[2] / Bd);
-        } else {
-          row[5] = (float)(sv[0] / Bd) * halve;
-          row[5 + RAI_MAX_K] = has_vclip ? (float)(sv[1] / Bd) : 0.f;
-        }
-      }
       if (!grads_mode) {
         const float mine = (float)ssum;
         const unsigned tag = (unsigned)(kk_mb + 1);
@@ -697,6 +712,42 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     STAMP(8);
   }
 
+  // ---- stats rows of every minibatch (CU 0): sum the CUs' partials in CU order ---------------------
+  // (every CU published minibatch k's partial before the counter wait CU 0 passed for k)
+  if (c == 0 && !S.bail && a.stats) {
+    for (int k = tid; k < nmb; k += MC_NT) {
+      const int srow = stat0 + k;
+      if (srow >= a.max_stats) continue;
+      const int64_t r0 = (int64_t)(mb_begin + k) * B;
+      const int rws = (int)min((int64_t)B, n_rows - r0);
+      double sv[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int cc = 0; cc < MC_G; ++cc) {
+        const int so = ((net * nmb + k) * MC_G + cc) * 32;
+        const auto d0 = __builtin_bit_cast(double __attribute__((ext_vector_type(2))),
+                                           __builtin_amdgcn_raw_buffer_load_b128(str, so, 0, 16));
+        const auto d1 = __builtin_bit_cast(double __attribute__((ext_vector_type(2))),
+                                           __builtin_amdgcn_raw_buffer_load_b128(str, so + 16, 0, 16));
+        sv[0] += d0[0];
+        sv[1] += d0[1];
+        sv[2] += d1[0];
+        sv[3] += d1[1];
+      }
+      float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
+      const double Bd = (double)rws * (double)a.world;
+      if (ACTOR) {
+        const float pi_loss = (float)(-sv[0] / Bd);
+        const float ent_loss = (float)(-sv[3] / Bd);
+        row[0] = pi_coef * pi_loss + ent_coef * ent_loss;  // host adds the value term
+        row[1] = pi_loss;
+        row[2] = ent_loss;
+        row[3] = (float)(sv[1] / Bd);
+        row[4] = (float)(sv[2] / Bd);
+      } else {
+        row[5] = (float)(sv[0] / Bd) * halve;
+        row[5 + RAI_MAX_K] = has_vclip ? (float)(sv[1] / Bd) : 0.f;
+      }
+    }
+  }
   // ---- write back parameters and optimizer moments (CU 0 of each network) -----------------------
   if (!grads_mode && c == 0) {
 #pragma unroll

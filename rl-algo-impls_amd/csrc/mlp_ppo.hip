@@ -77,8 +77,11 @@ struct MlpArgs {
   int32_t* err;
   // per-minibatch (mean, den) of the advantage normalisation: moments[2*mb], moments[2*mb+1]
   const float* moments;
-  // row-tile layout only: per-wave partial gradients [2 nets][NW][parts][64] (workspace)
+  // row-tile layout: per-wave partial gradients [2 nets][NW][parts][64]; multi-CU layout: the
+  // exchange slots (workspace)
   float* scratch;
+  // multi-CU layout: per-CU loss-statistic partials [2 nets][minibatches][MC_G][4] (workspace)
+  double* statp;
   // data-parallel "grads" mode (grad_out != nullptr): process minibatches
   // [mb_begin, mb_begin + mb_count), scale the loss means by 1/(rows*world), write the
   // raw gradients to grad_out and stop (the caller all-reduces them and runs
@@ -1540,6 +1543,12 @@ int mlp_layout() {
 int64_t num_minibatches(int64_t n_rows, int32_t batch_size) {
   return batch_size > 0 ? (n_rows + batch_size - 1) / batch_size : 0;
 }
+int64_t moments_bytes(int64_t n_rows, int32_t batch_size) {
+  return ((8 * num_minibatches(n_rows, batch_size) + 255) / 256) * 256;
+}
+int64_t statp_bytes(int64_t n_rows, int32_t batch_size) {
+  return 2 * num_minibatches(n_rows, batch_size) * MC_G * 4 * (int64_t)sizeof(double);
+}
 
 int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, void* workspace,
                int64_t workspace_bytes, void* stream) {
@@ -1570,6 +1579,8 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
     RAI_LAUNCH_CHECK();
     a.moments = mom;
   }
+  a.statp = reinterpret_cast<double*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES + SCRATCH_BYTES +
+                                      moments_bytes(n_rows, batch_size));
   const int layout = mlp_layout();
   if (a.in_dim <= 4 && a.n_act <= 2 && layout == 0) {
     // multi-CU layout: MC_G CUs per network, partial-gradient all-reduce per minibatch
@@ -1590,8 +1601,7 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
 }  // namespace
 
 extern "C" int64_t rai_mlp_ppo_workspace_bytes(int64_t n_rows, int32_t batch_size) {
-  const int64_t mom = 8 * num_minibatches(n_rows, batch_size);
-  return XCHG_BYTES + SCRATCH_BYTES + ((mom + 255) / 256) * 256;
+  return XCHG_BYTES + SCRATCH_BYTES + moments_bytes(n_rows, batch_size) + statp_bytes(n_rows, batch_size);
 }
 
 extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
