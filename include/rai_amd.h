@@ -36,6 +36,7 @@ enum {
   RAI_E_TOO_MANY_COLUMNS = -4,
   RAI_E_WORKSPACE = -5,
   RAI_E_UNSUPPORTED = -6,
+  RAI_E_DP_BASE = -1000, /* RCCL failure r is reported as RAI_E_DP_BASE - r */
 };
 
 int rai_abi_version(void);
@@ -217,6 +218,34 @@ int rai_mlp_ppo_grads(const float* params, const float* obs, const int64_t* acti
                       const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
                       rai_train_state* state, float* grad_out, float* stats, int32_t max_stats,
                       void* workspace, int64_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------------------------------
+ * Data-parallel runtime: one process per GPU, an RCCL
+ * communicator over xGMI, and the natively driven per-minibatch loop
+ *   rai_mlp_ppo_grads -> in-place sum all-reduce of the flat gradient -> rai_clip_optim_step
+ * for one epoch (replaces the single-process optimizer loop of
+ * rl_algo_impls/ppo/ppo.py:290-411; every rank applies the identical update).
+ * RCCL is resolved at run time from the process's librccl.so.1 (the one PyTorch-ROCm
+ * maps); rai_dp_available() reports whether it was found.  The unique id is created
+ * on rank 0 and shipped to the other ranks by the caller (e.g. torch.distributed).
+ * grads: flat fp32 buffer of P elements (same order as params).  moments: global
+ * per-minibatch (mean, den) pairs as for rai_mlp_ppo_grads.
+ * ------------------------------------------------------------------------ */
+#define RAI_DP_UID_BYTES 128
+int rai_dp_available(void);
+int rai_dp_unique_id(void* out, int32_t out_bytes);
+int rai_dp_comm_init(void** comm_out, const void* uid_bytes, int32_t world, int32_t rank);
+int rai_dp_comm_destroy(void* comm);
+int rai_dp_allreduce_sum_f32(void* comm, float* buf, int64_t n, void* stream);
+int rai_mlp_ppo_epoch_dp(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t P,
+                         const float* obs, const int64_t* actions, const float* old_logp,
+                         const float* old_values, const float* advantages, const float* returns,
+                         int64_t n_rows, int32_t batch_size, const float* moments, int32_t world,
+                         int32_t in_dim, int32_t hidden, int32_t n_actions, int32_t activation,
+                         const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
+                         rai_train_state* state, float* stats, int32_t max_stats, float* norms,
+                         int32_t max_norms, void* comm, void* workspace, int64_t workspace_bytes,
+                         void* optim_workspace, int64_t optim_workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

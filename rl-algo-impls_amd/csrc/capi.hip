@@ -15,5 +15,6 @@ extern "C" const char* rai_strerror(int code) {
     default: break;
   }
   if (code > 0) return hipGetErrorString(static_cast<hipError_t>(code));
+  if (code <= RAI_E_DP_BASE) return "RCCL call failed (ncclResult_t = RAI_E_DP_BASE - code)";
   return "unknown error";
 }

@@ -79,9 +79,10 @@ class PPO:
         self._mlp_ws: Optional[torch.Tensor] = None
         self.dp_group = None
         self.world = 1
+        self._dp_comm = None
 
     # -- data parallel (one process per GPU) ------------------------------------------------
-    def enable_data_parallel(self, group=None) -> None:
+    def enable_data_parallel(self, group=None, native_dp: bool = True) -> None:
         """Weak-scaling data parallelism: every rank owns its own env group and HBM rollout;
         a global minibatch is the union of the ranks' minibatch slices, gradients are summed
         over ranks with one RCCL all-reduce per optimizer step (rccl/xGMI via
@@ -93,6 +94,9 @@ class PPO:
 
         self.dp_group = group
         self.world = dist.get_world_size(group)
+        self._dp_comm = None
+        if self.flat.flat.is_cuda and dist.get_backend(group) == "nccl" and native_dp:
+            self._dp_comm = self._native_comm(group)
         with torch.no_grad():  # identical starting weights everywhere
             src = dist.get_global_rank(group, 0) if group is not None else 0
             if self.flat.flat.is_cuda and dist.get_backend(group) == "gloo":
@@ -101,6 +105,29 @@ class PPO:
                 self.flat.flat.copy_(h)
             else:
                 dist.broadcast(self.flat.flat, src=src, group=group)
+
+    def _native_comm(self, group):
+        """An RCCL communicator of our own (same ranks as `group`) for the natively driven
+        per-minibatch loop (rai_mlp_ppo_epoch_dp); the unique id travels over `group`."""
+        import ctypes as C
+
+        import torch.distributed as dist
+
+        L = _lib.lib()
+        if not L.rai_dp_available():
+            raise RuntimeError("librccl.so.1 is not mapped in this process: native data parallelism unavailable")
+        uid = torch.zeros(_lib.RAI_DP_UID_BYTES, dtype=torch.uint8)
+        if dist.get_rank(group) == 0:
+            buf = (C.c_uint8 * _lib.RAI_DP_UID_BYTES)()
+            _lib.check(L.rai_dp_unique_id(buf, _lib.RAI_DP_UID_BYTES), "rai_dp_unique_id")
+            uid.copy_(torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8))
+        dev_uid = uid.to(self.device)
+        dist.broadcast(dev_uid, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        raw = bytes(dev_uid.cpu().numpy().tobytes())
+        comm = C.c_void_p()
+        torch.cuda.synchronize(self.device)
+        _lib.check(L.rai_dp_comm_init(C.byref(comm), raw, self.world, dist.get_rank(group)), "rai_dp_comm_init")
+        return comm
 
     def _all_reduce(self, t: torch.Tensor, average: bool = False) -> None:
         import torch.distributed as dist
@@ -158,6 +185,20 @@ class PPO:
             moments = self._global_adv_moments(b.advantages, nmb)
             obs = (b.obs if b.obs.dtype == torch.float32 else b.obs.float()).contiguous()
             acts = b.actions.contiguous()
+            if self._dp_comm is not None:  # natively driven: grads -> RCCL all-reduce -> clip+Adam
+                f = self.flat
+                rc = L.rai_mlp_ppo_epoch_dp(
+                    f.flat.data_ptr(), f.grad.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), f.P,
+                    obs.data_ptr(), acts.data_ptr(), b.logprobs.data_ptr(), b.values.data_ptr(),
+                    b.advantages.data_ptr(), b.returns.data_ptr(), r.total_steps, self.batch_size,
+                    moments.data_ptr(), self.world, spec["in_dim"], 64, spec["n_act"], spec["activation"],
+                    blocks.hp.data_ptr(), opt.hp_dev.data_ptr(), blocks.state.data_ptr(), blocks.stats.data_ptr(),
+                    int(blocks.stats.shape[0]), blocks.norms.data_ptr(), int(blocks.norms.shape[0]), self._dp_comm,
+                    self._mlp_ws.data_ptr(), self._mlp_ws.numel(), opt.workspace.data_ptr(), opt.workspace.numel(),
+                    st)
+                _lib.check(rc, "rai_mlp_ppo_epoch_dp")
+                opt.step_count += nmb
+                continue
             for i in range(nmb):
                 rc = L.rai_mlp_ppo_grads(
                     self.flat.flat.data_ptr(), obs.data_ptr(), acts.data_ptr(), b.logprobs.data_ptr(),

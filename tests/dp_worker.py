@@ -8,12 +8,18 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
 
-def _init(rank, world, port):
+def _init(rank, world, port, backend="gloo"):
+    import torch
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
 def moments_worker(rank, world, port, q):
@@ -46,12 +52,13 @@ def moments_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def fused_dp_worker(rank, world, port, q):
-    """DP fused update on rank-local data (gloo, all ranks on cuda:0)."""
+def fused_dp_worker(rank, world, port, q, backend="gloo"):
+    """DP fused update on rank-local data (gloo: all ranks on cuda:0, Python-driven loop;
+    nccl (world 1 on a one-GPU box): the natively driven RCCL loop, rai_mlp_ppo_epoch_dp)."""
     import numpy as np
     import torch
 
-    _init(rank, world, port)
+    _init(rank, world, port, backend)
     import _pkgload
 
     _pkgload.load()
@@ -64,6 +71,7 @@ def fused_dp_worker(rank, world, port, q):
     policy = nets.build("cartpole").to(dev)
     algo = PPO(policy, dev, None, batch_size=128, n_epochs=2, learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
     algo.enable_data_parallel()
+    assert (algo._dp_comm is not None) == (backend == "nccl")
     data = make_rank_data(rank, dev)
 
     class R:

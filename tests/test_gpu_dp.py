@@ -77,3 +77,36 @@ def test_fused_dp_world2_matches_single_process_global_minibatches():
     np.testing.assert_allclose(n0, norms, rtol=1e-4)
     np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)
+
+
+def _run_world1(backend):
+    import queue
+    import time
+
+    import dp_worker
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=dp_worker.fused_dp_worker, args=(0, 1, _port(), q, backend))
+    p.start()
+    deadline = time.time() + 240
+    while True:
+        try:
+            res = q.get(timeout=2)
+            break
+        except queue.Empty:
+            assert p.exitcode in (None, 0), f"worker exited with {p.exitcode}"
+            assert time.time() < deadline, "worker did not report in time"
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    return res
+
+
+def test_native_rccl_epoch_loop_matches_python_loop_world1():
+    """rai_mlp_ppo_epoch_dp (RCCL communicator, natively driven per-minibatch loop) against the
+    Python-driven loop over the same kernels (gloo): identical operations, identical bits."""
+    _, pn, sn, nn = _run_world1("nccl")
+    _, pg, sg, ng = _run_world1("gloo")
+    np.testing.assert_array_equal(pn, pg)
+    np.testing.assert_array_equal(nn, ng)
+    np.testing.assert_array_equal(sn, sg)
