@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--roofline-reps", type=int, default=200)
     p.add_argument("--num-envs", type=int, default=None, help="override (rehearsal/debug only; not a bench line)")
+    p.add_argument("--dp-rehearsal", action="store_true",
+                   help="single process: run the data-parallel update path over a 1-rank RCCL group "
+                        "(measures the per-step DP machinery; not a bench line)")
     return p.parse_args()
 
 
@@ -80,6 +83,11 @@ def main():
     backend = os.environ.get("RAI_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI; gloo only to rehearse
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local_rank % max(ndev, 1))
+    if args.dp_rehearsal and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        torch.cuda.set_device(dev)
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     if world > 1:
         torch.cuda.set_device(dev)
         if backend == "nccl":
@@ -104,7 +112,7 @@ def main():
                 torch.distributed.broadcast(p.data, 0)
     gen = SyncStepRolloutGenerator(policy, env, n_steps=T, seed=1234 + rank)
     algo = PPO(policy, dev, None, **algo_kw)
-    if world > 1:
+    if world > 1 or args.dp_rehearsal:
         algo.enable_data_parallel()
 
     def barrier():
@@ -216,8 +224,10 @@ def main():
             "roofline_gae": roof_gae,
             "cpu_baseline": cpu,
         }
+        if args.dp_rehearsal or world > 1:
+            line["dp_path"] = "native RCCL loop" if algo._dp_comm is not None else "python loop (" + backend + ")"
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

@@ -229,7 +229,11 @@ int rai_mlp_ppo_grads(const float* params, const float* obs, const int64_t* acti
  * maps); rai_dp_available() reports whether it was found.  The unique id is created
  * on rank 0 and shipped to the other ranks by the caller (e.g. torch.distributed).
  * grads: flat fp32 buffer of P elements (same order as params).  moments: global
- * per-minibatch (mean, den) pairs as for rai_mlp_ppo_grads.
+ * per-minibatch (mean, den) pairs as for rai_mlp_ppo_grads.  grads_alt (optional, P
+ * elements): with it, CartPole-class policies take the two-launch step (the multi-CU
+ * kernel applies the previous all-reduced gradient, then computes the next partial one;
+ * one RCCL all-reduce per step); without it, or for other shapes, each step is
+ * rai_mlp_ppo_grads -> all-reduce -> rai_clip_optim_step.
  * ------------------------------------------------------------------------ */
 #define RAI_DP_UID_BYTES 128
 int rai_dp_available(void);
@@ -244,8 +248,9 @@ int rai_mlp_ppo_epoch_dp(float* params, float* grads, float* exp_avg, float* exp
                          int32_t in_dim, int32_t hidden, int32_t n_actions, int32_t activation,
                          const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
                          rai_train_state* state, float* stats, int32_t max_stats, float* norms,
-                         int32_t max_norms, void* comm, void* workspace, int64_t workspace_bytes,
-                         void* optim_workspace, int64_t optim_workspace_bytes, void* stream);
+                         int32_t max_norms, void* comm, float* grads_alt, void* workspace,
+                         int64_t workspace_bytes, void* optim_workspace, int64_t optim_workspace_bytes,
+                         void* stream);
 
 #ifdef __cplusplus
 }

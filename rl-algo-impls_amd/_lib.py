@@ -99,7 +99,7 @@ _SIGNATURES = {
     "rai_dp_allreduce_sum_f32": (C.c_int, [_vp, _vp, _i64, _vp]),
     "rai_mlp_ppo_epoch_dp": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp,
                                        _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp,
-                                       _vp, _i64, _vp, _i64, _vp]),
+                                       _vp, _vp, _i64, _vp, _i64, _vp]),
 }
 RAI_DP_UID_BYTES = 128
 EXPORTED = tuple(_SIGNATURES)

@@ -62,6 +62,19 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch) {
   __syncthreads();
 }
 
+// beta^n for the Adam bias corrections by binary exponentiation: <= 2*log2(n) double
+// multiplies (a few ulps from libm's pow, far below fp32) instead of the double-precision
+// pow() sequence, which costs tens of microseconds of FP64 work per launch.
+__device__ __forceinline__ double ipow(double b, long long n) {
+  double r = 1.0;
+  while (n > 0) {
+    if (n & 1) r *= b;
+    b *= b;
+    n >>= 1;
+  }
+  return r;
+}
+
 // ---- Philox4x32-10 counter RNG ---------------------------------------------
 struct Philox4 {
   uint32_t x, y, z, w;

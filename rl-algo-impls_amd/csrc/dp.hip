@@ -59,6 +59,16 @@ int rccl_rc(int r) { return r == 0 ? RAI_OK : RAI_E_DP_BASE - r; }
 
 }  // namespace
 
+// mlp_ppo.hip (C++ linkage): multi-CU grads kernel that first applies the previous all-reduced step
+int rai_mlp_ppo_dp_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grad_in, int32_t P_total,
+                        const float* obs, const int64_t* actions, const float* old_logp, const float* old_values,
+                        const float* advantages, const float* returns, int64_t n_rows, int32_t batch_size,
+                        int32_t mb, int32_t mb_count, const float* moments, int32_t world, int32_t in_dim,
+                        int32_t hidden, int32_t n_actions, int32_t activation, const rai_ppo_hparams* hp,
+                        const rai_optim_hparams* ohp, rai_train_state* state, float* grad_out, float* stats,
+                        int32_t max_stats, float* norms, int32_t max_norms, int32_t sync_base, void* workspace,
+                        int64_t workspace_bytes, void* stream);
+
 extern "C" int rai_dp_available(void) { return rccl().ok ? 1 : 0; }
 
 extern "C" int rai_dp_unique_id(void* out, int32_t out_bytes) {
@@ -101,11 +111,35 @@ extern "C" int rai_mlp_ppo_epoch_dp(float* params, float* grads, float* exp_avg,
                                     int32_t in_dim, int32_t hidden, int32_t n_actions, int32_t activation,
                                     const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
                                     rai_train_state* state, float* stats, int32_t max_stats, float* norms,
-                                    int32_t max_norms, void* comm, void* workspace, int64_t workspace_bytes,
-                                    void* optim_workspace, int64_t optim_workspace_bytes, void* stream) {
+                                    int32_t max_norms, void* comm, float* grads_alt, void* workspace,
+                                    int64_t workspace_bytes, void* optim_workspace, int64_t optim_workspace_bytes,
+                                    void* stream) {
   if (!comm || !grads || !moments) return RAI_E_NULLPTR;
   if (batch_size < 1 || n_rows < 1 || P < 1) return RAI_E_SHAPE;
   const int64_t nmb = (n_rows + batch_size - 1) / batch_size;
+  if (grads_alt && P <= INT32_MAX) {
+    // Two launches per optimizer step: the multi-CU kernel applies step k-1's all-reduced gradient
+    // (clip + Adam on every CU's weight copy) and computes step k's partial gradient; RCCL sums it.
+    // The gradient buffers alternate so step k's kernel never overwrites what it is applying.
+    float* buf[2] = {grads, grads_alt};
+    int rc = RAI_OK;
+    for (int64_t mb = 0; mb <= nmb; ++mb) {
+      const float* gin = mb == 0 ? nullptr : buf[(mb - 1) & 1];
+      float* gout = buf[mb & 1];
+      rc = rai_mlp_ppo_dp_step(params, exp_avg, exp_avg_sq, gin, (int32_t)P, obs, actions, old_logp, old_values,
+                               advantages, returns, n_rows, batch_size, (int32_t)(mb < nmb ? mb : 0),
+                               mb < nmb ? 1 : 0, moments, world, in_dim, hidden, n_actions, activation, hp, ohp,
+                               state, gout, stats, max_stats, norms, max_norms, (int32_t)mb, workspace,
+                               workspace_bytes, stream);
+      if (rc == RAI_E_UNSUPPORTED && mb == 0) break;  // not the multi-CU layout: three-call loop below
+      if (rc != RAI_OK) return rc;
+      if (mb < nmb) {
+        rc = rai_dp_allreduce_sum_f32(comm, gout, P, stream);
+        if (rc != RAI_OK) return rc;
+      }
+    }
+    if (rc == RAI_OK) return RAI_OK;
+  }
   for (int64_t mb = 0; mb < nmb; ++mb) {
     int rc = rai_mlp_ppo_grads(params, obs, actions, old_logp, old_values, advantages, returns, n_rows, batch_size,
                                (int32_t)mb, 1, moments, world, in_dim, hidden, n_actions, activation, hp, ohp, state,

@@ -69,30 +69,32 @@ struct SmemM {
 template <int OUTP>
 __device__ __forceinline__ int wl_b3() { return WL_W3 + OUTP * LD; }
 
-// weight-layout index -> flat torch parameters() index of this network (-1: padding)
+// weight-layout index -> flat torch parameters() index of this network (-1: padding).
+// Branch-free (every region computed, the right one selected): per-lane branches here split the
+// gathers that use it into separate basic blocks, each waiting for its own load.
 template <int OUTP>
 __device__ __forceinline__ int wl_to_flat(int e, int IN, int OUT, int base) {
   const int fW1 = base, fb1 = fW1 + HID * IN, fW2 = fb1 + HID, fb2 = fW2 + HID * HID, fW3 = fb2 + HID,
             fb3 = fW3 + OUT * HID;
-  if (e < WL_B1) {
-    const int j = e >> 2, k = e & 3;
-    return k < IN ? fW1 + j * IN + k : -1;
-  }
-  if (e < WL_W2) return fb1 + (e - WL_B1);
-  if (e < WL_B2) {
-    const int q = e - WL_W2, j = q / LD, k = q % LD;
-    return k < HID ? fW2 + j * HID + k : -1;
-  }
-  if (e < WL_W3) return fb2 + (e - WL_B2);
-  if (e < wl_b3<OUTP>()) {
-    const int q = e - WL_W3, o = q / LD, k = q % LD;
-    return (o < OUT && k < HID) ? fW3 + o * HID + k : -1;
-  }
-  if (e < wl_b3<OUTP>() + 8) {
-    const int o = e - wl_b3<OUTP>();
-    return o < OUT ? fb3 + o : -1;
-  }
-  return -1;
+  constexpr int WL_B3 = WL_W3 + OUTP * LD;
+  const int j1 = e >> 2, k1 = e & 3;
+  const int r1 = k1 < IN ? fW1 + j1 * IN + k1 : -1;
+  const int r_b1 = fb1 + (e - WL_B1);
+  const int q2 = e - WL_W2, j2 = q2 / LD, k2 = q2 - j2 * LD;
+  const int r2 = k2 < HID ? fW2 + j2 * HID + k2 : -1;
+  const int r_b2 = fb2 + (e - WL_B2);
+  const int q3 = e - WL_W3, o3 = q3 / LD, k3 = q3 - o3 * LD;
+  const int r3 = (o3 < OUT && k3 < HID) ? fW3 + o3 * HID + k3 : -1;
+  const int o4 = e - WL_B3;
+  const int r4 = (o4 >= 0 && o4 < OUT) ? fb3 + o4 : -1;
+  int f = -1;
+  f = e < WL_B3 + 8 ? r4 : f;
+  f = e < WL_B3 ? r3 : f;
+  f = e < WL_W3 ? r_b2 : f;
+  f = e < WL_B2 ? r2 : f;
+  f = e < WL_W2 ? r_b1 : f;
+  f = e < WL_B1 ? r1 : f;
+  return f;
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mc_rsrc(const void* p, int bytes) {
@@ -155,6 +157,14 @@ __device__ __forceinline__ void adam_update_fast(float& p, float& m, float& v, f
   p = p + neg_step * (m * __builtin_amdgcn_rcpf(denom));
 }
 
+// Branch-free gather: the load is issued unconditionally (clamped index) and masked after, so
+// a run of them stays in one basic block with all loads in flight (a guarded load becomes a
+// branch, and the wait for its data is then placed before the next one is issued).
+__device__ __forceinline__ float ld_or0(const float* p, int f) {
+  const float v = p[f >= 0 ? f : 0];
+  return f >= 0 ? v : 0.f;
+}
+
 template <int OUTP, bool ACTOR, int RELU>
 __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const int c) {
   constexpr int net = ACTOR ? 0 : 1;
@@ -163,6 +173,9 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
   constexpr int WL_B3 = WL_W3 + OUTP * LD;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef RAI_STAMPS
+  const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+#endif
   const int IN = a.in_dim;
   const int NA = a.n_act;
   const int OUT = ACTOR ? NA : 1;
@@ -173,7 +186,9 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
   const float beta2 = a.ohp->beta2, adam_eps = a.ohp->eps, lr = a.ohp->lr;
   const double beta1_d = a.ohp->beta1_d, beta2_d = a.ohp->beta2_d;
   const bool grads_mode = a.grad_out != nullptr;
+  const bool apply_in = grads_mode && a.grad_in != nullptr;  // data-parallel step: apply grad_in first
   const float max_grad_norm = a.ohp->max_grad_norm;
+  const unsigned long long sbase = (unsigned long long)a.sync_base;
   unsigned long long* const sync = a.xchg;
   float* const slots = a.scratch;  // [2 nets][2 parities][MC_G][MC_SLOT]
   const int slot_bytes = 2 * 2 * MC_G * MC_SLOT * (int)sizeof(float);
@@ -185,30 +200,49 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
   const int base = net == 0 ? 0 : szA;
 
   // ---- weights -> LDS (weight layout); partial-gradient buffer zeroed (padding stays 0) -------
-  for (int e = tid; e < WL_N; e += MC_NT) {
-    const int f = wl_to_flat<OUTP>(e, IN, OUT, base);
-    S.Wt[e] = f >= 0 ? a.params[f] : 0.f;
-    S.Gb[e] = 0.f;
+  {
+    // fully unrolled so all ~19 loads per thread are in flight at once (a rolled loop waits for
+    // each load before the next: ~19 memory latencies, paid on every data-parallel launch)
+    constexpr int NE = (WL_N + MC_NT - 1) / MC_NT;
+    float wv[NE];
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + MC_NT * i;
+      const int f = e < WL_N ? wl_to_flat<OUTP>(e, IN, OUT, base) : -1;
+      wv[i] = ld_or0(a.params, f);
+    }
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + MC_NT * i;
+      if (e < WL_N) {
+        S.Wt[e] = wv[i];
+        S.Gb[e] = 0.f;
+      }
+    }
   }
   // ---- Adam moments of the owned chunks (chunk ch = tid + MC_NT * i), in registers -----------
+#ifdef RAI_STAMPS
+  const unsigned long long t_w = __builtin_amdgcn_s_memtime();
+#endif
   f4 mreg[MC_CPT], vreg[MC_CPT];
 #pragma unroll
   for (int i = 0; i < MC_CPT; ++i) {
     mreg[i] = f4{0.f, 0.f, 0.f, 0.f};
     vreg[i] = f4{0.f, 0.f, 0.f, 0.f};
     const int ch = tid + MC_NT * i;
-    if (!grads_mode && ch < WL_CH) {
+    if (!grads_mode || apply_in) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int f = wl_to_flat<OUTP>(4 * ch + q, IN, OUT, base);
-        if (f >= 0) {
-          mreg[i][q] = a.exp_avg[f];
-          vreg[i][q] = a.exp_avg_sq[f];
-        }
+        const int f = ch < WL_CH ? wl_to_flat<OUTP>(4 * ch + q, IN, OUT, base) : -1;
+        mreg[i][q] = ld_or0(a.exp_avg, f);
+        vreg[i][q] = ld_or0(a.exp_avg_sq, f);
       }
     }
   }
 
+#ifdef RAI_STAMPS
+  const unsigned long long t_mv = __builtin_amdgcn_s_memtime();
+#endif
   const int B = a.batch;
   const int64_t n_rows = a.n_rows;
   const int nmb_total = (int)((n_rows + B - 1) / B);
@@ -247,15 +281,94 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       r_d = a.moments[2 * mb + 1];
     }
   };
-  prefetch(mb_begin);
+  if (nmb > 0) prefetch(mb_begin);
   if (tid == 0) {
-    S.pw[0] = pow(beta1_d, (double)step0);
-    S.pw[1] = pow(beta2_d, (double)step0);
+    S.pw[0] = ipow(beta1_d, step0);
+    S.pw[1] = ipow(beta2_d, step0);
     S.bail = 0;
   }
+  __syncthreads();
+#ifdef RAI_STAMPS
+  const unsigned long long t_pre = __builtin_amdgcn_s_memtime();
+  unsigned long long t_ss = t_pre;
+#endif
+  if (apply_in) {
+    // ---- data-parallel step: clip_grad_norm_ + Adam with the previous step's all-reduced gradient.
+    // Every CU of both networks computes the same global norm over the same flat vector in the
+    // same order, so every copy of the weights gets the identical update. -----------------------
+    double ss = 0.0;
+    {
+      constexpr int U = 16;  // loads in flight per thread per batch
+      for (int i0 = tid; i0 < a.P_total; i0 += MC_NT * U) {
+        float gv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = i0 + u * MC_NT;
+          gv[u] = ld_or0(a.grad_in, i < a.P_total ? i : -1);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) ss += (double)gv[u] * gv[u];
+      }
+    }
+    ss = wave_sum_v(ss);
+    if (lane == 0) S.red[w] = ss;
+    __syncthreads();
+#ifdef RAI_STAMPS
+    t_ss = __builtin_amdgcn_s_memtime();
+#endif
+    double tot = 0.0;
+    for (int q = 0; q < MC_NW; ++q) tot += S.red[q];
+    const float total_norm = (float)sqrt(tot);
+    float coef = 1.f;
+    if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
+    const double bc1 = 1.0 - ipow(beta1_d, step0 + 1);
+    const double bc2 = 1.0 - ipow(beta2_d, step0 + 1);
+    const float inv_bc2_sqrt = 1.f / (float)sqrt(bc2), neg_step = (float)(-((double)lr / bc1));
+    const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
+    f4 gin[MC_CPT];  // all gathers first (one batch in flight), then the updates
+#pragma unroll
+    for (int i = 0; i < MC_CPT; ++i) {
+      const int ch = tid + MC_NT * i;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        gin[i][q] = ld_or0(a.grad_in, ch < WL_CH ? wl_to_flat<OUTP>(4 * ch + q, IN, OUT, base) : -1);
+    }
+#pragma unroll
+    for (int i = 0; i < MC_CPT; ++i) {
+      const int ch = tid + MC_NT * i;
+      if (ch < WL_CH) {
+        f4 p = *reinterpret_cast<const f4*>(&S.Wt[4 * ch]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int f = wl_to_flat<OUTP>(4 * ch + q, IN, OUT, base);
+          const float gq = gin[i][q];
+          float pq = p[q], mq = mreg[i][q], vq = vreg[i][q];
+          adam_update_fast(pq, mq, vq, gq * coef, w1, w2, beta2, inv_bc2_sqrt, neg_step, adam_eps);
+          if (f >= 0) {
+            p[q] = pq;
+            mreg[i][q] = mq;
+            vreg[i][q] = vq;
+          }
+        }
+        *reinterpret_cast<f4*>(&S.Wt[4 * ch]) = p;
+      }
+    }
+    if (ACTOR && c == 0 && tid == 0 && a.norms && norm0 < a.max_norms) a.norms[norm0] = total_norm;
+    __syncthreads();
+  }
+#ifdef RAI_STAMPS
+  const unsigned long long t_ap = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef RAI_STAMPS
   if (tid < 32) S.stamps[tid] = 0;
-  if (tid == 0) S.t_last = __builtin_amdgcn_s_memtime();
+  if (tid == 0) {
+    S.stamps[14] = t_w - t_entry;      // weights -> LDS
+    S.stamps[15] = t_mv - t_w;         // Adam moments -> registers
+    S.stamps[16] = t_pre - t_mv;       // prefetch issue, pw, barrier
+    S.stamps[17] = apply_in ? t_ss - t_pre : 0;  // apply: global |g|^2
+    S.stamps[18] = t_ap - (apply_in ? t_ss : t_pre);  // apply: Adam
+    S.t_last = __builtin_amdgcn_s_memtime();
+  }
 #endif
   __syncthreads();
 
@@ -599,7 +712,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     __syncthreads();
     if (tid == 0) {
       __hip_atomic_fetch_add(&sync[MC_CNT + net], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long want = (unsigned long long)MC_G * (unsigned long long)(kk_mb + 1);
+      const unsigned long long want = (unsigned long long)MC_G * (sbase + (unsigned long long)(kk_mb + 1));
       unsigned long long spins = 0;
       while (__hip_atomic_load(&sync[MC_CNT + net], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
         if (++spins > MC_SPINS) { atomicExch(a.err, 1); S.bail = 1; break; }
@@ -615,19 +728,24 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       RELANE();
       const int pbase = (net * 2 + par) * MC_G * MC_SLOT * (int)sizeof(float);
       double ss = 0.0;
+      // every load of the phase issued up front (clamped chunk index, masked after the sums)
+      f4 v[MC_CPT][MC_G];
+#pragma unroll
+      for (int i = 0; i < MC_CPT; ++i) {
+        const int chl = min(tid + MC_NT * i, WL_CH - 1);
+#pragma unroll
+        for (int cc = 0; cc < MC_G; ++cc)
+          v[i][cc] = as_f4(__builtin_amdgcn_raw_buffer_load_b128(
+              srs, pbase + cc * MC_SLOT * (int)sizeof(float) + 16 * chl, 0, 16));
+      }
 #pragma unroll
       for (int i = 0; i < MC_CPT; ++i) {
         const int ch = tid + MC_NT * i;
         gr[i] = f4{0.f, 0.f, 0.f, 0.f};
         if (ch < WL_CH) {
-          f4 v[MC_G];
+          f4 sum = v[i][0];
 #pragma unroll
-          for (int cc = 0; cc < MC_G; ++cc)
-            v[cc] = as_f4(__builtin_amdgcn_raw_buffer_load_b128(
-                srs, pbase + cc * MC_SLOT * (int)sizeof(float) + 16 * ch, 0, 16));
-          f4 sum = v[0];
-#pragma unroll
-          for (int cc = 1; cc < MC_G; ++cc) sum += v[cc];
+          for (int cc = 1; cc < MC_G; ++cc) sum += v[i][cc];
           gr[i] = sum;
 #pragma unroll
           for (int q = 0; q < 4; ++q) ss += (double)sum[q] * sum[q];
@@ -635,11 +753,11 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       }
       ss = wave_sum_v(ss);
       if (lane == 0) S.red[w] = ss;
-      if (grads_mode && c == 0) {  // raw gradients out in flat order (one CU per network)
+      if (grads_mode) {  // raw gradients out in flat order (every CU holds them: each writes 1/G)
 #pragma unroll
         for (int i = 0; i < MC_CPT; ++i) {
           const int ch = tid + MC_NT * i;
-          if (ch < WL_CH) {
+          if (ch < WL_CH && ch % MC_G == c) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int f = wl_to_flat<OUTP>(4 * ch + q, IN, OUT, base);
@@ -712,6 +830,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     STAMP(8);
   }
 
+  STAMP(12);
   // ---- stats rows of every minibatch (CU 0): sum the CUs' partials in CU order ---------------------
   // (every CU published minibatch k's partial before the counter wait CU 0 passed for k)
   if (c == 0 && !S.bail && a.stats) {
@@ -748,12 +867,12 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       }
     }
   }
-  // ---- write back parameters and optimizer moments (CU 0 of each network) -----------------------
-  if (!grads_mode && c == 0) {
+  // ---- write back parameters and optimizer moments -----------------------------------------------
+  if ((!grads_mode || apply_in) && !S.bail) {  // identical copies on every CU: each writes 1/G
 #pragma unroll
     for (int i = 0; i < MC_CPT; ++i) {
       const int ch = tid + MC_NT * i;
-      if (ch < WL_CH) {
+      if (ch < WL_CH && ch % MC_G == c) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int f = wl_to_flat<OUTP>(4 * ch + q, IN, OUT, base);
@@ -766,15 +885,17 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       }
     }
   }
+  STAMP(13);
 #ifdef RAI_STAMPS
-  if (c == 0 && tid < 32) g_stamps[net][tid] = S.stamps[tid];
+  if (c == 0 && tid < 32) atomicAdd(&g_stamps[net][tid], S.stamps[tid]);  // summed over launches
 #endif
   if (grads_mode && tid == 0) {  // the actor's CU 0 advances stat_index after every critic CU read it
     if (!ACTOR) {
       __hip_atomic_fetch_add(&sync[MC_DONE], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else if (c == 0) {
       unsigned long long spins = 0;
-      while (__hip_atomic_load(&sync[MC_DONE], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)MC_G) {
+      while (__hip_atomic_load(&sync[MC_DONE], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <
+             (unsigned long long)MC_G * (sbase + 1)) {
         if (++spins > MC_SPINS) { atomicExch(a.err, 1); break; }
         __builtin_amdgcn_s_sleep(1);
       }
@@ -785,6 +906,9 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     if (!grads_mode) {
       a.state->opt_step = step0 + nmb;
       a.state->norm_index = norm0 + nmb;
+    } else if (apply_in) {
+      a.state->opt_step = step0 + 1;
+      a.state->norm_index = norm0 + 1;
     }
   }
 }

@@ -90,6 +90,12 @@ struct MlpArgs {
   int32_t mb_begin;
   int32_t mb_count;
   int32_t world;
+  // multi-CU data-parallel step (grads mode only): before the minibatch, apply clip_grad_norm_ +
+  // Adam with the all-reduced flat gradient of the previous step (grad_in, P_total elements: both
+  // networks); sync_base = number of earlier launches since the sync words were last zeroed
+  const float* grad_in;
+  int32_t P_total;
+  int32_t sync_base;
 };
 
 #ifdef RAI_STAMPS
@@ -348,8 +354,8 @@ __device__ __forceinline__ void mlp_net(const MlpArgs& a, Smem<INP, OUTP>& S) {
   };
   prefetch(mb_begin);
   if (tid == 0) {  // running powers beta^step (bias corrections), advanced once per minibatch
-    S.pw[0] = pow(beta1_d, (double)step0);
-    S.pw[1] = pow(beta2_d, (double)step0);
+    S.pw[0] = ipow(beta1_d, step0);
+    S.pw[1] = ipow(beta2_d, step0);
   }
 #ifdef RAI_STAMPS
   if (tid < 32) S.stamps[tid] = 0;
@@ -1004,8 +1010,8 @@ __device__ __forceinline__ void mlp_rows(const MlpArgs& a, SmemR<OUTP>& S) {
   };
   prefetch(mb_begin);
   if (tid == 0) {
-    S.pw[0] = pow(beta1_d, (double)step0);
-    S.pw[1] = pow(beta2_d, (double)step0);
+    S.pw[0] = ipow(beta1_d, step0);
+    S.pw[1] = ipow(beta2_d, step0);
   }
 #ifdef RAI_STAMPS
   if (tid < 32) S.stamps[tid] = 0;
@@ -1562,15 +1568,17 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
   if (!a.grad_out && (!a.exp_avg || !a.exp_avg_sq)) return RAI_E_NULLPTR;
   if (workspace_bytes < rai_mlp_ppo_workspace_bytes(n_rows, batch_size)) return RAI_E_WORKSPACE;
   if (n_rows % batch_size == 1 && !a.moments) return RAI_E_SHAPE;  // 1-row minibatch: no std
-  if (a.grad_out && (int64_t)a.mb_begin * batch_size >= n_rows) return RAI_E_SHAPE;
+  if (a.grad_out && a.mb_count > 0 && (int64_t)a.mb_begin * batch_size >= n_rows) return RAI_E_SHAPE;
   a.n_rows = n_rows;
   a.batch = batch_size;
   a.xchg = reinterpret_cast<unsigned long long*>(workspace);
   a.err = &a.state->err;
   hipStream_t s = rai_stream(stream);
-  hipError_t e = hipMemsetAsync(workspace, 0, XCHG_BYTES, s);
+  if (a.sync_base == 0) {  // later launches of a data-parallel epoch keep counting on the same words
+    hipError_t e = hipMemsetAsync(workspace, 0, XCHG_BYTES, s);
+    if (e != hipSuccess) return (int)e;
+  }
   a.scratch = reinterpret_cast<float*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES);
-  if (e != hipSuccess) return (int)e;
   if (!a.moments) {
     float* mom = reinterpret_cast<float*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES + SCRATCH_BYTES);
     const int64_t nmb = num_minibatches(n_rows, batch_size);
@@ -1621,6 +1629,35 @@ extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_s
   a.stats = stats; a.max_stats = max_stats; a.norms = norms; a.max_norms = max_norms;
   a.grad_out = nullptr; a.moments = nullptr;
   a.mb_begin = 0; a.mb_count = 1 << 30; a.world = 1;
+  a.grad_in = nullptr; a.P_total = 0; a.sync_base = 0;
+  return mlp_launch(a, hidden, batch_size, n_rows, workspace, workspace_bytes, stream);
+}
+
+// Multi-CU data-parallel step (used by rai_mlp_ppo_epoch_dp): apply the previous all-reduced
+// gradient (grad_in; nullptr on the first step) then compute minibatch mb's partial gradient into
+// grad_out (mb_count 0: apply only).  Returns RAI_E_UNSUPPORTED for shapes outside the multi-CU
+// layout; the caller then uses the three-call sequence.
+int rai_mlp_ppo_dp_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grad_in, int32_t P_total,
+                        const float* obs, const int64_t* actions, const float* old_logp, const float* old_values,
+                        const float* advantages, const float* returns, int64_t n_rows, int32_t batch_size,
+                        int32_t mb, int32_t mb_count, const float* moments, int32_t world, int32_t in_dim,
+                        int32_t hidden, int32_t n_actions, int32_t activation, const rai_ppo_hparams* hp,
+                        const rai_optim_hparams* ohp, rai_train_state* state, float* grad_out, float* stats,
+                        int32_t max_stats, float* norms, int32_t max_norms, int32_t sync_base, void* workspace,
+                        int64_t workspace_bytes, void* stream) {
+  if (!(in_dim <= 4 && n_actions <= 2 && mlp_layout() == 0)) return RAI_E_UNSUPPORTED;
+  if (!grad_out || !moments || !exp_avg || !exp_avg_sq) return RAI_E_NULLPTR;
+  if (mb < 0 || mb_count < 0 || sync_base < 0) return RAI_E_SHAPE;
+  MlpArgs a = {};
+  a.params = params; a.exp_avg = exp_avg; a.exp_avg_sq = exp_avg_sq;
+  a.obs = obs; a.actions = actions; a.old_logp = old_logp; a.old_values = old_values;
+  a.adv = advantages; a.ret = returns;
+  a.in_dim = in_dim; a.n_act = n_actions; a.act_fn = activation;
+  a.hp = hp; a.ohp = ohp; a.state = state;
+  a.stats = stats; a.max_stats = max_stats; a.norms = norms; a.max_norms = max_norms;
+  a.grad_out = grad_out; a.moments = moments;
+  a.mb_begin = mb; a.mb_count = mb_count; a.world = world;
+  a.grad_in = grad_in; a.P_total = P_total; a.sync_base = sync_base;
   return mlp_launch(a, hidden, batch_size, n_rows, workspace, workspace_bytes, stream);
 }
 
@@ -1636,6 +1673,7 @@ extern "C" int rai_mlp_ppo_grads(const float* params, const float* obs, const in
   if (!grad_out) return RAI_E_NULLPTR;
   if (mb_begin < 0 || mb_count < 1) return RAI_E_SHAPE;
   MlpArgs a = {};
+  a.grad_in = nullptr; a.P_total = 0; a.sync_base = 0;
   a.params = const_cast<float*>(params);
   a.obs = obs; a.actions = actions; a.old_logp = old_logp; a.old_values = old_values;
   a.adv = advantages; a.ret = returns;

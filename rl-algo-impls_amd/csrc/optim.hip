@@ -75,8 +75,8 @@ __global__ __launch_bounds__(OPT_THREADS) void clip_optim_kernel(
   }
   const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
   if (hp.kind == 0) {
-    const double bc1 = 1.0 - pow(hp.beta1_d, (double)step);
-    const double bc2 = 1.0 - pow(hp.beta2_d, (double)step);
+    const double bc1 = 1.0 - ipow(hp.beta1_d, step);
+    const double bc2 = 1.0 - ipow(hp.beta2_d, step);
     const float w1 = (float)(1.0 - hp.beta1_d);   // lerp weight (torch: 1 - beta1 in Python)
     const float w2 = (float)(1.0 - hp.beta2_d);   // addcmul value
     const float bc2_sqrt = (float)sqrt(bc2);

@@ -80,6 +80,7 @@ class PPO:
         self.dp_group = None
         self.world = 1
         self._dp_comm = None
+        self.dp_enabled = False  # enable_data_parallel() called (any world size, incl. 1-rank rehearsal)
 
     # -- data parallel (one process per GPU) ------------------------------------------------
     def enable_data_parallel(self, group=None, native_dp: bool = True) -> None:
@@ -93,6 +94,7 @@ class PPO:
         import torch.distributed as dist
 
         self.dp_group = group
+        self.dp_enabled = True
         self.world = dist.get_world_size(group)
         self._dp_comm = None
         if self.flat.flat.is_cuda and dist.get_backend(group) == "nccl" and native_dp:
@@ -187,6 +189,8 @@ class PPO:
             acts = b.actions.contiguous()
             if self._dp_comm is not None:  # natively driven: grads -> RCCL all-reduce -> clip+Adam
                 f = self.flat
+                if getattr(self, "_grad_alt", None) is None or self._grad_alt.numel() != f.P:
+                    self._grad_alt = torch.zeros_like(f.grad)
                 rc = L.rai_mlp_ppo_epoch_dp(
                     f.flat.data_ptr(), f.grad.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), f.P,
                     obs.data_ptr(), acts.data_ptr(), b.logprobs.data_ptr(), b.values.data_ptr(),
@@ -194,8 +198,8 @@ class PPO:
                     moments.data_ptr(), self.world, spec["in_dim"], 64, spec["n_act"], spec["activation"],
                     blocks.hp.data_ptr(), opt.hp_dev.data_ptr(), blocks.state.data_ptr(), blocks.stats.data_ptr(),
                     int(blocks.stats.shape[0]), blocks.norms.data_ptr(), int(blocks.norms.shape[0]), self._dp_comm,
-                    self._mlp_ws.data_ptr(), self._mlp_ws.numel(), opt.workspace.data_ptr(), opt.workspace.numel(),
-                    st)
+                    self._grad_alt.data_ptr(), self._mlp_ws.data_ptr(), self._mlp_ws.numel(),
+                    opt.workspace.data_ptr(), opt.workspace.numel(), st)
                 _lib.check(rc, "rai_mlp_ppo_epoch_dp")
                 opt.step_count += nmb
                 continue
@@ -363,7 +367,7 @@ class PPO:
         returns the per-minibatch stats rows and grad norms (one D2H copy)."""
         spec = self.fused_mlp_spec() if hasattr(r, "epoch_batch") else None
         if spec is not None:
-            return self._update_fused_dp(r, spec) if self.world > 1 else self._update_fused(r, spec)
+            return self._update_fused_dp(r, spec) if self.dp_enabled else self._update_fused(r, spec)
         nmb = r.num_minibatches(self.batch_size)
         n_steps = self.n_epochs * nmb
         n_norms = self.n_epochs if self.gradient_accumulation else n_steps
@@ -383,15 +387,15 @@ class PPO:
                                                  mb.returns, K)
                 torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
                 if not self.gradient_accumulation:
-                    if self.world > 1:
+                    if self.dp_enabled:
                         self._all_reduce(self.flat.grad, average=True)
                     self.optimizer.step(blocks.state, blocks.norms)
             if self.gradient_accumulation:
-                if self.world > 1:
+                if self.dp_enabled:
                     self._all_reduce(self.flat.grad, average=True)
                 self.optimizer.step(blocks.state, blocks.norms)
         stats_t = blocks.stats[:n_steps]
-        if self.world > 1:
+        if self.dp_enabled:
             stats_t = stats_t.clone()
             self._all_reduce(stats_t, average=True)
         host = torch.cat([stats_t.reshape(-1), blocks.norms[:n_norms]]).cpu().numpy()
