@@ -157,17 +157,16 @@ def main():
     # park the stream behind a ~20 ms spin so every (event, launch, event) triple below is queued
     # before the GPU reaches it: the pairs then time the kernel, not the Python launch gap
     torch.cuda._sleep(50_000_000)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.roofline_reps)]
-    for e0, e1 in evs:
-        e0.record()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.roofline_reps):  # back to back: kernel time + the kernel-boundary gap
         gae()
-        e1.record()
+    e1.record()
     torch.cuda.synchronize()
-    gae_us = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs])) * 1e3
+    gae_us = e0.elapsed_time(e1) * 1e3 / args.roofline_reps
     workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
     pmc = {}
-    pmc_path = ROOT / "profiles" / "r1_pmc.json"
+    pmc_path = ROOT / "profiles" / "r1_pmc_final.json"
     if pmc_path.exists():
         pmc = json.loads(pmc_path.read_text()).get(workload, {})
 
@@ -183,9 +182,10 @@ def main():
         flops = 52352.0 * T * N
         ms = float(np.mean(epoch_ms))
         tf = flops / (ms * 1e-3) / 1e12
-        roofline = {"kernel": "mlp_ppo_epoch_kernel (rai_mlp_ppo_epoch)", "bound": "mfma", "achieved": round(tf, 4),
-                    "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
-                    "traffic": traffic("mlp_ppo_epoch_kernel"), "avg_ms": round(ms, 3),
+        kname = "mlp_ppo_mc_kernel<%d>" % int(cfg["policy"].get("activation_fn", "tanh") == "relu")
+        roofline = {"kernel": kname + " (rai_mlp_ppo_epoch, 4 CUs per network)", "bound": "mfma",
+                    "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
+                    "traffic": traffic(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
     else:
         roofline = roof_gae
