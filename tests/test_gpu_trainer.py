@@ -218,3 +218,71 @@ def test_synthetic_training_end_to_end(kind, tmp_path):
     assert set(sd) == set(policy.state_dict())
     opt = torch.load(tmp_path / "optimizer.pt", weights_only=True)
     assert float(opt["state"][0]["step"]) == algo.optimizer.step_count
+
+
+class _SpaceEnv:
+    """Just the spaces ActorCritic reads (obs Box(d), Discrete(n))."""
+
+    def __init__(self, d, n):
+        from rl_algo_impls_amd.envs import Box, Discrete
+
+        self.single_observation_space = Box(-1.0, 1.0, shape=(d,))
+        self.single_action_space = Discrete(n)
+        self.num_envs = 1
+
+
+def _random_rollout(T, N, d, n, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    t = lambda x: x.to(DEV)
+    obs = t(torch.randn(T, N, d, generator=g))
+    act = t(torch.randint(0, n, (T, N), generator=g))
+    rew = t(torch.randn(T, N, generator=g))
+    starts = t((torch.rand(T, N, generator=g) < 0.05).to(torch.uint8))
+    vals = t(torch.randn(T, N, generator=g))
+    logp = t(torch.log(torch.full((T, N), 1.0 / n)) + 0.1 * torch.randn(T, N, generator=g))
+    nstarts = t((torch.rand(N, generator=g) < 0.05).to(torch.uint8))
+    nvals = t(torch.randn(N, generator=g))
+    return obs, act, rew, starts, vals, logp, nstarts, nvals
+
+
+@pytest.mark.parametrize("d,n,act,bs,T,N,layout", [
+    (4, 2, "tanh", 256, 8, 96, "mc"),        # CartPole class, ragged last minibatch (768 % 256 = 0 -> 3 full)
+    (4, 2, "tanh", 200, 9, 100, "mc"),       # B < 256, ragged tail (900 % 200 = 100)
+    (4, 2, "relu", 64, 8, 64, "mc"),         # B = 64: CUs 1..3 see no rows
+    (2, 2, "tanh", 128, 5, 77, "mc"),        # in_dim 2 (padding columns), tail of 1 row avoided (385 % 128 = 1?)
+    (3, 1, "tanh", 96, 6, 50, "mc"),         # one action
+    (4, 2, "tanh", 256, 8, 96, "rows"),      # diagnostic one-CU row-tile layout
+    (4, 2, "tanh", 256, 8, 96, "chunk"),     # chunked one-CU layout
+    (6, 3, "tanh", 128, 8, 64, "chunk"),     # Acrobot-like: generic (8, 8) instantiation
+    (8, 8, "relu", 256, 4, 200, "chunk"),    # maximum shape of the chunked kernel
+])
+def test_fused_epoch_matches_generic_path(d, n, act, bs, T, N, layout, monkeypatch):
+    """One epoch of the fused kernel (given layout) vs the per-minibatch PyTorch path, same
+    rollout and permutation.  fp32 tolerances: different summation orders and the fused
+    kernel's hardware sqrt/rcp Adam."""
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    if (T * N) % bs == 1:
+        pytest.skip("1-row minibatch has no unbiased std")
+    if layout != "mc":
+        monkeypatch.setenv("RAI_MLP_LAYOUT", layout)
+    roll = _random_rollout(T, N, d, n, seed=d * 100 + n * 10 + bs)
+    results = []
+    for generic in (False, True):
+        torch.manual_seed(5)
+        policy = ActorCritic(_SpaceEnv(d, n), activation_fn=act).to(DEV)
+        algo = PPO(policy, DEV, None, batch_size=bs, n_epochs=2, learning_rate=3e-3, ent_coef=0.01,
+                   clip_range=0.2, gamma=0.98, gae_lambda=0.9)
+        algo.force_generic = generic
+        assert (algo.fused_mlp_spec() is None) == generic
+        obs, a_, rew, starts, vals, logp, nstarts, nvals = roll
+        perms = [torch.randperm(T * N, generator=torch.Generator().manual_seed(s)) for s in (1, 2)]
+        r = DeviceRollout(DEV, nstarts, nvals, obs, a_, rew, starts, vals, logp, None, 0.98, 0.9,
+                          perm_source=lambda k: perms.pop(0))
+        stats, norms, _ = algo.update(r)
+        results.append((algo.flat.flat.cpu().numpy(), stats, norms, algo.optimizer.state1.cpu().numpy()))
+    (pf, sf, nf, mf), (pg, sg, ng, mg) = results
+    np.testing.assert_allclose(nf, ng, rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(sf[:, :6], sg[:, :6], rtol=2e-3, atol=2e-6)
+    np.testing.assert_allclose(pf, pg, rtol=1e-3, atol=2e-5)
+    np.testing.assert_allclose(mf, mg, rtol=2e-2, atol=1e-6)
