@@ -252,6 +252,37 @@ int rai_mlp_ppo_epoch_dp(float* params, float* grads, float* exp_avg, float* exp
                          int64_t workspace_bytes, void* optim_workspace, int64_t optim_workspace_bytes,
                          void* stream);
 
+/* --------------------------------------------------------------------------
+ * In-kernel cross-GPU gradient all-reduce over xGMI peer memory (CartPole-class
+ * policies, the multi-CU epoch kernel).  Each rank allocates one exchange region
+ * (uncached device memory, rai_xdp_alloc(rai_xdp_region_bytes(world))), exports
+ * it by IPC handle, maps every other rank's region (rai_xdp_open) and passes the
+ * device array of all world region pointers (own included, rank order) to
+ * rai_mlp_ppo_epoch_xdp: one launch per epoch; per optimizer step the kernel
+ * pushes this rank's gradient share into every region, waits for every rank's
+ * step flag, sums the world slots in rank order and applies the identical
+ * clip + Adam on every rank.  step_base = optimizer steps already run through the
+ * regions (the flags hold monotonic step ids and are zeroed only at allocation).
+ * world <= 8.  Replaces the per-step RCCL all-reduce of rai_mlp_ppo_epoch_dp for
+ * this policy class (same semantics, no per-step launches).
+ * ------------------------------------------------------------------------ */
+int64_t rai_xdp_region_bytes(int32_t world);
+int rai_xdp_handle_bytes(void);
+int rai_xdp_alloc(int64_t bytes, void** region_out);
+int rai_xdp_free(void* region);
+int rai_xdp_handle(void* region, void* handle_out, int32_t out_bytes);
+int rai_xdp_open(const void* handle, void** peer_region_out);
+int rai_xdp_close(void* peer_region);
+int rai_mlp_ppo_epoch_xdp(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
+                          const int64_t* actions, const float* old_logp, const float* old_values,
+                          const float* advantages, const float* returns, int64_t n_rows,
+                          int32_t batch_size, const float* moments, int32_t world, int32_t rank,
+                          void* const* peers, int64_t step_base, int32_t in_dim, int32_t hidden,
+                          int32_t n_actions, int32_t activation, const rai_ppo_hparams* hp,
+                          const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
+                          int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
+                          int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,6 +100,16 @@ _SIGNATURES = {
     "rai_mlp_ppo_epoch_dp": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp,
                                        _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp,
                                        _vp, _vp, _i64, _vp, _i64, _vp]),
+    "rai_xdp_region_bytes": (_i64, [_i32]),
+    "rai_xdp_handle_bytes": (C.c_int, []),
+    "rai_xdp_alloc": (C.c_int, [_i64, C.POINTER(C.c_void_p)]),
+    "rai_xdp_free": (C.c_int, [_vp]),
+    "rai_xdp_handle": (C.c_int, [_vp, _vp, _i32]),
+    "rai_xdp_open": (C.c_int, [_vp, C.POINTER(C.c_void_p)]),
+    "rai_xdp_close": (C.c_int, [_vp]),
+    "rai_mlp_ppo_epoch_xdp": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i32, _i32,
+                                        _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32,
+                                        _vp, _i64, _vp]),
 }
 RAI_DP_UID_BYTES = 128
 EXPORTED = tuple(_SIGNATURES)

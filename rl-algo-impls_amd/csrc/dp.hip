@@ -153,3 +153,50 @@ extern "C" int rai_mlp_ppo_epoch_dp(float* params, float* grads, float* exp_avg,
   }
   return RAI_OK;
 }
+
+// ---- cross-GPU exchange regions (in-kernel all-reduce over xGMI peer memory) -------------------
+// Uncached device memory (every access goes to HBM, so a peer's stores are visible to this
+// device's loads without cache maintenance), shared with the other ranks' processes by IPC.
+extern "C" int rai_xdp_alloc(int64_t bytes, void** region_out) {
+  if (!region_out) return RAI_E_NULLPTR;
+  if (bytes <= 0) return RAI_E_SHAPE;
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(p, 0, (size_t)bytes);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return (int)e;
+  }
+  *region_out = p;
+  return RAI_OK;
+}
+
+extern "C" int rai_xdp_free(void* region) {
+  if (!region) return RAI_E_NULLPTR;
+  return (int)hipFree(region);
+}
+
+extern "C" int rai_xdp_handle(void* region, void* handle_out, int32_t out_bytes) {
+  if (!region || !handle_out) return RAI_E_NULLPTR;
+  if (out_bytes < (int32_t)sizeof(hipIpcMemHandle_t)) return RAI_E_SHAPE;
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, region);
+  if (e != hipSuccess) return (int)e;
+  memcpy(handle_out, &h, sizeof(h));
+  return RAI_OK;
+}
+
+extern "C" int rai_xdp_open(const void* handle, void** peer_region_out) {
+  if (!handle || !peer_region_out) return RAI_E_NULLPTR;
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(peer_region_out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+extern "C" int rai_xdp_close(void* peer_region) {
+  if (!peer_region) return RAI_E_NULLPTR;
+  return (int)hipIpcCloseMemHandle(peer_region);
+}
+
+extern "C" int rai_xdp_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }

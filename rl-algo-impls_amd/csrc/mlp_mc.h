@@ -41,6 +41,17 @@ constexpr int MC_CPT = (WL_CH + MC_NT - 1) / MC_NT;  // chunks owned per thread
 constexpr int MC_SLOT = WL_N;
 static_assert(WL_W3 + 2 * LD + 8 <= WL_N, "weight layout");
 
+// Cross-GPU exchange region (one per rank, IPC-mapped by every other rank):
+//   [0, 512)   u64 flags[2 nets][XDP_MAXW ranks][MC_G CUs]: step id of the last share pushed
+//   [512, ...) floats slots[2 parities][world][2 nets][WL_N]: each rank's gradient of the step
+constexpr int XDP_MAXW = 8;
+constexpr int XDP_FLAGS_BYTES = 512;
+static_assert(2 * XDP_MAXW * MC_G * 8 <= XDP_FLAGS_BYTES, "xdp flags");
+__host__ __device__ constexpr long long xdp_region_bytes(int world) {
+  return XDP_FLAGS_BYTES + 2LL * world * 2 * WL_N * (long long)sizeof(float);
+}
+constexpr int XDP_AUX = 17;  // sc0 | sc1: system-scope (cross-device) stores and loads
+
 // sync words (u64) at the start of the workspace, zeroed before every launch
 constexpr int MC_CNT = 0;     // [2 nets] arrival counters
 constexpr int MC_XG = 8;      // [2 nets][MC_G][2 parities] norm granules
@@ -747,10 +758,65 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
 #pragma unroll
           for (int cc = 1; cc < MC_G; ++cc) sum += v[i][cc];
           gr[i] = sum;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ss += (double)sum[q] * sum[q];
         }
       }
+      if (a.xworld > 1) {
+        // ---- cross-GPU sum over xGMI peer memory: CU c pushes its 1/G share of this rank's
+        // gradient into every rank's region (system-scope 16-B stores), drains, then stamps one
+        // flag per receiver; each CU waits for all world*G flags of this step in its own region
+        // and sums the world slots in rank order (identical bits on every rank). ------------------
+        const int W = a.xworld;
+        const unsigned long long step_id = (unsigned long long)(a.xbase + kk_mb + 1);
+        const int slot_off = XDP_FLAGS_BYTES + ((par * W + a.xrank) * 2 + net) * WL_N * (int)sizeof(float);
+        for (int pr = 0; pr < W; ++pr) {
+          const __amdgpu_buffer_rsrc_t prs = mc_rsrc(a.xpeers[pr], (int)xdp_region_bytes(W));
+#pragma unroll
+          for (int i = 0; i < MC_CPT; ++i) {
+            const int ch = tid + MC_NT * i;
+            if (ch < WL_CH && ch % MC_G == c)
+              __builtin_amdgcn_raw_buffer_store_b128(as_u4(gr[i]), prs, slot_off + 16 * ch, 0, XDP_AUX);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: shares landed
+        __syncthreads();
+        if (tid < W) {  // one flag store per receiver, after the whole workgroup drained
+          unsigned long long* fl = reinterpret_cast<unsigned long long*>(a.xpeers[tid]) +
+                                   (net * XDP_MAXW + a.xrank) * MC_G + c;
+          __hip_atomic_store(fl, step_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (w == 0) {  // one wave polls this rank's W*G flags of this network
+          const unsigned long long* fl = reinterpret_cast<const unsigned long long*>(a.xpeers[a.xrank]) +
+                                         net * XDP_MAXW * MC_G;
+          unsigned long long spins = 0;
+          for (;;) {
+            bool ok = true;
+            if (lane < W * MC_G)
+              ok = __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= step_id;
+            if (__all(ok)) break;
+            if (++spins > MC_SPINS) {
+              if (lane == 0) { atomicExch(a.err, 1); S.bail = 1; }
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        __syncthreads();
+        const __amdgpu_buffer_rsrc_t lrs = mc_rsrc(a.xpeers[a.xrank], (int)xdp_region_bytes(W));
+#pragma unroll
+        for (int i = 0; i < MC_CPT; ++i) {
+          const int chl = min(tid + MC_NT * i, WL_CH - 1);
+          f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+          for (int pr = 0; pr < W; ++pr) {
+            const int off = XDP_FLAGS_BYTES + ((par * W + pr) * 2 + net) * WL_N * (int)sizeof(float);
+            sum += as_f4(__builtin_amdgcn_raw_buffer_load_b128(lrs, off + 16 * chl, 0, XDP_AUX));
+          }
+          if (tid + MC_NT * i < WL_CH) gr[i] = sum;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MC_CPT; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ss += (double)gr[i][q] * gr[i][q];
       ss = wave_sum_v(ss);
       if (lane == 0) S.red[w] = ss;
       if (grads_mode) {  // raw gradients out in flat order (every CU holds them: each writes 1/G)
@@ -768,6 +834,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
       }
     }
     lds_barrier();
+    if (S.bail) break;
     STAMP(6);
     // ============ stats row (CU 0), norm exchange with the other network, bias corrections ============
     if (tid == 0) {

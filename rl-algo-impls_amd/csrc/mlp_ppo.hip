@@ -96,6 +96,13 @@ struct MlpArgs {
   const float* grad_in;
   int32_t P_total;
   int32_t sync_base;
+  // in-kernel cross-GPU exchange (multi-CU layout, epoch mode): xpeers[r] = rank r's exchange
+  // region (IPC-mapped device memory, uncached), xbase = optimizer steps already exchanged
+  // through these regions (flags are monotonic step ids, never re-zeroed)
+  void* const* xpeers;
+  int32_t xrank;
+  int32_t xworld;
+  int64_t xbase;
 };
 
 #ifdef RAI_STAMPS
@@ -1631,6 +1638,36 @@ extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_s
   a.mb_begin = 0; a.mb_count = 1 << 30; a.world = 1;
   a.grad_in = nullptr; a.P_total = 0; a.sync_base = 0;
   return mlp_launch(a, hidden, batch_size, n_rows, workspace, workspace_bytes, stream);
+}
+
+extern "C" int rai_mlp_ppo_epoch_xdp(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
+                                     const int64_t* actions, const float* old_logp, const float* old_values,
+                                     const float* advantages, const float* returns, int64_t n_rows,
+                                     int32_t batch_size, const float* moments, int32_t world, int32_t rank,
+                                     void* const* peers, int64_t step_base, int32_t in_dim, int32_t hidden,
+                                     int32_t n_actions, int32_t activation, const rai_ppo_hparams* hp,
+                                     const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
+                                     int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
+                                     int64_t workspace_bytes, void* stream) {
+  if (!(in_dim <= 4 && n_actions <= 2 && mlp_layout() == 0)) return RAI_E_UNSUPPORTED;
+  if (!moments || !peers) return RAI_E_NULLPTR;
+  if (world < 2 || world > XDP_MAXW || rank < 0 || rank >= world || step_base < 0) return RAI_E_SHAPE;
+  MlpArgs a = {};
+  a.params = params; a.exp_avg = exp_avg; a.exp_avg_sq = exp_avg_sq;
+  a.obs = obs; a.actions = actions; a.old_logp = old_logp; a.old_values = old_values;
+  a.adv = advantages; a.ret = returns;
+  a.in_dim = in_dim; a.n_act = n_actions; a.act_fn = activation;
+  a.hp = hp; a.ohp = ohp; a.state = state;
+  a.stats = stats; a.max_stats = max_stats; a.norms = norms; a.max_norms = max_norms;
+  a.grad_out = nullptr; a.moments = moments;
+  a.mb_begin = 0; a.mb_count = 1 << 30; a.world = world;
+  a.grad_in = nullptr; a.P_total = 0; a.sync_base = 0;
+  a.xpeers = peers; a.xrank = rank; a.xworld = world; a.xbase = step_base;
+  return mlp_launch(a, hidden, batch_size, n_rows, workspace, workspace_bytes, stream);
+}
+
+extern "C" int64_t rai_xdp_region_bytes(int32_t world) {
+  return world < 1 || world > XDP_MAXW ? 0 : xdp_region_bytes(world);
 }
 
 // Multi-CU data-parallel step (used by rai_mlp_ppo_epoch_dp): apply the previous all-reduced

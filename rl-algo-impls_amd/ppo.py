@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import gc
 import logging
+import os
 from time import perf_counter
 from typing import List, Optional, Tuple
 
@@ -83,7 +84,7 @@ class PPO:
         self.dp_enabled = False  # enable_data_parallel() called (any world size, incl. 1-rank rehearsal)
 
     # -- data parallel (one process per GPU) ------------------------------------------------
-    def enable_data_parallel(self, group=None, native_dp: bool = True) -> None:
+    def enable_data_parallel(self, group=None, native_dp: bool = True, xdp: Optional[bool] = None) -> None:
         """Weak-scaling data parallelism: every rank owns its own env group and HBM rollout;
         a global minibatch is the union of the ranks' minibatch slices, gradients are summed
         over ranks with one RCCL all-reduce per optimizer step (rccl/xGMI via
@@ -97,6 +98,17 @@ class PPO:
         self.dp_enabled = True
         self.world = dist.get_world_size(group)
         self._dp_comm = None
+        self._xdp = None
+        if xdp is None:
+            xdp = os.environ.get("RAI_XDP", "1") != "0"
+        spec = self.fused_mlp_spec()
+        if (xdp and self.flat.flat.is_cuda and self.world > 1 and spec is not None and spec["in_dim"] <= 4
+                and spec["n_act"] <= 2 and self.world <= 8):
+            try:
+                self._xdp = self._setup_xdp(group)
+            except RuntimeError as e:  # e.g. IPC unavailable: fall back to the per-step RCCL loop
+                logging.warning(f"in-kernel cross-GPU exchange unavailable ({e}); using the RCCL loop")
+                self._xdp = None
         if self.flat.flat.is_cuda and dist.get_backend(group) == "nccl" and native_dp:
             self._dp_comm = self._native_comm(group)
         with torch.no_grad():  # identical starting weights everywhere
@@ -107,6 +119,49 @@ class PPO:
                 self.flat.flat.copy_(h)
             else:
                 dist.broadcast(self.flat.flat, src=src, group=group)
+
+    def _setup_xdp(self, group) -> dict:
+        """Exchange regions for the in-kernel cross-GPU all-reduce (rai_mlp_ppo_epoch_xdp): one
+        uncached device region per rank, shared by IPC handle over `group`, mapped by every rank."""
+        import ctypes as C
+
+        import torch.distributed as dist
+
+        L = _lib.lib()
+        rank = dist.get_rank(group)
+        nbytes = int(L.rai_xdp_region_bytes(self.world))
+        region = C.c_void_p()
+        torch.cuda.synchronize(self.device)
+        _lib.check(L.rai_xdp_alloc(nbytes, C.byref(region)), "rai_xdp_alloc")
+        hb = int(L.rai_xdp_handle_bytes())
+        hbuf = (C.c_uint8 * hb)()
+        _lib.check(L.rai_xdp_handle(region, hbuf, hb), "rai_xdp_handle")
+        handles = [None] * self.world
+        dist.all_gather_object(handles, bytes(hbuf), group=group)
+        ptrs, opened = [], []
+        for r, h in enumerate(handles):
+            if r == rank:
+                ptrs.append(region.value)
+                continue
+            peer = C.c_void_p()
+            _lib.check(L.rai_xdp_open(h, C.byref(peer)), "rai_xdp_open")
+            opened.append(peer)
+            ptrs.append(peer.value)
+        peers = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)  # every region zeroed and mapped before any kernel pushes into it
+        return dict(region=region, opened=opened, peers=peers, rank=rank, step=0)
+
+    def _params_agree(self) -> bool:
+        """Cheap cross-rank consistency check of the (bitwise-identical by construction) weights."""
+        import torch.distributed as dist
+
+        v = self.flat.flat.double()
+        t = torch.stack([v.sum(), (v * v).sum(), -v.sum(), -(v * v).sum()])
+        if dist.get_backend(self.dp_group) == "gloo":
+            t = t.cpu()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.dp_group)
+        return bool((t[0] == -t[2]) and (t[1] == -t[3]))
 
     def _native_comm(self, group):
         """An RCCL communicator of our own (same ranks as `group`) for the natively driven
@@ -187,6 +242,21 @@ class PPO:
             moments = self._global_adv_moments(b.advantages, nmb)
             obs = (b.obs if b.obs.dtype == torch.float32 else b.obs.float()).contiguous()
             acts = b.actions.contiguous()
+            if self._xdp is not None:  # one launch per epoch, cross-GPU sums inside the kernel
+                x = self._xdp
+                f = self.flat
+                rc = L.rai_mlp_ppo_epoch_xdp(
+                    f.flat.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), obs.data_ptr(), acts.data_ptr(),
+                    b.logprobs.data_ptr(), b.values.data_ptr(), b.advantages.data_ptr(), b.returns.data_ptr(),
+                    r.total_steps, self.batch_size, moments.data_ptr(), self.world, x["rank"],
+                    x["peers"].data_ptr(), x["step"], spec["in_dim"], 64, spec["n_act"], spec["activation"],
+                    blocks.hp.data_ptr(), opt.hp_dev.data_ptr(), blocks.state.data_ptr(), blocks.stats.data_ptr(),
+                    int(blocks.stats.shape[0]), blocks.norms.data_ptr(), int(blocks.norms.shape[0]),
+                    self._mlp_ws.data_ptr(), self._mlp_ws.numel(), st)
+                _lib.check(rc, "rai_mlp_ppo_epoch_xdp")
+                x["step"] += nmb
+                opt.step_count += nmb
+                continue
             if self._dp_comm is not None:  # natively driven: grads -> RCCL all-reduce -> clip+Adam
                 f = self.flat
                 if getattr(self, "_grad_alt", None) is None or self._grad_alt.numel() != f.P:
@@ -216,9 +286,15 @@ class PPO:
                 opt.step(blocks.state, blocks.norms)
         stats_t = blocks.stats[:n_steps].clone()
         self._all_reduce(stats_t)  # every rank holds its share of the global means
-        host = torch.cat([stats_t.reshape(-1), blocks.norms[:n_steps]]).cpu().numpy()
+        host = torch.cat([stats_t.reshape(-1), blocks.norms[:n_steps],
+                          blocks.state.view(torch.float32)]).cpu().numpy()
         stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE).copy()
-        norms = host[n_steps * _lib.RAI_STAT_STRIDE:]
+        norms = host[n_steps * _lib.RAI_STAT_STRIDE: n_steps * _lib.RAI_STAT_STRIDE + n_steps]
+        state = host[n_steps * _lib.RAI_STAT_STRIDE + n_steps:].view(np.int32)
+        if state[5] != 0:
+            raise RuntimeError("fused data-parallel update: a device-side exchange timed out (err flag set)")
+        if self._xdp is not None and not self._params_agree():
+            raise RuntimeError("ranks' parameters diverged after the in-kernel cross-GPU exchange")
         stats[:, 0] += float(self.vf_coef) * stats[:, 5]
         return stats, norms, 1
 

@@ -18,7 +18,16 @@ def _port():
     return p
 
 
-def test_fused_dp_world2_matches_single_process_global_minibatches():
+@pytest.mark.parametrize("xdp", ["1", "0"], ids=["in_kernel_xgmi_exchange", "per_step_loop"])
+def test_fused_dp_world2_matches_single_process_global_minibatches(xdp, monkeypatch):
+    """xdp=1: one launch per epoch per rank, gradients summed across the two processes inside
+    the kernel through IPC-mapped regions (both ranks on this one GPU, running concurrently);
+    xdp=0: the per-step loop (grads kernel -> gloo all-reduce -> clip+Adam)."""
+    monkeypatch.setenv("RAI_XDP", xdp)
+    _fused_dp_world2_check()
+
+
+def _fused_dp_world2_check():
     import dp_worker
     import make_golden_networks as nets
     from rl_algo_impls_amd.ppo import PPO
