@@ -225,7 +225,12 @@ def main():
             "cpu_baseline": cpu,
         }
         if args.dp_rehearsal or world > 1:
-            line["dp_path"] = "native RCCL loop" if algo._dp_comm is not None else "python loop (" + backend + ")"
+            if algo._xdp is not None:
+                line["dp_path"] = "in-kernel cross-GPU exchange (IPC-mapped xGMI regions), one launch per epoch"
+            elif algo._dp_comm is not None:
+                line["dp_path"] = "native RCCL loop (all-reduce per optimizer step)"
+            else:
+                line["dp_path"] = "python loop (" + backend + ")"
         print(json.dumps(line), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()

@@ -245,6 +245,10 @@ class PPO:
             if self._xdp is not None:  # one launch per epoch, cross-GPU sums inside the kernel
                 x = self._xdp
                 f = self.flat
+                ev = None
+                if self.kernel_events is not None:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()
                 rc = L.rai_mlp_ppo_epoch_xdp(
                     f.flat.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), obs.data_ptr(), acts.data_ptr(),
                     b.logprobs.data_ptr(), b.values.data_ptr(), b.advantages.data_ptr(), b.returns.data_ptr(),
@@ -254,6 +258,9 @@ class PPO:
                     int(blocks.stats.shape[0]), blocks.norms.data_ptr(), int(blocks.norms.shape[0]),
                     self._mlp_ws.data_ptr(), self._mlp_ws.numel(), st)
                 _lib.check(rc, "rai_mlp_ppo_epoch_xdp")
+                if ev is not None:
+                    ev[1].record()
+                    self.kernel_events.append(ev)
                 x["step"] += nmb
                 opt.step_count += nmb
                 continue
