@@ -273,6 +273,10 @@ int rai_xdp_free(void* region);
 int rai_xdp_handle(void* region, void* handle_out, int32_t out_bytes);
 int rai_xdp_open(const void* handle, void** peer_region_out);
 int rai_xdp_close(void* peer_region);
+/* Setup canary: same memory, scopes and flag protocol on a known payload; bad[0] counts wrong
+ * values, bad[1] timeouts (device int32[2], zeroed by the caller).  tag: a fresh id >= 1. */
+int rai_xdp_selftest(void* const* peers, int32_t world, int32_t rank, int64_t tag, int32_t* bad,
+                     void* stream);
 int rai_mlp_ppo_epoch_xdp(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
                           const int64_t* actions, const float* old_logp, const float* old_values,
                           const float* advantages, const float* returns, int64_t n_rows,

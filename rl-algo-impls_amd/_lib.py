@@ -107,6 +107,7 @@ _SIGNATURES = {
     "rai_xdp_handle": (C.c_int, [_vp, _vp, _i32]),
     "rai_xdp_open": (C.c_int, [_vp, C.POINTER(C.c_void_p)]),
     "rai_xdp_close": (C.c_int, [_vp]),
+    "rai_xdp_selftest": (C.c_int, [_vp, _i32, _i32, _i64, _vp, _vp]),
     "rai_mlp_ppo_epoch_xdp": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i32, _i32,
                                         _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32,
                                         _vp, _i64, _vp]),

@@ -42,10 +42,11 @@ constexpr int MC_SLOT = WL_N;
 static_assert(WL_W3 + 2 * LD + 8 <= WL_N, "weight layout");
 
 // Cross-GPU exchange region (one per rank, IPC-mapped by every other rank):
-//   [0, 512)   u64 flags[2 nets][XDP_MAXW ranks][MC_G CUs]: step id of the last share pushed
-//   [512, ...) floats slots[2 parities][world][2 nets][WL_N]: each rank's gradient of the step
+//   [0, 512)    u64 flags[2 nets][XDP_MAXW ranks][MC_G CUs]: step id of the last share pushed
+//   [512, 576)  u64 self-test flags[XDP_MAXW ranks]
+//   [1024, ...) floats slots[2 parities][world][2 nets][WL_N]: each rank's gradient of the step
 constexpr int XDP_MAXW = 8;
-constexpr int XDP_FLAGS_BYTES = 512;
+constexpr int XDP_FLAGS_BYTES = 1024;  // [0,512): step flags; [512,576): self-test flags
 static_assert(2 * XDP_MAXW * MC_G * 8 <= XDP_FLAGS_BYTES, "xdp flags");
 __host__ __device__ constexpr long long xdp_region_bytes(int world) {
   return XDP_FLAGS_BYTES + 2LL * world * 2 * WL_N * (long long)sizeof(float);

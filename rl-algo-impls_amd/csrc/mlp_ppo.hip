@@ -1666,6 +1666,49 @@ extern "C" int rai_mlp_ppo_epoch_xdp(float* params, float* exp_avg, float* exp_a
   return mlp_launch(a, hidden, batch_size, n_rows, workspace, workspace_bytes, stream);
 }
 
+// Setup-time canary for the cross-GPU regions: the same memory, scopes and flag protocol as
+// the epoch kernel on a known payload.  bad[0] counts wrong values, bad[1] timeouts.
+__global__ __launch_bounds__(64) void xdp_selftest_kernel(void* const* peers, int W, int rank,
+                                                          unsigned long long tag, int* bad) {
+  const int lane = threadIdx.x;
+  for (int p = 0; p < W; ++p) {
+    float* dst = reinterpret_cast<float*>(static_cast<char*>(peers[p]) + XDP_FLAGS_BYTES) + rank * 64 + lane;
+    __hip_atomic_store(dst, (float)(rank * 1000 + lane) + (float)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (lane < W) {
+    unsigned long long* fl = reinterpret_cast<unsigned long long*>(static_cast<char*>(peers[lane]) + 512) + rank;
+    __hip_atomic_store(fl, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const unsigned long long* own = reinterpret_cast<const unsigned long long*>(static_cast<char*>(peers[rank]) + 512);
+  unsigned long long spins = 0;
+  for (;;) {
+    bool ok = lane >= W || __hip_atomic_load(own + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= tag;
+    if (__all(ok)) break;
+    if (++spins > (1ull << 22)) {
+      if (lane == 0) atomicAdd(&bad[1], 1);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const float* src = reinterpret_cast<const float*>(static_cast<const char*>(peers[rank]) + XDP_FLAGS_BYTES);
+  for (int r = 0; r < W; ++r) {
+    const float v = __hip_atomic_load(src + r * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v != (float)(r * 1000 + lane) + (float)tag) atomicAdd(&bad[0], 1);
+  }
+}
+
+extern "C" int rai_xdp_selftest(void* const* peers, int32_t world, int32_t rank, int64_t tag, int32_t* bad,
+                                void* stream) {
+  if (!peers || !bad) return RAI_E_NULLPTR;
+  if (world < 1 || world > XDP_MAXW || rank < 0 || rank >= world || tag < 1) return RAI_E_SHAPE;
+  hipLaunchKernelGGL(xdp_selftest_kernel, dim3(1), dim3(64), 0, rai_stream(stream), peers, (int)world, (int)rank,
+                     (unsigned long long)tag, bad);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
 extern "C" int64_t rai_xdp_region_bytes(int32_t world) {
   return world < 1 || world > XDP_MAXW ? 0 : xdp_region_bytes(world);
 }

@@ -109,7 +109,7 @@ class PPO:
             except RuntimeError as e:  # e.g. IPC unavailable: fall back to the per-step RCCL loop
                 logging.warning(f"in-kernel cross-GPU exchange unavailable ({e}); using the RCCL loop")
                 self._xdp = None
-        if self.flat.flat.is_cuda and dist.get_backend(group) == "nccl" and native_dp:
+        if self._xdp is None and self.flat.flat.is_cuda and dist.get_backend(group) == "nccl" and native_dp:
             self._dp_comm = self._native_comm(group)
         with torch.no_grad():  # identical starting weights everywhere
             src = dist.get_global_rank(group, 0) if group is not None else 0
@@ -150,6 +150,17 @@ class PPO:
         peers = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
         torch.cuda.synchronize(self.device)
         dist.barrier(group=group)  # every region zeroed and mapped before any kernel pushes into it
+        # canary: the epoch kernel's memory, scopes and flag protocol on a known payload, on every rank
+        bad = torch.zeros(2, dtype=torch.int32, device=self.device)
+        _lib.check(L.rai_xdp_selftest(peers.data_ptr(), self.world, rank, 1, bad.data_ptr(),
+                                      _lib.stream_handle(self.device)), "rai_xdp_selftest")
+        torch.cuda.synchronize(self.device)
+        verdict = bad.to(torch.int64)
+        if dist.get_backend(group) == "gloo":
+            verdict = verdict.cpu()
+        dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=group)
+        if int(verdict.sum()) != 0:
+            raise RuntimeError(f"cross-GPU exchange self-test failed (wrong values, timeouts) = {verdict.tolist()}")
         return dict(region=region, opened=opened, peers=peers, rank=rank, step=0)
 
     def _params_agree(self) -> bool:

@@ -71,8 +71,8 @@ def fused_dp_worker(rank, world, port, q, backend="gloo"):
     policy = nets.build("cartpole").to(dev)
     algo = PPO(policy, dev, None, batch_size=128, n_epochs=2, learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
     algo.enable_data_parallel(xdp=os.environ.get("RAI_XDP", "1") != "0")
-    assert (algo._dp_comm is not None) == (backend == "nccl")
     expect_xdp = world > 1 and os.environ.get("RAI_XDP", "1") != "0"
+    assert (algo._dp_comm is not None) == (backend == "nccl" and not expect_xdp)
     assert (algo._xdp is not None) == expect_xdp, "in-kernel exchange not set up"
     data = make_rank_data(rank, dev)
 
