@@ -25,7 +25,8 @@ from __future__ import annotations
 import dataclasses
 from abc import ABC, abstractmethod
 from dataclasses import dataclass
-from typing import Callable, Dict, Iterator, List, Optional
+from collections import deque
+from typing import Callable, Deque, Dict, Iterator, List, Optional
 
 import ctypes as C
 import numpy as np
@@ -296,6 +297,11 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         self.h_done = torch.zeros((N,), dtype=torch.bool).pin_memory()
         self.h_act = torch.zeros((N,) + self.act_shape, dtype=act_dtype).pin_memory()
         self.next_obs_dev = torch.zeros((N,) + tuple(obs_space.shape), dtype=self.obs_dtype, device=dev)
+        # finished episodes' returns / lengths (gymnasium RecordEpisodeStatistics convention
+        # info["episode"], info["_episode"]; what EpisodeStatsWriter logs as train_rolling/*,
+        # rl_algo_impls/wrappers/episode_stats_writer.py:65-112), last 100
+        self.episode_returns: Deque[float] = deque(maxlen=100)
+        self.episode_lengths: Deque[int] = deque(maxlen=100)
         self.next_episode_starts = torch.ones((N,), dtype=torch.bool, device=dev)
         self._act_ready = torch.cuda.Event()
         obs, _ = vec_env.reset()
@@ -338,7 +344,11 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             self.h_act.copy_(src, non_blocking=True)
             self._act_ready.record()
             self._act_ready.synchronize()
-            obs, rew, term, trunc, _ = self.vec_env.step(self.h_act.numpy())
+            obs, rew, term, trunc, info = self.vec_env.step(self.h_act.numpy())
+            if info and "episode" in info:
+                done_mask = np.asarray(info.get("_episode", np.ones(self.num_envs, dtype=bool)))
+                self.episode_returns.extend(np.asarray(info["episode"]["r"])[done_mask].tolist())
+                self.episode_lengths.extend(np.asarray(info["episode"]["l"])[done_mask].tolist())
             np.copyto(self.h_rew.numpy(), rew, casting="same_kind")
             np.logical_or(term, trunc, out=self.h_done.numpy())
             self.rewards[s].copy_(self.h_rew, non_blocking=True)

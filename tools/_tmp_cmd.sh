@@ -1,3 +1,2 @@
 R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out && cd $R && export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests/test_gpu_dp.py -q -x > gpurun_out/pytest_xdp.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/pytest_xdp.log | grep -E "passed|failed|Error|error|assert" | head -20; [ $rc -eq 0 ] || exit $rc
-RAI_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 2 --warmup 1 > gpurun_out/bench2_xdp.log 2>&1; rc=$?; grep '^{' gpurun_out/bench2_xdp.log | cut -c1-200; grep -o '"roofline": {[^}]*}' gpurun_out/bench2_xdp.log; grep -o '"dp_path.*' gpurun_out/bench2_xdp.log; exit $rc
+timeout -k 10 600 python -m pytest tests/test_gpu_trainer.py -q -k "learns_cartpole" --durations=3 > gpurun_out/pytest_learn.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/pytest_learn.log | grep -E "passed|failed|assert|reached|s call" | head -10; exit $rc
