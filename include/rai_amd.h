@@ -180,6 +180,22 @@ int rai_gaussian_sample(const float* mu, const float* log_std, int64_t N, int32_
                         const float* v_in, float* v_out, int32_t K, void* stream);
 
 /* --------------------------------------------------------------------------
+ * Fused rollout step for CartPole-class MLP actor-critics (Flatten encoder,
+ * [in_dim -> 64 -> 64 -> out] actor and critic, Categorical head; in_dim <= 8,
+ * n_actions <= 8): both forward passes, the categorical sample and the slot
+ * writes in one launch.  Replaces rl_algo_impls/shared/policy/actor_critic.py:
+ * 306-318 + rl_algo_impls/rollout/sync_step_rollout.py:193-201 for this class
+ * (and ActorCritic.value, actor_critic.py:298-304, when actions_out/logp_out are
+ * NULL).  pi_params / v_params: host arrays of 6 device pointers {W1, b1, W2, b2,
+ * W3, b3} (torch Linear layout, weight [out][in]).  Sampling is the stream of
+ * rai_categorical_sample (same seed/offset/row keying).
+ * ------------------------------------------------------------------------ */
+int rai_mlp_policy_step(const float* const* pi_params, const float* const* v_params, const float* obs,
+                        int64_t N, int32_t in_dim, int32_t hidden, int32_t n_actions,
+                        int32_t activation, uint64_t seed, uint64_t offset, int64_t* actions_out,
+                        float* logp_out, float* values_out, void* stream);
+
+/* --------------------------------------------------------------------------
  * Fused PPO epoch for MLP actor-critics (Flatten encoder, separate
  * [in_dim -> 64 -> 64 -> out] actor and critic MLPs, Categorical head; the
  * CartPole-class policies of rl_algo_impls/shared/policy/actor_critic_network/

@@ -92,6 +92,8 @@ _SIGNATURES = {
     "rai_categorical_sample": (C.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp, _vp, _vp, _i32, _vp]),
     "rai_gaussian_sample": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp,
                                       _i32, _vp]),
+    "rai_mlp_policy_step": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _u64, _u64, _vp, _vp, _vp,
+                                      _vp]),
     "rai_dp_available": (C.c_int, []),
     "rai_dp_unique_id": (C.c_int, [_vp, _i32]),
     "rai_dp_comm_init": (C.c_int, [C.POINTER(C.c_void_p), _vp, _i32, _i32]),

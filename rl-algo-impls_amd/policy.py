@@ -393,3 +393,29 @@ def clamp_actions(actions, action_space, squash_output: bool):
             return low + 0.5 * (actions + 1) * (high - low)
         return np.clip(actions, low, high)
     return actions
+
+
+def mlp_actor_critic_spec(pol) -> Optional[dict]:
+    """The CartPole-class structure the fused kernels implement (rai_mlp_ppo_epoch,
+    rai_mlp_policy_step): an ActorCritic with a Flatten encoder, separate [in -> 64 -> 64 -> out]
+    actor and critic MLPs (tanh or relu), a Categorical head, in_dim <= 8, n_actions <= 8,
+    parameters() in the order actor W1,b1,W2,b2,W3,b3 then critic.  None otherwise."""
+    if not isinstance(pol, ActorCritic):
+        return None
+    net = pol.network
+    if net._feature_extractor.kind != "flat" or not isinstance(net._pi, CategoricalActorHead):
+        return None
+    if net.pi_hidden_sizes != (64, 64) or net.v_hidden_sizes != (64, 64):
+        return None
+    if net.activation_fn not in ("tanh", "relu"):
+        return None
+    in_dim, n_act = net._feature_extractor.out_dim, net._pi.act_dim
+    if not (1 <= in_dim <= 8 and 1 <= n_act <= 8):
+        return None
+    shapes = [tuple(p.shape) for p in pol.parameters()]
+    want = []
+    for out in (n_act, 1):
+        want += [(64, in_dim), (64,), (64, 64), (64,), (out, 64), (out,)]
+    if shapes != want:
+        return None
+    return dict(in_dim=in_dim, n_act=n_act, activation=0 if net.activation_fn == "tanh" else 1)

@@ -381,32 +381,18 @@ class PPO:
         """Shape descriptor if the policy/options fit rai_mlp_ppo_epoch (CartPole-class MLP
         actor-critic: Flatten encoder, [in -> 64 -> 64 -> out] actor and critic, Categorical
         head); None otherwise (the generic per-minibatch path then runs)."""
-        from .policy import ActorCritic, CategoricalActorHead
+        from .policy import mlp_actor_critic_spec
 
-        pol = self.policy
-        if self.force_generic or not isinstance(pol, ActorCritic):
+        if self.force_generic:
             return None
-        net = pol.network
-        if net._feature_extractor.kind != "flat" or not isinstance(net._pi, CategoricalActorHead):
-            return None
-        if net.pi_hidden_sizes != (64, 64) or net.v_hidden_sizes != (64, 64):
-            return None
-        if net.activation_fn not in ("tanh", "relu"):
-            return None
-        in_dim, n_act = net._feature_extractor.out_dim, net._pi.act_dim
-        if not (1 <= in_dim <= 8 and 1 <= n_act <= 8 and 2 <= self.batch_size <= 256):
+        spec = mlp_actor_critic_spec(self.policy)
+        if spec is None or not (2 <= self.batch_size <= 256):
             return None
         if (self.gradient_accumulation or self.kl_cutoff is not None or self.multi_reward_weights is not None
                 or self.vf_weights is not None or self.normalize_advantages_after_scaling
                 or np.ndim(self.vf_coef) > 0):
             return None
-        shapes = [tuple(p.shape) for p in pol.parameters()]
-        want = []
-        for out in (n_act, 1):
-            want += [(64, in_dim), (64,), (64, 64), (64,), (out, 64), (out,)]
-        if shapes != want:
-            return None
-        return dict(in_dim=in_dim, n_act=n_act, activation=0 if net.activation_fn == "tanh" else 1)
+        return spec
 
     def _ensure_mlp_workspace(self, n_rows: int) -> None:
         need = int(_lib.lib().rai_mlp_ppo_workspace_bytes(n_rows, self.batch_size))

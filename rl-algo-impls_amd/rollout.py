@@ -304,8 +304,41 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         self.episode_lengths: Deque[int] = deque(maxlen=100)
         self.next_episode_starts = torch.ones((N,), dtype=torch.bool, device=dev)
         self._act_ready = torch.cuda.Event()
+        # CartPole-class MLP policies: one fused launch per env step (rai_mlp_policy_step)
+        from .policy import mlp_actor_critic_spec
+
+        self.fused_step = None
+        spec = mlp_actor_critic_spec(policy)
+        if spec is not None and self.discrete and self.obs_dtype == torch.float32 and len(obs_space.shape) == 1:
+            self.fused_step = spec
         obs, _ = vec_env.reset()
         self._stage_obs(obs)
+
+    def _layer_ptrs(self):
+        ps = [p.detach() for p in self.policy.parameters()]
+        for p in ps:
+            assert p.is_contiguous() and p.dtype == torch.float32
+        arr = lambda xs: (C.c_void_p * 6)(*[x.data_ptr() for x in xs])
+        return arr(ps[:6]), arr(ps[6:12])
+
+    def _fused_step(self, s: Optional[int]) -> None:
+        """Actor + critic forward, sample and slot writes for env step s (s None: bootstrap values
+        of next_obs_dev into self._next_values)."""
+        L = _lib.lib()
+        sp = self.fused_step
+        pi, v = self._layer_ptrs()
+        N = self.num_envs
+        st = _lib.stream_handle(self.device)
+        if s is None:
+            rc = L.rai_mlp_policy_step(None, v, self.next_obs_dev.data_ptr(), N, sp["in_dim"], 64, sp["n_act"],
+                                       sp["activation"], self.seed, self.rng_offset, None, None,
+                                       self._next_values.data_ptr(), st)
+        else:
+            rc = L.rai_mlp_policy_step(pi, v, self.obs[s].data_ptr(), N, sp["in_dim"], 64, sp["n_act"],
+                                       sp["activation"], self.seed, self.rng_offset, self.actions[s].data_ptr(),
+                                       self.logprobs[s].data_ptr(), self.values[s].data_ptr(), st)
+            self.rng_offset += 1
+        _lib.check(rc, "rai_mlp_policy_step")
 
     def _stage_obs(self, obs: np.ndarray) -> None:
         np.copyto(self.h_obs.numpy(), obs, casting="same_kind")
@@ -338,8 +371,11 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         for s in range(self.n_steps):
             self.obs[s].copy_(self.next_obs_dev)
             self.episode_starts[s].copy_(self.next_episode_starts)
-            params, v = net.dist_params_and_value(self.obs[s])
-            self._sample(params, v, s)
+            if self.fused_step is not None:
+                self._fused_step(s)
+            else:
+                params, v = net.dist_params_and_value(self.obs[s])
+                self._sample(params, v, s)
             src = self.actions[s] if self.discrete else self.clamped
             self.h_act.copy_(src, non_blocking=True)
             self._act_ready.record()
@@ -354,7 +390,14 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             self.rewards[s].copy_(self.h_rew, non_blocking=True)
             self.next_episode_starts.copy_(self.h_done, non_blocking=True)
             self._stage_obs(obs)
-        next_values = net.value(self.next_obs_dev).float() if output_next_values else None
+        next_values = None
+        if output_next_values:
+            if self.fused_step is not None:
+                self._next_values = torch.empty((self.num_envs,), dtype=torch.float32, device=self.device)
+                self._fused_step(None)
+                next_values = self._next_values
+            else:
+                next_values = net.value(self.next_obs_dev).float()
         self.policy.train()
         return next_values
 

@@ -322,3 +322,56 @@ def test_gaussian_sample_moments_logp_clamp():
     np.testing.assert_allclose(lp.cpu().numpy(), oracle.gaussian_logp(a, mu.cpu().numpy(), log_std.cpu().numpy()),
                                rtol=1e-5, atol=1e-5)
     np.testing.assert_array_equal(cl.cpu().numpy(), np.clip(a, -1, 1))
+
+
+@pytest.mark.parametrize("d,n,act", [(4, 2, "tanh"), (4, 2, "relu"), (6, 3, "tanh"), (8, 8, "relu")])
+def test_fused_policy_step_matches_torch_forward_and_sampler(d, n, act):
+    """rai_mlp_policy_step (both MLP forwards + categorical sample + slot writes) vs the PyTorch
+    forward followed by rai_categorical_sample with the same seed/offset: values and log-probs
+    within fp32 tolerance; actions identical except where the uniform draw falls within the
+    forward's rounding of a CDF boundary."""
+    import ctypes as C
+
+    from rl_algo_impls_amd.envs import Box, Discrete
+    from rl_algo_impls_amd.policy import ActorCritic, mlp_actor_critic_spec
+
+    class E:
+        single_observation_space = Box(-1.0, 1.0, shape=(d,))
+        single_action_space = Discrete(n)
+        num_envs = 1
+
+    torch.manual_seed(3)
+    pol = ActorCritic(E(), activation_fn=act).to(DEV)
+    spec = mlp_actor_critic_spec(pol)
+    assert spec is not None
+    N = 5000
+    obs = torch.randn(N, d, device=DEV) * 2
+    ps = [p.detach() for p in pol.parameters()]
+    arr = lambda xs: (C.c_void_p * 6)(*[x.data_ptr() for x in xs])
+    a1 = torch.empty(N, dtype=torch.int64, device=DEV)
+    l1 = torch.empty(N, device=DEV)
+    v1 = torch.empty(N, device=DEV)
+    L = _lib.lib()
+    st = _lib.stream_handle(DEV)
+    _lib.check(L.rai_mlp_policy_step(arr(ps[:6]), arr(ps[6:]), obs.data_ptr(), N, d, 64, n, spec["activation"], 77, 5,
+                                     a1.data_ptr(), l1.data_ptr(), v1.data_ptr(), st), "policy_step")
+    with torch.no_grad():
+        logits, v = pol.network.dist_params_and_value(obs)
+    logits = logits.contiguous().float()
+    v = v.contiguous().float()
+    a2 = torch.empty(N, dtype=torch.int64, device=DEV)
+    l2 = torch.empty(N, device=DEV)
+    v2 = torch.empty(N, device=DEV)
+    _lib.check(L.rai_categorical_sample(logits.data_ptr(), None, N, n, 77, 5, a2.data_ptr(), l2.data_ptr(),
+                                        v.data_ptr(), v2.data_ptr(), 1, st), "categorical_sample")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(v1.cpu().numpy(), v2.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    same = (a1 == a2).cpu().numpy()
+    assert same.mean() > 0.999, same.mean()
+    np.testing.assert_allclose(l1.cpu().numpy()[same], l2.cpu().numpy()[same], rtol=1e-4, atol=1e-5)
+    # value-only call (bootstrap): same values
+    v3 = torch.empty(N, device=DEV)
+    _lib.check(L.rai_mlp_policy_step(None, arr(ps[6:]), obs.data_ptr(), N, d, 64, n, spec["activation"], 0, 0,
+                                     None, None, v3.data_ptr(), st), "policy_step values")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(v3.cpu().numpy(), v1.cpu().numpy())
