@@ -38,6 +38,8 @@ algo = PPO(policy, dev, None, batch_size=256, n_epochs=1, learning_rate=1e-3, ga
 r = gen.rollout(gamma=0.98, gae_lambda=0.8)
 algo.update(r)  # warm
 torch.cuda.synchronize()
+out0 = (C.c_ulonglong * 64)()
+assert _lib.lib().rai_mlp_debug_stamps(out0) == 0  # the kernels accumulate: take the difference
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
 algo.update(r)
@@ -46,7 +48,7 @@ ev1.synchronize()
 out = (C.c_ulonglong * 64)()
 rc = _lib.lib().rai_mlp_debug_stamps(out)
 assert rc == 0, rc
-st = np.array(out, dtype=np.float64).reshape(2, 32)
+st = (np.array(out, dtype=np.float64) - np.array(out0, dtype=np.float64)).reshape(2, 32)
 nmb = r.total_steps // 256
 print(f"epoch {ev0.elapsed_time(ev1):.2f} ms for {nmb} minibatches -> {ev0.elapsed_time(ev1) * 1e3 / nmb:.2f} us/mb")
 for net in range(2):
