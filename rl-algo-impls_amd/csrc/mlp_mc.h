@@ -42,12 +42,13 @@ constexpr int MC_SLOT = WL_N;
 static_assert(WL_W3 + 2 * LD + 8 <= WL_N, "weight layout");
 
 // Cross-GPU exchange region (one per rank, IPC-mapped by every other rank):
-//   [0, 512)    u64 flags[2 nets][XDP_MAXW ranks][MC_G CUs]: step id of the last share pushed
-//   [512, 576)  u64 self-test flags[XDP_MAXW ranks]
-//   [1024, ...) floats slots[2 parities][world][2 nets][WL_N]: each rank's gradient of the step
+//   [0, 2048)    u64 flags[2 nets][XDP_MAXW ranks][CUs per network]: step id of the last share pushed
+//   [2048, 2112) u64 self-test flags[XDP_MAXW ranks]
+//   [4096, ...)  floats slots[2 parities][world][2 nets][WL_N]: each rank's gradient of the step
 constexpr int XDP_MAXW = 8;
-constexpr int XDP_FLAGS_BYTES = 1024;  // [0,512): step flags; [512,576): self-test flags
-static_assert(2 * XDP_MAXW * MC_G * 8 <= XDP_FLAGS_BYTES, "xdp flags");
+constexpr int XDP_TEST_OFF = 2048;     // self-test flags
+constexpr int XDP_FLAGS_BYTES = 4096;  // slots start here
+static_assert(2 * XDP_MAXW * MC_G * 8 <= XDP_TEST_OFF, "xdp flags");
 __host__ __device__ constexpr long long xdp_region_bytes(int world) {
   return XDP_FLAGS_BYTES + 2LL * world * 2 * WL_N * (long long)sizeof(float);
 }
@@ -183,7 +184,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
   constexpr int relu = RELU;
   constexpr int NPART = OUTP + 6;
   constexpr int WL_B3 = WL_W3 + OUTP * LD;
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef RAI_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memtime();

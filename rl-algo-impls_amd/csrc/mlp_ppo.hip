@@ -1516,6 +1516,7 @@ __global__ __launch_bounds__(NT) void mlp_ppo_rows_kernel(const MlpArgs a) {
 }
 
 #include "mlp_mc.h"
+#include "mlp_mc8.h"
 
 template <int INP, int NAP, int RELU>
 __global__ __launch_bounds__(NT) void mlp_ppo_epoch_kernel(const MlpArgs a) {
@@ -1543,14 +1544,22 @@ namespace {
 constexpr int64_t XCHG_BYTES = 256;  // exchange words (first 64 B zeroed per launch), padded
 constexpr int64_t SCRATCH_ROWS = 2LL * NW * (MAXOUT + 2 + 4) * HID * sizeof(float);
 constexpr int64_t SCRATCH_MC = 2LL * 2 * MC_G * MC_SLOT * sizeof(float);
-constexpr int64_t SCRATCH_BYTES = SCRATCH_ROWS > SCRATCH_MC ? SCRATCH_ROWS : SCRATCH_MC;
+constexpr int64_t SCRATCH_MAX2 = SCRATCH_ROWS > SCRATCH_MC ? SCRATCH_ROWS : SCRATCH_MC;
+constexpr int64_t SCRATCH_BYTES = SCRATCH_MAX2 > M8_SCRATCH ? SCRATCH_MAX2 : M8_SCRATCH;
 
-// Kernel layout for the CartPole class (diagnostics / A-B only: RAI_MLP_LAYOUT=rows|chunk|mc)
+// Kernel layout for the CartPole class (diagnostics / A-B only: RAI_MLP_LAYOUT=rows|chunk|mc4)
 int mlp_layout() {
   const char* e = getenv("RAI_MLP_LAYOUT");
   if (e && !strcmp(e, "rows")) return 1;
   if (e && !strcmp(e, "chunk")) return 2;
-  return 0;  // multi-CU
+  if (e && !strcmp(e, "mc4")) return 3;
+  return 0;  // multi-CU: 8 CUs per network (epoch mode), 4 (data-parallel grads mode)
+}
+
+// CUs per network of the default epoch kernel (A-B: RAI_MLP_CUS=8|16)
+int mlp_cus_per_net() {
+  const char* e = getenv("RAI_MLP_CUS");
+  return (e && !strcmp(e, "8")) ? 8 : 16;
 }
 
 int64_t num_minibatches(int64_t n_rows, int32_t batch_size) {
@@ -1560,7 +1569,7 @@ int64_t moments_bytes(int64_t n_rows, int32_t batch_size) {
   return ((8 * num_minibatches(n_rows, batch_size) + 255) / 256) * 256;
 }
 int64_t statp_bytes(int64_t n_rows, int32_t batch_size) {
-  return 2 * num_minibatches(n_rows, batch_size) * MC_G * 4 * (int64_t)sizeof(double);
+  return 2 * num_minibatches(n_rows, batch_size) * (MC_G > M8_GMAX ? MC_G : M8_GMAX) * 4 * (int64_t)sizeof(double);
 }
 
 int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, void* workspace,
@@ -1597,8 +1606,17 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
   a.statp = reinterpret_cast<double*>(static_cast<unsigned char*>(workspace) + XCHG_BYTES + SCRATCH_BYTES +
                                       moments_bytes(n_rows, batch_size));
   const int layout = mlp_layout();
-  if (a.in_dim <= 4 && a.n_act <= 2 && layout == 0) {
-    // multi-CU layout: MC_G CUs per network, partial-gradient all-reduce per minibatch
+  if (a.in_dim <= 4 && a.n_act <= 2 && layout == 0 && !a.grad_out) {
+    // multi-CU layout, G CUs per network: reduce-scatter + all-gather per minibatch
+    if (mlp_cus_per_net() == 16) {
+      if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_mc8_kernel<1, 16>), dim3(M8Geo<16>::GRID), dim3(M8_NT), 0, s, a);
+      else hipLaunchKernelGGL((mlp_ppo_mc8_kernel<0, 16>), dim3(M8Geo<16>::GRID), dim3(M8_NT), 0, s, a);
+    } else {
+      if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_mc8_kernel<1, 8>), dim3(M8Geo<8>::GRID), dim3(M8_NT), 0, s, a);
+      else hipLaunchKernelGGL((mlp_ppo_mc8_kernel<0, 8>), dim3(M8Geo<8>::GRID), dim3(M8_NT), 0, s, a);
+    }
+  } else if (a.in_dim <= 4 && a.n_act <= 2 && (layout == 0 || layout == 3)) {
+    // multi-CU layout, MC_G CUs per network, partial-gradient all-reduce per minibatch
     if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_mc_kernel<1>), dim3(MC_GRID), dim3(MC_NT), 0, s, a);
     else hipLaunchKernelGGL((mlp_ppo_mc_kernel<0>), dim3(MC_GRID), dim3(MC_NT), 0, s, a);
   } else if (a.in_dim <= 4 && a.n_act <= 2 && layout == 1) {
@@ -1649,7 +1667,7 @@ extern "C" int rai_mlp_ppo_epoch_xdp(float* params, float* exp_avg, float* exp_a
                                      const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
                                      int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
                                      int64_t workspace_bytes, void* stream) {
-  if (!(in_dim <= 4 && n_actions <= 2 && mlp_layout() == 0)) return RAI_E_UNSUPPORTED;
+  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3))) return RAI_E_UNSUPPORTED;
   if (!moments || !peers) return RAI_E_NULLPTR;
   if (world < 2 || world > XDP_MAXW || rank < 0 || rank >= world || step_base < 0) return RAI_E_SHAPE;
   MlpArgs a = {};
@@ -1678,10 +1696,10 @@ __global__ __launch_bounds__(64) void xdp_selftest_kernel(void* const* peers, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (lane < W) {
-    unsigned long long* fl = reinterpret_cast<unsigned long long*>(static_cast<char*>(peers[lane]) + 512) + rank;
+    unsigned long long* fl = reinterpret_cast<unsigned long long*>(static_cast<char*>(peers[lane]) + XDP_TEST_OFF) + rank;
     __hip_atomic_store(fl, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  const unsigned long long* own = reinterpret_cast<const unsigned long long*>(static_cast<char*>(peers[rank]) + 512);
+  const unsigned long long* own = reinterpret_cast<const unsigned long long*>(static_cast<char*>(peers[rank]) + XDP_TEST_OFF);
   unsigned long long spins = 0;
   for (;;) {
     bool ok = lane >= W || __hip_atomic_load(own + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= tag;
@@ -1725,7 +1743,7 @@ int rai_mlp_ppo_dp_step(float* params, float* exp_avg, float* exp_avg_sq, const 
                         const rai_optim_hparams* ohp, rai_train_state* state, float* grad_out, float* stats,
                         int32_t max_stats, float* norms, int32_t max_norms, int32_t sync_base, void* workspace,
                         int64_t workspace_bytes, void* stream) {
-  if (!(in_dim <= 4 && n_actions <= 2 && mlp_layout() == 0)) return RAI_E_UNSUPPORTED;
+  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3))) return RAI_E_UNSUPPORTED;
   if (!grad_out || !moments || !exp_avg || !exp_avg_sq) return RAI_E_NULLPTR;
   if (mb < 0 || mb_count < 0 || sync_base < 0) return RAI_E_SHAPE;
   MlpArgs a = {};

@@ -23,7 +23,6 @@ constexpr int HID = 64;
 constexpr int LD = 66;
 constexpr int NT = 256;        // 4 waves x 16 rows
 constexpr int ROWS = 64;
-constexpr float F32_MIN = -3.4028234663852886e38f;
 
 struct NetPtrs {
   const float* W1;  // [64][in]

@@ -248,7 +248,13 @@ def _random_rollout(T, N, d, n, seed):
 @pytest.mark.parametrize("d,n,act,bs,T,N,layout", [
     (4, 2, "tanh", 256, 8, 96, "mc"),        # CartPole class, ragged last minibatch (768 % 256 = 0 -> 3 full)
     (4, 2, "tanh", 200, 9, 100, "mc"),       # B < 256, ragged tail (900 % 200 = 100)
-    (4, 2, "relu", 64, 8, 64, "mc"),         # B = 64: CUs 1..3 see no rows
+    (4, 2, "relu", 64, 8, 64, "mc"),         # B = 64: CUs 4..15 see no rows
+    (4, 2, "tanh", 40, 5, 50, "mc"),         # B = 40: CU 2's tile half-filled, ragged tail
+    (4, 2, "tanh", 256, 8, 96, "mc8"),       # 8 CUs per network (two 16-row tiles per CU)
+    (4, 2, "relu", 40, 5, 50, "mc8"),        # B = 40: CU 1's second tile half-filled
+    (3, 1, "tanh", 96, 6, 50, "mc8"),
+    (4, 2, "tanh", 256, 8, 96, "mc4"),       # 4-CU-per-network layout (the data-parallel grads kernel)
+    (4, 2, "relu", 200, 9, 100, "mc4"),
     (2, 2, "tanh", 128, 5, 77, "mc"),        # in_dim 2 (padding columns), tail of 1 row avoided (385 % 128 = 1?)
     (3, 1, "tanh", 96, 6, 50, "mc"),         # one action
     (4, 2, "tanh", 256, 8, 96, "rows"),      # diagnostic one-CU row-tile layout
@@ -257,14 +263,17 @@ def _random_rollout(T, N, d, n, seed):
     (8, 8, "relu", 256, 4, 200, "chunk"),    # maximum shape of the chunked kernel
 ])
 def test_fused_epoch_matches_generic_path(d, n, act, bs, T, N, layout, monkeypatch):
-    """One epoch of the fused kernel (given layout) vs the per-minibatch PyTorch path, same
+    """One epoch of the fused kernel (given layout; "mc" = the default, 16 CUs per network) vs
+    the per-minibatch PyTorch path, same
     rollout and permutation.  fp32 tolerances: different summation orders and the fused
     kernel's hardware sqrt/rcp Adam."""
     from rl_algo_impls_amd.policy import ActorCritic
 
     if (T * N) % bs == 1:
         pytest.skip("1-row minibatch has no unbiased std")
-    if layout != "mc":
+    if layout == "mc8":
+        monkeypatch.setenv("RAI_MLP_CUS", "8")
+    elif layout != "mc":
         monkeypatch.setenv("RAI_MLP_LAYOUT", layout)
     roll = _random_rollout(T, N, d, n, seed=d * 100 + n * 10 + bs)
     results = []
@@ -292,7 +301,7 @@ def test_ppo_learns_cartpole_v1():
     """Return check on the real CartPole-v1 dynamics (envs.CartPoleVecEnv, gymnasium 0.29's
     public equations) with the reference's CartPole PPO hyperparameters
     (rl_algo_impls/hyperparams/ppo.yml:1-23: 8 envs x 32 steps, batch 256, 20 epochs, lr 1e-3,
-    gamma 0.98, lambda 0.8, clip 0.2; the YAML's linear lr/clip decay is not applied).
+    gamma 0.98, lambda 0.8, clip 0.2, and its linear lr/clip decay to 0 over the 100k steps).
     Statistical, not bit-level: the rolling mean of the last 100 episode returns must pass 475
     (the 500-step cap is CartPole-v1's maximum) within 100k steps, as the reference does."""
     from rl_algo_impls_amd.envs import CartPoleVecEnv
@@ -308,6 +317,10 @@ def test_ppo_learns_cartpole_v1():
     best = 0.0
     steps = 0
     while steps < 100_000:
+        # the YAML's hyperparam_transitions: lr 1e-3 -> 0 and clip 0.2 -> 0, linear in progress
+        # (rl_algo_impls/shared/callbacks/hyperparam_transitions.py:85-100, interpolate "linear")
+        prog = steps / 100_000
+        algo.learning_rate, algo.clip_range = 1e-3 * (1 - prog), 0.2 * (1 - prog)
         steps, _ = algo.learn_epoch(steps, 100_000, gen, None)
         if len(gen.episode_returns) >= 20:
             best = max(best, float(np.mean(gen.episode_returns)))

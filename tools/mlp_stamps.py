@@ -21,9 +21,12 @@ from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
 from rl_algo_impls_amd.ppo import PPO  # noqa: E402
 from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 
-LAYOUT = os.environ.get("RAI_MLP_LAYOUT", "mc")
+LAYOUT = os.environ.get("RAI_MLP_LAYOUT", "mc8")
 NAMES = {
-    "mc": ["F1+F2 forward", "out layer + loss + dZ2", "dH1 + partials + barrier", "P_B dW2 + sums",
+    "mc8": ["F1 (own columns) + barrier", "F2 + output partials + barrier", "loss + dZ2 + barrier",
+            "dH1 + dZ1 + partials + barrier", "P_B dW2 + sums", "round 1: publish + counter wait",
+            "share sum + round 2 publish + wait", "all-gather + norm + adam"],
+    "mc4": ["F1+F2 forward", "out layer + loss + dZ2", "dH1 + partials + barrier", "P_B dW2 + sums",
            "publish + counter wait", "reduce G slots + |g|^2", "stats + norm exchange", "adam"],
     "rows": ["F1 layer1 (wave-local)", "F2 layer2 + epilogue", "out layer + loss + dZ2", "dH1 MFMA",
              "dZ1/partials + barrier", "P_B dW2 MFMA", "E2 owner sums + norm", "E3 stats + exchange",
