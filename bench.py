@@ -166,7 +166,7 @@ def main():
     gae_us = e0.elapsed_time(e1) * 1e3 / args.roofline_reps
     workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
     pmc = {}
-    pmc_path = ROOT / "profiles" / "r1_pmc_final.json"
+    pmc_path = ROOT / "profiles" / "r1_pmc.json"
     if pmc_path.exists():
         pmc = json.loads(pmc_path.read_text()).get(workload, {})
 
@@ -182,8 +182,12 @@ def main():
         flops = 52352.0 * T * N
         ms = float(np.mean(epoch_ms))
         tf = flops / (ms * 1e-3) / 1e12
-        kname = "mlp_ppo_mc_kernel<%d>" % int(cfg["policy"].get("activation_fn", "tanh") == "relu")
-        roofline = {"kernel": kname + " (rai_mlp_ppo_epoch, 4 CUs per network)", "bound": "mfma",
+        # the kernel rai_mlp_ppo_epoch dispatches for in_dim <= 4, n_actions <= 2 (csrc/mlp_ppo.hip
+        # mlp_launch): G = 16 CUs per network unless RAI_MLP_CUS=8
+        act = int(cfg["policy"].get("activation_fn", "tanh") == "relu")
+        G = 8 if os.environ.get("RAI_MLP_CUS") == "8" else 16
+        kname = "mlp_ppo_mc8_kernel<%d, %d>" % (act, G)
+        roofline = {"kernel": kname + f" (rai_mlp_ppo_epoch, {G} CUs per network)", "bound": "mfma",
                     "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
                     "traffic": traffic(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}

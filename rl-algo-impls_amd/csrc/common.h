@@ -23,6 +23,17 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// ---- bounded spins ----------------------------------------------------------
+// Spin limits are wall-clock: s_memrealtime is the constant 100 MHz counter (s_memtime, the shader
+// clock, was seen to jump under rocprofv3 kernel tracing and fail a healthy wait).  The elapsed
+// time is compared signed, so a counter that steps backwards never expires a wait.
+constexpr long long RAI_SPIN_LOCAL = 200000000LL;    // 2 s: partners on the same GPU
+constexpr long long RAI_SPIN_REMOTE = 6000000000LL;  // 60 s: other ranks (they may still be launching)
+__device__ __forceinline__ unsigned long long rai_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool rai_expired(unsigned long long t0, long long limit) {
+  return (long long)(rai_clock() - t0) > limit;
+}
+
 // ---- wave64 reductions (fixed order -> deterministic) ----------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -388,7 +388,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
   // Bounded waits, by elapsed shader-clock ticks (~2.4 GHz): 2 s for partners on this GPU (they are
   // co-resident and a minibatch apart at most), 60 s for other GPUs (their ranks can start an
   // epoch later by host-side jitter: rollouts, collectives).  A timeout sets err and stops the CU.
-  constexpr unsigned long long MC_WAIT_LOCAL = 5000000000ull, MC_WAIT_REMOTE = 150000000000ull;
+  constexpr long long MC_WAIT_LOCAL = RAI_SPIN_LOCAL, MC_WAIT_REMOTE = RAI_SPIN_REMOTE;
   for (int mb = mb_begin; mb < mb_end; ++mb) {
     const int kk_mb = mb - mb_begin;
     const int par = mb & 1;
@@ -729,9 +729,9 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     if (tid == 0) {
       __hip_atomic_fetch_add(&sync[MC_CNT + net], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned long long want = (unsigned long long)MC_G * (sbase + (unsigned long long)(kk_mb + 1));
-      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      const unsigned long long t0 = rai_clock();
       while (__hip_atomic_load(&sync[MC_CNT + net], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-        if (__builtin_amdgcn_s_memtime() - t0 > MC_WAIT_LOCAL) { atomicExch(a.err, 1); S.bail = 1; break; }
+        if (rai_expired(t0, MC_WAIT_LOCAL)) { atomicExch(a.err, 1); S.bail = 1; break; }
         __builtin_amdgcn_s_sleep(1);
       }
     }
@@ -792,13 +792,13 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
         if (w == 0) {  // one wave polls this rank's W*G flags of this network
           const unsigned long long* fl = reinterpret_cast<const unsigned long long*>(a.xpeers[a.xrank]) +
                                          net * XDP_MAXW * MC_G;
-          const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+          const unsigned long long t0 = rai_clock();
           for (;;) {
             bool ok = true;
             if (lane < W * MC_G)
               ok = __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= step_id;
             if (__all(ok)) break;
-            if (__builtin_amdgcn_s_memtime() - t0 > MC_WAIT_REMOTE) {
+            if (rai_expired(t0, MC_WAIT_REMOTE)) {
               if (lane == 0) { atomicExch(a.err, 1); S.bail = 1; }
               break;
             }
@@ -851,12 +851,12 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
         const unsigned long long gv = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(mine);
         __hip_atomic_store(&sync[MC_XG + (net * MC_G + c) * 2 + par], gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         float other = 0.f;
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long t0 = rai_clock();
         for (;;) {
           const unsigned long long x = __hip_atomic_load(&sync[MC_XG + ((1 - net) * MC_G + c) * 2 + par],
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((unsigned)(x >> 32) == tag) { other = __uint_as_float((unsigned)x); break; }
-          if (__builtin_amdgcn_s_memtime() - t0 > MC_WAIT_LOCAL) { atomicExch(a.err, 1); S.bail = 1; break; }
+          if (rai_expired(t0, MC_WAIT_LOCAL)) { atomicExch(a.err, 1); S.bail = 1; break; }
           __builtin_amdgcn_s_sleep(1);
         }
         S.bcast[0] = net == 0 ? mine : other;
@@ -965,10 +965,10 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
     if (!ACTOR) {
       __hip_atomic_fetch_add(&sync[MC_DONE], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else if (c == 0) {
-      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      const unsigned long long t0 = rai_clock();
       while (__hip_atomic_load(&sync[MC_DONE], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <
              (unsigned long long)MC_G * (sbase + 1)) {
-        if (__builtin_amdgcn_s_memtime() - t0 > MC_WAIT_LOCAL) { atomicExch(a.err, 1); break; }
+        if (rai_expired(t0, MC_WAIT_LOCAL)) { atomicExch(a.err, 1); break; }
         __builtin_amdgcn_s_sleep(1);
       }
     }

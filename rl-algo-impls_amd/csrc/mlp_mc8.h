@@ -163,11 +163,11 @@ __device__ __forceinline__ void ppo_row_loss(const float (&z)[OUTP], const RowLo
 
 // bounded spin of one lane until sync[i0] and sync[i1] both reach `want`
 __device__ __forceinline__ bool m8_wait2(unsigned long long* sync, int i0, int i1, unsigned long long want,
-                                         unsigned long long limit) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+                                         long long limit) {
+  const unsigned long long t0 = rai_clock();
   while (__hip_atomic_load(&sync[i0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want ||
          __hip_atomic_load(&sync[i1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-    if (__builtin_amdgcn_s_memtime() - t0 > limit) return false;
+    if (rai_expired(t0, limit)) return false;
     __builtin_amdgcn_s_sleep(1);
   }
   return true;
@@ -284,7 +284,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
   if (tid == 0) S.t_last = __builtin_amdgcn_s_memtime();
 #endif
 
-  constexpr unsigned long long MC_WAIT_LOCAL = 5000000000ull, MC_WAIT_REMOTE = 150000000000ull;
+  constexpr long long MC_WAIT_LOCAL = RAI_SPIN_LOCAL, MC_WAIT_REMOTE = RAI_SPIN_REMOTE;
   for (int mb = 0; mb < nmb; ++mb) {
     const int par = mb & 1;
     const int64_t row0 = (int64_t)mb * B;
@@ -627,12 +627,12 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         if (w == 0) {
           const unsigned long long* fl = reinterpret_cast<const unsigned long long*>(a.xpeers[a.xrank]) +
                                          (net * XDP_MAXW + lane) * G + c;
-          const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+          const unsigned long long t0 = rai_clock();
           for (;;) {
             bool ok = true;
             if (lane < W) ok = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= step_id;
             if (__all(ok)) break;
-            if (__builtin_amdgcn_s_memtime() - t0 > MC_WAIT_REMOTE) {
+            if (rai_expired(t0, MC_WAIT_REMOTE)) {
               if (lane == 0) { atomicExch(a.err, 1); S.bail = 1; }
               break;
             }

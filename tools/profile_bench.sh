@@ -1,0 +1,38 @@
+#!/bin/bash
+# GPU-box profiling run for the bench workload(s): rocprofv3 kernel-trace stats of bench.py, then one
+# PMC pass per TCC counter (FETCH_SIZE and WRITE_SIZE cannot share a pass), each step under its own
+# time limit; stops at the first step that does not exit 0.  Output: gpurun_out/prof_<tag>/...
+#   TAG=r1b CONFIGS="cartpole pong" bash tools/profile_bench.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-r1}
+CONFIGS=${CONFIGS:-cartpole}
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+  grep -v amdgpu.ids "$OUT/$name.log" | tail -3
+  [ $rc -eq 0 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
+}
+for c in $CONFIGS; do
+  extra=${EXTRA:-}
+  run "stats_$c" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_$c" -o run -- \
+      python3 bench.py --config "$c" --steps 2 --warmup 1 --no-cpu-baseline $extra
+  if [ "${PMC:-1}" = 1 ]; then
+    run "fetch_$c" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$c" -o run -- \
+        python3 bench.py --config "$c" --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 $extra
+    run "write_$c" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$c" -o run -- \
+        python3 bench.py --config "$c" --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 $extra
+  fi
+  if [ -n "${MFMA_PMC:-}" ]; then
+    run "mfma_$c" 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
+        --output-format csv -d "$OUT/mfma_$c" -o run -- \
+        python3 bench.py --config "$c" --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 $extra
+  fi
+done
+exit 0
