@@ -106,3 +106,31 @@ def make_rank_data(rank, dev, n=512):
     ret = vals + adv
     t = lambda x: x.to(dev)
     return Batch(t(obs), t(logp), t(act), None, None, t(vals), t(adv), t(ret))
+
+
+def rms_worker(rank, world, port, q):
+    """Normalize wrappers over a ragged env split with the cross-rank RunningMeanStd merge."""
+    import numpy as np
+    import torch.distributed as dist
+
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd import wrappers
+    from test_host_wrappers import FixtureEnv
+
+    _init(rank, world, port)
+    z = np.load(ROOT / "tests" / "golden" / "host_wrappers.npz", allow_pickle=False)
+    n = z["env_obs"].shape[1]
+    # ragged split: rank 0 owns 3 envs, rank 1 the other 5
+    envs = slice(0, 3) if rank == 0 else slice(3, n)
+    env = wrappers.NormalizeReward(wrappers.NormalizeObservation(FixtureEnv(z, envs), group=dist.group.WORLD),
+                                   gamma=0.97, group=dist.group.WORLD)
+    o, _ = env.reset()
+    obs, rew = [o], []
+    for _ in range(z["env_rew"].shape[0]):
+        o, r, *_ = env.step(None)
+        obs.append(o)
+        rew.append(r)
+    q.put((rank, np.stack(obs), np.stack(rew), env.env.rms.mean, env.rms.var))
+    dist.destroy_process_group()
