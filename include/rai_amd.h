@@ -165,6 +165,32 @@ int rai_gather_rows(int32_t n_fields, const void* const* src, void* const* dst,
                     const int64_t* row_bytes, const int64_t* idx, int64_t n_rows, void* stream);
 
 /* --------------------------------------------------------------------------
+ * Device-indexed minibatch gather for graph-replayed updates.  The source
+ * fields, the epoch permutation and the minibatch counter live in a device
+ * descriptor, so one captured launch sequence (gather -> forward -> loss ->
+ * backward -> optimizer) is replayed for every minibatch of an epoch without
+ * host work.  rai_gather_minibatch copies rows perm[mb*B + i] (identity order
+ * when perm is NULL), i < min(B, n_rows - mb*B), of every field into dst;
+ * rai_minibatch_advance then increments desc->mb (a separate launch, so every
+ * block of the gather has read mb).  Same rows as Batch.__getitem__ over
+ * VecRollout.minibatches (rl_algo_impls/rollout/vec_rollout.py:166-175,
+ * rollout.py:56-69).  Row sizes: multiples of 16, 4 or 1 bytes.
+ * ------------------------------------------------------------------------ */
+typedef struct rai_minibatch_desc {
+  const void* src[RAI_MAX_FIELDS];
+  int64_t row_bytes[RAI_MAX_FIELDS];
+  const int64_t* perm;  /* epoch permutation of [0, n_rows), or NULL */
+  int64_t n_rows;       /* rows in the rollout (T*N) */
+  int64_t batch_size;
+  int64_t mb;           /* next minibatch, advanced on device */
+  int32_t n_fields;
+  int32_t pad;
+} rai_minibatch_desc;
+int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
+                         const int64_t* row_bytes, int64_t batch_size, void* stream);
+int rai_minibatch_advance(rai_minibatch_desc* desc, void* stream);
+
+/* --------------------------------------------------------------------------
  * Rollout post-head: sample actions from the policy head and write the
  * rollout-buffer slot.  Replaces rl_algo_impls/shared/policy/actor_critic.py:
  * 306-318 (pi.sample, pi.log_prob, .cpu()) and the slot writes of

@@ -47,6 +47,21 @@ class PPOHparams(C.Structure):
     ]
 
 
+class MinibatchDesc(C.Structure):
+    """Mirror of rai_minibatch_desc."""
+
+    _fields_ = [
+        ("src", C.c_void_p * RAI_MAX_FIELDS),
+        ("row_bytes", C.c_int64 * RAI_MAX_FIELDS),
+        ("perm", C.c_void_p),
+        ("n_rows", C.c_int64),
+        ("batch_size", C.c_int64),
+        ("mb", C.c_int64),
+        ("n_fields", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
 class OptimHparams(C.Structure):
     _fields_ = [
         ("lr", C.c_float),
@@ -84,6 +99,8 @@ _SIGNATURES = {
     "rai_optim_workspace_bytes": (_i64, [_i64]),
     "rai_clip_optim_step": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_gather_rows": (C.c_int, [_i32, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "rai_gather_minibatch": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
+    "rai_minibatch_advance": (C.c_int, [_vp, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, [C.c_int64, C.c_int32]),
     "rai_mlp_ppo_grads": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _i32,
                                     _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),

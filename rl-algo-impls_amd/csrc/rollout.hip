@@ -46,6 +46,41 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
   }
 }
 
+// Minibatch gather driven by a device descriptor (graph replay: the launch is fixed, the
+// minibatch index advances on device).  blockIdx.y = field; dst pointers are launch arguments.
+struct MbDst {
+  uint8_t* dst[RAI_MAX_FIELDS];
+  int64_t units[RAI_MAX_FIELDS];
+  int32_t gran[RAI_MAX_FIELDS];
+};
+__global__ __launch_bounds__(256) void gather_minibatch_kernel(const rai_minibatch_desc* __restrict__ d,
+                                                               const MbDst o) {
+  const int fi = blockIdx.y;
+  const int64_t mb = d->mb, B = d->batch_size;
+  const int64_t row0 = mb * B;
+  const int64_t rows = min(B, d->n_rows - row0);
+  const int64_t units = o.units[fi];
+  const int gran = o.gran[fi];
+  const uint8_t* src = static_cast<const uint8_t*>(d->src[fi]);
+  const int64_t* perm = d->perm;
+  const int64_t total = rows * units;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total; u += stride) {
+    const int64_t r = u / units;
+    const int64_t j = u - r * units;
+    const int64_t sr = perm ? perm[row0 + r] : row0 + r;
+    if (gran == 16) {
+      reinterpret_cast<uint4*>(o.dst[fi])[u] = reinterpret_cast<const uint4*>(src)[sr * units + j];
+    } else if (gran == 4) {
+      reinterpret_cast<uint32_t*>(o.dst[fi])[u] = reinterpret_cast<const uint32_t*>(src)[sr * units + j];
+    } else {
+      o.dst[fi][u] = src[sr * units + j];
+    }
+  }
+}
+
+__global__ void minibatch_advance_kernel(rai_minibatch_desc* d) { d->mb += 1; }
+
 // One thread per env row.  Masked logits follow MaskedCategorical
 // (torch.where(mask, logits, finfo.min)); torch.distributions normalises
 // logits by logsumexp; log_prob(a) = logits[a] - logsumexp.
@@ -157,6 +192,35 @@ extern "C" int rai_gather_rows(int32_t n_fields, const void* const* src, void* c
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks, (unsigned)n_fields), dim3(256), 0,
                      rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
+                                    const int64_t* row_bytes, int64_t batch_size, void* stream) {
+  if (n_fields < 1 || n_fields > RAI_MAX_FIELDS || batch_size < 1) return RAI_E_SHAPE;
+  if (!desc || !dst || !row_bytes) return RAI_E_NULLPTR;
+  MbDst o;
+  int64_t max_units = 1;
+  for (int i = 0; i < n_fields; ++i) {
+    if (!dst[i] || row_bytes[i] < 1) return RAI_E_NULLPTR;
+    const int gran = (row_bytes[i] % 16 == 0) ? 16 : ((row_bytes[i] % 4 == 0) ? 4 : 1);
+    o.dst[i] = static_cast<uint8_t*>(dst[i]);
+    o.gran[i] = gran;
+    o.units[i] = row_bytes[i] / gran;
+    if (o.units[i] > max_units) max_units = o.units[i];
+  }
+  int64_t blocks = (batch_size * max_units + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(gather_minibatch_kernel, dim3((unsigned)blocks, (unsigned)n_fields), dim3(256), 0,
+                     rai_stream(stream), desc, o);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_minibatch_advance(rai_minibatch_desc* desc, void* stream) {
+  if (!desc) return RAI_E_NULLPTR;
+  hipLaunchKernelGGL(minibatch_advance_kernel, dim3(1), dim3(1), 0, rai_stream(stream), desc);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

@@ -1,0 +1,136 @@
+"""HIP-graph replay of the generic per-minibatch update (policies the fused epoch kernels do not
+cover: NatureCNN, Gaussian / 256-wide MLPs, A2C).
+
+The reference runs one eager minibatch step per Python iteration (rl_algo_impls/ppo/ppo.py:
+290-411): ~100 small launches (forward, loss, autograd backward, clip + Adam) whose host launch
+cost exceeds their GPU time at these batch sizes.  Here the step is captured ONCE into a hipGraph
+(torch.cuda.CUDAGraph) and replayed for every minibatch of every epoch:
+
+    rai_gather_minibatch   rows perm[mb*B + i] of every rollout field -> static minibatch buffers
+    rai_minibatch_advance  mb += 1 (device-side counter in a rai_minibatch_desc)
+    policy forward         PyTorch-ROCm (MIOpen / hipBLASLt), static inputs
+    rai_ppo_loss           loss + dLoss/d(logp, entropy, v), stats row at state.stat_index
+    autograd backward      into the flat .grad buffer
+    rai_clip_optim_step    clip_grad_norm_ + Adam/RMSprop (omitted under data parallel or
+                           gradient accumulation: the all-reduce / epoch step stays eager)
+
+Everything a replay needs to vary lives in device memory: the minibatch index (descriptor), the
+hyperparameters and train state (stat_index, opt_step, kl latch), so a replay takes no host
+input.  Per update the host writes the descriptor once (rollout field pointers) and per epoch
+copies the permutation into a persistent buffer and zeroes the counter.
+
+The first minibatches of the first update run eagerly on the capture stream (warm-up: lazy
+library handles, autograd stream state), the capture itself executes nothing, and a ragged tail
+minibatch always runs eagerly through the same gather with its own buffers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+_DESC_MB_OFFSET = _lib.MinibatchDesc.mb.offset
+
+
+class MinibatchStepGraph:
+    """Static buffers + captured graph for one (batch_size, field layout) of one trainer."""
+
+    WARMUP = 2
+
+    def __init__(self, device: torch.device, fields: List[torch.Tensor], batch_size: int,
+                 step: Callable[[List[torch.Tensor]], None]):
+        self.device = device
+        self.B = int(batch_size)
+        self.step = step
+        self.row_bytes = [int(f[0].numel() * f.element_size()) for f in fields]
+        self.static = [torch.empty((self.B,) + tuple(f.shape[1:]), dtype=f.dtype, device=device) for f in fields]
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.eager_runs = 0
+
+    def gather(self, desc: torch.Tensor, bufs: List[torch.Tensor]) -> None:
+        n = len(bufs)
+        dst = (C.c_void_p * n)(*[b.data_ptr() for b in bufs])
+        rb = (C.c_int64 * n)(*self.row_bytes)
+        st = _lib.stream_handle(self.device)
+        L = _lib.lib()
+        _lib.check(L.rai_gather_minibatch(desc.data_ptr(), n, C.cast(dst, C.c_void_p), C.cast(rb, C.c_void_p),
+                                          int(bufs[0].shape[0]), st), "rai_gather_minibatch")
+        _lib.check(L.rai_minibatch_advance(desc.data_ptr(), st), "rai_minibatch_advance")
+
+    def _body(self, desc: torch.Tensor) -> None:
+        self.gather(desc, self.static)
+        self.step(self.static)
+
+    def run(self, desc: torch.Tensor, stream: torch.cuda.Stream) -> None:
+        """One minibatch on `stream` (the caller has made it current)."""
+        if self.graph is not None:
+            self.graph.replay()
+            return
+        if self.eager_runs < self.WARMUP:
+            self._body(desc)
+            self.eager_runs += 1
+            return
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            self._body(desc)
+        self.graph = g
+        g.replay()  # the capture executed nothing: this replay is the minibatch
+
+
+class GraphedUpdate:
+    """Per-trainer cache of minibatch graphs and the device descriptor."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.stream = torch.cuda.Stream(device)
+        self.desc = torch.zeros(C.sizeof(_lib.MinibatchDesc), dtype=torch.uint8, device=device)
+        self.graphs: Dict[Tuple, MinibatchStepGraph] = {}
+        self.perm: Optional[torch.Tensor] = None
+        self._tail_bufs: Dict[Tuple, List[torch.Tensor]] = {}
+
+    def key(self, fields: List[torch.Tensor], B: int, tag) -> Tuple:
+        return (B, tag) + tuple((f.dtype, tuple(f.shape[1:])) for f in fields)
+
+    def set_rollout(self, fields: List[torch.Tensor], batch_size: int, shuffle: bool) -> None:
+        n = int(fields[0].shape[0])
+        if shuffle and (self.perm is None or self.perm.numel() != n):
+            self.perm = torch.empty(n, dtype=torch.int64, device=self.device)
+        d = _lib.MinibatchDesc()
+        for i, f in enumerate(fields):
+            assert f.is_contiguous() and f.shape[0] == n
+            d.src[i] = f.data_ptr()
+            d.row_bytes[i] = int(f[0].numel() * f.element_size())
+        d.perm = self.perm.data_ptr() if shuffle else None
+        d.n_rows, d.batch_size, d.mb, d.n_fields = n, int(batch_size), 0, len(fields)
+        raw = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8)
+        self.desc.copy_(raw, non_blocking=False)
+
+    def start_epoch(self, perm: Optional[torch.Tensor]) -> None:
+        if perm is not None:
+            self.perm.copy_(perm, non_blocking=True)
+        self.desc[_DESC_MB_OFFSET:_DESC_MB_OFFSET + 8].view(torch.int64).zero_()
+
+    def graph_for(self, fields: List[torch.Tensor], B: int, tag, step) -> MinibatchStepGraph:
+        k = self.key(fields, B, tag)
+        g = self.graphs.get(k)
+        if g is None:
+            g = MinibatchStepGraph(self.device, fields, B, step)
+            self.graphs[k] = g
+        g.step = step
+        return g
+
+    def tail(self, fields: List[torch.Tensor], rows: int, step) -> None:
+        """Eager ragged last minibatch through the same device gather."""
+        k = self.key(fields, rows, "tail")
+        bufs = self._tail_bufs.get(k)
+        if bufs is None:
+            bufs = [torch.empty((rows,) + tuple(f.shape[1:]), dtype=f.dtype, device=self.device) for f in fields]
+            self._tail_bufs[k] = bufs
+        helper = MinibatchStepGraph.__new__(MinibatchStepGraph)
+        helper.device = self.device
+        helper.row_bytes = [int(f[0].numel() * f.element_size()) for f in fields]
+        helper.gather(self.desc, bufs)
+        step(bufs)

@@ -93,8 +93,9 @@ class FlatOptimizer:
                                beta2_d=float(self.betas[1]))
         struct_to_device(hp, self.device, self.hp_dev)
 
-    def step(self, state_dev: torch.Tensor, norms: Optional[torch.Tensor]) -> None:
-        """Enqueue clip + update (+ zero grads); no host sync."""
+    def step(self, state_dev: torch.Tensor, norms: Optional[torch.Tensor], count: bool = True) -> None:
+        """Enqueue clip + update (+ zero grads); no host sync.  count=False for launches recorded
+        into a graph (the caller accounts for the replays in step_count)."""
         f = self.flat
         rc = _lib.lib().rai_clip_optim_step(
             f.flat.data_ptr(), f.grad.data_ptr(), self.state1.data_ptr(),
@@ -103,7 +104,8 @@ class FlatOptimizer:
             0 if norms is None else int(norms.numel()), self.workspace.data_ptr(), self.workspace.numel(),
             _lib.stream_handle(self.device))
         _lib.check(rc, "rai_clip_optim_step")
-        self.step_count += 1
+        if count:
+            self.step_count += 1
 
     # -- torch-format checkpoint ------------------------------------------------------
     def state_dict(self) -> Dict:

@@ -35,6 +35,8 @@ from .envs import is_box, is_discrete
 
 ACTIVATION = {"tanh": nn.Tanh, "relu": nn.ReLU, "identity": nn.Identity, "sigmoid": nn.Sigmoid}
 MODEL_FILENAME = "model.pth"
+NORMALIZE_OBSERVATION_FILENAME = "norm_obs.npz"
+NORMALIZE_REWARD_FILENAME = "norm_reward.npz"
 F32_MIN = torch.finfo(torch.float32).min
 
 
@@ -290,6 +292,14 @@ class ActorCritic(nn.Module):
                                             activation_fn, log_std_init, cnn_flatten_dim, cnn_style,
                                             cnn_layers_init_orthogonal)
         self._device: Optional[torch.device] = None
+        # policy.py:31-36: the env's normalisation statistics travel with the checkpoint
+        from .wrappers import NormalizeObservation, NormalizeReward, find_wrapper
+
+        norm_obs = find_wrapper(env, NormalizeObservation)
+        self.norm_observation_rms = norm_obs.rms if norm_obs else None
+        norm_rew = find_wrapper(env, NormalizeReward)
+        self.norm_reward_rms = norm_rew.rms if norm_rew else None
+        self.load_path: Optional[str] = None
 
     # -- reference API ------------------------------------------------------------
     def to(self, device=None, *args, **kwargs):
@@ -363,12 +373,40 @@ class ActorCritic(nn.Module):
         self.load_state_dict(torch.load(os.path.join(path, MODEL_FILENAME), map_location=self._device,
                                         weights_only=True))
 
-    def save(self, path: str) -> None:
+    def save(self, path: str) -> None:  # policy.py:76-85
         os.makedirs(path, exist_ok=True)
+        if self.norm_observation_rms:
+            self.norm_observation_rms.save(os.path.join(path, NORMALIZE_OBSERVATION_FILENAME))
+        if self.norm_reward_rms:
+            self.norm_reward_rms.save(os.path.join(path, NORMALIZE_REWARD_FILENAME))
         self.save_weights(path)
 
-    def load(self, path: str, load_norm_rms_count_override=None) -> None:
+    def load(self, path: str, load_norm_rms_count_override=None) -> None:  # policy.py:87-101
+        self.load_path = path
         self.load_weights(path)
+        if self.norm_observation_rms:
+            self.norm_observation_rms.load(os.path.join(path, NORMALIZE_OBSERVATION_FILENAME),
+                                           count_override=load_norm_rms_count_override)
+        if self.norm_reward_rms:
+            self.norm_reward_rms.load(os.path.join(path, NORMALIZE_REWARD_FILENAME),
+                                      count_override=load_norm_rms_count_override)
+
+    def sync_normalization(self, destination_env) -> None:  # policy.py:141-152
+        from copy import deepcopy
+
+        from .wrappers import NormalizeObservation, NormalizeReward
+
+        current = destination_env
+        while current is not current.unwrapped:
+            if isinstance(current, NormalizeObservation):
+                assert self.norm_observation_rms
+                current.rms = deepcopy(self.norm_observation_rms)
+            elif isinstance(current, NormalizeReward):
+                assert self.norm_reward_rms
+                current.rms = deepcopy(self.norm_reward_rms)
+            current = getattr(current, "env", None)
+            if current is None:
+                raise AttributeError("wrapper chain without an env attribute")
 
     def num_parameters(self) -> int:
         return sum(p.numel() for p in self.parameters())

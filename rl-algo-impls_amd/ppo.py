@@ -75,6 +75,10 @@ class PPO:
         self.blocks = DeviceBlocks(self.device)
         self.last_update_seconds: Optional[float] = None
         self.force_generic = False  # True: always use the per-minibatch (PyTorch network) path
+        # generic path: capture the minibatch step into a hipGraph and replay it (graphs.py);
+        # RAI_GRAPHS=0 keeps the eager loop
+        self.use_graphs = os.environ.get("RAI_GRAPHS", "1") != "0"
+        self._graphed = None
         # bench/profiling hook: when a list, (start, end) HIP events bracket every fused epoch launch
         self.kernel_events: Optional[list] = None
         self._mlp_ws: Optional[torch.Tensor] = None
@@ -455,6 +459,11 @@ class PPO:
         blocks.ensure_tables(n_steps, n_norms)
         K = None
         self.flat.check_views()
+        if (self.use_graphs and self.flat.flat.is_cuda and hasattr(r, "_flat_fields")
+                and r.logprobs is not None and not (self.dp_enabled and self.world > 1
+                                                    and torch.distributed.get_backend(self.dp_group) != "nccl")):
+            K = self._update_graphed(r, nmb)
+            return self._read_stats(n_steps, n_norms, K)
         for _ in range(self.n_epochs):
             for mb in r.minibatches(self.batch_size, shuffle=not self.gradient_accumulation):
                 logp, ent, v = self.policy(mb.obs, mb.actions, action_masks=mb.action_masks)
@@ -474,6 +483,10 @@ class PPO:
                 if self.dp_enabled:
                     self._all_reduce(self.flat.grad, average=True)
                 self.optimizer.step(blocks.state, blocks.norms)
+        return self._read_stats(n_steps, n_norms, K)
+
+    def _read_stats(self, n_steps: int, n_norms: int, K: Optional[int]) -> Tuple[np.ndarray, np.ndarray, int]:
+        blocks = self.blocks
         stats_t = blocks.stats[:n_steps]
         if self.dp_enabled:
             stats_t = stats_t.clone()
@@ -481,6 +494,72 @@ class PPO:
         host = torch.cat([stats_t.reshape(-1), blocks.norms[:n_norms]]).cpu().numpy()
         stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE)
         return stats, host[n_steps * _lib.RAI_STAT_STRIDE:], K or 1
+
+    def _update_graphed(self, r, nmb: int) -> int:
+        """The generic update with the minibatch step replayed from a hipGraph (graphs.py).
+        Same minibatches, same kernels, same order as the eager loop above."""
+        from .graphs import GraphedUpdate
+
+        if self._graphed is None:
+            self._graphed = GraphedUpdate(self.device)
+        gu = self._graphed
+        blocks = self.blocks
+        fields = r._flat_fields()
+        shuffle = not self.gradient_accumulation
+        n = r.total_steps
+        B = min(self.batch_size, n)
+        n_full, tail = n // B, n % B
+        optim_in_step = not self.gradient_accumulation and not self.dp_enabled
+        has_masks = r.action_masks is not None
+        K_box = [None]
+
+        def step(bufs):
+            obs, actions, values, adv, ret, logprobs = bufs[:6]
+            masks = bufs[6] if has_masks else None
+            logp, ent, v = self.policy(obs, actions, action_masks=masks)
+            if K_box[0] is None:
+                K_box[0] = value_columns(v)
+            d_logp, d_ent, d_v = launch_loss(blocks, logp, ent, v, logprobs, values, adv, ret, K_box[0])
+            torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
+            if optim_in_step:
+                self.optimizer.step(blocks.state, blocks.norms, count=False)
+
+        # K (value columns) before the device blocks are written: one forward of one row
+        with torch.no_grad():
+            _, _, v0 = self.policy(fields[0][:1], fields[1][:1],
+                                   action_masks=fields[6][:1] if has_masks else None)
+        K = value_columns(v0)
+        K_box[0] = K
+        blocks.upload(self._hparams(K, nmb), self.optimizer.step_count)
+        # a graph bakes in every device pointer it touches: key it on the ones that can change
+        tag = (optim_in_step, blocks.stats.data_ptr(), blocks.norms.data_ptr(), blocks.hp.data_ptr(),
+               blocks.state.data_ptr(), self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
+               self.optimizer.hp_dev.data_ptr())
+        g = gu.graph_for(fields, B, tag, step)
+        cur = torch.cuda.current_stream(self.device)
+        gu.stream.wait_stream(cur)
+        with torch.cuda.stream(gu.stream):
+            gu.set_rollout(fields, B, shuffle)
+            for _ in range(self.n_epochs):
+                gu.start_epoch(r.permutation() if shuffle else None)
+                for _ in range(n_full):
+                    g.run(gu.desc, gu.stream)
+                    if not optim_in_step and not self.gradient_accumulation:
+                        self._all_reduce(self.flat.grad, average=True)
+                        self.optimizer.step(blocks.state, blocks.norms)
+                if tail:
+                    gu.tail(fields, tail, step)
+                    if not optim_in_step and not self.gradient_accumulation:
+                        self._all_reduce(self.flat.grad, average=True)
+                        self.optimizer.step(blocks.state, blocks.norms)
+                if self.gradient_accumulation:
+                    if self.dp_enabled:
+                        self._all_reduce(self.flat.grad, average=True)
+                    self.optimizer.step(blocks.state, blocks.norms)
+        cur.wait_stream(gu.stream)
+        if optim_in_step:  # replays stepped the optimizer on device; keep the host count in sync
+            self.optimizer.step_count += self.n_epochs * (n_full + (1 if tail else 0))
+        return K
 
     def _train_stats(self, stats: np.ndarray, norms: np.ndarray, K: int, nmb: int, explained_var: float):
         last = stats[-nmb:].astype(np.float64)  # only the last epoch's stats are kept (ppo.py:288-289)

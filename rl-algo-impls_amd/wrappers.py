@@ -48,6 +48,16 @@ def get_infos(infos: dict, key: Any, num_envs: int, default_value: Any) -> List[
     return [default_value for _ in range(num_envs)]
 
 
+def find_wrapper(env, wrapper_class):
+    """vector_wrapper.py:26-32: the outermost wrapper of `wrapper_class` in env's chain."""
+    current = env
+    while current is not None and current is not getattr(current, "unwrapped", current):
+        if isinstance(current, wrapper_class):
+            return current
+        current = getattr(current, "env", None)
+    return None
+
+
 class VectorWrapper:
     """Attribute-forwarding base (gymnasium VectorWrapper semantics the reference relies on)."""
 

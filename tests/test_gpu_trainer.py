@@ -334,3 +334,72 @@ def test_ppo_learns_cartpole_v1():
     fp32 summation order: tools/learn_probe.py)."""
     bests = [_cartpole_best_return(seed) for seed in (1, 2, 3)]
     assert sum(b > 475 for b in bests) >= 2, f"best rolling mean returns per seed: {bests}"
+
+
+def _policy_for(kind):
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    env = SyntheticVecEnv(4, kind, seed=3)
+    pkw = dict(activation_fn="relu") if kind == "pong" else {}
+    if kind == "halfcheetah":
+        pkw = dict(pi_hidden_sizes=[256, 256], v_hidden_sizes=[256, 256], activation_fn="relu", log_std_init=-2,
+                   init_layers_orthogonal=False)
+    return env, ActorCritic(env, **pkw)
+
+
+@pytest.mark.parametrize("kind,T,N,bs,extra", [
+    ("cartpole", 16, 40, 64, {}),                              # 640 rows: 10 full minibatches
+    ("cartpole", 9, 50, 64, dict(clip_range_vf=0.1)),          # 450 rows: ragged tail of 2
+    ("halfcheetah", 16, 24, 64, dict(ent_coef=0.01)),          # Gaussian head, 384 rows
+    ("pong", 8, 12, 32, dict(ent_coef=0.01)),                  # NatureCNN, 96 rows
+    ("cartpole", 8, 32, 64, dict(gradient_accumulation=True)),  # optimizer step once per epoch (eager)
+])
+def test_graphed_update_matches_eager(kind, T, N, bs, extra):
+    """The hipGraph-replayed minibatch step (graphs.py) runs the same kernels on the same
+    minibatches as the eager loop: parameters, optimizer state and stats agree over two updates
+    (capture on the first, pure replay on the second)."""
+    results = []
+    for graphs in (False, True):
+        torch.manual_seed(7)
+        env, policy = _policy_for(kind)
+        policy = policy.to(DEV)
+        algo = PPO(policy, DEV, None, batch_size=bs, n_epochs=3, learning_rate=3e-4, **extra)
+        algo.force_generic = True
+        algo.use_graphs = graphs
+        g = torch.Generator(device="cpu").manual_seed(11)
+        shp = env.single_observation_space.shape
+        obs = (torch.randint(0, 256, (T, N) + shp, generator=g, dtype=torch.uint8) if kind == "pong"
+               else torch.randn((T, N) + shp, generator=g))
+        if kind == "halfcheetah":
+            act = torch.randn(T, N, 6, generator=g).clamp(-1, 1)
+        else:
+            act = torch.randint(0, env.single_action_space.n, (T, N), generator=g)
+        t = lambda x: x.to(DEV)
+        rew, vals = torch.randn(T, N, generator=g), torch.randn(T, N, generator=g)
+        starts = (torch.rand(T, N, generator=g) < 0.05).to(torch.uint8)
+        logp = -1.0 + 0.1 * torch.randn(T, N, generator=g)
+        perm_g = torch.Generator(device="cpu").manual_seed(5)
+        r = DeviceRollout(DEV, t(torch.zeros(N, dtype=torch.uint8)), t(torch.randn(N, generator=g)), t(obs), t(act),
+                          t(rew), t(starts), t(vals), t(logp), None, 0.99, 0.95,
+                          perm_source=lambda n: torch.randperm(n, generator=perm_g))
+        out = []
+        for _ in range(2):
+            stats, norms, _ = algo.update(r)
+            out.append((stats.copy(), norms.copy()))
+        torch.cuda.synchronize()
+        results.append((algo.flat.flat.cpu().numpy(), algo.optimizer.state1.cpu().numpy(), out,
+                        algo.optimizer.step_count, algo._graphed))
+    (p0, m0, o0, c0, _), (p1, m1, o1, c1, gu) = results
+    assert c0 == c1
+    if not extra.get("gradient_accumulation"):
+        assert gu is not None and any(gr.graph is not None for gr in gu.graphs.values()), "no graph was captured"
+    # MIOpen's convolution backward is not bitwise reproducible run to run (solver choice /
+    # split-K accumulation order), so the NatureCNN case gets an fp32 tolerance; the MLP cases
+    # run identical kernels and agree to the last bits
+    atol = 2e-6 if kind == "pong" else 1e-7
+    np.testing.assert_allclose(p1, p0, rtol=1e-6, atol=atol)
+    np.testing.assert_allclose(m1, m0, rtol=1e-4 if kind == "pong" else 1e-5, atol=1e-9)
+    for (s0, n0), (s1, n1) in zip(o0, o1):
+        np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(n1, n0, rtol=1e-5)

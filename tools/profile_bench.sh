@@ -23,6 +23,7 @@ for c in $CONFIGS; do
   extra=${EXTRA:-}
   run "stats_$c" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_$c" -o run -- \
       python3 bench.py --config "$c" --steps 2 --warmup 1 --no-cpu-baseline $extra
+  rm -f "$OUT/stats_$c/run_kernel_trace.csv"  # traces run to 100s of MB (gpurun returns <= 64 MiB); stats stay
   if [ "${PMC:-1}" = 1 ]; then
     run "fetch_$c" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$c" -o run -- \
         python3 bench.py --config "$c" --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 $extra
