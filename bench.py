@@ -95,6 +95,8 @@ def main():
         else:
             torch.distributed.init_process_group(backend)
     _lib.lib()
+    if os.environ.get("RAI_CUDNN_BENCHMARK", "0") == "1":  # MIOpen find mode for the CNN convolutions
+        torch.backends.cudnn.benchmark = True
 
     cfg = CONFIGS[args.config]
     N, T = (args.num_envs or cfg["num_envs"]), cfg["n_steps"]

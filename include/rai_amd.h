@@ -65,6 +65,35 @@ int rai_gae(const float* rewards, const float* values, const uint8_t* episode_st
             int32_t mode, float* adv_out, float* returns_out, void* stream);
 
 /* --------------------------------------------------------------------------
+ * Per-trajectory GAE over a ragged batch (one launch for many trajectories).
+ * Rows of all trajectories are concatenated: rewards/values/adv/returns are
+ * (sum L, K) row-major fp32; offsets (n_traj + 1, int64, device) gives each
+ * trajectory's first row.  next_values (n_traj, K) may be NULL (zeros).
+ *
+ * rai_gae_trajectories replaces rl_algo_impls/rollout/trajectory.py:56-92
+ * (TrajectoryBuilder.trajectory = compute_advantages over one trajectory with
+ * episode_starts = [True, dones[:-1]], next_episode_starts = dones[-1]); dones is
+ * per row (uint8).  gamma/gae_lambda/gamma_is_vector/mode as in rai_gae.
+ *
+ * rai_gae_skips replaces rl_algo_impls/rollout/discrete_skips_trajectory_builder.py:
+ * 64-109 (semi-MDP GAE: gamma ** steps_elapsed[t] in the bootstrap and the carry).
+ * steps_elapsed is per row (int32, 0..max_steps); traj_done (n_traj, uint8, may be
+ * NULL) zeroes the last bootstrap; gk / gkl are device tables (max_steps + 1, K)
+ * of gamma ** s and (gamma ** s) * lambda, computed by the caller exactly as numpy
+ * evaluates them (the reference's own pow).  mode 0 = the numpy >= 2 fp64 sequence
+ * (bit-exact), 1 = fp32 with fp32-rounded coefficients (= numpy < 2 promotion for
+ * K-column values with a scalar gamma).  returns_out may be NULL.
+ * ------------------------------------------------------------------------ */
+int rai_gae_trajectories(const float* rewards, const float* values, const uint8_t* dones,
+                         const int64_t* offsets, int64_t n_traj, int32_t K, const float* next_values,
+                         const double* gamma, const double* gae_lambda, int32_t gamma_is_vector,
+                         int32_t mode, float* adv_out, float* returns_out, void* stream);
+int rai_gae_skips(const float* rewards, const float* values, const int32_t* steps_elapsed,
+                  const int64_t* offsets, int64_t n_traj, int32_t K, const float* next_values,
+                  const uint8_t* traj_done, const double* gk, const double* gkl, int32_t max_steps,
+                  int32_t mode, float* adv_out, float* returns_out, void* stream);
+
+/* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.
  * These live in HBM so a captured hipGraph replays against values the host
  * rewrites once per update (schedules: rl_algo_impls/shared/callbacks/

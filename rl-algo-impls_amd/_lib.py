@@ -99,6 +99,8 @@ _SIGNATURES = {
     "rai_optim_workspace_bytes": (_i64, [_i64]),
     "rai_clip_optim_step": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_gather_rows": (C.c_int, [_i32, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "rai_gae_trajectories": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _f64p, _f64p, _i32, _i32, _vp, _vp, _vp]),
+    "rai_gae_skips": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "rai_gather_minibatch": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_minibatch_advance": (C.c_int, [_vp, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, [C.c_int64, C.c_int32]),

@@ -38,6 +38,7 @@ MODEL_FILENAME = "model.pth"
 NORMALIZE_OBSERVATION_FILENAME = "norm_obs.npz"
 NORMALIZE_REWARD_FILENAME = "norm_reward.npz"
 F32_MIN = torch.finfo(torch.float32).min
+_CHANNELS_LAST = os.environ.get("RAI_CHANNELS_LAST", "0") == "1"
 
 
 class Step(NamedTuple):  # actor_critic.py:42-46
@@ -119,6 +120,8 @@ class NatureCnnEncoder(nn.Module):
         if obs.dim() == 3:
             obs = obs.unsqueeze(0)
         x = obs.float() / self.range_size
+        if _CHANNELS_LAST:
+            x = x.contiguous(memory_format=torch.channels_last)
         return self.fc(self.cnn(x))
 
 
