@@ -94,6 +94,29 @@ int rai_gae_skips(const float* rewards, const float* values, const int32_t* step
                   int32_t mode, float* adv_out, float* returns_out, void* stream);
 
 /* --------------------------------------------------------------------------
+ * GridNet masked-categorical head (MicroRTS per-cell sub-actions).
+ * Replaces rl_algo_impls/shared/actor/gridnet.py:38-200 (GridnetDistribution.log_prob,
+ * .entropy over MaskedCategorical, rl_algo_impls/shared/actor/categorical.py:12-54)
+ * and their autograd backward.
+ * logits / mask / d_logits: (B, C, A) row-major, A = sum(nvec) <= RAI_GRID_MAX_A,
+ * C = cells (map H*W); actions (B, C, G) int64, G = len(nvec) <= RAI_GRID_MAX_G.
+ * nvec / sub_ref / sub_val are host arrays of length G: group g's log-prob counts only
+ * where actions[..., sub_ref[g]] == sub_val[g] (ValueDependentMask, gridnet.py:21-35;
+ * sub_ref[g] = -1 or sub_ref = NULL: always counts).  Entropy is never gated.
+ * logp_out / entropy_out (B,) fp32, either may be NULL (actions may be NULL when only
+ * the entropy is wanted).  rai_gridnet_backward writes dL/dlogits for upstream
+ * d_logp, d_entropy (B,).
+ * ------------------------------------------------------------------------ */
+#define RAI_GRID_MAX_G 8
+#define RAI_GRID_MAX_A 256
+int rai_gridnet_logp_entropy(const float* logits, const uint8_t* mask, const int64_t* actions, int64_t B,
+                             int32_t C, int32_t G, const int32_t* nvec, const int32_t* sub_ref,
+                             const int32_t* sub_val, float* logp_out, float* entropy_out, void* stream);
+int rai_gridnet_backward(const float* logits, const uint8_t* mask, const int64_t* actions, int64_t B, int32_t C,
+                         int32_t G, const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val,
+                         const float* d_logp, const float* d_entropy, float* d_logits, void* stream);
+
+/* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.
  * These live in HBM so a captured hipGraph replays against values the host
  * rewrites once per update (schedules: rl_algo_impls/shared/callbacks/

@@ -17,6 +17,8 @@ from .build import lib_path
 
 RAI_MAX_K = 8
 RAI_MAX_FIELDS = 8
+RAI_GRID_MAX_G = 8
+RAI_GRID_MAX_A = 256
 RAI_STAT_STRIDE = 5 + 2 * RAI_MAX_K
 ABI_VERSION = 1
 
@@ -100,6 +102,8 @@ _SIGNATURES = {
     "rai_clip_optim_step": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_gather_rows": (C.c_int, [_i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "rai_gae_trajectories": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _f64p, _f64p, _i32, _i32, _vp, _vp, _vp]),
+    "rai_gridnet_logp_entropy": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rai_gridnet_backward": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rai_gae_skips": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "rai_gather_minibatch": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_minibatch_advance": (C.c_int, [_vp, _vp]),

@@ -1,0 +1,226 @@
+// GridNet masked-categorical head (MicroRTS) on gfx950: fused log-prob + entropy and their
+// backward, for every cell and sub-action of a minibatch in one launch each.
+//
+// Restates rl_algo_impls/shared/actor/gridnet.py:38-200 (GridnetDistribution.log_prob / entropy)
+// over rl_algo_impls/shared/actor/categorical.py:12-54 (MaskedCategorical).  Per sample b, per cell
+// c (C = H*W cells) the A = sum(nvec) logits are split into G sub-action groups (MicroRTS:
+// nvec = [6, 4, 4, 4, 4, 7, 49]); group g of cell c is a categorical over its masked logits
+//   zm = mask ? z : FLT_MIN_NORMAL_NEG (torch.finfo(f32).min),  l = zm - logsumexp(zm),  p = exp(l)
+//   logp_g = l[a_g]  (x 0 when a ValueDependentMask gates it: actions[ref] != value)
+//   H_g    = -sum_j mask_j * l_j * p_j          (the masked entropy approximation)
+// and logp(b) = sum over cells and groups of logp_g, entropy(b) = sum of H_g.  A group with no
+// valid action has l = 0 (torch's logsumexp of all-finfo.min rows), logp 0 and H 0.
+// Backward for upstream (dL/dlogp(b), dL/dH(b)) = (gl, ge), through torch.where's zero gradient
+// on masked entries:
+//   dz_j = mask_j * ( gl * gate * ([j == a] - p_j)  -  ge * p_j * (l_j + H_g) )
+// (closed form of autograd through logsumexp/softmax; within fp32 rounding of torch's).
+//
+// Layout: logits / masks / d_logits are (B, C, A) row-major (A fastest), actions (B, C, G) int64.
+// One 256-thread workgroup per sample walks its cells in 64-cell tiles: the tile's 64*A logits and
+// mask bytes are one contiguous span, loaded coalesced into LDS; the 64*G (cell, group) items are
+// spread over the threads; the backward writes dz into the LDS tile in place and stores the span
+// coalesced.  Sums over a sample's items are fixed-order block reductions (deterministic).
+#include "common.h"
+
+namespace {
+
+constexpr int GN_THREADS = 256;
+constexpr int GN_CELLS = 64;  // cells per LDS tile
+constexpr float GN_NEG = -3.4028234663852886e38f;  // torch.finfo(torch.float32).min
+
+struct GridArgs {
+  const float* logits;
+  const uint8_t* mask;
+  const int64_t* actions;
+  const float* d_logp;
+  const float* d_ent;
+  float* logp;
+  float* ent;
+  float* d_logits;
+  int64_t B;
+  int32_t C, A, G;
+  int32_t off[RAI_GRID_MAX_G + 1];  // group g: logits [off[g], off[g+1])
+  int32_t sub_ref[RAI_GRID_MAX_G];  // -1: no gate
+  int32_t sub_val[RAI_GRID_MAX_G];
+};
+
+struct GroupStats {
+  float lse;  // logsumexp of the masked logits (torch: max + log(sum(exp(x - max))))
+  float H;    // masked entropy
+  int nvalid;
+};
+
+__device__ __forceinline__ GroupStats group_stats(const float* z, const uint8_t* m, int n) {
+  float mx = GN_NEG;
+  int nv = 0;
+  for (int j = 0; j < n; ++j) {
+    const float v = m[j] ? z[j] : GN_NEG;
+    mx = fmaxf(mx, v);
+    nv += m[j] ? 1 : 0;
+  }
+  float s = 0.f;
+  for (int j = 0; j < n; ++j) {
+    const float v = m[j] ? z[j] : GN_NEG;
+    s += expf(v - mx);
+  }
+  GroupStats g;
+  g.lse = mx + logf(s);
+  g.nvalid = nv;
+  float h = 0.f;
+  if (nv > 0) {
+    for (int j = 0; j < n; ++j) {
+      if (m[j]) {
+        const float l = z[j] - g.lse;
+        h -= l * expf(l);
+      }
+    }
+  }
+  g.H = h;
+  return g;
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(GN_THREADS) void gridnet_kernel(const GridArgs a) {
+  extern __shared__ float smem[];
+  const int A = a.A, G = a.G, C = a.C;
+  float* zt = smem;                                                     // [GN_CELLS][A]
+  uint8_t* mt = reinterpret_cast<uint8_t*>(smem + GN_CELLS * A);       // [GN_CELLS][A]
+  __shared__ double red[2 * (GN_THREADS / 64)];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float gl = BWD ? a.d_logp[b] : 0.f;
+  const float ge = BWD ? a.d_ent[b] : 0.f;
+  double acc_lp = 0.0, acc_h = 0.0;
+  for (int c0 = 0; c0 < C; c0 += GN_CELLS) {
+    const int nc = min(GN_CELLS, C - c0);
+    const int64_t base = (b * C + c0) * (int64_t)A;
+    const int span = nc * A;
+    for (int i = tid; i < span; i += GN_THREADS) {
+      zt[i] = a.logits[base + i];
+      mt[i] = a.mask[base + i];
+    }
+    __syncthreads();
+    const int items = nc * G;
+    for (int it = tid; it < items; it += GN_THREADS) {
+      const int cl = it / G, g = it - cl * G;
+      const int o = a.off[g], n = a.off[g + 1] - o;
+      float* z = zt + cl * A + o;
+      const uint8_t* m = mt + cl * A + o;
+      const int64_t* act = a.actions ? a.actions + (b * C + c0 + cl) * (int64_t)G : nullptr;
+      const GroupStats s = group_stats(z, m, n);
+      const int ag = act ? (int)act[g] : 0;
+      const bool gate = !act || a.sub_ref[g] < 0 || act[a.sub_ref[g]] == (int64_t)a.sub_val[g];
+      if (!BWD) {
+        if (act && gate) {
+          const bool ok = ag >= 0 && ag < n;
+          const float za = ok ? (m[ag] ? z[ag] : GN_NEG) : 0.f;
+          acc_lp += (double)(s.nvalid > 0 ? za - s.lse : 0.f);  // all-masked: l = 0
+        }
+        acc_h += (double)s.H;
+      } else {
+        for (int j = 0; j < n; ++j) {
+          float d = 0.f;
+          if (m[j]) {
+            const float l = z[j] - s.lse;
+            const float p = expf(l);
+            if (act && gate) d = gl * ((j == ag ? 1.f : 0.f) - p);
+            d -= ge * p * (l + s.H);
+          }
+          z[j] = d;  // the item owns these LDS slots: dz overwrites its logits in place
+        }
+      }
+    }
+    __syncthreads();
+    if (BWD) {
+      for (int i = tid; i < span; i += GN_THREADS) a.d_logits[base + i] = zt[i];
+      __syncthreads();
+    }
+  }
+  if (!BWD) {
+    const int lane = tid & 63, w = tid >> 6;
+    acc_lp = wave_sum(acc_lp);
+    acc_h = wave_sum(acc_h);
+    if (lane == 0) {
+      red[w] = acc_lp;
+      red[GN_THREADS / 64 + w] = acc_h;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double lp = 0.0, h = 0.0;
+      for (int i = 0; i < GN_THREADS / 64; ++i) {
+        lp += red[i];
+        h += red[GN_THREADS / 64 + i];
+      }
+      if (a.logp) a.logp[b] = (float)lp;
+      if (a.ent) a.ent[b] = (float)h;
+    }
+  }
+}
+
+int setup(GridArgs& a, const float* logits, const uint8_t* mask, const int64_t* actions, int64_t B, int32_t C,
+          int32_t G, const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val) {
+  if (B < 0 || C < 1 || G < 1) return RAI_E_SHAPE;
+  if (G > RAI_GRID_MAX_G) return RAI_E_UNSUPPORTED;
+  if (!nvec) return RAI_E_NULLPTR;
+  a = GridArgs{};
+  a.logits = logits;
+  a.mask = mask;
+  a.actions = actions;
+  a.B = B;
+  a.C = C;
+  a.G = G;
+  int A = 0;
+  for (int g = 0; g < G; ++g) {
+    if (nvec[g] < 1) return RAI_E_SHAPE;
+    a.off[g] = A;
+    A += nvec[g];
+    const int r = sub_ref ? sub_ref[g] : -1;
+    if (r >= G || r == g) return RAI_E_SHAPE;
+    a.sub_ref[g] = r;
+    a.sub_val[g] = sub_val && r >= 0 ? sub_val[g] : 0;
+  }
+  if (A > RAI_GRID_MAX_A) return RAI_E_UNSUPPORTED;
+  a.off[G] = A;
+  a.A = A;
+  if (B > 0 && (!logits || !mask)) return RAI_E_NULLPTR;
+  return RAI_OK;
+}
+
+size_t smem_bytes(int A) { return (size_t)GN_CELLS * A * (sizeof(float) + 1); }
+
+}  // namespace
+
+extern "C" int rai_gridnet_logp_entropy(const float* logits, const uint8_t* mask, const int64_t* actions,
+                                        int64_t B, int32_t C, int32_t G, const int32_t* nvec,
+                                        const int32_t* sub_ref, const int32_t* sub_val, float* logp_out,
+                                        float* entropy_out, void* stream) {
+  GridArgs a;
+  int rc = setup(a, logits, mask, actions, B, C, G, nvec, sub_ref, sub_val);
+  if (rc != RAI_OK) return rc;
+  if (logp_out && !actions) return RAI_E_NULLPTR;
+  if (B == 0) return RAI_OK;
+  a.logp = logp_out;
+  a.ent = entropy_out;
+  hipLaunchKernelGGL(gridnet_kernel<false>, dim3((unsigned)B), dim3(GN_THREADS), smem_bytes(a.A),
+                     rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_gridnet_backward(const float* logits, const uint8_t* mask, const int64_t* actions, int64_t B,
+                                    int32_t C, int32_t G, const int32_t* nvec, const int32_t* sub_ref,
+                                    const int32_t* sub_val, const float* d_logp, const float* d_entropy,
+                                    float* d_logits, void* stream) {
+  GridArgs a;
+  int rc = setup(a, logits, mask, actions, B, C, G, nvec, sub_ref, sub_val);
+  if (rc != RAI_OK) return rc;
+  if (B == 0) return RAI_OK;
+  if (!actions || !d_logp || !d_entropy || !d_logits) return RAI_E_NULLPTR;
+  a.d_logp = d_logp;
+  a.d_ent = d_entropy;
+  a.d_logits = d_logits;
+  hipLaunchKernelGGL(gridnet_kernel<true>, dim3((unsigned)B), dim3(GN_THREADS), smem_bytes(a.A),
+                     rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

@@ -66,10 +66,17 @@ class SyntheticVecEnv:
     kind = "halfcheetah": obs ~ N(0,1) f32 (N,17), Box(6) actions in [-1,1],
                        reward ~ N(0,1), termination ~ Bernoulli(1/1000)
     Truncations are always False (the reference treats them like terminations).
+
+    Observation batches are drawn from a pool of `obs_pool` batches generated at construction
+    (a uniformly chosen pool entry per step): the env's own cost would otherwise sit inside the
+    timed rollout (numpy generates the 29 MB of uniform bytes of a 1024-env Pong step in ~45 ms,
+    more than the whole device step) while saying nothing about the hot path.  Rewards and
+    terminations are drawn fresh every step.  Returned observation arrays are shared with the
+    pool: consumers copy them (the rollout stages them into pinned memory) and must not write.
     """
 
     def __init__(self, num_envs: int, kind: str = "cartpole", seed: int = 1,
-                 term_prob: Optional[float] = None):
+                 term_prob: Optional[float] = None, obs_pool: Optional[int] = None):
         self.num_envs = int(num_envs)
         self.kind = kind
         self.rng = np.random.default_rng(seed)
@@ -87,13 +94,20 @@ class SyntheticVecEnv:
             self.term_prob = 1 / 1000 if term_prob is None else term_prob
         else:
             raise ValueError(f"unknown synthetic env kind {kind}")
-        self._obs_buf: Optional[np.ndarray] = None
+        batch_bytes = self.num_envs * int(np.prod(self.single_observation_space.shape)) * \
+            np.dtype(self.single_observation_space.dtype).itemsize
+        if obs_pool is None:  # up to 16 batches within ~256 MB
+            obs_pool = int(max(2, min(16, (256 << 20) // max(batch_bytes, 1))))
+        self._pool = [self._draw_obs() for _ in range(int(obs_pool))]
 
     @property
     def unwrapped(self):
         return self
 
     def _obs(self) -> np.ndarray:
+        return self._pool[int(self.rng.integers(len(self._pool)))]
+
+    def _draw_obs(self) -> np.ndarray:
         N = self.num_envs
         shp = self.single_observation_space.shape
         if self.kind == "pong":
