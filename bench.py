@@ -122,13 +122,20 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    def progress(tag, i, t_start):
+        if rank == 0:
+            print(f"[bench] {tag} update {i}: {time.perf_counter() - t_start:.2f} s", file=sys.stderr, flush=True)
+
+    for i in range(args.warmup):
+        tw = time.perf_counter()
         algo.learn_epoch(0, 1, gen, None)
+        progress("warmup", i, tw)
     barrier()
     algo.kernel_events = []  # HIP events around every fused epoch launch (same stream as the kernel)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         algo.learn_epoch(0, 1, gen, None)
+        progress("timed", i, t0)
     barrier()
     elapsed = time.perf_counter() - t0
     epoch_ms = [e0.elapsed_time(e1) for e0, e1 in algo.kernel_events]

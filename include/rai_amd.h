@@ -314,6 +314,45 @@ int rai_mlp_ppo_grads(const float* params, const float* obs, const int64_t* acti
                       void* workspace, int64_t workspace_bytes, void* stream);
 
 /* --------------------------------------------------------------------------
+ * Wide MLP actor-critic minibatch step (HalfCheetah-class policies: Flatten
+ * encoder, separate [in -> H -> H -> out] actor and critic, H in {64,128,192,256},
+ * Gaussian (head 1) or Categorical (head 0) actor, scalar critic).  Replaces the
+ * per-minibatch PyTorch forward of rl_algo_impls/shared/policy/actor_critic_network/
+ * connected_trio.py (+ shared/actor/gaussian.py:11-61, categorical.py, shared/policy/
+ * critic.py) and its autograd backward inside rl_algo_impls/ppo/ppo.py:290-377.
+ *   rai_mlp_wide_forward:  3 launches -> logp (B), entropy (B*out for Gaussian, B for
+ *                          Categorical), v (B) for rai_ppo_loss
+ *   rai_mlp_wide_backward: 2 launches -> gradients of every parameter (written, or added
+ *                          when accumulate) from rai_ppo_loss's d_logp, d_entropy, d_v
+ * w[n] / g[n]: network n (0 actor, 1 critic) W1 (H,in), b1, W2 (H,H), b2, W3 (out,H),
+ * b3 and their gradient views; actions: (B, out) fp32 (Gaussian) or (B,) int64.
+ * workspace: rai_mlp_wide_workspace_bytes(B, H) bytes, shared by the two calls.
+ * ------------------------------------------------------------------------ */
+#define RAI_WIDE_MAX_B 256
+#define RAI_WIDE_MAX_H 256
+#define RAI_WIDE_MAX_IN 64
+#define RAI_WIDE_MAX_OUT 8
+typedef struct rai_mlp_wide_desc {
+  const float* w[2][6];
+  float* g[2][6];
+  const float* log_std; /* Gaussian head: (out) */
+  float* g_log_std;
+  int32_t in_dim;
+  int32_t hidden;
+  int32_t out_pi;
+  int32_t head;       /* 0 Categorical, 1 Gaussian */
+  int32_t activation; /* 0 tanh, 1 relu */
+  int32_t accumulate; /* 1: gradients are added (gradient accumulation) */
+} rai_mlp_wide_desc;
+int64_t rai_mlp_wide_workspace_bytes(int64_t B, int32_t hidden);
+int rai_mlp_wide_forward(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,
+                         float* logp_out, float* entropy_out, float* v_out, void* workspace,
+                         int64_t workspace_bytes, void* stream);
+int rai_mlp_wide_backward(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,
+                          const float* d_logp, const float* d_entropy, const float* d_v, void* workspace,
+                          int64_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------------------------------
  * Data-parallel runtime: one process per GPU, an RCCL
  * communicator over xGMI, and the natively driven per-minibatch loop
  *   rai_mlp_ppo_grads -> in-place sum all-reduce of the flat gradient -> rai_clip_optim_step

@@ -19,6 +19,10 @@ RAI_MAX_K = 8
 RAI_MAX_FIELDS = 8
 RAI_GRID_MAX_G = 8
 RAI_GRID_MAX_A = 256
+RAI_WIDE_MAX_B = 256
+RAI_WIDE_MAX_H = 256
+RAI_WIDE_MAX_IN = 64
+RAI_WIDE_MAX_OUT = 8
 RAI_STAT_STRIDE = 5 + 2 * RAI_MAX_K
 ABI_VERSION = 1
 
@@ -64,6 +68,23 @@ class MinibatchDesc(C.Structure):
     ]
 
 
+class MlpWideDesc(C.Structure):
+    """Mirror of rai_mlp_wide_desc."""
+
+    _fields_ = [
+        ("w", (C.c_void_p * 6) * 2),
+        ("g", (C.c_void_p * 6) * 2),
+        ("log_std", C.c_void_p),
+        ("g_log_std", C.c_void_p),
+        ("in_dim", C.c_int32),
+        ("hidden", C.c_int32),
+        ("out_pi", C.c_int32),
+        ("head", C.c_int32),
+        ("activation", C.c_int32),
+        ("accumulate", C.c_int32),
+    ]
+
+
 class OptimHparams(C.Structure):
     _fields_ = [
         ("lr", C.c_float),
@@ -104,6 +125,9 @@ _SIGNATURES = {
     "rai_gae_trajectories": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _f64p, _f64p, _i32, _i32, _vp, _vp, _vp]),
     "rai_gridnet_logp_entropy": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rai_gridnet_backward": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rai_mlp_wide_workspace_bytes": (_i64, [_i64, _i32]),
+    "rai_mlp_wide_forward": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "rai_mlp_wide_backward": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "rai_gae_skips": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "rai_gather_minibatch": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_minibatch_advance": (C.c_int, [_vp, _vp]),

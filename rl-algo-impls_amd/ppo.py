@@ -79,6 +79,11 @@ class PPO:
         # RAI_GRAPHS=0 keeps the eager loop
         self.use_graphs = os.environ.get("RAI_GRAPHS", "1") != "0"
         self._graphed = None
+        # wide MLP actor-critics (HalfCheetah class): fused forward/backward kernels instead of the
+        # PyTorch module + autograd (mlp_wide.py); RAI_WIDE=0 keeps the PyTorch network path
+        self.use_wide = os.environ.get("RAI_WIDE", "1") != "0"
+        self._wide = None
+        self._wide_out: dict = {}
         # bench/profiling hook: when a list, (start, end) HIP events bracket every fused epoch launch
         self.kernel_events: Optional[list] = None
         self._mlp_ws: Optional[torch.Tensor] = None
@@ -446,6 +451,42 @@ class PPO:
         stats[:, 0] += float(self.vf_coef) * stats[:, 5]  # value term of the loss
         return stats, norms, 1
 
+    def _wide_step(self):
+        """The wide-MLP fused step for this policy, or None (structure / options not covered)."""
+        if self.force_generic or not self.use_wide or not self.flat.flat.is_cuda:
+            return None
+        if self._wide is None:
+            from .mlp_wide import WideStep, wide_mlp_spec
+
+            if wide_mlp_spec(self.policy) is None or not (1 <= self.batch_size <= _lib.RAI_WIDE_MAX_B):
+                self._wide = False
+            else:
+                self._wide = WideStep(self.policy, self.device, accumulate=self.gradient_accumulation)
+        if self._wide is False:
+            return None
+        self._wide.check_pointers()
+        return self._wide
+
+    def _minibatch_loss_grads(self, wide, obs, actions, masks, values, adv, ret, logprobs, K_box) -> None:
+        """Forward, fused loss and backward of one minibatch into the flat gradient buffer: the
+        wide-MLP kernels when available, else the PyTorch network + autograd."""
+        if wide is not None and masks is None:
+            B = int(obs.shape[0])
+            outs = self._wide_out.get(B)
+            if outs is None:
+                outs = self._wide_out[B] = wide.outputs(B)
+            logp, ent, v = outs
+            wide.forward(obs, actions, logp, ent, v)
+            K_box[0] = 1
+            d_logp, d_ent, d_v = launch_loss(self.blocks, logp, ent, v, logprobs, values, adv, ret, 1)
+            wide.backward(obs, actions, d_logp, d_ent, d_v)
+            return
+        logp, ent, v = self.policy(obs, actions, action_masks=masks)
+        if K_box[0] is None:
+            K_box[0] = value_columns(v)
+        d_logp, d_ent, d_v = launch_loss(self.blocks, logp, ent, v, logprobs, values, adv, ret, K_box[0])
+        torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
+
     def update(self, r) -> Tuple[np.ndarray, np.ndarray, int]:
         """All epochs x minibatches of one update, enqueued without host syncs;
         returns the per-minibatch stats rows and grad norms (one D2H copy)."""
@@ -464,17 +505,18 @@ class PPO:
                                                     and torch.distributed.get_backend(self.dp_group) != "nccl")):
             K = self._update_graphed(r, nmb)
             return self._read_stats(n_steps, n_norms, K)
+        wide = self._wide_step()
         for _ in range(self.n_epochs):
             for mb in r.minibatches(self.batch_size, shuffle=not self.gradient_accumulation):
-                logp, ent, v = self.policy(mb.obs, mb.actions, action_masks=mb.action_masks)
                 if K is None:
-                    K = value_columns(v)
+                    with torch.no_grad():  # K (value columns) before the device blocks are written
+                        K = value_columns(self.policy(mb.obs[:1], mb.actions[:1], action_masks=(
+                            mb.action_masks[:1] if mb.action_masks is not None else None))[2])
                     blocks.upload(self._hparams(K, nmb), self.optimizer.step_count)
                 if mb.logprobs is None:
                     raise ValueError("PPO needs rollout logprobs (include_logp=True)")
-                d_logp, d_ent, d_v = launch_loss(blocks, logp, ent, v, mb.logprobs, mb.values, mb.advantages,
-                                                 mb.returns, K)
-                torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
+                self._minibatch_loss_grads(wide, mb.obs, mb.actions, mb.action_masks, mb.values, mb.advantages,
+                                           mb.returns, mb.logprobs, [K])
                 if not self.gradient_accumulation:
                     if self.dp_enabled:
                         self._all_reduce(self.flat.grad, average=True)
@@ -513,14 +555,12 @@ class PPO:
         has_masks = r.action_masks is not None
         K_box = [None]
 
+        wide = self._wide_step()
+
         def step(bufs):
             obs, actions, values, adv, ret, logprobs = bufs[:6]
             masks = bufs[6] if has_masks else None
-            logp, ent, v = self.policy(obs, actions, action_masks=masks)
-            if K_box[0] is None:
-                K_box[0] = value_columns(v)
-            d_logp, d_ent, d_v = launch_loss(blocks, logp, ent, v, logprobs, values, adv, ret, K_box[0])
-            torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
+            self._minibatch_loss_grads(wide, obs, actions, masks, values, adv, ret, logprobs, K_box)
             if optim_in_step:
                 self.optimizer.step(blocks.state, blocks.norms, count=False)
 
@@ -532,7 +572,7 @@ class PPO:
         K_box[0] = K
         blocks.upload(self._hparams(K, nmb), self.optimizer.step_count)
         # a graph bakes in every device pointer it touches: key it on the ones that can change
-        tag = (optim_in_step, blocks.stats.data_ptr(), blocks.norms.data_ptr(), blocks.hp.data_ptr(),
+        tag = (optim_in_step, wide is not None, blocks.stats.data_ptr(), blocks.norms.data_ptr(), blocks.hp.data_ptr(),
                blocks.state.data_ptr(), self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
                self.optimizer.hp_dev.data_ptr())
         g = gu.graph_for(fields, B, tag, step)

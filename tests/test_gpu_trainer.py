@@ -54,9 +54,13 @@ def _device_batches(z, name, n, with_logp=True):
     return out
 
 
+@pytest.mark.parametrize("wide", [True, False], ids=["wide_kernels", "pytorch_network"])
 @pytest.mark.parametrize("name", ["cp_default", "cp_vclip_ent", "cp_gradacc", "cp_klcut", "hc_gauss", "mc_mrw",
                                   "mc_after", "mc_huber_w"])
-def test_ppo_minibatch_steps_match_reference(golden, name):
+def test_ppo_minibatch_steps_match_reference(golden, name, wide):
+    """Per-minibatch path against the reference's PPO steps.  The MLP cases (cp_*, hc_gauss: 64-wide
+    actor/critic) run through the fused wide-MLP kernels (mlp_wide.py) or the PyTorch network +
+    autograd; the multi-critic cases (mc_*) always take the PyTorch network."""
     z = golden("ppo_steps.npz")
     meta = json.loads(str(z["index"]))[name]
     policy = nets.build(meta["policy"])
@@ -64,6 +68,7 @@ def test_ppo_minibatch_steps_match_reference(golden, name):
     policy = policy.to(DEV)
     kw = dict(meta["kw"])
     algo = PPO(policy, DEV, Recorder(), n_epochs=1, **kw)
+    algo.use_wide = wide
     r = FixedDeviceRollout(_device_batches(z, name, meta["n"]))
     stats, norms, K = algo.update(r)
     ref_params = z[f"{name}/params"]
@@ -83,6 +88,7 @@ def test_ppo_minibatch_steps_match_reference(golden, name):
     assert float(sd["state"][0]["step"]) == meta["opt_step"]
     s1 = torch.cat([s["exp_avg"].reshape(-1) for s in sd["state"].values()]).cpu().numpy()
     np.testing.assert_allclose(s1, z[f"{name}/opt_state1"], rtol=2e-3, atol=2e-7, err_msg=name)
+    assert (algo._wide not in (None, False)) == (wide and not name.startswith("mc_")), "wide path not taken"
 
 
 @pytest.mark.parametrize("generic", [False, True], ids=["fused_mlp_kernel", "generic_path"])
@@ -403,3 +409,49 @@ def test_graphed_update_matches_eager(kind, T, N, bs, extra):
     for (s0, n0), (s1, n1) in zip(o0, o1):
         np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-7)
         np.testing.assert_allclose(n1, n0, rtol=1e-5)
+
+
+@pytest.mark.parametrize("kind,hidden,act,extra", [
+    ("halfcheetah", 256, "relu", dict(ent_coef=0.01)),                     # the C4 policy
+    ("halfcheetah", 128, "tanh", dict(clip_range_vf=0.2)),
+    ("cartpole", 256, "tanh", dict(ent_coef=0.01)),                        # Categorical head, 256 wide
+    ("halfcheetah", 64, "relu", dict(gradient_accumulation=True)),         # accumulate mode
+])
+def test_wide_mlp_kernels_match_pytorch_path(kind, hidden, act, extra):
+    """Fused wide-MLP forward/backward (graph-replayed) vs the PyTorch network + autograd (eager)
+    on the same minibatches: two updates x 3 epochs, fp32 tolerance (different reduction order)."""
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    T, N, bs = 16, 24, 64  # 384 rows: 6 minibatches
+    res = []
+    for wide in (True, False):
+        torch.manual_seed(7)
+        env = SyntheticVecEnv(4, kind, seed=3)
+        pkw = dict(pi_hidden_sizes=[hidden, hidden], v_hidden_sizes=[hidden, hidden], activation_fn=act)
+        if kind == "halfcheetah":
+            pkw.update(log_std_init=-1.0, init_layers_orthogonal=False)
+        policy = ActorCritic(env, **pkw).to(DEV)
+        algo = PPO(policy, DEV, None, batch_size=bs, n_epochs=3, learning_rate=3e-4, **extra)
+        algo.use_wide = wide
+        algo.use_graphs = wide
+        g = torch.Generator(device="cpu").manual_seed(11)
+        shp = env.single_observation_space.shape
+        obs = torch.randn((T, N) + shp, generator=g)
+        act_t = (torch.randn(T, N, 6, generator=g).clamp(-1, 1) if kind == "halfcheetah"
+                 else torch.randint(0, 2, (T, N), generator=g))
+        t = lambda x: x.to(DEV)
+        perm_g = torch.Generator(device="cpu").manual_seed(5)
+        r = DeviceRollout(DEV, t(torch.zeros(N, dtype=torch.uint8)), t(torch.randn(N, generator=g)), t(obs), t(act_t),
+                          t(torch.randn(T, N, generator=g)), t((torch.rand(T, N, generator=g) < 0.05).to(torch.uint8)),
+                          t(torch.randn(T, N, generator=g)), t(-1.0 + 0.1 * torch.randn(T, N, generator=g)), None,
+                          0.99, 0.95, perm_source=lambda n: torch.randperm(n, generator=perm_g))
+        out = [algo.update(r)[:2] for _ in range(2)]
+        torch.cuda.synchronize()
+        res.append((algo.flat.flat.cpu().numpy(), out, algo._wide))
+    (p_w, o_w, w), (p_t, o_t, _) = res
+    assert w not in (None, False), "wide path not taken"
+    np.testing.assert_allclose(p_w, p_t, rtol=1e-4, atol=2e-6)
+    for (s_w, n_w), (s_t, n_t) in zip(o_w, o_t):
+        np.testing.assert_allclose(s_w[:, :6], s_t[:, :6], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(n_w, n_t, rtol=1e-4)
