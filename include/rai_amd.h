@@ -236,11 +236,15 @@ typedef struct rai_minibatch_desc {
   int64_t batch_size;
   int64_t mb;           /* next minibatch, advanced on device */
   int32_t n_fields;
-  int32_t pad;
+  int32_t arrivals;     /* rai_gather_minibatch_next's block-arrival counter; 0 between launches */
 } rai_minibatch_desc;
 int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
                          const int64_t* row_bytes, int64_t batch_size, void* stream);
 int rai_minibatch_advance(rai_minibatch_desc* desc, void* stream);
+/* Gather + advance in ONE launch: the last workgroup to finish (after every workgroup has read
+ * desc->mb) increments desc->mb and re-arms desc->arrivals. */
+int rai_gather_minibatch_next(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
+                              const int64_t* row_bytes, int64_t batch_size, void* stream);
 
 /* --------------------------------------------------------------------------
  * Rollout post-head: sample actions from the policy head and write the

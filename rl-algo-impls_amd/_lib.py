@@ -64,7 +64,7 @@ class MinibatchDesc(C.Structure):
         ("batch_size", C.c_int64),
         ("mb", C.c_int64),
         ("n_fields", C.c_int32),
-        ("pad", C.c_int32),
+        ("arrivals", C.c_int32),
     ]
 
 
@@ -131,6 +131,7 @@ _SIGNATURES = {
     "rai_gae_skips": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "rai_gather_minibatch": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_minibatch_advance": (C.c_int, [_vp, _vp]),
+    "rai_gather_minibatch_next": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, [C.c_int64, C.c_int32]),
     "rai_mlp_ppo_grads": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _i32,
                                     _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),

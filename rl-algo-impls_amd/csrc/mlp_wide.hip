@@ -32,7 +32,6 @@ namespace {
 constexpr int WT = 256;   // threads per workgroup
 constexpr int SL = 16;    // hidden units per slice
 constexpr int OUTM = RAI_WIDE_MAX_OUT;
-constexpr int KC = 64;    // k-chunk staged through LDS
 
 __device__ __forceinline__ float act_f(int act, float z) { return act ? fmaxf(z, 0.f) : tanhf(z); }
 // derivative from the activation's OUTPUT h: relu: h > 0; tanh: 1 - h^2
@@ -80,96 +79,193 @@ __device__ __forceinline__ void put(float* g, int64_t i, float val, int accumula
   else g[i] = val;
 }
 
+// Every operand a workgroup reuses is staged into LDS first with coalesced (float4 where the rows
+// allow) loads; the arithmetic then runs out of LDS / registers only.  Rows are processed in chunks
+// of RC = 64 (one chunk at the usual B = 64).
+constexpr int RC = 64;
+constexpr int HP = RAI_WIDE_MAX_H + 4;  // padded LDS row (floats) for H-long rows
+constexpr int RPT = RC / (WT / SL);     // rows per thread in the (16 columns x 64 rows) tiles = 4
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// Cooperative copies into LDS.  Loads are issued in batches of U per thread before any LDS store,
+// so a workgroup pays a few global round trips per staged tile, not one per element (a plain
+// load -> ds_write loop waits on every load).
+template <int U>
+__device__ __forceinline__ void stage1(float* dst, int dst_ld, const float* src, int64_t src_ld, int rows, int cols) {
+  const int total = rows * cols;
+  for (int base = threadIdx.x; base < total; base += WT * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * WT;
+      if (i < total) {
+        const int r = i / cols, c = i - r * cols;
+        v[u] = src[r * src_ld + c];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * WT;
+      if (i < total) {
+        const int r = i / cols, c = i - r * cols;
+        dst[r * dst_ld + c] = v[u];
+      }
+    }
+  }
+}
+// 16-B loads when the source rows are 16-B aligned (parameter views inside the flat buffer need not
+// be), else the 4-B path
+__device__ __forceinline__ void stage4(float* dst, int dst_ld, const float* src, int64_t src_ld, int rows, int cols) {
+  if (((reinterpret_cast<uintptr_t>(src) & 15) != 0) || (src_ld & 3) || (cols & 3) || (dst_ld & 3)) {
+    stage1<16>(dst, dst_ld, src, src_ld, rows, cols);
+    return;
+  }
+  constexpr int U = 8;
+  const int c4 = cols >> 2, total = rows * c4;
+  for (int base = threadIdx.x; base < total; base += WT * U) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * WT;
+      if (i < total) {
+        const int r = i / c4, c = (i - r * c4) << 2;
+        v[u] = *reinterpret_cast<const f4*>(src + r * src_ld + c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * WT;
+      if (i < total) {
+        const int r = i / c4, c = (i - r * c4) << 2;
+        *reinterpret_cast<f4*>(dst + r * dst_ld + c) = v[u];
+      }
+    }
+  }
+}
+
+// One wave's 16-row x 16-column tile of  Rows[16w .. 16w+16) (LDS, ld HP) x Cols^T  over k in [0, H),
+// with Cols[j][k] in LDS (ld HP): v_mfma_f32_16x16x4f32 (exact fp32 products, fp32 accumulation).
+// Lane (li = lane & 15, g = lane >> 4) feeds A = Rows[li][k], B = Cols[li][k] for k in the lane
+// group's contiguous quarter [g*H/4, (g+1)*H/4) (16-B LDS reads of 4 consecutive k); the result
+// element r of the lane is row 4g + r, column li of the tile.  Two accumulators halve the chain.
+__device__ __forceinline__ f4 tile_dot(const float* rows, const float* cols, int H, int lane) {
+  const int li = lane & 15, g = lane >> 4, KQ = H >> 2;
+  const float* ra = rows + li * HP + g * KQ;
+  const float* cb = cols + li * HP + g * KQ;
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int kk = 0; kk < KQ; kk += 4) {
+    const f4 av = *reinterpret_cast<const f4*>(ra + kk);
+    const f4 bv = *reinterpret_cast<const f4*>(cb + kk);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc1, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+
 // ---- layer 1 forward: H1[:, slice] ------------------------------------------------------------
 __global__ __launch_bounds__(WT) void wide_fwd1_kernel(const WideArgs a) {
   __shared__ float w1s[SL][RAI_WIDE_MAX_IN + 1];
+  __shared__ float xs[RC][RAI_WIDE_MAX_IN + 1];
   __shared__ float b1s[SL];
   const int s = blockIdx.x, n = blockIdx.y, t = threadIdx.x;
   const rai_mlp_wide_desc& d = a.d;
   const int H = d.hidden, IN = d.in_dim, B = a.B;
-  const float* W1 = d.w[n][0];
-  for (int i = t; i < SL * IN; i += WT) w1s[i / IN][i % IN] = W1[(int64_t)(s * SL + i / IN) * IN + i % IN];
+  stage1<16>(&w1s[0][0], RAI_WIDE_MAX_IN + 1, d.w[n][0] + (int64_t)s * SL * IN, IN, SL, IN);
   if (t < SL) b1s[t] = d.w[n][1][s * SL + t];
-  __syncthreads();
   const WideWs w = ws_of(a.ws, n, B, H);
-  const int j = t % SL;
-  for (int b = t / SL; b < B; b += WT / SL) {
-    const float* x = a.obs + (int64_t)b * IN;
-    float acc = 0.f;
-    for (int i = 0; i < IN; ++i) acc += x[i] * w1s[j][i];
-    w.H1[(int64_t)b * H + s * SL + j] = act_f(d.activation, acc + b1s[j]);
+  const int j = t % SL, r0 = t / SL;
+  for (int c0 = 0; c0 < B; c0 += RC) {
+    const int nr = min(RC, B - c0);
+    __syncthreads();
+    stage1<16>(&xs[0][0], RAI_WIDE_MAX_IN + 1, a.obs + (int64_t)c0 * IN, IN, nr, IN);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int b = r0 + q * (WT / SL);
+      if (b < nr) {
+        float acc = 0.f;
+        for (int i = 0; i < IN; ++i) acc += xs[b][i] * w1s[j][i];
+        w.H1[(int64_t)(c0 + b) * H + s * SL + j] = act_f(d.activation, acc + b1s[j]);
+      }
+    }
   }
 }
 
 // ---- layer 2 forward + output-layer partials ---------------------------------------------------
 __global__ __launch_bounds__(WT) void wide_fwd2_kernel(const WideArgs a) {
-  __shared__ float w2s[SL][KC + 4];
-  __shared__ float hs[RAI_WIDE_MAX_B][KC + 4];  // H1 rows, one k-chunk
-  __shared__ float h2s[RAI_WIDE_MAX_B][SL + 1];
+  __shared__ float w2s[SL][HP];    // W2[slice, :]
+  __shared__ float hs[RC][HP];     // H1 rows of the chunk
+  __shared__ float h2s[RC][SL + 1];
+  __shared__ float w3s[OUTM][SL];
   const int s = blockIdx.x, n = blockIdx.y, t = threadIdx.x;
   const rai_mlp_wide_desc& d = a.d;
   const int H = d.hidden, B = a.B, O = out_dim(d, n);
   const WideWs w = ws_of(a.ws, n, B, H);
-  const float* W2 = d.w[n][2];
-  const int j = t % SL, r0 = t / SL;  // rows r0, r0 + 16, ...
-  constexpr int RMAX = RAI_WIDE_MAX_B / (WT / SL);
-  float acc[RMAX];
-#pragma unroll
-  for (int q = 0; q < RMAX; ++q) acc[q] = 0.f;
-  for (int k0 = 0; k0 < H; k0 += KC) {
+  stage4(&w2s[0][0], HP, d.w[n][2] + (int64_t)s * SL * H, H, SL, H);
+  for (int i = t; i < O * SL; i += WT) w3s[i / SL][i % SL] = d.w[n][4][(int64_t)(i / SL) * H + s * SL + i % SL];
+  for (int c0 = 0; c0 < B; c0 += RC) {
+    const int nr = min(RC, B - c0);
     __syncthreads();
-    for (int i = t; i < SL * KC; i += WT) w2s[i / KC][i % KC] = W2[(int64_t)(s * SL + i / KC) * H + k0 + i % KC];
-    for (int i = t; i < B * KC; i += WT) hs[i / KC][i % KC] = w.H1[(int64_t)(i / KC) * H + k0 + i % KC];
+    stage4(&hs[0][0], HP, w.H1 + (int64_t)c0 * H, H, nr, H);
     __syncthreads();
+    {  // wave w: rows [16w, 16w + 16) of the chunk (the tile's rows >= nr are computed and dropped)
+      const int wv = t >> 6, lane = t & 63;
+      const f4 z = tile_dot(&hs[16 * wv][0], &w2s[0][0], H, lane);
+      const int jj = lane & 15, g = lane >> 4;
+      const float bjj = d.w[n][3][s * SL + jj];
 #pragma unroll
-    for (int q = 0; q < RMAX; ++q) {
-      const int b = r0 + q * (WT / SL);
-      if (b < B) {
-        float sacc = acc[q];
-        for (int k = 0; k < KC; ++k) sacc += hs[b][k] * w2s[j][k];
-        acc[q] = sacc;
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * wv + 4 * g + r;
+        if (b < nr) {
+          const float h = act_f(d.activation, z[r] + bjj);
+          h2s[b][jj] = h;
+          w.H2[(int64_t)(c0 + b) * H + s * SL + jj] = h;
+        }
       }
     }
-  }
-  const float bj = d.w[n][3][s * SL + j];
+    __syncthreads();
+    for (int i = t; i < nr * O; i += WT) {
+      const int b = i / O, o = i - b * O;
+      float p = 0.f;
 #pragma unroll
-  for (int q = 0; q < RMAX; ++q) {
-    const int b = r0 + q * (WT / SL);
-    if (b < B) {
-      const float h = act_f(d.activation, acc[q] + bj);
-      h2s[b][j] = h;
-      w.H2[(int64_t)b * H + s * SL + j] = h;
+      for (int jj = 0; jj < SL; ++jj) p += h2s[b][jj] * w3s[o][jj];
+      w.P[((int64_t)s * B + c0 + b) * OUTM + o] = p;
     }
-  }
-  __syncthreads();
-  const float* W3 = d.w[n][4];
-  for (int i = t; i < B * O; i += WT) {
-    const int b = i / O, o = i % O;
-    float p = 0.f;
-#pragma unroll
-    for (int jj = 0; jj < SL; ++jj) p += h2s[b][jj] * W3[(int64_t)o * H + s * SL + jj];
-    w.P[((int64_t)s * B + b) * OUTM + o] = p;
   }
 }
 
 // ---- head: outputs, log-prob, entropy, value --------------------------------------------------
 __global__ __launch_bounds__(WT) void wide_head_kernel(const WideArgs a) {
+  __shared__ float outs[RAI_WIDE_MAX_B][OUTM + 1];
   const rai_mlp_wide_desc& d = a.d;
-  const int H = d.hidden, B = a.B, S = H / SL, A = d.out_pi;
+  const int H = d.hidden, B = a.B, S = H / SL, A = d.out_pi, t = threadIdx.x;
+  constexpr int SMAX = RAI_WIDE_MAX_H / SL;
   const WideWs wp = ws_of(a.ws, 0, B, H), wv = ws_of(a.ws, 1, B, H);
-  for (int b = blockIdx.x * WT + threadIdx.x; b < B; b += gridDim.x * WT) {
-    float out[OUTM];
-    for (int o = 0; o < A; ++o) {
-      float acc = 0.f;
-      for (int s = 0; s < S; ++s) acc += wp.P[((int64_t)s * B + b) * OUTM + o];
-      out[o] = acc + d.w[0][5][o];
-      wp.OUT[(int64_t)b * OUTM + o] = out[o];
-    }
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += wv.P[((int64_t)s * B + b) * OUTM];
-    v += d.w[1][5][0];
-    wv.OUT[(int64_t)b * OUTM] = v;
-    a.v[b] = v;
+  // (1) every (row, output) sums its S slice partials in slice order (loads issued together)
+  const int per = A + 1;  // actor outputs, then the critic's value
+  for (int i = t; i < B * per; i += WT) {
+    const int b = i / per, o = i - b * per;
+    const bool critic = o == A;
+    const float* P = critic ? wv.P : wp.P;
+    const int oo = critic ? 0 : o;
+    float part[SMAX];
+#pragma unroll
+    for (int q = 0; q < SMAX; ++q) part[q] = q < S ? P[((int64_t)q * B + b) * OUTM + oo] : 0.f;
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < SMAX; ++q)
+      if (q < S) acc += part[q];
+    const float val = acc + (critic ? d.w[1][5][0] : d.w[0][5][o]);
+    outs[b][o] = val;
+    (critic ? wv.OUT : wp.OUT)[(int64_t)b * OUTM + oo] = val;
+  }
+  __syncthreads();
+  // (2) one row per thread: the head's log-prob / entropy, and v
+  for (int b = t; b < B; b += WT) {
+    a.v[b] = outs[b][A];
     if (d.head == 1) {  // Normal(mu, exp(log_std)): torch.distributions.Normal.log_prob / entropy
       const float* act = static_cast<const float*>(a.actions) + (int64_t)b * A;
       float lp = 0.f;
@@ -177,31 +273,34 @@ __global__ __launch_bounds__(WT) void wide_head_kernel(const WideArgs a) {
         const float scale = expf(d.log_std[o]);
         const float var = scale * scale;
         const float log_scale = logf(scale);
-        const float x = act[o] - out[o];
+        const float x = act[o] - outs[b][o];
         lp += -(x * x) / (2.f * var) - log_scale - 0.91893853320467274f;  // log(sqrt(2*pi))
-        a.ent[(int64_t)b * A + o] = 1.4189385332046727f + log_scale;  // (0.5 + 0.5*log(2*pi)) + log(scale)
+        a.ent[(int64_t)b * A + o] = 1.4189385332046727f + log_scale;     // (0.5 + 0.5*log(2*pi)) + log(scale)
       }
       a.logp[b] = lp;
     } else {  // Categorical(logits)
       const int64_t ai = static_cast<const int64_t*>(a.actions)[b];
-      float mx = out[0];
-      for (int o = 1; o < A; ++o) mx = fmaxf(mx, out[o]);
+      float mx = outs[b][0];
+      for (int o = 1; o < A; ++o) mx = fmaxf(mx, outs[b][o]);
       float se = 0.f;
-      for (int o = 0; o < A; ++o) se += expf(out[o] - mx);
+      for (int o = 0; o < A; ++o) se += expf(outs[b][o] - mx);
       const float lse = mx + logf(se);
       float h = 0.f;
       for (int o = 0; o < A; ++o) {
-        const float l = out[o] - lse;
+        const float l = outs[b][o] - lse;
         h -= fmaxf(l, -3.4028234663852886e38f) * expf(l);
       }
-      a.logp[b] = out[ai >= 0 && ai < A ? ai : 0] - lse;
+      a.logp[b] = outs[b][ai >= 0 && ai < A ? ai : 0] - lse;
       a.ent[b] = h;
     }
   }
 }
 
-// dLoss/dOut for row b of network n (recomputed by every workgroup that needs it)
-__device__ __forceinline__ void d_out_row(const WideArgs& a, const WideWs& w, int n, int b, float* dout) {
+// dLoss/dOut for row b of network n (recomputed by every workgroup that needs it); for the Gaussian
+// actor also the row's dLoss/dlog_std terms.  (Staging these operands through LDS first measured
+// slower: the per-row loads of different threads already overlap.)
+__device__ __forceinline__ void d_out_row(const WideArgs& a, const WideWs& w, int n, int b, float* dout,
+                                          float* dls) {
   const rai_mlp_wide_desc& d = a.d;
   const int A = d.out_pi;
   if (n == 1) {
@@ -211,9 +310,13 @@ __device__ __forceinline__ void d_out_row(const WideArgs& a, const WideWs& w, in
   const float* out = w.OUT + (int64_t)b * OUTM;
   if (d.head == 1) {
     const float* act = static_cast<const float*>(a.actions) + (int64_t)b * A;
+    const float gl = a.d_logp[b];
     for (int o = 0; o < A; ++o) {
       const float scale = expf(d.log_std[o]);
-      dout[o] = a.d_logp[b] * ((act[o] - out[o]) / (scale * scale));
+      const float var = scale * scale;
+      const float x = act[o] - out[o];
+      dout[o] = gl * (x / var);
+      dls[o] = gl * ((x * x) / var - 1.f) + a.d_ent[(int64_t)b * A + o];
     }
   } else {
     const int64_t ai = static_cast<const int64_t*>(a.actions)[b];
@@ -238,121 +341,147 @@ __device__ __forceinline__ void d_out_row(const WideArgs& a, const WideWs& w, in
 // ---- backward through layers 3 and 2 ---------------------------------------------------------
 __global__ __launch_bounds__(WT) void wide_bwd2_kernel(const WideArgs a) {
   __shared__ float douts[RAI_WIDE_MAX_B][OUTM];
-  __shared__ float dz2s[RAI_WIDE_MAX_B][SL];
+  __shared__ float dlss[RAI_WIDE_MAX_B][OUTM];
+  __shared__ float hs[RC][HP];        // H1 rows of the chunk
+  __shared__ float h2s[RC][SL + 1];   // H2[:, slice] rows of the chunk
+  __shared__ float dz2s[RC][SL];
   __shared__ float w3s[OUTM][SL];
   const int s = blockIdx.x, n = blockIdx.y, t = threadIdx.x;
   const rai_mlp_wide_desc& d = a.d;
   const int H = d.hidden, B = a.B, O = out_dim(d, n), acc_mode = d.accumulate;
+  const bool do_ls = n == 0 && s == 0 && d.head == 1;
   const WideWs w = ws_of(a.ws, n, B, H);
   for (int b = t; b < B; b += WT) {
-    float dout[OUTM];
-    d_out_row(a, w, n, b, dout);
-    for (int o = 0; o < O; ++o) douts[b][o] = dout[o];
+    float dout[OUTM], dls[OUTM];
+    d_out_row(a, w, n, b, dout, dls);
+    for (int o = 0; o < O; ++o) {
+      douts[b][o] = dout[o];
+      if (do_ls) dlss[b][o] = dls[o];
+    }
   }
   for (int i = t; i < O * SL; i += WT) w3s[i / SL][i % SL] = d.w[n][4][(int64_t)(i / SL) * H + s * SL + i % SL];
-  __syncthreads();
-  // dZ2 slice
-  for (int i = t; i < B * SL; i += WT) {
-    const int b = i / SL, j = i % SL;
-    float dh = 0.f;
-    for (int o = 0; o < O; ++o) dh += douts[b][o] * w3s[o][j];
-    const float h2 = w.H2[(int64_t)b * H + s * SL + j];
-    const float dz = dh * act_d(d.activation, h2);
-    dz2s[b][j] = dz;
-    w.DZ2[(int64_t)b * H + s * SL + j] = dz;
+  // dW2[slice, :] = dZ2[:, slice]^T H1: thread k owns column k of the slice's 16 rows (VALU; an MFMA
+  // version over 16-row k-tiles measured slower at B = 64: its chains are only 16 deep)
+  float gw2v[SL];
+#pragma unroll
+  for (int jj = 0; jj < SL; ++jj) gw2v[jj] = 0.f;
+  float gw3 = 0.f, gb = 0.f;  // dW3[o][j] for pair t < O*SL; db2[t] (t < SL)
+  for (int c0 = 0; c0 < B; c0 += RC) {
+    const int nr = min(RC, B - c0);
+    __syncthreads();
+    stage4(&hs[0][0], HP, w.H1 + (int64_t)c0 * H, H, nr, H);
+    stage1<16>(&h2s[0][0], SL + 1, w.H2 + (int64_t)c0 * H + s * SL, H, nr, SL);
+    __syncthreads();
+    for (int i = t; i < nr * SL; i += WT) {
+      const int b = i / SL, j = i - b * SL;
+      float dh = 0.f;
+      for (int o = 0; o < O; ++o) dh += douts[c0 + b][o] * w3s[o][j];
+      const float dz = dh * act_d(d.activation, h2s[b][j]);
+      dz2s[b][j] = dz;
+      w.DZ2[(int64_t)(c0 + b) * H + s * SL + j] = dz;
+    }
+    __syncthreads();
+    if (t < O * SL) {
+      const int o = t / SL, j = t - o * SL;
+      for (int b = 0; b < nr; ++b) gw3 += douts[c0 + b][o] * h2s[b][j];
+    }
+    if (t < SL)
+      for (int b = 0; b < nr; ++b) gb += dz2s[b][t];
+    if (t < H) {  // thread k owns column k of every row in the slice
+      for (int b = 0; b < nr; ++b) {
+        const float h1 = hs[b][t];
+#pragma unroll
+        for (int q = 0; q < SL / 4; ++q) {
+          const f4 z = *reinterpret_cast<const f4*>(&dz2s[b][4 * q]);
+          gw2v[4 * q + 0] += z.x * h1;
+          gw2v[4 * q + 1] += z.y * h1;
+          gw2v[4 * q + 2] += z.z * h1;
+          gw2v[4 * q + 3] += z.w * h1;
+        }
+      }
+    }
   }
-  __syncthreads();
-  // dW3[:, slice] = dOut^T H2[:, slice]; db3 (slice 0)
-  for (int i = t; i < O * SL; i += WT) {
-    const int o = i / SL, j = i % SL;
-    float g = 0.f;
-    for (int b = 0; b < B; ++b) g += douts[b][o] * w.H2[(int64_t)b * H + s * SL + j];
-    put(d.g[n][4], (int64_t)o * H + s * SL + j, g, acc_mode);
+  if (t < O * SL) put(d.g[n][4], (int64_t)(t / SL) * H + s * SL + t % SL, gw3, acc_mode);
+  if (t < SL) put(d.g[n][3], s * SL + t, gb, acc_mode);
+  if (t < H) {
+#pragma unroll
+    for (int jj = 0; jj < SL; ++jj) put(d.g[n][2], (int64_t)(s * SL + jj) * H + t, gw2v[jj], acc_mode);
   }
   if (s == 0 && t < O) {
-    float g = 0.f;
-    for (int b = 0; b < B; ++b) g += douts[b][t];
-    put(d.g[n][5], t, g, acc_mode);
+    float sum = 0.f;
+    for (int b = 0; b < B; ++b) sum += douts[b][t];
+    put(d.g[n][5], t, sum, acc_mode);
   }
-  // db2[slice]
-  if (t < SL) {
-    float g = 0.f;
-    for (int b = 0; b < B; ++b) g += dz2s[b][t];
-    put(d.g[n][3], s * SL + t, g, acc_mode);
-  }
-  // dW2[slice, :] = dZ2[:, slice]^T H1: thread k owns column k of every row in the slice
-  for (int k = t; k < H; k += WT) {
-    float g[SL];
-#pragma unroll
-    for (int j = 0; j < SL; ++j) g[j] = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const float h1 = w.H1[(int64_t)b * H + k];
-#pragma unroll
-      for (int j = 0; j < SL; ++j) g[j] += dz2s[b][j] * h1;
-    }
-#pragma unroll
-    for (int j = 0; j < SL; ++j) put(d.g[n][2], (int64_t)(s * SL + j) * H + k, g[j], acc_mode);
-  }
-  // dlog_std (Gaussian actor): sum_b d_logp * ((a - mu)^2 / var - 1) + d_entropy
-  if (n == 0 && s == 0 && d.head == 1 && t < d.out_pi) {
-    const int A = d.out_pi, o = t;
-    const float scale = expf(d.log_std[o]);
-    const float var = scale * scale;
-    float g = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const float x = static_cast<const float*>(a.actions)[(int64_t)b * A + o] - w.OUT[(int64_t)b * OUTM + o];
-      g += a.d_logp[b] * ((x * x) / var - 1.f) + a.d_ent[(int64_t)b * A + o];
-    }
-    put(d.g_log_std, o, g, acc_mode);
+  if (do_ls && t < d.out_pi) {
+    float sum = 0.f;
+    for (int b = 0; b < B; ++b) sum += dlss[b][t];
+    put(d.g_log_std, t, sum, acc_mode);
   }
 }
 
 // ---- backward through layer 1 ----------------------------------------------------------------
 __global__ __launch_bounds__(WT) void wide_bwd1_kernel(const WideArgs a) {
-  __shared__ float w2s[KC][SL + 1];               // W2[k-chunk, slice]
-  __shared__ float zs[RAI_WIDE_MAX_B][KC + 4];     // dZ2 rows, one k-chunk
-  __shared__ float dz1s[RAI_WIDE_MAX_B][SL + 1];
+  __shared__ float w2t[SL][HP];                     // W2[:, slice] transposed: [j][k]
+  __shared__ float zs[RC][HP];                      // dZ2 rows of the chunk
+  __shared__ float xs[RC][RAI_WIDE_MAX_IN + 1];     // obs rows of the chunk
+  __shared__ float dz1s[RC][SL + 1];
   const int s = blockIdx.x, n = blockIdx.y, t = threadIdx.x;
   const rai_mlp_wide_desc& d = a.d;
   const int H = d.hidden, B = a.B, IN = d.in_dim, acc_mode = d.accumulate;
   const WideWs w = ws_of(a.ws, n, B, H);
   const float* W2 = d.w[n][2];
-  const int j = t % SL, r0 = t / SL;
-  constexpr int RMAX = RAI_WIDE_MAX_B / (WT / SL);
-  float acc[RMAX];
+  for (int base = t; base < H * SL; base += WT * 16) {  // row k of W2 holds the slice's 16 floats
+    float v[16];
 #pragma unroll
-  for (int q = 0; q < RMAX; ++q) acc[q] = 0.f;
-  for (int k0 = 0; k0 < H; k0 += KC) {
-    __syncthreads();
-    for (int i = t; i < KC * SL; i += WT) w2s[i / SL][i % SL] = W2[(int64_t)(k0 + i / SL) * H + s * SL + i % SL];
-    for (int i = t; i < B * KC; i += WT) zs[i / KC][i % KC] = w.DZ2[(int64_t)(i / KC) * H + k0 + i % KC];
-    __syncthreads();
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + u * WT;
+      if (i < H * SL) v[u] = W2[(int64_t)(i / SL) * H + s * SL + i % SL];
+    }
 #pragma unroll
-    for (int q = 0; q < RMAX; ++q) {
-      const int b = r0 + q * (WT / SL);
-      if (b < B) {
-        float sacc = acc[q];
-        for (int k = 0; k < KC; ++k) sacc += zs[b][k] * w2s[k][j];
-        acc[q] = sacc;
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + u * WT;
+      if (i < H * SL) w2t[i % SL][i / SL] = v[u];
+    }
+  }
+  float gw1[(SL * RAI_WIDE_MAX_IN + WT - 1) / WT];
+#pragma unroll
+  for (int q = 0; q < (SL * RAI_WIDE_MAX_IN + WT - 1) / WT; ++q) gw1[q] = 0.f;
+  float gb = 0.f;
+  for (int c0 = 0; c0 < B; c0 += RC) {
+    const int nr = min(RC, B - c0);
+    __syncthreads();
+    stage4(&zs[0][0], HP, w.DZ2 + (int64_t)c0 * H, H, nr, H);
+    stage1<16>(&xs[0][0], RAI_WIDE_MAX_IN + 1, a.obs + (int64_t)c0 * IN, IN, nr, IN);
+    __syncthreads();
+    {  // dH1 tile of wave w on MFMA, then dZ1 = dH1 * act'(H1)
+      const int wv = t >> 6, lane = t & 63;
+      const f4 z = tile_dot(&zs[16 * wv][0], &w2t[0][0], H, lane);
+      const int jj = lane & 15, g = lane >> 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * wv + 4 * g + r;
+        if (b < nr) dz1s[b][jj] = z[r] * act_d(d.activation, w.H1[(int64_t)(c0 + b) * H + s * SL + jj]);
+      }
+    }
+    __syncthreads();
+    if (t < SL)
+      for (int b = 0; b < nr; ++b) gb += dz1s[b][t];
+#pragma unroll
+    for (int q = 0; q < (SL * RAI_WIDE_MAX_IN + WT - 1) / WT; ++q) {
+      const int i = t + q * WT;
+      if (i < SL * IN) {
+        const int jj = i / IN, c = i - jj * IN;
+        float g = gw1[q];
+        for (int b = 0; b < nr; ++b) g += dz1s[b][jj] * xs[b][c];
+        gw1[q] = g;
       }
     }
   }
+  if (t < SL) put(d.g[n][1], s * SL + t, gb, acc_mode);
 #pragma unroll
-  for (int q = 0; q < RMAX; ++q) {
-    const int b = r0 + q * (WT / SL);
-    if (b < B) dz1s[b][j] = acc[q] * act_d(d.activation, w.H1[(int64_t)b * H + s * SL + j]);
-  }
-  __syncthreads();
-  if (t < SL) {
-    float g = 0.f;
-    for (int b = 0; b < B; ++b) g += dz1s[b][t];
-    put(d.g[n][1], s * SL + t, g, acc_mode);
-  }
-  for (int i = t; i < SL * IN; i += WT) {
-    const int jj = i / IN, c = i % IN;
-    float g = 0.f;
-    for (int b = 0; b < B; ++b) g += dz1s[b][jj] * a.obs[(int64_t)b * IN + c];
-    put(d.g[n][0], (int64_t)(s * SL + jj) * IN + c, g, acc_mode);
+  for (int q = 0; q < (SL * RAI_WIDE_MAX_IN + WT - 1) / WT; ++q) {
+    const int i = t + q * WT;
+    if (i < SL * IN) put(d.g[n][0], (int64_t)(s * SL + i / IN) * IN + i % IN, gw1[q], acc_mode);
   }
 }
 

@@ -53,10 +53,13 @@ struct MbDst {
   int64_t units[RAI_MAX_FIELDS];
   int32_t gran[RAI_MAX_FIELDS];
 };
-__global__ __launch_bounds__(256) void gather_minibatch_kernel(const rai_minibatch_desc* __restrict__ d,
-                                                               const MbDst o) {
+__global__ __launch_bounds__(256) void gather_minibatch_kernel(rai_minibatch_desc* __restrict__ d, const MbDst o,
+                                                               const int advance) {
+  __shared__ int64_t mb_s;
+  if (threadIdx.x == 0) mb_s = d->mb;
+  __syncthreads();
   const int fi = blockIdx.y;
-  const int64_t mb = d->mb, B = d->batch_size;
+  const int64_t mb = mb_s, B = d->batch_size;
   const int64_t row0 = mb * B;
   const int64_t rows = min(B, d->n_rows - row0);
   const int64_t units = o.units[fi];
@@ -75,6 +78,17 @@ __global__ __launch_bounds__(256) void gather_minibatch_kernel(const rai_minibat
       reinterpret_cast<uint32_t*>(o.dst[fi])[u] = reinterpret_cast<const uint32_t*>(src)[sr * units + j];
     } else {
       o.dst[fi][u] = src[sr * units + j];
+    }
+  }
+  if (advance && threadIdx.x == 0) {
+    // every block has read mb (above) before it arrives; the last to arrive advances the minibatch
+    // for the next launch and re-arms the counter
+    __threadfence();
+    const int nblocks = (int)(gridDim.x * gridDim.y);
+    if (atomicAdd(&d->arrivals, 1) == nblocks - 1) {
+      d->arrivals = 0;
+      d->mb = mb + 1;
+      __threadfence();
     }
   }
 }
@@ -196,8 +210,8 @@ extern "C" int rai_gather_rows(int32_t n_fields, const void* const* src, void* c
   return RAI_OK;
 }
 
-extern "C" int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
-                                    const int64_t* row_bytes, int64_t batch_size, void* stream) {
+static int gather_minibatch(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst, const int64_t* row_bytes,
+                            int64_t batch_size, int advance, void* stream) {
   if (n_fields < 1 || n_fields > RAI_MAX_FIELDS || batch_size < 1) return RAI_E_SHAPE;
   if (!desc || !dst || !row_bytes) return RAI_E_NULLPTR;
   MbDst o;
@@ -213,9 +227,19 @@ extern "C" int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fi
   int64_t blocks = (batch_size * max_units + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(gather_minibatch_kernel, dim3((unsigned)blocks, (unsigned)n_fields), dim3(256), 0,
-                     rai_stream(stream), desc, o);
+                     rai_stream(stream), desc, o, advance);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
+}
+
+extern "C" int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
+                                    const int64_t* row_bytes, int64_t batch_size, void* stream) {
+  return gather_minibatch(const_cast<rai_minibatch_desc*>(desc), n_fields, dst, row_bytes, batch_size, 0, stream);
+}
+
+extern "C" int rai_gather_minibatch_next(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
+                                         const int64_t* row_bytes, int64_t batch_size, void* stream) {
+  return gather_minibatch(desc, n_fields, dst, row_bytes, batch_size, 1, stream);
 }
 
 extern "C" int rai_minibatch_advance(rai_minibatch_desc* desc, void* stream) {

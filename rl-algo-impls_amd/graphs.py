@@ -6,8 +6,8 @@ The reference runs one eager minibatch step per Python iteration (rl_algo_impls/
 cost exceeds their GPU time at these batch sizes.  Here the step is captured ONCE into a hipGraph
 (torch.cuda.CUDAGraph) and replayed for every minibatch of every epoch:
 
-    rai_gather_minibatch   rows perm[mb*B + i] of every rollout field -> static minibatch buffers
-    rai_minibatch_advance  mb += 1 (device-side counter in a rai_minibatch_desc)
+    rai_gather_minibatch_next  rows perm[mb*B + i] of every rollout field -> static minibatch
+                           buffers; the last workgroup to finish advances mb (device-side counter)
     policy forward         PyTorch-ROCm (MIOpen / hipBLASLt), static inputs
     rai_ppo_loss           loss + dLoss/d(logp, entropy, v), stats row at state.stat_index
     autograd backward      into the flat .grad buffer
@@ -56,9 +56,8 @@ class MinibatchStepGraph:
         rb = (C.c_int64 * n)(*self.row_bytes)
         st = _lib.stream_handle(self.device)
         L = _lib.lib()
-        _lib.check(L.rai_gather_minibatch(desc.data_ptr(), n, C.cast(dst, C.c_void_p), C.cast(rb, C.c_void_p),
-                                          int(bufs[0].shape[0]), st), "rai_gather_minibatch")
-        _lib.check(L.rai_minibatch_advance(desc.data_ptr(), st), "rai_minibatch_advance")
+        _lib.check(L.rai_gather_minibatch_next(desc.data_ptr(), n, C.cast(dst, C.c_void_p), C.cast(rb, C.c_void_p),
+                                               int(bufs[0].shape[0]), st), "rai_gather_minibatch_next")
 
     def _body(self, desc: torch.Tensor) -> None:
         self.gather(desc, self.static)
