@@ -142,6 +142,10 @@ typedef struct rai_ppo_hparams {
   float vf_coef[RAI_MAX_K];
   float vf_weights[RAI_MAX_K];
   float multi_reward_weights[RAI_MAX_K];
+  /* Data parallel (K == 1, not normalize_after_scaling): device (n_steps, 2) table of the GLOBAL
+   * minibatch's advantage (mean, den) for stats row stat_index (den includes +1e-8 and the
+   * normalize / standardize choice), replacing the per-rank moments; NULL: the minibatch's own. */
+  const float* ext_moments;
 } rai_ppo_hparams;
 
 typedef struct rai_optim_hparams {

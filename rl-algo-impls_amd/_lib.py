@@ -50,6 +50,7 @@ class PPOHparams(C.Structure):
         ("vf_coef", C.c_float * RAI_MAX_K),
         ("vf_weights", C.c_float * RAI_MAX_K),
         ("multi_reward_weights", C.c_float * RAI_MAX_K),
+        ("ext_moments", C.c_void_p),
     ]
 
 

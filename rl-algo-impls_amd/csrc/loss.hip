@@ -173,6 +173,14 @@ __global__ __launch_bounds__(LOSS_THREADS) void pg_loss_kernel(const LossArgs a)
       nm_s.smean = mean;
       nm_s.sden = (float)sqrt(acc[0] / (double)(B - 1)) + 1e-8f;
     }
+  } else if (need_cols && hp.ext_moments && K == 1) {
+    // data parallel: the global minibatch's moments, reduced across ranks by the host (ppo.py:313-316
+    // over the union of the ranks' minibatch slices)
+    if (tid == 0) {
+      const int si = a.state->stat_index;
+      nm_s.mean[0] = hp.ext_moments[2 * si];
+      nm_s.den[0] = hp.ext_moments[2 * si + 1];
+    }
   } else if (need_cols) {
     double acc[KM];
 #pragma unroll

@@ -506,13 +506,30 @@ class PPO:
             K = self._update_graphed(r, nmb)
             return self._read_stats(n_steps, n_norms, K)
         wide = self._wide_step()
-        for _ in range(self.n_epochs):
-            for mb in r.minibatches(self.batch_size, shuffle=not self.gradient_accumulation):
+        shuffle = not self.gradient_accumulation
+        ext = None
+        for e in range(self.n_epochs):
+            if hasattr(r, "epoch_batch"):  # DeviceRollout: the epoch's permuted copy, sliced
+                full = r.epoch_batch(shuffle)
+                mbs = [r._batch_from([full.obs, full.actions, full.values, full.advantages, full.returns]
+                                     + ([full.logprobs] if full.logprobs is not None else [])
+                                     + ([full.action_masks] if full.action_masks is not None else []),
+                                     slice(i, i + self.batch_size)) for i in range(0, r.total_steps, self.batch_size)]
+            else:
+                full, mbs = None, r.minibatches(self.batch_size, shuffle=shuffle)
+            for mb in mbs:
                 if K is None:
                     with torch.no_grad():  # K (value columns) before the device blocks are written
                         K = value_columns(self.policy(mb.obs[:1], mb.actions[:1], action_masks=(
                             mb.action_masks[:1] if mb.action_masks is not None else None))[2])
-                    blocks.upload(self._hparams(K, nmb), self.optimizer.step_count)
+                    ext = self._dp_moments_table(K, n_steps)
+                    hp = self._hparams(K, nmb)
+                    hp.ext_moments = ext.data_ptr() if ext is not None else None
+                    blocks.upload(hp, self.optimizer.step_count)
+                    if ext is not None and full is not None:
+                        self._fill_epoch_moments(ext, e, full.advantages, nmb)
+                elif ext is not None and mb is mbs[0] and full is not None:
+                    self._fill_epoch_moments(ext, e, full.advantages, nmb)
                 if mb.logprobs is None:
                     raise ValueError("PPO needs rollout logprobs (include_logp=True)")
                 self._minibatch_loss_grads(wide, mb.obs, mb.actions, mb.action_masks, mb.values, mb.advantages,
@@ -526,6 +543,22 @@ class PPO:
                     self._all_reduce(self.flat.grad, average=True)
                 self.optimizer.step(blocks.state, blocks.norms)
         return self._read_stats(n_steps, n_norms, K)
+
+    def _dp_moments_table(self, K: int, n_steps: int) -> Optional[torch.Tensor]:
+        """Data parallel on the per-minibatch path: the global minibatches' advantage (mean, den),
+        one row per stats row, for the loss kernel (rai_ppo_hparams.ext_moments); None when the
+        minibatch's own moments are the reference's (single rank) or the options are not covered
+        (K > 1 value columns, normalize-after-scaling: normalised per rank)."""
+        if not self.dp_enabled or self.world == 1 or K != 1 or self.normalize_advantages_after_scaling:
+            return None
+        if not (self.normalize_advantage or self.standardize_advantage):
+            return None
+        return torch.zeros((n_steps, 2), dtype=torch.float32, device=self.device)
+
+    def _fill_epoch_moments(self, ext: torch.Tensor, epoch: int, adv_epoch: torch.Tensor, nmb: int) -> None:
+        """Rows [epoch*nmb, (epoch+1)*nmb) of the table from this rank's permuted advantages (one
+        small all-reduce; stream-ordered before the epoch's loss launches)."""
+        ext[epoch * nmb:(epoch + 1) * nmb].copy_(self._global_adv_moments(adv_epoch, nmb))
 
     def _read_stats(self, n_steps: int, n_norms: int, K: Optional[int]) -> Tuple[np.ndarray, np.ndarray, int]:
         blocks = self.blocks
@@ -570,7 +603,10 @@ class PPO:
                                    action_masks=fields[6][:1] if has_masks else None)
         K = value_columns(v0)
         K_box[0] = K
-        blocks.upload(self._hparams(K, nmb), self.optimizer.step_count)
+        ext = self._dp_moments_table(K, self.n_epochs * nmb)
+        hp = self._hparams(K, nmb)
+        hp.ext_moments = ext.data_ptr() if ext is not None else None
+        blocks.upload(hp, self.optimizer.step_count)
         # a graph bakes in every device pointer it touches: key it on the ones that can change
         tag = (optim_in_step, wide is not None, blocks.stats.data_ptr(), blocks.norms.data_ptr(), blocks.hp.data_ptr(),
                blocks.state.data_ptr(), self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
@@ -580,8 +616,11 @@ class PPO:
         gu.stream.wait_stream(cur)
         with torch.cuda.stream(gu.stream):
             gu.set_rollout(fields, B, shuffle)
-            for _ in range(self.n_epochs):
-                gu.start_epoch(r.permutation() if shuffle else None)
+            for e in range(self.n_epochs):
+                perm = r.permutation() if shuffle else None
+                if ext is not None:
+                    self._fill_epoch_moments(ext, e, fields[3][perm] if perm is not None else fields[3], nmb)
+                gu.start_epoch(perm)
                 for _ in range(n_full):
                     g.run(gu.desc, gu.stream)
                     if not optim_in_step and not self.gradient_accumulation:

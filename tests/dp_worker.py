@@ -134,3 +134,56 @@ def rms_worker(rank, world, port, q):
         rew.append(r)
     q.put((rank, np.stack(obs), np.stack(rew), env.env.rms.mean, env.rms.var))
     dist.destroy_process_group()
+
+
+def make_wide_rank_data(rank, dev, T=16, N=16):
+    """Rank-local (T, N, ...) rollout tensors for a HalfCheetah-shaped policy (17-dim obs, Box(6))."""
+    import torch
+
+    g = torch.Generator().manual_seed(31 + rank)
+    return dict(obs=torch.randn(T, N, 17, generator=g), act=torch.randn(T, N, 6, generator=g).clamp(-1, 1),
+                rew=torch.randn(T, N, generator=g) + 0.2 * rank, vals=torch.randn(T, N, generator=g),
+                starts=(torch.rand(T, N, generator=g) < 0.05).to(torch.uint8),
+                logp=-8.0 + 0.3 * torch.randn(T, N, generator=g), nv=torch.randn(N, generator=g),
+                nes=torch.zeros(N, dtype=torch.uint8))
+
+
+def wide_policy_and_rollout(d, dev, hidden=128):
+    """(policy seeded identically everywhere, DeviceRollout with the identity permutation)."""
+    import torch
+
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.rollout import DeviceRollout
+
+    torch.manual_seed(0)
+    env = SyntheticVecEnv(2, "halfcheetah", seed=3)
+    policy = ActorCritic(env, pi_hidden_sizes=[hidden, hidden], v_hidden_sizes=[hidden, hidden], activation_fn="relu",
+                         log_std_init=-1.0, init_layers_orthogonal=False).to(dev)
+    t = lambda x: x.to(dev)
+    r = DeviceRollout(dev, t(d["nes"]), t(d["nv"]), t(d["obs"]), t(d["act"]), t(d["rew"]), t(d["starts"]),
+                      t(d["vals"]), t(d["logp"]), None, 0.99, 0.95, perm_source=lambda n: torch.arange(n))
+    return policy, r
+
+
+def wide_dp_worker(rank, world, port, q):
+    """Data-parallel update through the wide-MLP kernels (gloo, all ranks on cuda:0): global advantage
+    moments per minibatch (rai_ppo_hparams.ext_moments), gradient all-reduce per step."""
+    import torch
+
+    _init(rank, world, port)
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.ppo import PPO
+
+    dev = torch.device("cuda", 0)
+    policy, r = wide_policy_and_rollout(make_wide_rank_data(rank, dev), dev)
+    algo = PPO(policy, dev, None, batch_size=64, n_epochs=2, learning_rate=3e-4, ent_coef=0.01)
+    algo.enable_data_parallel()
+    stats, norms, _ = algo.update(r)
+    assert algo._wide not in (None, False), "wide path not taken"
+    q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()

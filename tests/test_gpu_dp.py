@@ -122,3 +122,48 @@ def test_native_rccl_epoch_loop_matches_python_loop_world1():
     np.testing.assert_allclose(nn, ng, rtol=1e-5)
     np.testing.assert_allclose(sn[:, :6], sg[:, :6], rtol=1e-4, atol=1e-7)
     np.testing.assert_allclose(pn, pg, rtol=1e-4, atol=1e-6)
+
+
+def test_wide_mlp_dp_world2_matches_single_process_global_minibatches():
+    """HalfCheetah-class policy on the wide-MLP kernels, 2 ranks (gloo, both on cuda:0) with the
+    identity permutation: rank r's minibatch i is its time steps [4i, 4i + 4) x 16 envs, so the
+    global minibatch i is time steps [4i, 4i + 4) x all 32 envs of the concatenated rollout.  The
+    single-process update over that rollout (batch 128) is the reference: advantage normalisation
+    over the GLOBAL minibatch, loss means over its 128 rows."""
+    import queue
+    import time
+
+    import dp_worker
+    from rl_algo_impls_amd.ppo import PPO
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.wide_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    deadline = time.time() + 240
+    while len(res) < 2:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"rank exited with {dead}"
+            assert time.time() < deadline, "ranks did not report in time"
+    res.sort(key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, s0, n0), (_, p1, s1, n1) = res
+    np.testing.assert_array_equal(p0, p1)
+
+    dev = torch.device("cuda", 0)
+    d0, d1 = dp_worker.make_wide_rank_data(0, dev), dp_worker.make_wide_rank_data(1, dev)
+    glob = {k: torch.cat([d0[k], d1[k]], dim=1 if d0[k].dim() > 1 else 0) for k in d0}
+    policy, r = dp_worker.wide_policy_and_rollout(glob, dev)
+    algo = PPO(policy, dev, None, batch_size=128, n_epochs=2, learning_rate=3e-4, ent_coef=0.01)
+    stats, norms, _ = algo.update(r)
+    np.testing.assert_allclose(n0, norms, rtol=1e-4)
+    np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=2e-6)
