@@ -97,10 +97,12 @@ class PPO:
         """Weak-scaling data parallelism: every rank owns its own env group and HBM rollout;
         a global minibatch is the union of the ranks' minibatch slices, gradients are summed
         over ranks with one RCCL all-reduce per optimizer step (rccl/xGMI via
-        torch.distributed), and every rank applies the identical clip+Adam step.  On the
-        fused MLP path the advantage normalisation uses global per-minibatch moments (one
-        small all-reduce per epoch), reproducing the reference's normalisation over the whole
-        (global) minibatch; the generic path normalises per rank."""
+        torch.distributed), and every rank applies the identical clip+Adam step.  The
+        advantage normalisation uses global per-minibatch moments (one small all-reduce per
+        epoch), reproducing the reference's normalisation over the whole (global) minibatch:
+        on the fused MLP path through the kernels' moments argument, on the per-minibatch path
+        through rai_ppo_hparams.ext_moments (single value column; multi-critic and
+        normalize-after-scaling configurations normalise per rank)."""
         import torch.distributed as dist
 
         self.dp_group = group
