@@ -4,9 +4,10 @@
 // rl_algo_impls/rollout/vec_rollout.py:88 (returns = advantages + values).
 //
 // Layout in HBM: rewards/values/adv/returns (T, C) fp32 with C = N*K columns,
-// episode_starts (T, N) u8.  A 512-thread block owns 64 consecutive columns (one
-// wave-wide, so every row load/store is a coalesced 256-B segment) and walks T
-// backwards in 64-row tiles:
+// episode_starts (T, N) u8.  A 512-thread block owns COLS consecutive columns (64: one
+// wave-wide coalesced 256-B row segment per load; 16 when C is small, so that the grid still
+// has a block per CU — at C2's 4096 columns 256 blocks instead of 64: 9.4 -> 5.9 us) and walks
+// T backwards in 64-row tiles:
 //   (1) all 8 waves hold 8 rows each in registers and write the carry-independent
 //       part delta_t (+ next_nonterminal) to LDS,
 //   (2) wave 0 runs the serial carry recurrence (two dependent FP64 ops per row,
@@ -23,6 +24,8 @@
 // multiply-add is fused differently from numpy.
 #include "common.h"
 
+#include <cstdlib>
+
 #pragma clang fp contract(off)
 
 namespace {
@@ -38,10 +41,12 @@ __device__ long long gae_stamps[8];
 #define GSTAMP(i) do { } while (0)
 #endif
 
-constexpr int GAE_COLS = 64;   // columns per block (one wave-wide row segment = 256 B)
 constexpr int GAE_WAVES = 8;   // 512 threads
 constexpr int GAE_TT = 64;     // rows per tile
 constexpr int RPW = GAE_TT / GAE_WAVES;  // rows per wave per tile
+// COLS columns per block: 64 (one wave-wide 256-B row segment per load) when there are enough
+// columns to fill the chip; 32 / 16 at smaller N (C2: 4096 columns are 64 blocks at 64 but 256 at
+// 16), a wave then covering 64 / COLS rows per load instruction.
 
 struct GaeArgs {
   const float* rewards;
@@ -90,16 +95,19 @@ struct Rows {
   uint8_t e[RPW];
 };
 
-template <typename Acc>
+template <typename Acc, int COLS>
 __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
-  __shared__ Acc delta_s[GAE_TT][GAE_COLS];  // delta_t, overwritten in place by the carry
-  __shared__ Acc coef_s[GAE_TT][GAE_COLS];   // (gamma*lambda) * next_nonterminal
+  __shared__ Acc delta_s[GAE_TT][COLS];  // delta_t, overwritten in place by the carry
+  __shared__ Acc coef_s[GAE_TT][COLS];   // (gamma*lambda) * next_nonterminal
+  constexpr int LPR = 64 / COLS;          // rows one wave instruction covers
 
-  const int lane = threadIdx.x & 63;
+  const int lane64 = threadIdx.x & 63;
+  const int lane = lane64 % COLS;         // column within the block
+  const int sub = lane64 / COLS;          // row within the instruction's row group
   // wave index made provably wave-uniform: row indices/addresses then live in SGPRs
   // (scalar base + per-lane column offset) instead of one 64-bit VGPR pair per row.
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t c = (int64_t)blockIdx.x * GAE_COLS + lane;
+  const int64_t c = (int64_t)blockIdx.x * COLS + lane;
   const bool valid = c < a.C;
   const int64_t cc = valid ? c : 0;
   const int64_t n = cc / a.K;
@@ -123,8 +131,8 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
   auto load = [&](Rows& R, int tile) {
     const int64_t lo = T - (int64_t)(tile + 1) * GAE_TT;
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      const int64_t t = lo + wave * RPW + j;
+    for (int j = 0; j < RPW / LPR; ++j) {
+      const int64_t t = lo + wave * RPW + j * LPR + sub;
       const int64_t tc = t < 0 ? 0 : t;
       const bool last = tc == T - 1;
       const float* vn_p = last ? next_values + cc : values + (tc + 1) * C + cc;
@@ -153,8 +161,8 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
     const int64_t lo = T - (int64_t)(tile + 1) * GAE_TT;
     // (1) carry-independent part of every row -> LDS
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      const int lr = wave * RPW + j;
+    for (int j = 0; j < RPW / LPR; ++j) {
+      const int lr = wave * RPW + j * LPR + sub;
       delta_s[lr][lane] = gae_delta<Acc>(cur.r[j], cur.v[j], cur.vn[j], cur.e[j], gvec, g32, g64);
       // gl * nn with nn in {0, 1} is exactly gl or +0.0 (gl > 0): a select, no multiply
       coef_s[lr][lane] = cur.e[j] ? (Acc)0 : gl;
@@ -164,7 +172,7 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
     GSTAMP(1);
     // (2) next tile's loads go out while wave 0 runs the serial recurrence
     if (!(GAE_DIAG & 4) && tile + 1 < ntiles) load(nxt, tile + 1);
-    if (!(GAE_DIAG & 1) && wave == 0) {
+    if (!(GAE_DIAG & 1) && wave == 0 && sub == 0) {
       // The only serial work: carry = delta + coef*carry (two dependent FP64 ops per row),
       // operands batched out of LDS, carries written back in place.  Rows with t < 0 (only in
       // the last-processed partial tile) lie below every valid row and are never stored.
@@ -205,8 +213,8 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
     GSTAMP(3);
     // (3) every wave stores its rows: adv and returns = adv + V (fp32), coalesced 256-B rows
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      const int lr = wave * RPW + j;
+    for (int j = 0; j < RPW / LPR; ++j) {
+      const int lr = wave * RPW + j * LPR + sub;
       const int64_t t = lo + lr;
       if (!(GAE_DIAG & 2) && t >= 0 && valid) {
         const float adv = (float)delta_s[lr][lane];
@@ -254,13 +262,23 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
     a.gamma32[k] = (float)gamma[kk];
     a.gl32[k] = (float)a.gl[k];
   }
-  const int64_t blocks = (a.C + GAE_COLS - 1) / GAE_COLS;
-  if (mode == RAI_GAE_EXACT)
-    hipLaunchKernelGGL(gae_kernel<double>, dim3((unsigned)blocks), dim3(GAE_WAVES * 64), 0,
-                       rai_stream(stream), a);
-  else
-    hipLaunchKernelGGL(gae_kernel<float>, dim3((unsigned)blocks), dim3(GAE_WAVES * 64), 0,
-                       rai_stream(stream), a);
+  // columns per block: the widest of 64 / 32 / 16 that still gives >= 256 blocks (one per CU)
+  int cols = 64;
+  if (const char* f = getenv("RAI_GAE_COLS")) cols = atoi(f);  // diagnostics (tools/gae_bench.py)
+  else if (a.C < 256LL * 64) cols = a.C < 256LL * 32 ? 16 : 32;
+  if (cols != 16 && cols != 32) cols = 64;
+  const int64_t blocks = (a.C + cols - 1) / cols;
+  const dim3 grid((unsigned)blocks), block(GAE_WAVES * 64);
+  hipStream_t st = rai_stream(stream);
+  if (mode == RAI_GAE_EXACT) {
+    if (cols == 16) hipLaunchKernelGGL((gae_kernel<double, 16>), grid, block, 0, st, a);
+    else if (cols == 32) hipLaunchKernelGGL((gae_kernel<double, 32>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((gae_kernel<double, 64>), grid, block, 0, st, a);
+  } else {
+    if (cols == 16) hipLaunchKernelGGL((gae_kernel<float, 16>), grid, block, 0, st, a);
+    else if (cols == 32) hipLaunchKernelGGL((gae_kernel<float, 32>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((gae_kernel<float, 64>), grid, block, 0, st, a);
+  }
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }
