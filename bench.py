@@ -185,9 +185,12 @@ def main():
     def traffic(kernel):
         return pmc.get(kernel, {}).get("traffic_bytes_per_launch")
 
-    roof_gae = {"kernel": "gae_kernel<double>", "bound": "hbm", "achieved": round(gae_bytes / (gae_us * 1e-6) / 1e9, 1),
+    # the instantiation rai_gae picks (csrc/gae.hip): columns per workgroup by column count
+    C = N * K
+    gae_name = "gae_kernel<double, %d>" % (64 if C >= 256 * 64 else (32 if C >= 256 * 32 else 16))
+    roof_gae = {"kernel": gae_name, "bound": "hbm", "achieved": round(gae_bytes / (gae_us * 1e-6) / 1e9, 1),
                 "peak": 8000.0, "unit": "GB/s", "frac": round(gae_bytes / (gae_us * 1e-6) / 1e9 / 8000.0, 4),
-                "traffic": traffic("gae_kernel<double>"), "avg_us": round(gae_us, 3), "bytes_per_launch": gae_bytes}
+                "traffic": traffic(gae_name), "avg_us": round(gae_us, 3), "bytes_per_launch": gae_bytes}
     if epoch_ms:
         # dominant kernel: one fused PPO epoch per launch = T*N samples of forward+backward at
         # SURVEY.md 8(d)'s 52,352 FLOP/sample (CartPole MLP, torch.utils.flop_counter), f32 MFMA peak

@@ -1,8 +1,7 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/exp && export TMPDIR=/tmp
-for c in 8 16 32; do
-  RAI_GAE_COLS=$c timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q --timeout 200 --timeout-method thread -k "gae" > gpurun_out/exp/pytest_gae_$c.log 2>&1 || { tail -20 gpurun_out/exp/pytest_gae_$c.log; exit 3; }
-  for cfg in cartpole halfcheetah; do
-    RAI_GAE_COLS=$c timeout -k 10 300 python -u bench.py --config $cfg --num-envs $([ $cfg = cartpole ] && echo 4096 || echo 2048) --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 400 > gpurun_out/exp/bench_gae_$c.log 2>&1 || exit 3
-    echo "cols=$c $cfg $(tail -1 gpurun_out/exp/bench_gae_$c.log | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['roofline_gae']['avg_us'], d['roofline_gae']['frac'])")"
-  done
-done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_dp.py tests/test_gpu_trainer.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_dp.log 2>&1; rc=$?
+tail -30 gpurun_out/pytest_dp.log | grep -v "^$" | tail -25
+[ $rc -eq 0 ] || exit 3
+timeout -k 10 250 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp/hcw_stats -o run -- python3 -u bench.py --config halfcheetah --num-envs 64 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/exp/hcw_stats.log 2>&1; echo "rc=$?"
+rm -f gpurun_out/exp/hcw_stats/run_kernel_trace.csv
+timeout -k 10 200 python -u bench.py --config halfcheetah --num-envs 256 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/exp/b_hc256w.log 2>&1; echo "rc=$?"; grep -v amdgpu.ids gpurun_out/exp/b_hc256w.log | cut -c1-220
