@@ -107,7 +107,14 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
   // wave index made provably wave-uniform: row indices/addresses then live in SGPRs
   // (scalar base + per-lane column offset) instead of one 64-bit VGPR pair per row.
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t c = (int64_t)blockIdx.x * COLS + lane;
+  // XCD-aware column groups: the dispatcher deals blocks round-robin over the 8 XCDs (block b ->
+  // XCD b % 8), so with the identity mapping the COLS-wide segments sharing one 128-B line of
+  // r / V / adv (and the 8-16 segments sharing a line of the u8 starts) land on different XCDs,
+  // each fetching the whole line into its own L2.  Remapped, XCD x owns a contiguous run of
+  // column groups and every line is fetched once.
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  const int grp = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int64_t c = (int64_t)grp * COLS + lane;
   const bool valid = c < a.C;
   const int64_t cc = valid ? c : 0;
   const int64_t n = cc / a.K;
