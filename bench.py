@@ -6,7 +6,7 @@ steps on the seeded synthetic CartPole-shaped VecEnv (host), GAE on device, and
 n_epochs x minibatches of fused loss / backward / clip+Adam — exactly the region
 the reference times as train/steps_per_second (rl_algo_impls/ppo/ppo.py:221,422-427).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config cartpole|pong|halfcheetah]
+    python bench.py [--gpus N --steps K --warmup W] [--config cartpole|pong|halfcheetah|microrts]
                     [--batch-policy yaml|scaled]
 
 Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), each rank
@@ -41,6 +41,22 @@ CONFIGS = {
                                     log_std_init=-2, init_layers_orthogonal=False),
                         algo=dict(batch_size=64, n_epochs=20, gamma=0.98, gae_lambda=0.92, ent_coef=0.000401762,
                                   max_grad_norm=0.8, vf_coef=0.58096, learning_rate=2.0633e-05, clip_range=0.1)),
+    # configs[4]: MicroRTS squnet-d16-128 GridNet selfplay, num_envs=512 (global; per-rank share under DP),
+    # n_steps=512 (ppo-Microrts.yml:274-299,511-558: Microrts-squnet-d16-128-sc-cos-ga-selfplay; first
+    # schedule phase :402-407); batch_size 6144 is the global minibatch (per rank 6144 / world)
+    "microrts": dict(env="microrts", num_envs=512, n_steps=512,
+                     policy=dict(actor_head_style="squeeze_unet", activation_fn="relu", cnn_flatten_dim=256,
+                                 channels_per_level=[128, 128, 128], strides_per_level=[[2, 2], [2, 2]],
+                                 deconv_strides_per_level=[[2, 2], [2, 2]],
+                                 encoder_residual_blocks_per_level=[3, 2, 4],
+                                 decoder_residual_blocks_per_level=[2, 3], increment_kernel_size_on_down_conv=True,
+                                 additional_critic_activation_functions=["tanh", "identity"],
+                                 subaction_mask={0: {1: 1, 2: 2, 3: 3, 4: 4, 5: 4, 6: 5}}),
+                     algo=dict(batch_size=6144, n_epochs=2, gamma=[0.99, 0.999, 0.999],
+                               gae_lambda=[0.95, 0.99, 0.99], clip_range=0.1, clip_range_vf=None,
+                               ppo2_vf_coef_halving=True, max_grad_norm=0.5, gradient_accumulation=True,
+                               multi_reward_weights=[0.8, 0.01, 0.19], vf_coef=[0.5, 0.1, 0.2], ent_coef=0.01,
+                               learning_rate=1e-4)),
 }
 
 
@@ -100,9 +116,13 @@ def main():
 
     cfg = CONFIGS[args.config]
     N, T = (args.num_envs or cfg["num_envs"]), cfg["n_steps"]
-    if args.config == "halfcheetah" and world > 1:
-        N = N // world  # configs[3] is quoted as a global env count across the node
     algo_kw = dict(cfg["algo"])
+    if args.config in ("halfcheetah", "microrts") and world > 1:
+        N = N // world  # configs[3] / configs[4] are quoted as a global env count across the node
+    if args.config == "microrts":
+        algo_kw["batch_size"] = max(1, algo_kw["batch_size"] // world)
+        if args.num_envs:  # rehearsal at fewer envs: keep the YAML's minibatches per epoch
+            algo_kw["batch_size"] = max(1, algo_kw["batch_size"] * N // cfg["num_envs"])
     if args.batch_policy == "scaled":
         algo_kw["batch_size"] = T * N // 4
     torch.manual_seed(1 + rank)
@@ -151,7 +171,7 @@ def main():
     # own HIP event pair on the stream it is launched on (torch's current stream = the stream passed
     # to rai_gae), so host launch overhead between launches is not counted as kernel time
     r = gen.rollout(gamma=algo.gamma, gae_lambda=algo.gae_lambda)
-    K = 1
+    K = int(r.values.shape[2]) if r.values.dim() > 2 else 1
     gae_bytes = (4 * T * N * K) * 4 + T * N + 4 * N * K + N  # r, V, adv, returns + starts + next V/starts
     adv = torch.empty_like(r.values)
     ret = torch.empty_like(r.values)

@@ -48,6 +48,24 @@ class Discrete:
         return np.int64(rng.integers(self.n))
 
 
+class MultiDiscrete:
+    def __init__(self, nvec):
+        self.nvec = np.asarray(nvec, dtype=np.int64)
+        self.shape = self.nvec.shape
+        self.dtype = np.dtype(np.int64)
+
+    def sample(self, rng: Optional[np.random.Generator] = None):
+        rng = rng or np.random.default_rng()
+        return rng.integers(0, self.nvec)
+
+
+MICRORTS_NVEC = (6, 4, 4, 4, 4, 7, 49)  # MicroRTS per-cell action planes (78 logits)
+
+
+def is_multidiscrete(space) -> bool:
+    return hasattr(space, "nvec")
+
+
 def is_discrete(space) -> bool:
     return hasattr(space, "n") and not hasattr(space, "nvec")
 
@@ -65,6 +83,11 @@ class SyntheticVecEnv:
                        termination ~ Bernoulli(1/1000)
     kind = "halfcheetah": obs ~ N(0,1) f32 (N,17), Box(6) actions in [-1,1],
                        reward ~ N(0,1), termination ~ Bernoulli(1/1000)
+    kind = "microrts": obs ~ U{0,1} f32 (N,74,16,16) (CHW planes), GridNet actions
+                       MultiDiscrete(tile(nvec, 256)) with action_plane_space
+                       MultiDiscrete([6,4,4,4,4,7,49]), all-true action masks (N,256,78) from
+                       get_action_mask(), K=3 rewards ~ N(0,1) (N,3), termination ~ Bernoulli(1/1000)
+                       
     Truncations are always False (the reference treats them like terminations).
 
     Observation batches are drawn from a pool of `obs_pool` batches generated at construction
@@ -92,6 +115,15 @@ class SyntheticVecEnv:
             self.single_observation_space = Box(-np.inf, np.inf, (17,), np.float32)
             self.single_action_space = Box(-1.0, 1.0, (6,), np.float32)
             self.term_prob = 1 / 1000 if term_prob is None else term_prob
+        elif kind == "microrts":
+            self.map_hw = (16, 16)
+            cells = self.map_hw[0] * self.map_hw[1]
+            self.single_observation_space = Box(0.0, 1.0, (74,) + self.map_hw, np.float32)
+            self.action_plane_space = MultiDiscrete(MICRORTS_NVEC)
+            self.single_action_space = MultiDiscrete(np.tile(MICRORTS_NVEC, cells))
+            self.term_prob = 1 / 1000 if term_prob is None else term_prob
+            self._mask = np.ones((self.num_envs, cells, int(sum(MICRORTS_NVEC))), dtype=np.bool_)
+            self.get_action_mask = lambda: self._mask
         else:
             raise ValueError(f"unknown synthetic env kind {kind}")
         batch_bytes = self.num_envs * int(np.prod(self.single_observation_space.shape)) * \
@@ -112,6 +144,8 @@ class SyntheticVecEnv:
         shp = self.single_observation_space.shape
         if self.kind == "pong":
             return self.rng.integers(0, 256, size=(N,) + shp, dtype=np.uint8)
+        if self.kind == "microrts":
+            return (self.rng.random((N,) + shp, dtype=np.float32) < 0.5).astype(np.float32)
         return self.rng.standard_normal((N,) + shp, dtype=np.float32)
 
     def reset(self, **kwargs) -> Tuple[np.ndarray, Dict[str, Any]]:
@@ -122,6 +156,8 @@ class SyntheticVecEnv:
         obs = self._obs()
         if self.kind == "cartpole":
             rew = np.ones(N, dtype=np.float32)
+        elif self.kind == "microrts":
+            rew = self.rng.standard_normal((N, 3), dtype=np.float32)
         else:
             rew = self.rng.standard_normal(N, dtype=np.float32)
         term = self.rng.random(N) < self.term_prob

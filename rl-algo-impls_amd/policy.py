@@ -278,22 +278,49 @@ class ActorCritic(nn.Module):
     def __init__(self, env, pi_hidden_sizes=None, v_hidden_sizes=None, init_layers_orthogonal=True,
                  activation_fn="tanh", log_std_init=-0.5, use_sde=False, full_std=True, squash_output=False,
                  share_features_extractor=True, cnn_flatten_dim=512, cnn_style="nature",
-                 cnn_layers_init_orthogonal=None, actor_head_style="single", **kwargs):
+                 cnn_layers_init_orthogonal=None, actor_head_style="single", critic_channels=64,
+                 num_additional_critics=0, additional_critic_activation_functions=None, channels_per_level=None,
+                 strides_per_level=None, deconv_strides_per_level=None, encoder_residual_blocks_per_level=None,
+                 decoder_residual_blocks_per_level=None, increment_kernel_size_on_down_conv=False,
+                 output_activation_fn="identity", subaction_mask=None, critic_shares_backbone=None,
+                 save_critic_separate=None, shared_critic_head=None, normalization=None, **kwargs):
         super().__init__()
         if use_sde or squash_output:
             raise NotImplementedError("gSDE / squash_output are outside the hot-path scope")
         if not share_features_extractor:
             raise NotImplementedError("SeparateActorCriticNetwork is outside the hot-path scope")
-        if actor_head_style != "single":
+        if actor_head_style not in ("single", "squeeze_unet"):
             raise NotImplementedError(f"actor_head_style={actor_head_style} is outside the hot-path scope")
         self.env = env
         self.action_space = env.single_action_space
         self.observation_space = env.single_observation_space
         self.squash_output = squash_output
-        self.network = ConnectedTrioNetwork(env.single_observation_space, env.single_action_space,
-                                            pi_hidden_sizes, v_hidden_sizes, init_layers_orthogonal,
-                                            activation_fn, log_std_init, cnn_flatten_dim, cnn_style,
-                                            cnn_layers_init_orthogonal)
+        self.gridnet = actor_head_style == "squeeze_unet"
+        if self.gridnet:  # actor_critic.py:200-229 (MicroRTS, config C5)
+            from .backbone import SqueezeUnetActorCriticNetwork
+
+            plane = getattr(env, "action_plane_space", None)
+            assert plane is not None, "squeeze_unet needs the env's action_plane_space"
+            self.network = SqueezeUnetActorCriticNetwork(
+                env.single_observation_space, env.single_action_space, plane,
+                init_layers_orthogonal=init_layers_orthogonal, cnn_layers_init_orthogonal=cnn_layers_init_orthogonal,
+                num_additional_critics=num_additional_critics,
+                additional_critic_activation_functions=additional_critic_activation_functions,
+                critic_channels=critic_channels, channels_per_level=channels_per_level,
+                strides_per_level=strides_per_level, deconv_strides_per_level=deconv_strides_per_level,
+                encoder_residual_blocks_per_level=encoder_residual_blocks_per_level,
+                decoder_residual_blocks_per_level=decoder_residual_blocks_per_level,
+                increment_kernel_size_on_down_conv=increment_kernel_size_on_down_conv,
+                output_activation_fn=output_activation_fn, subaction_mask=subaction_mask,
+                critic_shares_backbone=critic_shares_backbone if critic_shares_backbone is not None else True,
+                save_critic_separate=save_critic_separate if save_critic_separate is not None else False,
+                shared_critic_head=shared_critic_head if shared_critic_head is not None else False,
+                normalization=normalization)
+        else:
+            self.network = ConnectedTrioNetwork(env.single_observation_space, env.single_action_space,
+                                                pi_hidden_sizes, v_hidden_sizes, init_layers_orthogonal,
+                                                activation_fn, log_std_init, cnn_flatten_dim, cnn_style,
+                                                cnn_layers_init_orthogonal)
         self._device: Optional[torch.device] = None
         # policy.py:31-36: the env's normalisation statistics travel with the checkpoint
         from .wrappers import NormalizeObservation, NormalizeReward, find_wrapper
@@ -318,15 +345,15 @@ class ActorCritic(nn.Module):
 
     @property
     def action_shape(self) -> Tuple[int, ...]:
-        return self.network._pi.action_shape
+        return self.network.action_shape if self.gridnet else self.network._pi.action_shape
 
     @property
     def value_shape(self) -> Tuple[int, ...]:
-        return ()
+        return self.network.value_shape if self.gridnet else ()
 
     @property
     def is_discrete(self) -> bool:
-        return isinstance(self.network._pi, CategoricalActorHead)
+        return not self.gridnet and isinstance(self.network._pi, CategoricalActorHead)
 
     def forward(self, obs, action, action_masks=None) -> ACForward:
         return ACForward(*self.network(obs, action, action_masks))
@@ -343,6 +370,12 @@ class ActorCritic(nn.Module):
         rollout uses the HBM-resident path in rollout.py instead."""
         with torch.no_grad():
             o = self._as_tensor(obs)
+            if self.gridnet:  # backbone_actor_critic.py:194-223 via actor_critic.py:306-318
+                pi, v = self.network.distribution_and_value(o, self._as_tensor(action_masks))
+                a = pi.sample()
+                logp = pi.log_prob(a)
+                a_np = a.cpu().numpy()
+                return Step(a_np, v.cpu().numpy(), logp.cpu().numpy(), a_np)
             params, v = self.network.dist_params_and_value(o)
             if self.is_discrete:
                 m = self._as_tensor(action_masks) if action_masks is not None else None
@@ -361,6 +394,9 @@ class ActorCritic(nn.Module):
             return self.step(obs, action_masks=action_masks).clamped_a
         with torch.no_grad():
             o = self._as_tensor(obs)
+            if self.gridnet:
+                pi, _ = self.network.distribution_and_value(o, self._as_tensor(action_masks))
+                return pi.mode.cpu().numpy()
             params, _ = self.network.dist_params_and_value(o)
             m = self._as_tensor(action_masks) if action_masks is not None else None
             a = self.network._pi.mode(params, m)
@@ -415,6 +451,12 @@ class ActorCritic(nn.Module):
         return sum(p.numel() for p in self.parameters())
 
     def freeze(self, freeze_policy_head: bool, freeze_value_head: bool, freeze_backbone: bool = True) -> None:
+        if self.gridnet:  # backbone_actor_critic.py:254-265
+            for mod, frz in ((self.network.actor_head, freeze_policy_head),
+                             (self.network.critic_heads, freeze_value_head), (self.network.backbone, freeze_backbone)):
+                for p in mod.parameters():
+                    p.requires_grad = not frz
+            return
         for p in self.network._pi.parameters():
             p.requires_grad = not freeze_policy_head
         for p in self.network._v.parameters():

@@ -256,8 +256,12 @@ class SyncStepRolloutGenerator(RolloutGenerator):
                                   rolling_num_envs_reset_every_prepare_step, 0)] if v != d]
         if bad or subaction_mask or full_batch_off_accelerator:
             raise NotImplementedError(f"rollout options outside the hot-path scope: {bad or 'subaction_mask/full_batch_off_accelerator'}")
-        if getattr(vec_env, "get_action_mask", None) is not None:
-            raise NotImplementedError("action-masked envs (MicroRTS/Lux) are outside the hot-path scope")
+        self.gridnet = bool(getattr(policy, "gridnet", False))
+        self.get_action_mask = getattr(vec_env, "get_action_mask", None)
+        if self.get_action_mask is not None and not self.gridnet:
+            raise NotImplementedError("action masks are on the hot path for GridNet (squeeze_unet) policies only")
+        if self.gridnet and self.get_action_mask is None:
+            raise AssertionError("GridNet policies need the env's get_action_mask()")
         self.n_steps = n_steps
         self.include_logp = include_logp
         self.scale_advantage_by_values_accuracy = scale_advantage_by_values_accuracy
@@ -277,14 +281,23 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         tdt = lambda d: torch.from_numpy(np.zeros((), dtype=d)).dtype
         self.obs_dtype = tdt(obs_space.dtype)
         self.discrete = is_discrete(act_space)
-        if not (self.discrete or is_box(act_space)):
+        if not (self.discrete or is_box(act_space) or self.gridnet):
             raise NotImplementedError(f"action space {act_space} is outside the hot-path scope")
-        self.act_shape = () if self.discrete else tuple(act_space.shape)
-        act_dtype = torch.int64 if self.discrete else torch.float32
+        # GridNet (MicroRTS): per-position actions (map cells, planes) i64, K critic columns
+        self.act_shape = tuple(policy.action_shape) if self.gridnet else (() if self.discrete else
+                                                                          tuple(act_space.shape))
+        act_dtype = torch.int64 if (self.discrete or self.gridnet) else torch.float32
+        vshape = tuple(policy.value_shape)
         self.obs = torch.zeros((T, N) + tuple(obs_space.shape), dtype=self.obs_dtype, device=dev)
-        self.rewards = torch.zeros((T, N), dtype=torch.float32, device=dev)
+        self.rewards = torch.zeros((T, N) + vshape, dtype=torch.float32, device=dev)
         self.episode_starts = torch.zeros((T, N), dtype=torch.bool, device=dev)
-        self.values = torch.zeros((T, N), dtype=torch.float32, device=dev)
+        self.values = torch.zeros((T, N) + vshape, dtype=torch.float32, device=dev)
+        self.action_masks = None
+        if self.gridnet:  # sync_step_rollout.py:119-131: (T, N, cells, sum(nvec)) bool
+            m0 = np.asarray(self.get_action_mask())
+            self.action_masks = torch.zeros((T,) + m0.shape, dtype=torch.bool, device=dev)
+            self.h_mask = torch.zeros(m0.shape, dtype=torch.bool).pin_memory()
+            self.next_masks_dev = torch.zeros(m0.shape, dtype=torch.bool, device=dev)
         self.logprobs = torch.zeros((T, N), dtype=torch.float32, device=dev)
         self.actions = torch.zeros((T, N) + self.act_shape, dtype=act_dtype, device=dev)
         self.clamped = torch.zeros((N,) + self.act_shape, dtype=act_dtype, device=dev)
@@ -293,7 +306,7 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             self.act_high = torch.as_tensor(np.asarray(act_space.high, np.float32), device=dev)
         # pinned host staging (H2D obs/rewards/dones, D2H actions)
         self.h_obs = torch.zeros((N,) + tuple(obs_space.shape), dtype=self.obs_dtype).pin_memory()
-        self.h_rew = torch.zeros((N,), dtype=torch.float32).pin_memory()
+        self.h_rew = torch.zeros((N,) + vshape, dtype=torch.float32).pin_memory()
         self.h_done = torch.zeros((N,), dtype=torch.bool).pin_memory()
         self.h_act = torch.zeros((N,) + self.act_shape, dtype=act_dtype).pin_memory()
         self.next_obs_dev = torch.zeros((N,) + tuple(obs_space.shape), dtype=self.obs_dtype, device=dev)
@@ -313,6 +326,21 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             self.fused_step = spec
         obs, _ = vec_env.reset()
         self._stage_obs(obs)
+        self._stage_masks()
+
+    def _stage_masks(self) -> None:
+        if self.action_masks is not None:
+            np.copyto(self.h_mask.numpy(), np.asarray(self.get_action_mask()))
+            self.next_masks_dev.copy_(self.h_mask, non_blocking=True)
+
+    def _gridnet_step(self, s: int) -> None:
+        """backbone_actor_critic.py:194-223 + gridnet.py sample: per-position actions, the fused
+        GridNet log-prob kernel, K critic values, written into slot s."""
+        pi, v = self.policy.network.distribution_and_value(self.obs[s], self.action_masks[s])
+        a = pi.sample()
+        self.actions[s].copy_(a.view(self.actions[s].shape))
+        self.logprobs[s].copy_(pi.log_prob(a))
+        self.values[s].copy_(v)
 
     def _layer_ptrs(self):
         ps = [p.detach() for p in self.policy.parameters()]
@@ -371,12 +399,16 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         for s in range(self.n_steps):
             self.obs[s].copy_(self.next_obs_dev)
             self.episode_starts[s].copy_(self.next_episode_starts)
+            if self.action_masks is not None:
+                self.action_masks[s].copy_(self.next_masks_dev)
             if self.fused_step is not None:
                 self._fused_step(s)
+            elif self.gridnet:
+                self._gridnet_step(s)
             else:
                 params, v = net.dist_params_and_value(self.obs[s])
                 self._sample(params, v, s)
-            src = self.actions[s] if self.discrete else self.clamped
+            src = self.actions[s] if (self.discrete or self.gridnet) else self.clamped
             self.h_act.copy_(src, non_blocking=True)
             self._act_ready.record()
             self._act_ready.synchronize()
@@ -390,6 +422,7 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             self.rewards[s].copy_(self.h_rew, non_blocking=True)
             self.next_episode_starts.copy_(self.h_done, non_blocking=True)
             self._stage_obs(obs)
+            self._stage_masks()
         next_values = None
         if output_next_values:
             if self.fused_step is not None:
@@ -405,6 +438,6 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         next_values = self._rollout(output_next_values=True)
         return DeviceRollout(
             self.device, self.next_episode_starts.clone(), next_values, self.obs, self.actions, self.rewards,
-            self.episode_starts, self.values, self.logprobs if self.include_logp else None, None, gamma,
+            self.episode_starts, self.values, self.logprobs if self.include_logp else None, self.action_masks, gamma,
             gae_lambda, self.scale_advantage_by_values_accuracy, self.gae_mode, self.perm_source,
             self.generator)

@@ -1,0 +1,189 @@
+"""Squeeze-U-Net GridNet actor-critic (BASELINE config C5) against the reference
+network run in this container (tests/golden/squnet_cases.npz, tests/golden/make_golden_squnet.py):
+
+  * CPU: the full-width C5 network's state_dict keys, shapes and parameter count (5,458,513);
+    seeded initialisation bit-identical to the reference's (same module construction order);
+    the critic values (torch CPU both sides, rtol 1e-5);
+  * GPU: forward (backbone on MIOpen, GridNet log-prob/entropy on the fused HIP kernel) and the
+    parameter gradients of sum(wl*logp + we*entropy + wv.v) against the reference's CPU autograd.
+    Tolerance (fp32 convolutions on different engines, 20+ layers deep): logp / entropy sums over
+    256 cells x 7 planes rtol 1e-4 atol 2e-3; values rtol 1e-4 atol 1e-5; gradients
+    atol 2e-4 + rtol 2e-3 of each tensor's max |grad|.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+NVEC = np.array([6, 4, 4, 4, 4, 7, 49])
+SUB = {0: {1: 1, 2: 2, 3: 3, 4: 4, 5: 4, 6: 5}}
+C5_KW = dict(strides_per_level=[[2, 2], [2, 2]], deconv_strides_per_level=[[2, 2], [2, 2]],
+             encoder_residual_blocks_per_level=[3, 2, 4], decoder_residual_blocks_per_level=[2, 3],
+             increment_kernel_size_on_down_conv=True, additional_critic_activation_functions=["tanh", "identity"],
+             subaction_mask=SUB, init_layers_orthogonal=True)
+
+
+@pytest.fixture(scope="module")
+def cases():
+    return np.load(GOLDEN / "squnet_cases.npz", allow_pickle=False)
+
+
+def _net(width, critic_channels=64, seed=None):
+    from rl_algo_impls_amd.backbone import SqueezeUnetActorCriticNetwork
+    from rl_algo_impls_amd.envs import Box, MultiDiscrete
+
+    obs = Box(0.0, 1.0, (74, 16, 16), np.float32)
+    if seed is not None:
+        torch.manual_seed(seed)
+    return SqueezeUnetActorCriticNetwork(obs, MultiDiscrete(np.tile(NVEC, 256)), MultiDiscrete(NVEC),
+                                         channels_per_level=[width] * 3, critic_channels=critic_channels, **C5_KW)
+
+
+def test_c5_state_dict_keys_shapes(cases):
+    net = _net(128)
+    sd = net.state_dict()
+    assert list(sd.keys()) == [str(k) for k in cases["c5_keys"]]
+    assert [",".join(map(str, v.shape)) for v in sd.values()] == [str(s) for s in cases["c5_shapes"]]
+    assert sum(v.numel() for v in sd.values()) == int(cases["c5_num_params"]) == 5458513
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_seeded_init_bit_identical(cases, i):
+    seed, width, _ = (int(x) for x in cases[f"c{i}_meta"])
+    net = _net(width, critic_channels=16, seed=seed)
+    for k, v in net.state_dict().items():
+        np.testing.assert_array_equal(v.numpy(), cases[f"c{i}_init/{k}"], err_msg=k)
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_values_cpu(cases, i):
+    seed, width, _ = (int(x) for x in cases[f"c{i}_meta"])
+    net = _net(width, critic_channels=16, seed=seed)
+    with torch.no_grad():
+        v = net.value(torch.tensor(cases[f"c{i}_obs"]))
+    np.testing.assert_allclose(v.numpy(), cases[f"c{i}_value"], rtol=1e-5, atol=1e-6)
+
+
+def test_actor_critic_builds_squeeze_unet_policy():
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    env = SyntheticVecEnv(2, kind="microrts", obs_pool=2)
+    pol = ActorCritic(env, actor_head_style="squeeze_unet", channels_per_level=[16, 16, 16], **{
+        k: v for k, v in C5_KW.items() if k != "init_layers_orthogonal"})
+    assert pol.action_shape == (256, 7) and pol.value_shape == (3,) and not pol.is_discrete
+    assert any(k.startswith("network.backbone.encoders.0.0.") for k in pol.state_dict())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", [0, 1])
+def test_forward_backward_vs_reference(cases, i):
+    dev = torch.device("cuda", 0)
+    seed, width, _ = (int(x) for x in cases[f"c{i}_meta"])
+    net = _net(width, critic_channels=16, seed=seed).to(dev)
+    obs = torch.tensor(cases[f"c{i}_obs"], device=dev)
+    acts = torch.tensor(cases[f"c{i}_actions"], device=dev)
+    masks = torch.tensor(cases[f"c{i}_masks"], device=dev)
+    logp, ent, v = net(obs, acts, action_masks=masks)
+    np.testing.assert_allclose(logp.detach().cpu().numpy(), cases[f"c{i}_logp"], rtol=1e-4, atol=2e-3)
+    np.testing.assert_allclose(ent.detach().cpu().numpy(), cases[f"c{i}_entropy"], rtol=1e-4, atol=2e-3)
+    np.testing.assert_allclose(v.detach().cpu().numpy(), cases[f"c{i}_v"], rtol=1e-4, atol=1e-5)
+    t = lambda k: torch.tensor(cases[f"c{i}_{k}"], device=dev)
+    ((t("wl") * logp).sum() + (t("we") * ent).sum() + (t("wv") * v).sum()).backward()
+    for k, p in net.named_parameters():
+        ref = cases[f"c{i}_grad/{k}"]
+        tol = 2e-4 + 2e-3 * float(np.abs(ref).max())
+        np.testing.assert_allclose(p.grad.cpu().numpy(), ref, rtol=0, atol=tol, err_msg=k)
+
+
+class _FixedRollout:
+    def __init__(self, batches):
+        self.batches = batches
+
+    @property
+    def total_steps(self):
+        return sum(len(b) for b in self.batches)
+
+    def num_minibatches(self, bs):
+        return len(self.batches)
+
+    def minibatches(self, bs, shuffle=True):
+        return iter(self.batches)
+
+    def explained_variance(self):
+        y = torch.cat([b.returns for b in self.batches]).double()
+        p = torch.cat([b.values for b in self.batches]).double()
+        return float(1 - torch.var(y - p, unbiased=False) / torch.var(y, unbiased=False))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["sq_c5_gradacc", "sq_steps_vclip"])
+def test_ppo_update_matches_reference(name):
+    """The C5 update path (squeeze-U-Net on MIOpen, fused GridNet head, rai_ppo_loss with K=3 critics
+    and multi_reward_weights, clip + Adam) against the reference's PPO.learn_epoch on the same
+    minibatches (tests/golden/squnet_ppo_steps.npz).  Tolerance: stats rtol 5e-4; parameters
+    atol 0.05 * lr (Adam's first steps move every parameter by ~lr * g / |g|, so a conv-gradient
+    entry near zero may differ in sign between the CPU reference and MIOpen); grad norms rtol 5e-4."""
+    import json
+
+    from make_golden_networks import load_flat
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import Batch
+
+    dev = torch.device("cuda", 0)
+    z = np.load(GOLDEN / "squnet_ppo_steps.npz", allow_pickle=False)
+    meta = json.loads(str(z["index"]))[name]
+    env = SyntheticVecEnv(1, kind="microrts", obs_pool=2)
+    pol = ActorCritic(env, actor_head_style="squeeze_unet", channels_per_level=[meta["width"]] * 3,
+                      critic_channels=16, **{k: v for k, v in C5_KW.items() if k != "init_layers_orthogonal"})
+    load_flat(pol, z[f"{name}/init"])
+    pol = pol.to(dev)
+    kw = dict(meta["kw"])
+    algo = PPO(pol, dev, None, **kw)
+    bs = []
+    for i in range(meta["n"]):
+        t = lambda k: torch.from_numpy(z[f"{name}/b{i}_{k}"]).to(dev)
+        bs.append(Batch(t("obs"), t("logprobs"), t("actions"), t("action_masks"), None, t("values"),
+                        t("advantages"), t("returns")))
+    stats, norms, K = algo.update(_FixedRollout(bs))
+    assert K == 3
+    ref = z[f"{name}/stats"]
+    np.testing.assert_allclose(stats[:, :5], ref[:, :5], rtol=5e-4, atol=2e-6)
+    np.testing.assert_allclose(stats[:, 5:8], ref[:, 5:8], rtol=5e-4, atol=2e-6)
+    np.testing.assert_allclose(norms, z[f"{name}/norms"], rtol=5e-4)
+    np.testing.assert_allclose(algo.flat.flat.cpu().numpy(), z[f"{name}/params"][-1], rtol=0,
+                               atol=0.05 * float(kw["learning_rate"]))
+    assert float(algo.optimizer.state_dict()["state"][0]["step"]) == meta["opt_step"]
+
+
+@pytest.mark.gpu
+def test_microrts_training_end_to_end(tmp_path):
+    """Rollout (per-position GridNet sampling under all-true masks, K=3 rewards and values) + GAE
+    with vector gamma + the C5 update with gradient accumulation; checkpoint round trip."""
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1)
+    env = SyntheticVecEnv(4, kind="microrts", seed=1, obs_pool=2)
+    pol = ActorCritic(env, actor_head_style="squeeze_unet", channels_per_level=[16, 16, 16],
+                      **{k: v for k, v in C5_KW.items() if k != "init_layers_orthogonal"}).to(dev)
+    gen = SyncStepRolloutGenerator(pol, env, n_steps=8)
+    algo = PPO(pol, dev, None, batch_size=8, n_epochs=2, gamma=[0.99, 0.999, 0.999], gae_lambda=[0.95, 0.99, 0.99],
+               clip_range=0.1, clip_range_vf=None, ppo2_vf_coef_halving=True, gradient_accumulation=True,
+               multi_reward_weights=[0.8, 0.01, 0.19], vf_coef=[0.5, 0.1, 0.2], ent_coef=0.01, learning_rate=1e-4)
+    algo.learn(2 * 8 * 4, gen)
+    ts = algo.last_train_stats
+    assert np.isfinite([ts.loss, ts.pi_loss, ts.entropy_loss, ts.approx_kl, ts.grad_norm]).all()
+    assert gen.actions.shape == (8, 4, 256, 7) and gen.values.shape == (8, 4, 3)
+    nvec = torch.tensor(NVEC, device=dev)
+    assert bool((gen.actions >= 0).all()) and bool((gen.actions < nvec).all())
+    assert bool(torch.isfinite(gen.logprobs).all())
+    pol.save(str(tmp_path))
+    sd = torch.load(tmp_path / "model.pth", weights_only=True)
+    assert set(sd) == set(pol.state_dict())
