@@ -483,7 +483,7 @@ def mlp_actor_critic_spec(pol) -> Optional[dict]:
     rai_mlp_policy_step): an ActorCritic with a Flatten encoder, separate [in -> 64 -> 64 -> out]
     actor and critic MLPs (tanh or relu), a Categorical head, in_dim <= 8, n_actions <= 8,
     parameters() in the order actor W1,b1,W2,b2,W3,b3 then critic.  None otherwise."""
-    if not isinstance(pol, ActorCritic):
+    if not isinstance(pol, ActorCritic) or pol.gridnet:
         return None
     net = pol.network
     if net._feature_extractor.kind != "flat" or not isinstance(net._pi, CategoricalActorHead):

@@ -301,7 +301,7 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         self.logprobs = torch.zeros((T, N), dtype=torch.float32, device=dev)
         self.actions = torch.zeros((T, N) + self.act_shape, dtype=act_dtype, device=dev)
         self.clamped = torch.zeros((N,) + self.act_shape, dtype=act_dtype, device=dev)
-        if not self.discrete:
+        if not (self.discrete or self.gridnet):
             self.act_low = torch.as_tensor(np.asarray(act_space.low, np.float32), device=dev)
             self.act_high = torch.as_tensor(np.asarray(act_space.high, np.float32), device=dev)
         # pinned host staging (H2D obs/rewards/dones, D2H actions)
