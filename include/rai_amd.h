@@ -115,6 +115,15 @@ int rai_gridnet_logp_entropy(const float* logits, const uint8_t* mask, const int
 int rai_gridnet_backward(const float* logits, const uint8_t* mask, const int64_t* actions, int64_t B, int32_t C,
                          int32_t G, const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val,
                          const float* d_logp, const float* d_entropy, float* d_logits, void* stream);
+/* Rollout sampling of the same head: GridnetDistribution.sample() + log_prob(sample)
+ * (rl_algo_impls/shared/actor/gridnet.py:195-205 then :101-160, as called by
+ * actor_critic.py:306-318 / sync_step_rollout.py:193-201).  Each (cell, plane) draws from its
+ * masked categorical by inverse CDF on Philox4x32-10 keyed (seed; counter (offset,
+ * (b*C + c)*G + g)); a plane with no valid action draws uniformly over all its n values
+ * (torch's equal finfo.min logits).  actions_out (B, C, G) int64; logp_out (B,) or NULL. */
+int rai_gridnet_sample(const float* logits, const uint8_t* mask, int64_t B, int32_t C, int32_t G,
+                       const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val, uint64_t seed,
+                       uint64_t offset, int64_t* actions_out, float* logp_out, void* stream);
 
 /* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.

@@ -32,6 +32,8 @@ struct GridArgs {
   const float* logits;
   const uint8_t* mask;
   const int64_t* actions;
+  int64_t* actions_out;  // sample mode
+  uint64_t seed, offset;
   const float* d_logp;
   const float* d_ent;
   float* logp;
@@ -157,6 +159,84 @@ __global__ __launch_bounds__(GN_THREADS) void gridnet_kernel(const GridArgs a) {
   }
 }
 
+// Rollout sampling (gridnet.py:195-205 sample() + log_prob): every (cell, group) draws its action
+// from its masked categorical by inverse CDF on a Philox4x32-10 uniform keyed (seed; counter
+// (offset, item)), item = (b * C + c) * G + g; a group with no valid action samples uniformly over
+// all n (torch: equal finfo.min logits).  Then, after the tile's actions are in LDS, the log-prob of
+// the sampled action under the same gating as log_prob (the ValueDependentMask reads the cell's
+// other sampled planes).  One workgroup per sample, 64-cell tiles as in the forward.
+__global__ __launch_bounds__(GN_THREADS) void gridnet_sample_kernel(const GridArgs a) {
+  extern __shared__ float smem[];
+  const int A = a.A, G = a.G, C = a.C;
+  float* zt = smem;                                                     // [GN_CELLS][A]
+  uint8_t* mt = reinterpret_cast<uint8_t*>(smem + GN_CELLS * A);       // [GN_CELLS][A]
+  __shared__ int act_s[GN_CELLS * RAI_GRID_MAX_G];
+  __shared__ double red[GN_THREADS / 64];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  double acc_lp = 0.0;
+  for (int c0 = 0; c0 < C; c0 += GN_CELLS) {
+    const int nc = min(GN_CELLS, C - c0);
+    const int64_t base = (b * C + c0) * (int64_t)A;
+    const int span = nc * A;
+    for (int i = tid; i < span; i += GN_THREADS) {
+      zt[i] = a.logits[base + i];
+      mt[i] = a.mask[base + i];
+    }
+    __syncthreads();
+    const int items = nc * G;
+    for (int it = tid; it < items; it += GN_THREADS) {
+      const int cl = it / G, g = it - cl * G;
+      const int o = a.off[g], n = a.off[g + 1] - o;
+      const float* z = zt + cl * A + o;
+      const uint8_t* m = mt + cl * A + o;
+      float mx = GN_NEG;
+      for (int j = 0; j < n; ++j) mx = fmaxf(mx, m[j] ? z[j] : GN_NEG);
+      float tot = 0.f;
+      for (int j = 0; j < n; ++j) tot += expf((m[j] ? z[j] : GN_NEG) - mx);
+      const uint64_t item = (uint64_t)((b * C + c0 + cl) * (int64_t)G + g);
+      const Philox4 r = philox4x32_10(a.offset, item, a.seed);
+      const float target = u01_open0(r.x) * tot;
+      int pick = -1, last = 0;
+      float cum = 0.f;
+      for (int j = 0; j < n; ++j) {
+        const float pj = expf((m[j] ? z[j] : GN_NEG) - mx);
+        if (pj > 0.f) last = j;
+        cum += pj;
+        if (pick < 0 && cum >= target && pj > 0.f) pick = j;
+      }
+      if (pick < 0) pick = last;  // rounding at the top of the CDF
+      act_s[cl * G + g] = pick;
+      a.actions_out[(b * C + c0 + cl) * (int64_t)G + g] = pick;
+    }
+    __syncthreads();
+    for (int it = tid; it < items; it += GN_THREADS) {
+      const int cl = it / G, g = it - cl * G;
+      const int o = a.off[g], n = a.off[g + 1] - o;
+      const float* z = zt + cl * A + o;
+      const uint8_t* m = mt + cl * A + o;
+      const int ref = a.sub_ref[g];
+      const bool gate = ref < 0 || act_s[cl * G + ref] == a.sub_val[g];
+      if (gate) {
+        const GroupStats st = group_stats(z, m, n);
+        const int ag = act_s[cl * G + g];
+        const float za = m[ag] ? z[ag] : GN_NEG;
+        acc_lp += (double)(st.nvalid > 0 ? za - st.lse : 0.f);
+      }
+    }
+    __syncthreads();
+  }
+  const int lane = tid & 63, w = tid >> 6;
+  acc_lp = wave_sum(acc_lp);
+  if (lane == 0) red[w] = acc_lp;
+  __syncthreads();
+  if (tid == 0) {
+    double lp = 0.0;
+    for (int i = 0; i < GN_THREADS / 64; ++i) lp += red[i];
+    if (a.logp) a.logp[b] = (float)lp;
+  }
+}
+
 int setup(GridArgs& a, const float* logits, const uint8_t* mask, const int64_t* actions, int64_t B, int32_t C,
           int32_t G, const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val) {
   if (B < 0 || C < 1 || G < 1) return RAI_E_SHAPE;
@@ -220,6 +300,25 @@ extern "C" int rai_gridnet_backward(const float* logits, const uint8_t* mask, co
   a.d_ent = d_entropy;
   a.d_logits = d_logits;
   hipLaunchKernelGGL(gridnet_kernel<true>, dim3((unsigned)B), dim3(GN_THREADS), smem_bytes(a.A),
+                     rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_gridnet_sample(const float* logits, const uint8_t* mask, int64_t B, int32_t C, int32_t G,
+                                  const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val,
+                                  uint64_t seed, uint64_t offset, int64_t* actions_out, float* logp_out,
+                                  void* stream) {
+  GridArgs a;
+  int rc = setup(a, logits, mask, nullptr, B, C, G, nvec, sub_ref, sub_val);
+  if (rc != RAI_OK) return rc;
+  if (B == 0) return RAI_OK;
+  if (!actions_out) return RAI_E_NULLPTR;
+  a.actions_out = actions_out;
+  a.logp = logp_out;
+  a.seed = seed;
+  a.offset = offset;
+  hipLaunchKernelGGL(gridnet_sample_kernel, dim3((unsigned)B), dim3(GN_THREADS), smem_bytes(a.A),
                      rai_stream(stream), a);
   RAI_LAUNCH_CHECK();
   return RAI_OK;

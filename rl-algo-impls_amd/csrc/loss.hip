@@ -138,7 +138,25 @@ __global__ __launch_bounds__(LOSS_THREADS) void pg_loss_kernel(const LossArgs a)
 
   // ---- pass 0: advantage moments (two-pass, fp64 accumulation; ppo.py:307-318) ---------
   const bool need_cols = !hp.normalize_after_scaling && (hp.normalize_advantage || hp.standardize_advantage);
-  if (hp.normalize_after_scaling) {
+  if (hp.ext_moments && (hp.normalize_after_scaling || need_cols)) {
+    // data parallel: the global minibatch's moments, reduced across ranks by the host (ppo.py:307-318
+    // over the union of the ranks' minibatch slices).  Row si holds K (mean, den) pairs per column,
+    // or one pair of the weighted advantage under normalize_advantages_after_scaling.
+    if (tid == 0) {
+      const int si = a.state->stat_index;
+      if (hp.normalize_after_scaling) {
+        nm_s.smean = hp.ext_moments[2 * si];
+        nm_s.sden = hp.ext_moments[2 * si + 1];
+      } else {
+#pragma unroll
+        for (int k = 0; k < KM; ++k)
+          if (k < K) {
+            nm_s.mean[k] = hp.ext_moments[2 * (si * K + k)];
+            nm_s.den[k] = hp.ext_moments[2 * (si * K + k) + 1];
+          }
+      }
+    }
+  } else if (hp.normalize_after_scaling) {
     double acc[1] = {0.0};
     for (int64_t b = tid; b < B; b += NT) {
       float x;
@@ -172,14 +190,6 @@ __global__ __launch_bounds__(LOSS_THREADS) void pg_loss_kernel(const LossArgs a)
     if (tid == 0) {
       nm_s.smean = mean;
       nm_s.sden = (float)sqrt(acc[0] / (double)(B - 1)) + 1e-8f;
-    }
-  } else if (need_cols && hp.ext_moments && K == 1) {
-    // data parallel: the global minibatch's moments, reduced across ranks by the host (ppo.py:313-316
-    // over the union of the ranks' minibatch slices)
-    if (tid == 0) {
-      const int si = a.state->stat_index;
-      nm_s.mean[0] = hp.ext_moments[2 * si];
-      nm_s.den[0] = hp.ext_moments[2 * si + 1];
     }
   } else if (need_cols) {
     double acc[KM];

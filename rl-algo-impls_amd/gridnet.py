@@ -6,7 +6,9 @@ MaskedCategoricals per minibatch and stacks ~30 eager kernels per sub-action for
 entropy (plus their autograd backward); here log_prob + entropy of every cell and sub-action is
 ONE launch (rai_gridnet_logp_entropy) and the backward ONE launch (rai_gridnet_backward), through
 `GridnetLogpEntropy` (a torch.autograd.Function, so the network upstream still backpropagates
-through PyTorch-ROCm).  sample()/mode (rollout only) stay per-group torch ops.  The Lux
+through PyTorch-ROCm).  The rollout samples every cell and plane and takes the sample's log-prob in
+ONE launch (rai_gridnet_sample, `sample_with_logp`); sample()/mode keep the per-group torch form for
+eval/enjoy.  The Lux
 "pick_position" variant is outside the hot path and rejected loudly.
 """
 from __future__ import annotations
@@ -139,6 +141,22 @@ class GridnetDistribution:  # gridnet.py:38-224 (per-position actions)
             lg = self.logits[..., offs[g]:offs[g + 1]]
             mk = self.masks[..., offs[g]:offs[g + 1]].bool()
             yield torch.where(mk, lg, torch.tensor(F32_MIN, dtype=lg.dtype, device=lg.device))
+
+    def sample_with_logp(self, seed: int, offset: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Rollout path: sample() + log_prob(sample) in ONE launch (rai_gridnet_sample; Philox keyed
+        (seed, offset), so a rollout step is reproducible without the torch generator)."""
+        z = self.logits.contiguous()
+        _lib.require_device(z)
+        m = _u8(self.masks)
+        B = int(z.shape[0])
+        act = torch.empty((B, self.map_size, self._spec.G), dtype=torch.int64, device=z.device)
+        logp = torch.empty(B, dtype=torch.float32, device=z.device)
+        nv, sr, sv = self._spec.ptrs()
+        rc = _lib.lib().rai_gridnet_sample(z.data_ptr(), m.data_ptr(), B, self.map_size, self._spec.G, nv, sr, sv,
+                                           int(seed), int(offset), act.data_ptr(), logp.data_ptr(),
+                                           _lib.stream_handle(z.device))
+        _lib.check(rc, "rai_gridnet_sample")
+        return act, logp
 
     def sample(self, sample_shape=torch.Size()) -> torch.Tensor:
         outs = [torch.distributions.Categorical(logits=zm).sample(sample_shape) for zm in self._groups()]

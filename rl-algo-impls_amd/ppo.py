@@ -101,8 +101,8 @@ class PPO:
         advantage normalisation uses global per-minibatch moments (one small all-reduce per
         epoch), reproducing the reference's normalisation over the whole (global) minibatch:
         on the fused MLP path through the kernels' moments argument, on the per-minibatch path
-        through rai_ppo_hparams.ext_moments (single value column; multi-critic and
-        normalize-after-scaling configurations normalise per rank)."""
+        through rai_ppo_hparams.ext_moments (per advantage column, or of the weighted advantage
+        under normalize_advantages_after_scaling)."""
         import torch.distributed as dist
 
         self.dp_group = group
@@ -221,32 +221,38 @@ class PPO:
             t.mul_(1.0 / self.world)
 
     def _global_adv_moments(self, adv: torch.Tensor, nmb: int) -> torch.Tensor:
-        """(mean, den) of every global minibatch of this epoch: local per-minibatch
-        (count, sum, sum of squares) in fp64, one all-reduce, unbiased std (ppo.py:313-316)."""
+        """(mean, den) of every global minibatch of this epoch, per advantage column (or of the
+        multi_reward_weights-weighted advantage under normalize_advantages_after_scaling):
+        local per-minibatch (count, sum, sum of squares) in fp64, one all-reduce, unbiased std
+        (ppo.py:307-318).  Returns (nmb, columns, 2) f32; the loss kernel applies the
+        normalize / standardize rule itself."""
         B = self.batch_size
-        a = adv.reshape(-1).double()
-        n_full = a.numel() // B
-        parts = [torch.stack([torch.full((n_full,), float(B), dtype=torch.float64, device=a.device),
-                              a[:n_full * B].view(n_full, B).sum(1), (a[:n_full * B].view(n_full, B) ** 2).sum(1)], 1)]
+        a = adv.double()
+        a = a.reshape(a.shape[0], -1)
+        if self.normalize_advantages_after_scaling:
+            w = self.multi_reward_weights
+            if w is not None:
+                a = (a.float() * torch.as_tensor(np.asarray(w, np.float32), device=a.device)).sum(1, keepdim=True)
+                a = a.double()
+            else:
+                a = a[:, :1]
+        rows, kc = a.shape
+        n_full = rows // B
+        full = a[:n_full * B].view(n_full, B, kc)
+        parts = [torch.stack([torch.full((n_full, kc), float(B), dtype=torch.float64, device=a.device),
+                              full.sum(1), (full ** 2).sum(1)], -1)]
         if n_full < nmb:
             tail = a[n_full * B:]
-            parts.append(torch.stack([torch.tensor(float(tail.numel()), dtype=torch.float64, device=a.device),
-                                      tail.sum(), (tail ** 2).sum()]).view(1, 3))
+            parts.append(torch.stack([torch.full((kc,), float(tail.shape[0]), dtype=torch.float64, device=a.device),
+                                      tail.sum(0), (tail ** 2).sum(0)], -1).view(1, kc, 3))
         m = torch.cat(parts, 0)
         self._all_reduce(m)
-        n, s1, s2 = m[:, 0], m[:, 1], m[:, 2]
+        n, s1, s2 = m[..., 0], m[..., 1], m[..., 2]
         mean = s1 / n
         std = torch.sqrt(torch.clamp(s2 - n * mean * mean, min=0.0) / (n - 1)).float()
-        out = torch.empty((nmb, 2), dtype=torch.float32, device=a.device)
-        if self.normalize_advantage:
-            out[:, 0] = mean.float()
-            out[:, 1] = std + 1e-8
-        elif self.standardize_advantage:
-            out[:, 0] = 0.0
-            out[:, 1] = std + 1e-8
-        else:
-            out[:, 0] = 0.0
-            out[:, 1] = 1.0
+        out = torch.empty((nmb, kc, 2), dtype=torch.float32, device=a.device)
+        out[..., 0] = mean.float()
+        out[..., 1] = std + 1e-8
         return out.contiguous()
 
     def _update_fused_dp(self, r, spec) -> Tuple[np.ndarray, np.ndarray, int]:
@@ -261,7 +267,12 @@ class PPO:
         st = _lib.stream_handle(self.device)
         for _ in range(self.n_epochs):
             b = r.epoch_batch(shuffle=True)
-            moments = self._global_adv_moments(b.advantages, nmb)
+            moments = self._global_adv_moments(b.advantages, nmb).view(nmb, 2)
+            # the fused epoch kernels apply A = (A - mean) / den as given: encode the reference's rule
+            if not self.normalize_advantage:
+                moments[:, 0] = 0.0
+                if not self.standardize_advantage:
+                    moments[:, 1] = 1.0
             obs = (b.obs if b.obs.dtype == torch.float32 else b.obs.float()).contiguous()
             acts = b.actions.contiguous()
             if self._xdp is not None:  # one launch per epoch, cross-GPU sums inside the kernel
@@ -549,13 +560,15 @@ class PPO:
     def _dp_moments_table(self, K: int, n_steps: int) -> Optional[torch.Tensor]:
         """Data parallel on the per-minibatch path: the global minibatches' advantage (mean, den),
         one row per stats row, for the loss kernel (rai_ppo_hparams.ext_moments); None when the
-        minibatch's own moments are the reference's (single rank) or the options are not covered
-        (K > 1 value columns, normalize-after-scaling: normalised per rank)."""
-        if not self.dp_enabled or self.world == 1 or K != 1 or self.normalize_advantages_after_scaling:
+        minibatch's own moments are the reference's (single rank) or no normalisation is asked for.
+        Layout (n_steps, columns, 2): K columns, or one under normalize_advantages_after_scaling."""
+        if not self.dp_enabled or self.world == 1:
             return None
+        if self.normalize_advantages_after_scaling:
+            return torch.zeros((n_steps, 1, 2), dtype=torch.float32, device=self.device)
         if not (self.normalize_advantage or self.standardize_advantage):
             return None
-        return torch.zeros((n_steps, 2), dtype=torch.float32, device=self.device)
+        return torch.zeros((n_steps, K, 2), dtype=torch.float32, device=self.device)
 
     def _fill_epoch_moments(self, ext: torch.Tensor, epoch: int, adv_epoch: torch.Tensor, nmb: int) -> None:
         """Rows [epoch*nmb, (epoch+1)*nmb) of the table from this rank's permuted advantages (one

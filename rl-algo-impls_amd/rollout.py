@@ -337,9 +337,10 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         """backbone_actor_critic.py:194-223 + gridnet.py sample: per-position actions, the fused
         GridNet log-prob kernel, K critic values, written into slot s."""
         pi, v = self.policy.network.distribution_and_value(self.obs[s], self.action_masks[s])
-        a = pi.sample()
+        a, logp = pi.sample_with_logp(self.seed, self.rng_offset)
+        self.rng_offset += 1
         self.actions[s].copy_(a.view(self.actions[s].shape))
-        self.logprobs[s].copy_(pi.log_prob(a))
+        self.logprobs[s].copy_(logp)
         self.values[s].copy_(v)
 
     def _layer_ptrs(self):

@@ -23,7 +23,8 @@ def _init(rank, world, port, backend="gloo"):
 
 
 def moments_worker(rank, world, port, q):
-    """Global advantage moments across ranks == moments of the concatenated minibatches."""
+    """Global advantage moments across ranks == moments of the concatenated minibatches: one column,
+    K=3 columns, and the multi_reward_weights-weighted advantage (normalize_advantages_after_scaling)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -34,21 +35,31 @@ def moments_worker(rank, world, port, q):
     _pkgload.load()
     from rl_algo_impls_amd.ppo import PPO
 
+    w = np.array([0.8, 0.01, 0.19])
+
     class Stub(PPO):
-        def __init__(self):
+        def __init__(self, after):
             self.batch_size, self.world, self.dp_group = 64, world, None
             self.normalize_advantage, self.standardize_advantage = True, False
+            self.normalize_advantages_after_scaling = after
+            self.multi_reward_weights = w if after else None
 
     g = torch.Generator().manual_seed(100 + rank)
-    adv = torch.randn(64 * 5 + 30, generator=g) * (1 + rank) + rank
-    out = Stub()._global_adv_moments(adv, 6)
-    allv = [torch.zeros_like(adv) for _ in range(world)]
-    dist.all_gather(allv, adv)
-    ref = []
-    for i in range(6):
-        mb = torch.cat([a[i * 64:(i + 1) * 64] for a in allv]).double()
-        ref.append([mb.mean().item(), mb.std().item() + 1e-8])
-    q.put((rank, out.numpy().tolist(), ref))
+    results = []
+    for K, after in ((1, False), (3, False), (3, True)):
+        adv = torch.randn(64 * 5 + 30, K, generator=g) * (1 + rank) + rank
+        adv = adv[:, 0] if K == 1 else adv
+        out = Stub(after)._global_adv_moments(adv, 6)
+        allv = [torch.zeros_like(adv) for _ in range(world)]
+        dist.all_gather(allv, adv)
+        ref = []
+        for i in range(6):
+            mb = torch.cat([a[i * 64:(i + 1) * 64] for a in allv]).double().reshape(-1, K)
+            if after:
+                mb = (mb.float() * torch.tensor(w, dtype=torch.float32)).sum(1, keepdim=True).double()
+            ref.append(torch.stack([mb.mean(0), mb.std(0) + 1e-8], -1).tolist())
+        results.append((out.numpy().tolist(), ref))
+    q.put((rank, results))
     dist.destroy_process_group()
 
 
@@ -183,6 +194,60 @@ def wide_dp_worker(rank, world, port, q):
     algo.enable_data_parallel()
     stats, norms, _ = algo.update(r)
     assert algo._wide not in (None, False), "wide path not taken"
+    q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+def make_mc_rank_data(rank, T=16, N=8):
+    """Rank-local rollout tensors for the 3-critic harness policy (4-dim obs, 3 actions)."""
+    import torch
+
+    g = torch.Generator().manual_seed(71 + rank)
+    return dict(obs=torch.randn(T, N, 4, generator=g), act=torch.randint(0, 3, (T, N), generator=g),
+                rew=torch.randn(T, N, 3, generator=g) + 0.3 * rank, vals=torch.randn(T, N, 3, generator=g),
+                starts=(torch.rand(T, N, generator=g) < 0.05).to(torch.uint8),
+                logp=-1.1 + 0.1 * torch.randn(T, N, generator=g), nv=torch.randn(N, 3, generator=g),
+                nes=torch.zeros(N, dtype=torch.uint8))
+
+
+MC_KW = dict(n_epochs=2, learning_rate=3e-4, ent_coef=0.01, clip_range_vf=0.2, multi_reward_weights=[0.8, 0.01, 0.19],
+             vf_coef=[0.5, 0.1, 0.2], ppo2_vf_coef_halving=True)
+
+
+def mc_policy_and_rollout(d, dev):
+    import numpy as np
+    import torch
+
+    import make_golden_networks as nets
+    from rl_algo_impls_amd.rollout import DeviceRollout
+
+    torch.manual_seed(0)
+    policy = nets.build("multicritic").to(dev)
+    t = lambda x: x.to(dev)
+    r = DeviceRollout(dev, t(d["nes"]), t(d["nv"]), t(d["obs"]), t(d["act"]), t(d["rew"]), t(d["starts"]),
+                      t(d["vals"]), t(d["logp"]), None, np.array([0.99, 0.999, 0.999]), np.array([0.95, 0.99, 0.99]),
+                      perm_source=lambda n: torch.arange(n))
+    return policy, r
+
+
+def mc_dp_worker(rank, world, port, q, after):
+    """Data-parallel per-minibatch update of a 3-critic policy (gloo, all ranks on cuda:0): global
+    advantage moments per column (or of the weighted advantage after scaling) through ext_moments."""
+    import torch
+
+    _init(rank, world, port)
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.ppo import PPO
+
+    dev = torch.device("cuda", 0)
+    policy, r = mc_policy_and_rollout(make_mc_rank_data(rank), dev)
+    algo = PPO(policy, dev, None, batch_size=32, normalize_advantages_after_scaling=after, **MC_KW)
+    algo.enable_data_parallel()
+    stats, norms, _ = algo.update(r)
     q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
     import torch.distributed as dist
 

@@ -26,6 +26,9 @@ def test_global_advantage_moments_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    outs = {r: (np.array(o), np.array(ref)) for r, o, ref in res}
-    np.testing.assert_array_equal(outs[0][0], outs[1][0])  # identical on every rank
-    np.testing.assert_allclose(outs[0][0], outs[0][1], rtol=1e-5, atol=1e-6)
+    outs = dict(res)
+    for case in range(3):  # one column; K=3 columns; weighted advantage (after scaling)
+        o0, ref0 = (np.array(x) for x in outs[0][case])
+        o1, _ = (np.array(x) for x in outs[1][case])
+        np.testing.assert_array_equal(o0, o1)  # identical on every rank
+        np.testing.assert_allclose(o0, ref0, rtol=1e-5, atol=1e-6)

@@ -167,3 +167,50 @@ def test_wide_mlp_dp_world2_matches_single_process_global_minibatches():
     np.testing.assert_allclose(n0, norms, rtol=1e-4)
     np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=2e-6)
+
+
+@pytest.mark.parametrize("after", [False, True], ids=["per_column", "after_scaling"])
+def test_multicritic_dp_world2_matches_single_process_global_minibatches(after):
+    """3-critic policy (multi_reward_weights, per-critic vf_coef, vector gamma), 2 ranks (gloo, both on
+    cuda:0), identity permutation: the global minibatch's advantage moments per column (or of the
+    weighted advantage under normalize_advantages_after_scaling) reach the loss kernel through
+    rai_ppo_hparams.ext_moments; compared with the single-process update over the concatenated
+    rollout (batch 64)."""
+    import queue
+    import time
+
+    import dp_worker
+    from rl_algo_impls_amd.ppo import PPO
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.mc_dp_worker, args=(r, 2, port, q, after)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    deadline = time.time() + 240
+    while len(res) < 2:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"rank exited with {dead}"
+            assert time.time() < deadline, "ranks did not report in time"
+    res.sort(key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, s0, n0), (_, p1, s1, n1) = res
+    np.testing.assert_array_equal(p0, p1)
+
+    dev = torch.device("cuda", 0)
+    d0, d1 = dp_worker.make_mc_rank_data(0), dp_worker.make_mc_rank_data(1)
+    glob = {k: torch.cat([d0[k], d1[k]], dim=1 if k not in ("nv", "nes") else 0) for k in d0}
+    policy, r = dp_worker.mc_policy_and_rollout(glob, dev)
+    algo = PPO(policy, dev, None, batch_size=64, normalize_advantages_after_scaling=after, **dp_worker.MC_KW)
+    stats, norms, K = algo.update(r)
+    assert K == 3
+    np.testing.assert_allclose(n0, norms, rtol=1e-4)
+    np.testing.assert_allclose(s0[:, :8], stats[:, :8], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=2e-6)
