@@ -126,6 +126,20 @@ int rai_gridnet_sample(const float* logits, const uint8_t* mask, int64_t B, int3
                        uint64_t offset, int64_t* actions_out, float* logp_out, void* stream);
 
 /* --------------------------------------------------------------------------
+ * Squeeze-excitation residual epilogue of the squeeze-U-Net backbone (config C5):
+ * out = GELU(x + r * s[b, c]) and its backward in one pass each, replacing the
+ * broadcast-multiply / add / GELU sequence of SEResidualBlock.forward
+ * (rl_algo_impls/shared/policy/actor_critic_network/double_cone.py:43-47,85-86) and
+ * its autograd.  x, r, out, dout, dx, dr: NHWC (channels_last) fp32, (B, HW, C) with C
+ * fastest; s, ds: (B, C).  GELU is the exact erf form.  C % 4 == 0 and C / 4 must
+ * divide 256 (RAI_E_SHAPE otherwise).
+ * ------------------------------------------------------------------------ */
+int rai_se_residual_fwd(const float* x, const float* r, const float* s, int64_t B, int32_t C, int32_t HW,
+                        float* out, void* stream);
+int rai_se_residual_bwd(const float* dout, const float* x, const float* r, const float* s, int64_t B, int32_t C,
+                        int32_t HW, float* dx, float* dr, float* ds, void* stream);
+
+/* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.
  * These live in HBM so a captured hipGraph replays against values the host
  * rewrites once per update (schedules: rl_algo_impls/shared/callbacks/

@@ -126,6 +126,8 @@ _SIGNATURES = {
     "rai_gae_trajectories": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _f64p, _f64p, _i32, _i32, _vp, _vp, _vp]),
     "rai_gridnet_logp_entropy": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rai_gridnet_backward": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rai_se_residual_fwd": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "rai_se_residual_bwd": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
     "rai_gridnet_sample": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                      _vp]),
     "rai_mlp_wide_workspace_bytes": (_i64, [_i64, _i32]),

@@ -17,6 +17,7 @@ MaskedCategoricals.  Normalisation layers (`normalization=...`), the non-shared 
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Union
 
 import numpy as np
@@ -26,6 +27,57 @@ import torch.nn as nn
 from .gridnet import GridnetDistribution, ValueDependentMask
 
 Strides = Sequence[Union[int, Sequence[int]]]
+# NHWC activations on the GPU (RAI_CHANNELS_LAST=0 keeps NCHW): MIOpen's implicit-GEMM solvers take
+# them without the NCHW<->NHWC transposes, and the fused SE epilogue below runs on them
+_CHANNELS_LAST = os.environ.get("RAI_CHANNELS_LAST", "1") == "1"
+if _CHANNELS_LAST:
+    os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC", "1")
+
+
+def _nhwc(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.float32 and t.dim() == 4 and t.is_contiguous(
+        memory_format=torch.channels_last)
+
+
+class _SEResidualEpilogue(torch.autograd.Function):
+    """GELU(x + r * s) (double_cone.py:43-47,85-86) as one HIP pass forward and one backward
+    (rai_se_residual_fwd / _bwd, csrc/se_block.hip); NHWC fp32 activations, s (B, C)."""
+
+    @staticmethod
+    def forward(ctx, x, r, s):
+        from . import _lib
+
+        B, C, H, W = (int(d) for d in x.shape)
+        s = s.contiguous()
+        out = torch.empty_like(x)
+        _lib.check(_lib.lib().rai_se_residual_fwd(x.data_ptr(), r.data_ptr(), s.data_ptr(), B, C, H * W,
+                                                  out.data_ptr(), _lib.stream_handle(x.device)),
+                   "rai_se_residual_fwd")
+        ctx.save_for_backward(x, r, s)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import _lib
+
+        x, r, s = ctx.saved_tensors
+        B, C, H, W = (int(d) for d in x.shape)
+        dout = dout.contiguous(memory_format=torch.channels_last)
+        dx, dr, ds = torch.empty_like(x), torch.empty_like(r), torch.empty_like(s)
+        _lib.check(_lib.lib().rai_se_residual_bwd(dout.data_ptr(), x.data_ptr(), r.data_ptr(), s.data_ptr(), B, C,
+                                                  H * W, dx.data_ptr(), dr.data_ptr(), ds.data_ptr(),
+                                                  _lib.stream_handle(x.device)), "rai_se_residual_bwd")
+        return dx, dr, ds
+
+
+def se_residual_epilogue(x: torch.Tensor, r: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """GELU(x + r * s[..., None, None]); the fused HIP pass for NHWC fp32 GPU activations whose C
+    the kernel tiles (C % 4 == 0, C / 4 divides 256), else the PyTorch composition."""
+    C = int(x.shape[1]) if x.dim() == 4 else 0
+    if (_nhwc(x) and _nhwc(r) and r.shape == x.shape and C % 4 == 0 and C >= 4 and 256 % (C // 4) == 0
+            and s.is_cuda and s.dtype == torch.float32):
+        return _SEResidualEpilogue.apply(x, r, s)
+    return torch.nn.functional.gelu(x + r * s.view(s.shape[0], s.shape[1], 1, 1))
 
 
 def _init(layer: nn.Module, orthogonal: bool, std: float = float(np.sqrt(2))) -> nn.Module:
@@ -66,7 +118,11 @@ class SEResidualBlock(nn.Module):  # double_cone.py:50-86 (normalization=None)
         self.gelu = nn.GELU()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.gelu(x + self.residual(x))
+        conv0, act, conv1, se = self.residual
+        r = conv1(act(conv0(x)))
+        b, c = r.shape[0], r.shape[1]
+        s = se.fc(se.avg_pool(r).view(b, c))
+        return se_residual_epilogue(x, r, s)  # == self.gelu(x + self.residual(x))
 
 
 class SqueezeUnetBackbone(nn.Module):  # squeeze_unet.py:20-195
@@ -212,7 +268,10 @@ class SqueezeUnetActorCriticNetwork(nn.Module):
     def _preprocess(self, obs: torch.Tensor) -> torch.Tensor:
         if obs.dim() == 3:
             obs = obs.unsqueeze(0)
-        return obs.float() / self.range_size
+        x = obs.float() / self.range_size
+        if _CHANNELS_LAST and x.is_cuda:  # NHWC activations for MIOpen's implicit-GEMM solvers
+            x = x.contiguous(memory_format=torch.channels_last)
+        return x
 
     def _values(self, x: torch.Tensor) -> torch.Tensor:
         v = self.critic_heads(x)

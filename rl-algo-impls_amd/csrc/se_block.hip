@@ -1,0 +1,112 @@
+// Squeeze-excitation residual epilogue of the squeeze-U-Net backbone (config C5) on gfx950.
+//
+// SEResidualBlock.forward (rl_algo_impls/shared/policy/actor_critic_network/double_cone.py:85-86)
+// ends with   out = GELU(x + r * s)   where r is the second 3x3 conv's output, s = sigmoid(fc(mean_hw r))
+// the squeeze-excitation scale (double_cone.py:43-47).  PyTorch runs that as a broadcast multiply,
+// an add and a GELU (three passes over the activation, two intermediates) and the backward as four
+// more kernels plus a reduction for ds.  Here:
+//   forward   one pass:  out = gelu(x + r * s[b, c])                          (reads x, r; writes out)
+//   backward  one pass:  g = dout * gelu'(x + r * s);  dx = g;  dr = g * s;  ds[b, c] = sum_hw g * r
+// GELU is the exact (erf) form of torch.nn.GELU(): gelu(t) = t * Phi(t), gelu'(t) = Phi(t) + t * phi(t).
+//
+// Layout: NHWC (channels_last) activations, (B, HW, C) row-major with C fastest; s, ds (B, C).
+// Forward: grid-stride float4 elementwise pass.  Backward: one 256-thread workgroup per sample; a
+// thread owns one float4 channel group (c4 = tid % C4) for HW rows tid / C4 + k * (256 / C4), keeps
+// its ds partial in registers, and the 256 / C4 row-groups are summed in a fixed order through LDS
+// (deterministic).  Needs C % 4 == 0 and C / 4 dividing 256 (C in {4, 8, ..., 1024}).
+#include "common.h"
+
+namespace {
+
+constexpr int SE_THREADS = 256;
+using f4 = float __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float gelu_f(float t) { return 0.5f * t * (1.f + erff(t * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float t) {
+  const float cdf = 0.5f * (1.f + erff(t * 0.70710678118654752f));
+  const float pdf = expf(-0.5f * t * t) * 0.39894228040143268f;
+  return cdf + t * pdf;
+}
+
+__global__ __launch_bounds__(SE_THREADS) void se_fwd_kernel(const f4* __restrict__ x, const f4* __restrict__ r,
+                                                            const f4* __restrict__ s, int C4, int64_t HWC4,
+                                                            int64_t n4, f4* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)SE_THREADS + threadIdx.x; i < n4; i += (int64_t)gridDim.x * SE_THREADS) {
+    const int64_t b = i / HWC4;
+    const int c4 = (int)(i % C4);
+    const f4 xv = x[i], rv = r[i], sv = s[b * C4 + c4];
+    f4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = gelu_f(xv[q] + rv[q] * sv[q]);
+    out[i] = o;
+  }
+}
+
+__global__ __launch_bounds__(SE_THREADS) void se_bwd_kernel(const f4* __restrict__ dout, const f4* __restrict__ x,
+                                                            const f4* __restrict__ r, const f4* __restrict__ s,
+                                                            int C4, int HW, f4* __restrict__ dx, f4* __restrict__ dr,
+                                                            f4* __restrict__ ds) {
+  __shared__ f4 part[SE_THREADS];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int c4 = tid % C4, row0 = tid / C4, rstep = SE_THREADS / C4;
+  const f4 sv = s[b * C4 + c4];
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  const int64_t base = b * (int64_t)HW * C4;
+  for (int h = row0; h < HW; h += rstep) {
+    const int64_t i = base + (int64_t)h * C4 + c4;
+    const f4 g0 = dout[i], xv = x[i], rv = r[i];
+    f4 g, dri;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      g[q] = g0[q] * gelu_grad(xv[q] + rv[q] * sv[q]);
+      dri[q] = g[q] * sv[q];
+      acc[q] += g[q] * rv[q];
+    }
+    dx[i] = g;
+    dr[i] = dri;
+  }
+  part[tid] = acc;
+  __syncthreads();
+  if (tid < C4) {
+    f4 t = part[tid];
+    for (int k = 1; k < rstep; ++k) t += part[tid + k * C4];
+    ds[b * C4 + tid] = t;
+  }
+}
+
+bool shape_ok(int64_t B, int32_t C, int32_t HW) {
+  if (B < 0 || C < 4 || HW < 1 || C % 4) return false;
+  const int C4 = C / 4;
+  return C4 <= SE_THREADS && SE_THREADS % C4 == 0;
+}
+
+}  // namespace
+
+extern "C" int rai_se_residual_fwd(const float* x, const float* r, const float* s, int64_t B, int32_t C, int32_t HW,
+                                   float* out, void* stream) {
+  if (!shape_ok(B, C, HW)) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!x || !r || !s || !out) return RAI_E_NULLPTR;
+  const int C4 = C / 4;
+  const int64_t n4 = B * (int64_t)HW * C4;
+  const int64_t blocks = std::min<int64_t>((n4 + SE_THREADS - 1) / SE_THREADS, 256 * 64);
+  hipLaunchKernelGGL(se_fwd_kernel, dim3((unsigned)blocks), dim3(SE_THREADS), 0, rai_stream(stream),
+                     reinterpret_cast<const f4*>(x), reinterpret_cast<const f4*>(r), reinterpret_cast<const f4*>(s),
+                     C4, (int64_t)HW * C4, n4, reinterpret_cast<f4*>(out));
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_se_residual_bwd(const float* dout, const float* x, const float* r, const float* s, int64_t B,
+                                   int32_t C, int32_t HW, float* dx, float* dr, float* ds, void* stream) {
+  if (!shape_ok(B, C, HW)) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!dout || !x || !r || !s || !dx || !dr || !ds) return RAI_E_NULLPTR;
+  hipLaunchKernelGGL(se_bwd_kernel, dim3((unsigned)B), dim3(SE_THREADS), 0, rai_stream(stream),
+                     reinterpret_cast<const f4*>(dout), reinterpret_cast<const f4*>(x),
+                     reinterpret_cast<const f4*>(r), reinterpret_cast<const f4*>(s), C / 4, HW,
+                     reinterpret_cast<f4*>(dx), reinterpret_cast<f4*>(dr), reinterpret_cast<f4*>(ds));
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

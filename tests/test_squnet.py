@@ -194,3 +194,27 @@ def test_microrts_training_end_to_end(tmp_path):
     pol.save(str(tmp_path))
     sd = torch.load(tmp_path / "model.pth", weights_only=True)
     assert set(sd) == set(pol.state_dict())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,H", [(3, 16, 16), (2, 128, 4), (5, 128, 1), (4, 32, 8)])
+def test_se_residual_epilogue_vs_pytorch(B, C, H):
+    """rai_se_residual_fwd / _bwd (csrc/se_block.hip) against the PyTorch composition
+    gelu(x + r * s) and its autograd, NHWC fp32.  Tolerance: rtol 1e-5 / atol 1e-6 (erf / exp in
+    fp32 on both sides; ds is a sum over H*W)."""
+    from rl_algo_impls_amd.backbone import _SEResidualEpilogue
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(B * 100 + C + H)
+    mk = lambda *s: torch.randn(*s, generator=g).to(dev)
+    x = mk(B, C, H, H).contiguous(memory_format=torch.channels_last).requires_grad_()
+    r = mk(B, C, H, H).contiguous(memory_format=torch.channels_last).requires_grad_()
+    s = torch.sigmoid(mk(B, C)).requires_grad_()
+    dout = mk(B, C, H, H).contiguous(memory_format=torch.channels_last)
+    out = _SEResidualEpilogue.apply(x, r, s)
+    dx, dr, ds = torch.autograd.grad(out, (x, r, s), dout)
+    ref = torch.nn.functional.gelu(x + r * s.view(B, C, 1, 1))
+    rx, rr, rs = torch.autograd.grad(ref, (x, r, s), dout)
+    for a, b_ in ((out, ref), (dx, rx), (dr, rr), (ds, rs)):
+        np.testing.assert_allclose(a.detach().cpu().numpy(), b_.detach().cpu().numpy(), rtol=1e-5, atol=1e-6)
+    assert out.is_contiguous(memory_format=torch.channels_last)
