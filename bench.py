@@ -144,7 +144,9 @@ def main():
 
     def progress(tag, i, t_start):
         if rank == 0:
-            print(f"[bench] {tag} update {i}: {time.perf_counter() - t_start:.2f} s", file=sys.stderr, flush=True)
+            print(f"[bench] {tag} update {i}: {time.perf_counter() - t_start:.2f} s "
+                  f"(this update: rollout {getattr(algo, 'last_rollout_seconds', 0.0):.3f} s of "
+                  f"{getattr(algo, 'last_update_seconds', 0.0):.3f} s)", file=sys.stderr, flush=True)
 
     for i in range(args.warmup):
         tw = time.perf_counter()

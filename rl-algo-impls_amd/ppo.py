@@ -380,6 +380,7 @@ class PPO:
         log_scalars(self.tb_writer, "charts", chart, timesteps_elapsed)
 
         r = rollout_generator.rollout(gamma=self.gamma, gae_lambda=self.gae_lambda)
+        self.last_rollout_seconds = perf_counter() - start_time  # host env + policy steps (synced per step)
         timesteps_elapsed += r.total_steps
         stats, norms, K = self.update(r)
         explained_var = r.explained_variance()

@@ -29,6 +29,8 @@ from collections import deque
 from typing import Callable, Deque, Dict, Iterator, List, Optional
 
 import ctypes as C
+import os
+
 import numpy as np
 import torch
 
@@ -293,6 +295,8 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         self.episode_starts = torch.zeros((T, N), dtype=torch.bool, device=dev)
         self.values = torch.zeros((T, N) + vshape, dtype=torch.float32, device=dev)
         self.action_masks = None
+        self.rollout_graph = os.environ.get("RAI_ROLLOUT_GRAPH", "1") == "1" and self.device.type == "cuda"
+        self._fwd_graph = None
         if self.gridnet:  # sync_step_rollout.py:119-131: (T, N, cells, sum(nvec)) bool
             m0 = np.asarray(self.get_action_mask())
             self.action_masks = torch.zeros((T,) + m0.shape, dtype=torch.bool, device=dev)
@@ -333,10 +337,34 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             np.copyto(self.h_mask.numpy(), np.asarray(self.get_action_mask()))
             self.next_masks_dev.copy_(self.h_mask, non_blocking=True)
 
+    def _gridnet_forward(self):
+        """The policy forward of one env step on next_obs_dev (a fixed buffer), replayed from a
+        hipGraph captured on first use: the squeeze-U-Net is ~100 small kernels at rollout batch
+        sizes, launch-bound when issued one by one.  RAI_ROLLOUT_GRAPH=0 runs it eagerly.  The
+        parameters are updated in place (flat buffer views), so the graph stays valid."""
+        net = self.policy.network
+        if not self.rollout_graph:
+            return net.logits_and_value(self.next_obs_dev)
+        if self._fwd_graph is None:
+            cur = torch.cuda.current_stream(self.device)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                for _ in range(2):  # warm-up outside capture (solver selection, workspaces)
+                    net.logits_and_value(self.next_obs_dev)
+            cur.wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._g_out = net.logits_and_value(self.next_obs_dev)
+            self._fwd_graph = g
+        self._fwd_graph.replay()
+        return self._g_out
+
     def _gridnet_step(self, s: int) -> None:
         """backbone_actor_critic.py:194-223 + gridnet.py sample: per-position actions, the fused
-        GridNet log-prob kernel, K critic values, written into slot s."""
-        pi, v = self.policy.network.distribution_and_value(self.obs[s], self.action_masks[s])
+        GridNet sample + log-prob kernel, K critic values, written into slot s."""
+        logits, v = self._gridnet_forward()
+        pi = self.policy.network.distribution(logits, self.next_masks_dev)
         a, logp = pi.sample_with_logp(self.seed, self.rng_offset)
         self.rng_offset += 1
         self.actions[s].copy_(a.view(self.actions[s].shape))
