@@ -337,25 +337,25 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             np.copyto(self.h_mask.numpy(), np.asarray(self.get_action_mask()))
             self.next_masks_dev.copy_(self.h_mask, non_blocking=True)
 
-    def _gridnet_forward(self):
-        """The policy forward of one env step on next_obs_dev (a fixed buffer), replayed from a
-        hipGraph captured on first use: the squeeze-U-Net is ~100 small kernels at rollout batch
-        sizes, launch-bound when issued one by one.  RAI_ROLLOUT_GRAPH=0 runs it eagerly.  The
-        parameters are updated in place (flat buffer views), so the graph stays valid."""
-        net = self.policy.network
+    def _policy_forward(self, fn):
+        """The policy forward of one env step, fn(next_obs_dev) with next_obs_dev a fixed buffer,
+        replayed from a hipGraph captured on first use: a CNN or MLP forward at rollout batch sizes
+        is tens of small kernels, launch-bound when issued one by one (squeeze-U-Net: ~100).
+        RAI_ROLLOUT_GRAPH=0 runs it eagerly.  The parameters are updated in place (flat buffer
+        views), so the graph stays valid across updates."""
         if not self.rollout_graph:
-            return net.logits_and_value(self.next_obs_dev)
+            return fn(self.next_obs_dev)
         if self._fwd_graph is None:
             cur = torch.cuda.current_stream(self.device)
             side = torch.cuda.Stream(self.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 for _ in range(2):  # warm-up outside capture (solver selection, workspaces)
-                    net.logits_and_value(self.next_obs_dev)
+                    fn(self.next_obs_dev)
             cur.wait_stream(side)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._g_out = net.logits_and_value(self.next_obs_dev)
+                self._g_out = fn(self.next_obs_dev)
             self._fwd_graph = g
         self._fwd_graph.replay()
         return self._g_out
@@ -363,7 +363,7 @@ class SyncStepRolloutGenerator(RolloutGenerator):
     def _gridnet_step(self, s: int) -> None:
         """backbone_actor_critic.py:194-223 + gridnet.py sample: per-position actions, the fused
         GridNet sample + log-prob kernel, K critic values, written into slot s."""
-        logits, v = self._gridnet_forward()
+        logits, v = self._policy_forward(self.policy.network.logits_and_value)
         pi = self.policy.network.distribution(logits, self.next_masks_dev)
         a, logp = pi.sample_with_logp(self.seed, self.rng_offset)
         self.rng_offset += 1
@@ -435,7 +435,7 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             elif self.gridnet:
                 self._gridnet_step(s)
             else:
-                params, v = net.dist_params_and_value(self.obs[s])
+                params, v = self._policy_forward(net.dist_params_and_value)
                 self._sample(params, v, s)
             src = self.actions[s] if (self.discrete or self.gridnet) else self.clamped
             self.h_act.copy_(src, non_blocking=True)
