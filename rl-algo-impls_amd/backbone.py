@@ -27,9 +27,10 @@ import torch.nn as nn
 from .gridnet import GridnetDistribution, ValueDependentMask
 
 Strides = Sequence[Union[int, Sequence[int]]]
-# NHWC activations on the GPU (RAI_CHANNELS_LAST=0 keeps NCHW): MIOpen's implicit-GEMM solvers take
-# them without the NCHW<->NHWC transposes, and the fused SE epilogue below runs on them
-_CHANNELS_LAST = os.environ.get("RAI_CHANNELS_LAST", "1") == "1"
+# NHWC activations on the GPU (RAI_SQUNET_NHWC=0 keeps NCHW): MIOpen's implicit-GEMM solvers take
+# them without the NCHW<->NHWC transposes, and the fused SE epilogue below runs on them.  (The
+# NatureCNN encoder's RAI_CHANNELS_LAST stays off by default: NHWC measured within noise on Pong.)
+_CHANNELS_LAST = os.environ.get("RAI_SQUNET_NHWC", "1") == "1"
 if _CHANNELS_LAST:
     os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC", "1")
 
