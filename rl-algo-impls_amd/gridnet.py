@@ -52,6 +52,17 @@ class _Spec:
         return p(self.nvec), p(self.sub_ref), p(self.sub_val)
 
 
+_CAT_SPECS: Dict[int, "_Spec"] = {}
+
+
+def categorical_spec(n: int) -> "_Spec":
+    """A flat Categorical(n) as a GridNet head with one cell and one plane."""
+    sp = _CAT_SPECS.get(n)
+    if sp is None:
+        sp = _CAT_SPECS[n] = _Spec([n], None)
+    return sp
+
+
 def _u8(m: torch.Tensor) -> torch.Tensor:
     m = m.contiguous()
     return m.view(torch.uint8) if m.dtype == torch.bool else m.to(torch.uint8)
