@@ -72,18 +72,18 @@ __global__ __launch_bounds__(256) void gather_minibatch_kernel(rai_minibatch_des
   for (int f = 0; f < nf; ++f) total += (int)o.units[f];  // workgroup's rows jointly
   const int G = (int)gridDim.x, b = (int)blockIdx.x;
   const int my_rows = rows > b ? (rows - b + G - 1) / G : 0;  // rows b, b + G, b + 2G, ...
-  const int64_t work = (int64_t)my_rows * total;
-  for (int64_t i0 = threadIdx.x; i0 < work; i0 += GM_BATCH * 256) {
+  const int work = my_rows * total;  // < 2^31: checked at launch (batch_size x total)
+  for (int i0 = threadIdx.x; i0 < work; i0 += GM_BATCH * 256) {
     uint4 v[GM_BATCH];
     int64_t so[GM_BATCH], doff[GM_BATCH];
     int fk[GM_BATCH];
 #pragma unroll
     for (int k = 0; k < GM_BATCH; ++k) {
-      const int64_t i = i0 + k * 256;
+      const int i = i0 + k * 256;
       fk[k] = -1;
       if (i < work) {
-        const int ri = (int)(i / total);
-        int j = (int)(i - (int64_t)ri * total);
+        const int ri = (int)((unsigned)i / (unsigned)total);
+        int j = i - ri * total;
         const int64_t r = b + (int64_t)ri * G;
         const int64_t sr = perm ? perm[row0 + r] : row0 + r;
         int f = 0;
@@ -259,6 +259,7 @@ static int gather_minibatch(rai_minibatch_desc* desc, int32_t n_fields, void* co
   // workgroups arrive on the advance counter when rows are small (HalfCheetah: 64 x ~30 units)
   int64_t total = 0;
   for (int i = 0; i < n_fields; ++i) total += o.units[i];
+  if (batch_size * total >= (1LL << 31)) return RAI_E_SHAPE;  // 32-bit (row, unit) indexing
   int64_t blocks = (batch_size * total + 255) / 256;
   if (blocks > batch_size) blocks = batch_size;
   if (blocks > 1024) blocks = 1024;

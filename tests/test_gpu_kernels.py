@@ -375,3 +375,47 @@ def test_fused_policy_step_matches_torch_forward_and_sampler(d, n, act):
                                      None, None, v3.data_ptr(), st), "policy_step values")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(v3.cpu().numpy(), v1.cpu().numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,B,shuffle", [(1000, 256, True), (300, 64, True), (77, 32, False), (4096, 1000, True)])
+def test_gather_minibatch_next_all_field_granularities(n, B, shuffle):
+    """rai_gather_minibatch_next (csrc/rollout.hip) on fields of 16-, 4- and 1-byte units (f32 image
+    rows, i64 actions, f32 scalars, u8 masks, odd-width u8 rows), a ragged last minibatch and the
+    on-device minibatch advance: every minibatch equals the index-gathered rows, bit for bit, and
+    desc->mb / desc->arrivals end at (number of minibatches, 0)."""
+    import ctypes as C
+
+    from rl_algo_impls_amd import _lib
+    from rl_algo_impls_amd.graphs import GraphedUpdate
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(n + B)
+    fields = [torch.randn(n, 4, 9, 7, generator=g).to(dev),                       # 1008 B rows (16-B units)
+              torch.randint(0, 9, (n, 3), generator=g).to(dev),                   # 24 B rows (4-B units)
+              torch.randn(n, generator=g).to(dev),                                # 4 B rows
+              (torch.rand(n, 5, 7, generator=g) < 0.5).to(dev),                   # 35 B rows (1-B units)
+              torch.randint(0, 255, (n, 48), generator=g, dtype=torch.uint8).to(dev)]  # 48 B rows
+    gu = GraphedUpdate(dev)
+    gu.set_rollout(fields, B, shuffle)
+    perm = torch.randperm(n, generator=g).to(dev) if shuffle else None
+    gu.start_epoch(perm)
+    idx = perm if shuffle else torch.arange(n, device=dev)
+    row_bytes = [int(f[0].numel() * f.element_size()) for f in fields]
+    nmb = (n + B - 1) // B
+    for mb in range(nmb):
+        rows = min(B, n - mb * B)
+        out = [torch.full((B,) + tuple(f.shape[1:]), 7, dtype=f.dtype, device=dev) for f in fields]
+        dst = (C.c_void_p * len(out))(*[o.data_ptr() for o in out])
+        rb = (C.c_int64 * len(out))(*row_bytes)
+        rc = _lib.lib().rai_gather_minibatch_next(gu.desc.data_ptr(), len(out), C.cast(dst, C.c_void_p),
+                                                  C.cast(rb, C.c_void_p), B, _lib.stream_handle(dev))
+        assert rc == 0
+        sel = idx[mb * B: mb * B + rows]
+        for f, o in zip(fields, out):
+            assert torch.equal(o[:rows], f[sel])
+            if rows < B:  # rows past the ragged tail are left untouched
+                assert torch.equal(o[rows:], torch.full_like(o[rows:], 7))
+    torch.cuda.synchronize()
+    d = _lib.MinibatchDesc.from_buffer_copy(bytes(gu.desc.cpu().numpy()))
+    assert d.mb == nmb and d.arrivals == 0
