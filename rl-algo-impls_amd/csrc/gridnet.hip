@@ -85,6 +85,7 @@ __device__ __forceinline__ GroupStats group_stats(const float* z, const uint8_t*
 // thread before any LDS store: a load -> store loop waits out one HBM round trip per element
 // (measured: 298 us per 64-sample rollout launch with the plain loop).
 constexpr int GN_BATCH = 8;
+constexpr int GN_REG = 64;  // planes up to this size are sampled from registers
 __device__ __forceinline__ void load_tile(const GridArgs& a, int64_t base, int span, float* zt, uint8_t* mt,
                                           int tid) {
   for (int i0 = tid; i0 < span; i0 += GN_BATCH * GN_THREADS) {
@@ -194,6 +195,7 @@ __global__ __launch_bounds__(GN_THREADS) void gridnet_sample_kernel(const GridAr
   float* zt = smem;                                                     // [GN_CELLS][A]
   uint8_t* mt = reinterpret_cast<uint8_t*>(smem + GN_CELLS * A);       // [GN_CELLS][A]
   __shared__ int act_s[GN_CELLS * RAI_GRID_MAX_G];
+  __shared__ float lp_s[GN_CELLS * RAI_GRID_MAX_G];  // log-prob of each drawn value (before gating)
   __shared__ double red[GN_THREADS / 64];
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -210,39 +212,73 @@ __global__ __launch_bounds__(GN_THREADS) void gridnet_sample_kernel(const GridAr
       const int o = a.off[g], n = a.off[g + 1] - o;
       const float* z = zt + cl * A + o;
       const uint8_t* m = mt + cl * A + o;
-      float mx = GN_NEG;
-      for (int j = 0; j < n; ++j) mx = fmaxf(mx, m[j] ? z[j] : GN_NEG);
-      float tot = 0.f;
-      for (int j = 0; j < n; ++j) tot += expf((m[j] ? z[j] : GN_NEG) - mx);
       const uint64_t item = (uint64_t)((b * C + c0 + cl) * (int64_t)G + g);
       const Philox4 r = philox4x32_10(a.offset, item, a.seed);
-      const float target = u01_open0(r.x) * tot;
-      int pick = -1, last = 0;
-      float cum = 0.f;
-      for (int j = 0; j < n; ++j) {
-        const float pj = expf((m[j] ? z[j] : GN_NEG) - mx);
-        if (pj > 0.f) last = j;
-        cum += pj;
-        if (pick < 0 && cum >= target && pj > 0.f) pick = j;
+      int pick;
+      float lp;
+      if (n <= GN_REG) {
+        // the plane's masked logits in registers: one pipelined sweep of LDS reads instead of three
+        // dependent sweeps (each iteration of the LDS loops below waits out an LDS round trip)
+        float v[GN_REG];
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < GN_REG; ++j) {
+          const bool on = j < n && m[j];
+          v[j] = on ? z[j] : GN_NEG;
+          any = any || on;
+        }
+        float mx = GN_NEG;
+#pragma unroll
+        for (int j = 0; j < GN_REG; ++j)
+          if (j < n) mx = fmaxf(mx, v[j]);
+        float tot = 0.f;
+#pragma unroll
+        for (int j = 0; j < GN_REG; ++j) {
+          v[j] = j < n ? expf(v[j] - mx) : 0.f;
+          tot += v[j];
+        }
+        const float target = u01_open0(r.x) * tot;
+        int last = 0;
+        float cum = 0.f;
+        pick = -1;
+#pragma unroll
+        for (int j = 0; j < GN_REG; ++j) {
+          if (v[j] > 0.f) last = j;
+          cum += v[j];
+          if (pick < 0 && cum >= target && v[j] > 0.f) pick = j;
+        }
+        if (pick < 0) pick = last;  // rounding at the top of the CDF
+        // log-prob exactly as group_stats + the forward kernel: lse = max + log(sum exp(x - max))
+        lp = any ? (m[pick] ? z[pick] : GN_NEG) - (mx + logf(tot)) : 0.f;
+      } else {
+        float mx = GN_NEG;
+        for (int j = 0; j < n; ++j) mx = fmaxf(mx, m[j] ? z[j] : GN_NEG);
+        float tot = 0.f;
+        for (int j = 0; j < n; ++j) tot += expf((m[j] ? z[j] : GN_NEG) - mx);
+        const float target = u01_open0(r.x) * tot;
+        int last = 0;
+        float cum = 0.f;
+        pick = -1;
+        for (int j = 0; j < n; ++j) {
+          const float pj = expf((m[j] ? z[j] : GN_NEG) - mx);
+          if (pj > 0.f) last = j;
+          cum += pj;
+          if (pick < 0 && cum >= target && pj > 0.f) pick = j;
+        }
+        if (pick < 0) pick = last;  // rounding at the top of the CDF
+        const GroupStats st = group_stats(z, m, n);
+        lp = st.nvalid > 0 ? (m[pick] ? z[pick] : GN_NEG) - st.lse : 0.f;
       }
-      if (pick < 0) pick = last;  // rounding at the top of the CDF
       act_s[cl * G + g] = pick;
+      lp_s[cl * G + g] = lp;
       a.actions_out[(b * C + c0 + cl) * (int64_t)G + g] = pick;
     }
     __syncthreads();
     for (int it = tid; it < items; it += GN_THREADS) {
       const int cl = it / G, g = it - cl * G;
-      const int o = a.off[g], n = a.off[g + 1] - o;
-      const float* z = zt + cl * A + o;
-      const uint8_t* m = mt + cl * A + o;
       const int ref = a.sub_ref[g];
       const bool gate = ref < 0 || act_s[cl * G + ref] == a.sub_val[g];
-      if (gate) {
-        const GroupStats st = group_stats(z, m, n);
-        const int ag = act_s[cl * G + g];
-        const float za = m[ag] ? z[ag] : GN_NEG;
-        acc_lp += (double)(st.nvalid > 0 ? za - st.lse : 0.f);
-      }
+      if (gate) acc_lp += (double)lp_s[cl * G + g];
     }
     __syncthreads();
   }
