@@ -379,6 +379,14 @@ int64_t rai_mlp_wide_workspace_bytes(int64_t B, int32_t hidden);
 int rai_mlp_wide_forward(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,
                          float* logp_out, float* entropy_out, float* v_out, void* workspace,
                          int64_t workspace_bytes, void* stream);
+/* rai_mlp_wide_forward followed by rai_ppo_loss (K = 1) with the head and the loss in ONE
+ * workgroup launch: same arguments as the two calls, same results (the loss body is shared). */
+int rai_mlp_wide_forward_loss(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,
+                              float* logp_out, float* entropy_out, float* v_out, const float* old_logp,
+                              const float* old_values, const float* advantages, const float* returns,
+                              const rai_ppo_hparams* hp, rai_train_state* state, float* d_logp, float* d_entropy,
+                              float* d_values, float* stats, int32_t max_stats, void* workspace,
+                              int64_t workspace_bytes, void* stream);
 int rai_mlp_wide_backward(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,
                           const float* d_logp, const float* d_entropy, const float* d_v, void* workspace,
                           int64_t workspace_bytes, void* stream);

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(WT) void wide_fwd2_kernel(const WideArgs a) {
 }
 
 // ---- head: outputs, log-prob, entropy, value --------------------------------------------------
-__global__ __launch_bounds__(WT) void wide_head_kernel(const WideArgs a) {
+__device__ __forceinline__ void wide_head_body(const WideArgs& a) {
   __shared__ float outs[RAI_WIDE_MAX_B][OUTM + 1];
   const rai_mlp_wide_desc& d = a.d;
   const int H = d.hidden, B = a.B, S = H / SL, A = d.out_pi, t = threadIdx.x;
@@ -294,6 +294,20 @@ __global__ __launch_bounds__(WT) void wide_head_kernel(const WideArgs a) {
       a.ent[b] = h;
     }
   }
+}
+
+__global__ __launch_bounds__(WT) void wide_head_kernel(const WideArgs a) { wide_head_body(a); }
+
+#include "loss_body.h"
+
+// Head + PPO loss in one workgroup: the head's logp / entropy / v rows go to global memory and,
+// after the workgroup barrier (workgroup-scope visibility of the block's own global stores), the
+// loss body reads them back with the same code and order as rai_ppo_loss.  One launch fewer on
+// the minibatch chain.
+__global__ __launch_bounds__(WT) void wide_head_loss_kernel(const WideArgs a, const LossArgs la) {
+  wide_head_body(a);
+  __syncthreads();
+  pg_loss_body<1>(la);
 }
 
 // dLoss/dOut for row b of network n (recomputed by every workgroup that needs it); for the Gaussian
@@ -533,6 +547,51 @@ extern "C" int rai_mlp_wide_forward(const rai_mlp_wide_desc* desc, const float* 
   hipLaunchKernelGGL(wide_fwd2_kernel, grid, dim3(WT), 0, st, a);
   RAI_LAUNCH_CHECK();
   hipLaunchKernelGGL(wide_head_kernel, dim3(1), dim3(WT), 0, st, a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_mlp_wide_forward_loss(const rai_mlp_wide_desc* desc, const float* obs, const void* actions,
+                                         int64_t B, float* logp_out, float* entropy_out, float* v_out,
+                                         const float* old_logp, const float* old_values, const float* advantages,
+                                         const float* returns, const rai_ppo_hparams* hp, rai_train_state* state,
+                                         float* d_logp, float* d_entropy, float* d_values, float* stats,
+                                         int32_t max_stats, void* workspace, int64_t workspace_bytes, void* stream) {
+  int rc = check(desc, B, obs, workspace, workspace_bytes);
+  if (rc != RAI_OK) return rc;
+  if (!actions || !logp_out || !entropy_out || !v_out || !advantages || !returns || !hp || !state || !d_logp ||
+      !d_entropy || !d_values)
+    return RAI_E_NULLPTR;
+  WideArgs a = make_args(desc, obs, B, workspace);
+  a.actions = actions;
+  a.logp = logp_out;
+  a.ent = entropy_out;
+  a.v = v_out;
+  LossArgs la;
+  la.new_logp = logp_out;
+  la.entropy = entropy_out;
+  la.new_values = v_out;
+  la.old_logp = old_logp ? old_logp : logp_out;
+  la.old_values = old_values ? old_values : v_out;
+  la.adv = advantages;
+  la.ret = returns;
+  la.hp = hp;
+  la.state = state;
+  la.d_logp = d_logp;
+  la.d_entropy = d_entropy;
+  la.d_values = d_values;
+  la.stats = stats;
+  la.B = B;
+  la.n_entropy = desc->head == 1 ? B * desc->out_pi : B;
+  la.K = 1;
+  la.max_stats = max_stats;
+  const dim3 grid(desc->hidden / SL, 2);
+  hipStream_t st = rai_stream(stream);
+  hipLaunchKernelGGL(wide_fwd1_kernel, grid, dim3(WT), 0, st, a);
+  RAI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(wide_fwd2_kernel, grid, dim3(WT), 0, st, a);
+  RAI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(wide_head_loss_kernel, dim3(1), dim3(WT), 0, st, a, la);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

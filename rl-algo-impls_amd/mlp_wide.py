@@ -3,8 +3,8 @@
 For ActorCritics whose network is ConnectedTrio with a Flatten encoder and separate
 [in -> H -> H -> out] actor / critic MLPs (H in {64, 128, 192, 256}; the HalfCheetah-class
 policies of rl_algo_impls/hyperparams/ppo.yml), the minibatch forward + backward of
-rl_algo_impls/ppo/ppo.py:290-377 runs as rai_mlp_wide_forward -> rai_ppo_loss ->
-rai_mlp_wide_backward (5 + 1 launches) instead of the PyTorch module forward and autograd.
+rl_algo_impls/ppo/ppo.py:290-377 runs as rai_mlp_wide_forward_loss (forward + head + loss) ->
+rai_mlp_wide_backward (5 launches) instead of the PyTorch module forward and autograd.
 The descriptor holds the parameter and flat-gradient pointers (stable for the trainer's life:
 FlatParams never reallocates), so the launches can be captured into the replayed minibatch graph.
 """
@@ -114,6 +114,25 @@ class WideStep:
                                              v.data_ptr(), ws.data_ptr(), ws.numel() * 4,
                                              _lib.stream_handle(self.device))
         _lib.check(rc, "rai_mlp_wide_forward")
+
+    def forward_loss(self, obs: torch.Tensor, actions: torch.Tensor, logp, ent, v, blocks, old_logp, old_values,
+                     adv, ret):
+        """forward() + rai_ppo_loss (K = 1) as rai_mlp_wide_forward_loss: the head and the loss share
+        one launch.  Returns the loss gradients (d_logp, d_entropy, d_v) for backward()."""
+        B = int(obs.shape[0])
+        if B > _lib.RAI_WIDE_MAX_B:
+            raise ValueError(f"minibatch of {B} rows exceeds RAI_WIDE_MAX_B={_lib.RAI_WIDE_MAX_B}")
+        obs = obs if obs.dtype == torch.float32 else obs.float()
+        ws = self.workspace(B)
+        d_logp, d_ent, d_v = blocks.grad_buffers(logp, ent, v)
+        p = lambda t: None if t is None else t.contiguous().data_ptr()
+        rc = _lib.lib().rai_mlp_wide_forward_loss(
+            C.byref(self.desc), obs.contiguous().data_ptr(), actions.contiguous().data_ptr(), B, logp.data_ptr(),
+            ent.data_ptr(), v.data_ptr(), p(old_logp), p(old_values), p(adv), p(ret), blocks.hp.data_ptr(),
+            blocks.state.data_ptr(), d_logp.data_ptr(), d_ent.data_ptr(), d_v.data_ptr(), blocks.stats.data_ptr(),
+            int(blocks.stats.shape[0]), ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(self.device))
+        _lib.check(rc, "rai_mlp_wide_forward_loss")
+        return d_logp, d_ent, d_v
 
     def backward(self, obs: torch.Tensor, actions: torch.Tensor, d_logp, d_ent, d_v) -> None:
         B = int(obs.shape[0])

@@ -490,9 +490,9 @@ class PPO:
             if outs is None:
                 outs = self._wide_out[B] = wide.outputs(B)
             logp, ent, v = outs
-            wide.forward(obs, actions, logp, ent, v)
             K_box[0] = 1
-            d_logp, d_ent, d_v = launch_loss(self.blocks, logp, ent, v, logprobs, values, adv, ret, 1)
+            d_logp, d_ent, d_v = wide.forward_loss(obs, actions, logp, ent, v, self.blocks, logprobs, values, adv,
+                                                   ret)
             wide.backward(obs, actions, d_logp, d_ent, d_v)
             return
         logp, ent, v = self.policy(obs, actions, action_masks=masks)
