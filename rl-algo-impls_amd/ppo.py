@@ -140,24 +140,48 @@ class PPO:
 
         L = _lib.lib()
         rank = dist.get_rank(group)
+
+        def agreed(ok: bool) -> bool:
+            # every rank learns whether every rank's local step succeeded, so a failure on one rank
+            # turns into the same RuntimeError (and the RCCL-loop fallback) on all of them instead
+            # of leaving the others blocked in the next collective
+            f = torch.tensor([0 if ok else 1], dtype=torch.int64, device=self.device)
+            if dist.get_backend(group) == "gloo":
+                f = f.cpu()
+            dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
+            return int(f.item()) == 0
+
         nbytes = int(L.rai_xdp_region_bytes(self.world))
         region = C.c_void_p()
         torch.cuda.synchronize(self.device)
-        _lib.check(L.rai_xdp_alloc(nbytes, C.byref(region)), "rai_xdp_alloc")
         hb = int(L.rai_xdp_handle_bytes())
         hbuf = (C.c_uint8 * hb)()
-        _lib.check(L.rai_xdp_handle(region, hbuf, hb), "rai_xdp_handle")
+        ok = L.rai_xdp_alloc(nbytes, C.byref(region)) == 0 and L.rai_xdp_handle(region, hbuf, hb) == 0
         handles = [None] * self.world
-        dist.all_gather_object(handles, bytes(hbuf), group=group)
+        dist.all_gather_object(handles, bytes(hbuf) if ok else b"", group=group)
+        def release(opened):
+            for p in opened:
+                L.rai_xdp_close(p)
+            if region.value:
+                L.rai_xdp_free(region)
+
+        if not all(handles):
+            release([])
+            raise RuntimeError("cross-GPU exchange: region allocation / IPC export failed on some rank")
         ptrs, opened = [], []
         for r, h in enumerate(handles):
             if r == rank:
                 ptrs.append(region.value)
                 continue
             peer = C.c_void_p()
-            _lib.check(L.rai_xdp_open(h, C.byref(peer)), "rai_xdp_open")
+            if L.rai_xdp_open(h, C.byref(peer)) != 0:
+                ok = False
+                break
             opened.append(peer)
             ptrs.append(peer.value)
+        if not agreed(ok):
+            release(opened)
+            raise RuntimeError("cross-GPU exchange: IPC mapping of a peer region failed on some rank")
         peers = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
         torch.cuda.synchronize(self.device)
         dist.barrier(group=group)  # every region zeroed and mapped before any kernel pushes into it
@@ -171,6 +195,7 @@ class PPO:
             verdict = verdict.cpu()
         dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=group)
         if int(verdict.sum()) != 0:
+            release(opened)
             raise RuntimeError(f"cross-GPU exchange self-test failed (wrong values, timeouts) = {verdict.tolist()}")
         return dict(region=region, opened=opened, peers=peers, rank=rank, step=0)
 
