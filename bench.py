@@ -197,7 +197,7 @@ def main():
     gae_us = e0.elapsed_time(e1) * 1e3 / args.roofline_reps
     workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
     pmc = {}
-    for name in ("r1f_pmc.json", "r1e_pmc.json", "r1d_pmc.json", "r1c_pmc.json", "r1_pmc.json"):  # newest PMC summary holding this workload
+    for name in ("r1g_pmc.json", "r1f_pmc.json", "r1e_pmc.json", "r1d_pmc.json", "r1c_pmc.json", "r1_pmc.json"):  # newest PMC summary holding this workload
         pmc_path = ROOT / "profiles" / name
         if pmc_path.exists():
             pmc = json.loads(pmc_path.read_text()).get(workload, {})
