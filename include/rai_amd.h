@@ -138,6 +138,12 @@ int rai_se_residual_fwd(const float* x, const float* r, const float* s, int64_t 
                         float* out, void* stream);
 int rai_se_residual_bwd(const float* dout, const float* x, const float* r, const float* s, int64_t B, int32_t C,
                         int32_t HW, float* dx, float* dr, float* ds, void* stream);
+/* Conv bias + GELU of the squeeze-U-Net's conv -> GELU pairs (squeeze_unet.py:56-70,117-137,
+ * double_cone.py:58-70, backbone_actor_critic.py:114-133): out = GELU(x + b[c]) over NHWC rows,
+ * and dx = dy * GELU'(x + b) (the bias gradient is dx summed over rows).  C % 4 == 0. */
+int rai_bias_gelu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream);
+int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b, int64_t rows, int32_t C, float* dx,
+                      void* stream);
 
 /* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.

@@ -71,6 +71,68 @@ class _SEResidualEpilogue(torch.autograd.Function):
         return dx, dr, ds
 
 
+class _BiasGelu(torch.autograd.Function):
+    """GELU(x + b) over an NHWC conv output (rai_bias_gelu_fwd / _bwd): MIOpen's separate bias pass and
+    the GELU kernel in one pass; the bias gradient is the rows-sum of dx."""
+
+    @staticmethod
+    def forward(ctx, x, b):
+        from . import _lib
+
+        C = int(x.shape[1])
+        out = torch.empty_like(x)
+        _lib.check(_lib.lib().rai_bias_gelu_fwd(x.data_ptr(), b.data_ptr(), x.numel() // C, C, out.data_ptr(),
+                                                _lib.stream_handle(x.device)), "rai_bias_gelu_fwd")
+        ctx.save_for_backward(x, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+
+        x, b = ctx.saved_tensors
+        C = int(x.shape[1])
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x)
+        _lib.check(_lib.lib().rai_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), b.data_ptr(), x.numel() // C, C,
+                                                dx.data_ptr(), _lib.stream_handle(x.device)), "rai_bias_gelu_bwd")
+        # NHWC: dx viewed (rows, C) is contiguous; the bias gradient is its column sum
+        db = dx.permute(0, 2, 3, 1).reshape(-1, C).sum(0)
+        return dx, db
+
+
+def conv_gelu(conv: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """GELU(conv(x)) for a Conv2d / ConvTranspose2d with bias: on NHWC fp32 GPU activations the
+    convolution runs bias-free on MIOpen and bias + GELU is one HIP pass; else the modules' own path."""
+    if _nhwc(x) and conv.bias is not None and conv.out_channels % 4 == 0:
+        if isinstance(conv, nn.ConvTranspose2d):
+            y = torch.nn.functional.conv_transpose2d(x, conv.weight, None, conv.stride, conv.padding,
+                                                     conv.output_padding, conv.groups, conv.dilation)
+        else:
+            y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation,
+                                           conv.groups)
+        if _nhwc(y):
+            return _BiasGelu.apply(y, conv.bias)
+        return torch.nn.functional.gelu(y + conv.bias.view(1, -1, 1, 1))
+    return torch.nn.functional.gelu(conv(x))
+
+
+def run_sequential(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    """seq(x) with every (conv, GELU) pair through conv_gelu (same modules, same state_dict)."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if (isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)) and i + 1 < len(mods)
+                and isinstance(mods[i + 1], nn.GELU) and mods[i + 1].approximate == "none"):
+            x = conv_gelu(m, x)
+            i += 2
+        else:
+            x = m(x)
+            i += 1
+    return x
+
+
 def se_residual_epilogue(x: torch.Tensor, r: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
     """GELU(x + r * s[..., None, None]); the fused HIP pass for NHWC fp32 GPU activations whose C
     the kernel tiles (C % 4 == 0, C / 4 divides 256), else the PyTorch composition."""
@@ -120,7 +182,7 @@ class SEResidualBlock(nn.Module):  # double_cone.py:50-86 (normalization=None)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         conv0, act, conv1, se = self.residual
-        r = conv1(act(conv0(x)))
+        r = conv1(conv_gelu(conv0, x))  # act = GELU
         b, c = r.shape[0], r.shape[1]
         s = se.fc(se.avg_pool(r).view(b, c))
         return se_residual_epilogue(x, r, s)  # == self.gelu(x + self.residual(x))
@@ -176,11 +238,11 @@ class SqueezeUnetBackbone(nn.Module):  # squeeze_unet.py:20-195
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         skips = []
         for enc in self.encoders:
-            x = enc(x)
+            x = run_sequential(enc, x)
             skips.append(x)
         d = None
         for e, dec in zip(reversed(skips), self.decoders):
-            d = dec(e if d is None else e + d)  # the reference adds zeros_like at the deepest level
+            d = run_sequential(dec, e if d is None else e + d)  # the reference adds zeros_like at the deepest level
         return d
 
 
@@ -195,7 +257,7 @@ class _Transpose(nn.Module):  # actor/gridnet_decoder.py:14-20
 
 class _HStack(nn.ModuleList):  # shared/module/stack.py
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return torch.hstack([m(x) for m in self])
+        return torch.hstack([run_sequential(m, x) for m in self])
 
 
 _OUT_ACT = {"tanh": nn.Tanh, "relu": nn.ReLU, "identity": nn.Identity, "sigmoid": nn.Sigmoid}

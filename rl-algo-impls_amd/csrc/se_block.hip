@@ -110,3 +110,60 @@ extern "C" int rai_se_residual_bwd(const float* dout, const float* x, const floa
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }
+
+// ---- conv bias + GELU epilogue (squeeze-U-Net conv -> GELU pairs) ------------------------------
+// y = gelu(x + b[c]) over NHWC rows (rows = B*H*W, C fastest): MIOpen's separate bias pass
+// (SubTensorOpWithScalar1d) and the GELU kernel become one pass.  Backward: dx = dy * gelu'(x + b);
+// the bias gradient is dx summed over rows (the caller's one reduction).
+namespace {
+// b is read as scalars: a bias is a view into the flat parameter buffer, 4-byte aligned only
+__device__ __forceinline__ f4 ld_bias4(const float* __restrict__ b, int c4) {
+  return f4{b[4 * c4], b[4 * c4 + 1], b[4 * c4 + 2], b[4 * c4 + 3]};
+}
+__global__ __launch_bounds__(SE_THREADS) void bias_gelu_fwd_kernel(const f4* __restrict__ x, const float* __restrict__ b,
+                                                                   int C4, int64_t n4, f4* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)SE_THREADS + threadIdx.x; i < n4; i += (int64_t)gridDim.x * SE_THREADS) {
+    const f4 xv = x[i], bv = ld_bias4(b, (int)(i % C4));
+    f4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = gelu_f(xv[q] + bv[q]);
+    out[i] = o;
+  }
+}
+__global__ __launch_bounds__(SE_THREADS) void bias_gelu_bwd_kernel(const f4* __restrict__ dy, const f4* __restrict__ x,
+                                                                   const float* __restrict__ b, int C4, int64_t n4,
+                                                                   f4* __restrict__ dx) {
+  for (int64_t i = blockIdx.x * (int64_t)SE_THREADS + threadIdx.x; i < n4; i += (int64_t)gridDim.x * SE_THREADS) {
+    const f4 g = dy[i], xv = x[i], bv = ld_bias4(b, (int)(i % C4));
+    f4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = g[q] * gelu_grad(xv[q] + bv[q]);
+    dx[i] = o;
+  }
+}
+int64_t ew_blocks(int64_t n4) { return std::min<int64_t>((n4 + SE_THREADS - 1) / SE_THREADS, 256 * 64); }
+}  // namespace
+
+extern "C" int rai_bias_gelu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream) {
+  if (rows < 0 || C < 4 || C % 4) return RAI_E_SHAPE;
+  if (rows == 0) return RAI_OK;
+  if (!x || !b || !out) return RAI_E_NULLPTR;
+  const int64_t n4 = rows * (C / 4);
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)ew_blocks(n4)), dim3(SE_THREADS), 0, rai_stream(stream),
+                     reinterpret_cast<const f4*>(x), b, C / 4, n4, reinterpret_cast<f4*>(out));
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b, int64_t rows, int32_t C, float* dx,
+                                 void* stream) {
+  if (rows < 0 || C < 4 || C % 4) return RAI_E_SHAPE;
+  if (rows == 0) return RAI_OK;
+  if (!dy || !x || !b || !dx) return RAI_E_NULLPTR;
+  const int64_t n4 = rows * (C / 4);
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((unsigned)ew_blocks(n4)), dim3(SE_THREADS), 0, rai_stream(stream),
+                     reinterpret_cast<const f4*>(dy), reinterpret_cast<const f4*>(x), b, C / 4, n4,
+                     reinterpret_cast<f4*>(dx));
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

@@ -218,3 +218,25 @@ def test_se_residual_epilogue_vs_pytorch(B, C, H):
     for a, b_ in ((out, ref), (dx, rx), (dr, rr), (ds, rs)):
         np.testing.assert_allclose(a.detach().cpu().numpy(), b_.detach().cpu().numpy(), rtol=1e-5, atol=1e-6)
     assert out.is_contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transpose", [False, True])
+def test_conv_bias_gelu_vs_pytorch(transpose):
+    """conv_gelu (bias-free MIOpen conv + rai_bias_gelu_fwd/_bwd) against GELU(conv(x)) with the
+    module's own bias, NHWC fp32: outputs and the gradients of input, weight and bias (rtol 1e-4 /
+    atol 1e-5: the same convolution, the bias added in another pass)."""
+    from rl_algo_impls_amd.backbone import conv_gelu
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    conv = (torch.nn.ConvTranspose2d(32, 64, 2, stride=2) if transpose else torch.nn.Conv2d(32, 64, 3, padding=1)).to(dev)
+    x = torch.randn(5, 32, 8, 8, device=dev).contiguous(memory_format=torch.channels_last).requires_grad_()
+    dy = torch.randn_like(conv(x)).contiguous(memory_format=torch.channels_last)
+    out = conv_gelu(conv, x)
+    got = torch.autograd.grad(out, (x, conv.weight, conv.bias), dy)
+    ref_out = torch.nn.functional.gelu(conv(x))
+    ref = torch.autograd.grad(ref_out, (x, conv.weight, conv.bias), dy)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref_out.detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
+    for a, b_ in zip(got, ref):
+        np.testing.assert_allclose(a.cpu().numpy(), b_.cpu().numpy(), rtol=1e-4, atol=1e-5)
