@@ -29,7 +29,7 @@ from .gridnet import GridnetDistribution, ValueDependentMask
 Strides = Sequence[Union[int, Sequence[int]]]
 # NHWC activations on the GPU (RAI_SQUNET_NHWC=0 keeps NCHW): MIOpen's implicit-GEMM solvers take
 # them without the NCHW<->NHWC transposes, and the fused SE epilogue below runs on them.  (The
-# NatureCNN encoder's RAI_CHANNELS_LAST stays off by default: NHWC measured within noise on Pong.)
+# NatureCNN encoder has its own switch, RAI_CHANNELS_LAST, also on by default.)
 _CHANNELS_LAST = os.environ.get("RAI_SQUNET_NHWC", "1") == "1"
 if _CHANNELS_LAST:
     os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC", "1")

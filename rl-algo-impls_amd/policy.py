@@ -38,7 +38,10 @@ MODEL_FILENAME = "model.pth"
 NORMALIZE_OBSERVATION_FILENAME = "norm_obs.npz"
 NORMALIZE_REWARD_FILENAME = "norm_reward.npz"
 F32_MIN = torch.finfo(torch.float32).min
-_CHANNELS_LAST = os.environ.get("RAI_CHANNELS_LAST", "0") == "1"
+# NatureCNN activations NHWC on the GPU (RAI_CHANNELS_LAST=0: NCHW).  Pong A/B with the fused
+# minibatch gather and Categorical head: 1.611 vs 1.667 s per update (MIOpen's NHWC solvers, no
+# layout transposes, contiguous bias-gradient reductions).
+_CHANNELS_LAST = os.environ.get("RAI_CHANNELS_LAST", "1") == "1"
 
 
 class Step(NamedTuple):  # actor_critic.py:42-46
@@ -120,7 +123,7 @@ class NatureCnnEncoder(nn.Module):
         if obs.dim() == 3:
             obs = obs.unsqueeze(0)
         x = obs.float() / self.range_size
-        if _CHANNELS_LAST:
+        if _CHANNELS_LAST and x.is_cuda:
             x = x.contiguous(memory_format=torch.channels_last)
         return self.fc(self.cnn(x))
 
