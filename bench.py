@@ -68,6 +68,11 @@ def parse():
     p.add_argument("--config", default="cartpole", choices=sorted(CONFIGS))
     p.add_argument("--batch-policy", default="yaml", choices=["yaml", "scaled"],
                    help="yaml: the YAML batch_size; scaled: batch = T*N/4 (4 minibatches/epoch)")
+    p.add_argument("--dp-batch", default="per-rank", choices=["per-rank", "global"],
+                   help="data-parallel minibatch rule, the same for every config: per-rank = every rank "
+                        "takes batch_size rows of its own rollout per optimizer step (global minibatch "
+                        "batch_size x world; weak scaling); global = SURVEY 8(e): batch_size / world rows "
+                        "per rank, so the global minibatch is the YAML batch_size")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--roofline-reps", type=int, default=200)
@@ -78,8 +83,101 @@ def parse():
     return p.parse_args()
 
 
+def latency_roofline(G: int, avg_ms: float, steps_per_launch: int, kname: str) -> dict:
+    """Per-optimizer-step latency floor of the fused CartPole epoch kernel (csrc/mlp_mc8.h) from the
+    MI355X price list (/opt/skills/guides/MI355X_MICROARCH.md), against the measured step time.
+
+    A launch is `steps_per_launch` DEPENDENT optimizer steps (step k+1's forward reads step k's Adam
+    output, rl_algo_impls/ppo/ppo.py:375,441-447), so the bound is the critical path of one step:
+      * the MFMA chain of one wave: at G = 16 a wave owns one 16-row tile x 16 hidden columns, so
+        layer 2 forward and dH1 are 16 dependent v_mfma_f32_16x16x4f32 each (40-cycle dependent
+        latency, constants table), layer 1 one more, and dW2 16 independent-accumulator MFMAs at
+        the 32-cycle issue rate: (1 + 16 + 16) x 40 + 16 x 32 = 1,832 cycles at 2.4 GHz (G = 8:
+        two tiles of 32 columns per wave, 3,136 cycles);
+      * two cross-CU all-to-all edges among the network's G CUs (reduce-scatter, then all-gather of
+        the summed gradient and the share norms), each at least the price list's 'allgather' row
+        at its cheapest (8 KB published by 32 CUs, parked: 2.4 us).
+    frac = floor / measured us per step: the share of the step the hardware's latencies account for."""
+    RC = 256 // G  # rows per CU; CT 16-column tiles per wave (csrc/mlp_mc8.h M8Geo)
+    CT = 64 // 16 // (4 // (RC // 16))
+    chain = lambda n_dep, n_issue: max(n_dep * 40, n_issue * 32)  # dependent latency vs issue rate
+    mfma_cycles = chain(1, CT) + 2 * chain(16, 16 * CT) + chain(RC // 4, RC)
+    t_mfma = mfma_cycles / 2.4e3  # us at 2.4 GHz
+    t_edge = 2.4
+    floor_us = t_mfma + 2 * t_edge
+    step_us = avg_ms * 1e3 / max(steps_per_launch, 1)
+    return {"kernel": kname, "bound": "latency", "achieved": round(step_us, 3), "peak": round(floor_us, 3),
+            "unit": "us per dependent optimizer step", "frac": round(floor_us / step_us, 4),
+            "floor_terms_us": {"mfma_chain": round(t_mfma, 3), "allgather_edges": 2 * t_edge},
+            "steps_per_launch": steps_per_launch}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(args, N: int, T: int, algo_kw: dict) -> dict:
+    """The reference's CPU trainer restated (oracle/cpu_trainer.py, pinned to the reference's own
+    learn_epoch and NatureCNN steps by tests/test_cpu_trainer.py) on the host cores, rank 0 only.
+    A whole C2 update is ~60 s of CPU, so the C2 line times the full rollout + GAE and a bounded
+    sample of the update's minibatch steps (extrapolated); the extrapolation's error is measured on a
+    whole update 32x smaller (N/32 envs, the same 20 epochs), timed whole and sampled at the same
+    fraction of its steps."""
+    import torch
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cpu_trainer  # checker/baseline only
+
+    torch.set_num_threads(min(os.cpu_count() or 1, 16))  # the box's CPU share (16 per GPU)
+    kw = dict(n_steps=T, batch_size=algo_kw["batch_size"], n_epochs=algo_kw["n_epochs"])
+    res = cpu_trainer.time_update(args.cpu_baseline_seconds, num_envs=N, **kw)
+    # the same sampled fraction of a whole update 32x smaller, against that update timed whole
+    frac = res["minibatches_timed"] / res["minibatches_total"]
+    small_n = max(1, N // 32)
+    full_small = cpu_trainer.time_update(None, num_envs=small_n, **kw)
+    budget = frac * (full_small["update_s"] - full_small["rollout_s"] - full_small["gae_s"])
+    est_small = cpu_trainer.time_update(max(budget, 0.05), num_envs=small_n, **kw)
+    err = est_small["update_s"] / full_small["update_s"] - 1.0
+    return {"value": round(res["env_steps_per_s"], 1), "unit": "env-steps/s", "cores": res["threads"],
+            "kind": "port", "cpu_model": cpu_model(),
+            "sample": (f"full rollout {T}x{N} + numpy GAE + {res['minibatches_timed']} of "
+                       f"{res['minibatches_total']} minibatch steps timed, update time extrapolated "
+                       f"(oracle/cpu_trainer.py, torch CPU eager like the reference)"),
+            "extrapolation_check": {"num_envs": small_n, "full_update_s": round(full_small["update_s"], 3),
+                                    "extrapolated_update_s": round(est_small["update_s"], 3),
+                                    "sampled_steps": est_small["minibatches_timed"],
+                                    "total_steps": est_small["minibatches_total"], "rel_error": round(err, 4)}}
+
+
+def _diagnostics(tag: str) -> None:
+    """RAI_DIAG_DIR=<dir>: Python stacks of every thread on a fatal signal (faulthandler) and
+    this process's /proc/self/maps at each stage, so a native crash's PCs (which are per process
+    under ASLR) can be mapped to a library and offset afterwards."""
+    d = os.environ.get("RAI_DIAG_DIR")
+    if not d:
+        return
+    import faulthandler
+
+    os.makedirs(d, exist_ok=True)
+    if not faulthandler.is_enabled():
+        _diagnostics.fh = open(os.path.join(d, f"faulthandler_{os.getpid()}.txt"), "w")
+        faulthandler.enable(file=_diagnostics.fh, all_threads=True)
+    with open("/proc/self/maps") as src, open(os.path.join(d, f"maps_{os.getpid()}_{tag}.txt"), "w") as dst:
+        dst.write(src.read())
+    print(f"[bench] diag: {tag} pid {os.getpid()}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
+    _diagnostics("start")
     import numpy as np
     import torch
 
@@ -117,14 +215,17 @@ def main():
     cfg = CONFIGS[args.config]
     N, T = (args.num_envs or cfg["num_envs"]), cfg["n_steps"]
     algo_kw = dict(cfg["algo"])
-    if args.config in ("halfcheetah", "microrts") and world > 1:
-        N = N // world  # configs[3] / configs[4] are quoted as a global env count across the node
-    if args.config == "microrts":
-        algo_kw["batch_size"] = max(1, algo_kw["batch_size"] // world)
-        if args.num_envs:  # rehearsal at fewer envs: keep the YAML's minibatches per epoch
-            algo_kw["batch_size"] = max(1, algo_kw["batch_size"] * N // cfg["num_envs"])
+    # env partition: configs[3] / configs[4] are quoted as a global env count across the node (each rank
+    # owns N / world envs); configs[1] / configs[2] are single-GPU configs (each rank owns N envs)
+    global_envs = args.config in ("halfcheetah", "microrts")
+    if global_envs and world > 1:
+        N = N // world
+    if args.config == "microrts" and args.num_envs:  # rehearsal at fewer envs: keep the YAML's minibatches
+        algo_kw["batch_size"] = max(1, algo_kw["batch_size"] * N // cfg["num_envs"])
     if args.batch_policy == "scaled":
         algo_kw["batch_size"] = T * N // 4
+    if args.dp_batch == "global" and algo_kw["batch_size"] % world:
+        raise SystemExit(f"--dp-batch global: batch_size {algo_kw['batch_size']} not divisible by {world}")
     torch.manual_seed(1 + rank)
     env = SyntheticVecEnv(N, cfg["env"], seed=1000 * rank + 1)
     policy = ActorCritic(env, **cfg["policy"]).to(dev)
@@ -134,8 +235,8 @@ def main():
                 torch.distributed.broadcast(p.data, 0)
     gen = SyncStepRolloutGenerator(policy, env, n_steps=T, seed=1234 + rank)
     algo = PPO(policy, dev, None, **algo_kw)
-    if world > 1 or args.dp_rehearsal:
-        algo.enable_data_parallel()
+    if world > 1 or args.dp_rehearsal:  # minibatch rule: one for every config, named in the JSON line
+        algo.enable_data_parallel(dp_batch=args.dp_batch)
 
     def barrier():
         if world > 1:
@@ -148,6 +249,7 @@ def main():
                   f"(this update: rollout {getattr(algo, 'last_rollout_seconds', 0.0):.3f} s of "
                   f"{getattr(algo, 'last_update_seconds', 0.0):.3f} s)", file=sys.stderr, flush=True)
 
+    _diagnostics("setup")
     for i in range(args.warmup):
         tw = time.perf_counter()
         algo.learn_epoch(0, 1, gen, None)
@@ -158,6 +260,8 @@ def main():
     for i in range(args.steps):
         algo.learn_epoch(0, 1, gen, None)
         progress("timed", i, t0)
+        if i == 0:
+            _diagnostics("update0")
     barrier()
     elapsed = time.perf_counter() - t0
     epoch_ms = [e0.elapsed_time(e1) for e0, e1 in algo.kernel_events]
@@ -228,21 +332,14 @@ def main():
                     "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
                     "traffic": traffic(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
+        roof_lat = latency_roofline(G, ms, (T * N + algo.batch_size - 1) // algo.batch_size, kname)
     else:
         roofline = roof_gae
+        roof_lat = None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "cartpole":
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import cpu_trainer  # checker/baseline only
-
-        res = cpu_trainer.time_sampled_update(budget_seconds=args.cpu_baseline_seconds, num_envs=N, n_steps=T,
-                                              batch_size=algo_kw["batch_size"], n_epochs=algo_kw["n_epochs"])
-        cpu = {"value": round(res["env_steps_per_s"], 1), "unit": "env-steps/s", "cores": res["threads"],
-               "kind": "port",
-               "sample": (f"full rollout {T}x{N} + numpy GAE + {res['minibatches_timed']} of "
-                          f"{res['minibatches_total']} minibatch steps timed, update time extrapolated "
-                          f"(oracle/cpu_trainer.py, torch CPU eager like the reference)")}
+        cpu = cpu_baseline(args, N, T, dict(algo_kw, batch_size=algo.batch_size))
 
     if rank == 0:
         line = {
@@ -259,9 +356,13 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded host VecEnv with the config's obs/action shapes; random-init policy)",
             "config": {"workload": workload,
-                       "global_batch": algo_kw["batch_size"] * world, "n_epochs": algo_kw["n_epochs"],
-                       "batch_policy": args.batch_policy, "seq_len": T, "parallelism": f"dp{world}"},
+                       "global_batch": algo.global_batch_size if algo.dp_enabled else algo.batch_size,
+                       "per_rank_batch": algo.batch_size,
+                       "dp_batch": args.dp_batch, "env_partition": "split" if global_envs else "per-rank",
+                       "n_epochs": algo_kw["n_epochs"], "batch_policy": args.batch_policy, "seq_len": T,
+                       "parallelism": f"dp{world}"},
             "roofline": roofline,
+            "roofline_latency": roof_lat,
             "roofline_gae": roof_gae,
             "cpu_baseline": cpu,
         }

@@ -385,9 +385,10 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
 #endif
   __syncthreads();
 
-  // Bounded waits, by elapsed shader-clock ticks (~2.4 GHz): 2 s for partners on this GPU (they are
-  // co-resident and a minibatch apart at most), 60 s for other GPUs (their ranks can start an
-  // epoch later by host-side jitter: rollouts, collectives).  A timeout sets err and stops the CU.
+  // Bounded waits, by elapsed s_memrealtime ticks (the constant 100 MHz counter, common.h
+  // rai_clock): 2 s for partners on this GPU (they are co-resident and a minibatch apart at most),
+  // 60 s for other GPUs (their ranks can start an epoch later by host-side jitter: rollouts,
+  // collectives).  A timeout sets err and stops the CU.
   constexpr long long MC_WAIT_LOCAL = RAI_SPIN_LOCAL, MC_WAIT_REMOTE = RAI_SPIN_REMOTE;
   for (int mb = mb_begin; mb < mb_end; ++mb) {
     const int kk_mb = mb - mb_begin;

@@ -91,23 +91,42 @@ class PPO:
         self.world = 1
         self._dp_comm = None
         self.dp_enabled = False  # enable_data_parallel() called (any world size, incl. 1-rank rehearsal)
+        self.dp_batch = "per-rank"
+        self.global_batch_size = batch_size
 
     # -- data parallel (one process per GPU) ------------------------------------------------
-    def enable_data_parallel(self, group=None, native_dp: bool = True, xdp: Optional[bool] = None) -> None:
-        """Weak-scaling data parallelism: every rank owns its own env group and HBM rollout;
-        a global minibatch is the union of the ranks' minibatch slices, gradients are summed
-        over ranks with one RCCL all-reduce per optimizer step (rccl/xGMI via
-        torch.distributed), and every rank applies the identical clip+Adam step.  The
+    def enable_data_parallel(self, group=None, native_dp: bool = True, xdp: Optional[bool] = None,
+                             dp_batch: str = "per-rank") -> None:
+        """Data parallelism: every rank owns its own env group and HBM rollout; a global
+        minibatch is the union of the ranks' minibatch slices, gradients are summed over ranks
+        with one all-reduce per optimizer step (RCCL over xGMI via torch.distributed, or the
+        in-kernel exchange), and every rank applies the identical clip+Adam step.  The
         advantage normalisation uses global per-minibatch moments (one small all-reduce per
         epoch), reproducing the reference's normalisation over the whole (global) minibatch:
         on the fused MLP path through the kernels' moments argument, on the per-minibatch path
         through rai_ppo_hparams.ext_moments (per advantage column, or of the weighted advantage
-        under normalize_advantages_after_scaling)."""
+        under normalize_advantages_after_scaling).
+
+        dp_batch: "per-rank" — each rank takes batch_size rows per optimizer step (global
+        minibatch batch_size x world); "global" — SURVEY.md 8(e)'s rule: batch_size / world rows
+        per rank, so the global minibatch is batch_size (rl_algo_impls/ppo/ppo.py:314,
+        rollout/vec_rollout.py:108-111) and the update equals the single-process one over the
+        ranks' interleaved rollouts."""
         import torch.distributed as dist
 
         self.dp_group = group
         self.dp_enabled = True
         self.world = dist.get_world_size(group)
+        if dp_batch not in ("per-rank", "global"):
+            raise ValueError(f"dp_batch must be 'per-rank' or 'global', not {dp_batch!r}")
+        self.dp_batch = dp_batch
+        self.global_batch_size = self.batch_size * self.world
+        if dp_batch == "global":
+            if self.batch_size % self.world:
+                raise ValueError(f"dp_batch='global': batch_size {self.batch_size} is not divisible by the "
+                                 f"world size {self.world}")
+            self.global_batch_size = self.batch_size
+            self.batch_size //= self.world
         self._dp_comm = None
         self._xdp = None
         if xdp is None:
@@ -187,10 +206,15 @@ class PPO:
         dist.barrier(group=group)  # every region zeroed and mapped before any kernel pushes into it
         # canary: the epoch kernel's memory, scopes and flag protocol on a known payload, on every rank
         bad = torch.zeros(2, dtype=torch.int32, device=self.device)
-        _lib.check(L.rai_xdp_selftest(peers.data_ptr(), self.world, rank, 1, bad.data_ptr(),
-                                      _lib.stream_handle(self.device)), "rai_xdp_selftest")
+        if os.environ.get("RAI_XDP_INJECT_FAIL_RANK", "") == str(rank):
+            rc = -1  # test hook: this rank's canary "fails" without launching (its partners time out)
+        else:
+            rc = L.rai_xdp_selftest(peers.data_ptr(), self.world, rank, 1, bad.data_ptr(),
+                                    _lib.stream_handle(self.device))
         torch.cuda.synchronize(self.device)
         verdict = bad.to(torch.int64)
+        if rc != 0:  # a launch failure joins the verdict instead of raising on this rank alone
+            verdict[0] += 1
         if dist.get_backend(group) == "gloo":
             verdict = verdict.cpu()
         dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=group)

@@ -63,12 +63,18 @@ def moments_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def fused_dp_worker(rank, world, port, q, backend="gloo"):
+def fused_dp_worker(rank, world, port, q, backend="gloo", dp_batch="per-rank", inject_fail_rank=None):
     """DP fused update on rank-local data (gloo: all ranks on cuda:0, Python-driven loop;
-    nccl (world 1 on a one-GPU box): the natively driven RCCL loop, rai_mlp_ppo_epoch_dp)."""
+    nccl (world 1 on a one-GPU box): the natively driven RCCL loop, rai_mlp_ppo_epoch_dp).
+    128 rows per rank per optimizer step under either minibatch rule: batch_size 128 with
+    dp_batch="per-rank", batch_size 256 (the global minibatch) with dp_batch="global".
+    inject_fail_rank: that rank's in-kernel exchange canary reports a failure (every rank must
+    then fall back to the per-step loop together)."""
     import numpy as np
     import torch
 
+    if inject_fail_rank is not None:
+        os.environ["RAI_XDP_INJECT_FAIL_RANK"] = str(inject_fail_rank)
     _init(rank, world, port, backend)
     import _pkgload
 
@@ -80,9 +86,11 @@ def fused_dp_worker(rank, world, port, q, backend="gloo"):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     policy = nets.build("cartpole").to(dev)
-    algo = PPO(policy, dev, None, batch_size=128, n_epochs=2, learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
-    algo.enable_data_parallel(xdp=os.environ.get("RAI_XDP", "1") != "0")
-    expect_xdp = world > 1 and os.environ.get("RAI_XDP", "1") != "0"
+    bs = 128 * (world if dp_batch == "global" else 1)
+    algo = PPO(policy, dev, None, batch_size=bs, n_epochs=2, learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
+    algo.enable_data_parallel(xdp=os.environ.get("RAI_XDP", "1") != "0", dp_batch=dp_batch)
+    assert algo.batch_size == 128 and algo.global_batch_size == 128 * world
+    expect_xdp = world > 1 and os.environ.get("RAI_XDP", "1") != "0" and inject_fail_rank is None
     assert (algo._dp_comm is not None) == (backend == "nccl" and not expect_xdp)
     assert (algo._xdp is not None) == expect_xdp, "in-kernel exchange not set up"
     data = make_rank_data(rank, dev)
@@ -177,9 +185,10 @@ def wide_policy_and_rollout(d, dev, hidden=128):
     return policy, r
 
 
-def wide_dp_worker(rank, world, port, q):
+def wide_dp_worker(rank, world, port, q, dp_batch="per-rank"):
     """Data-parallel update through the wide-MLP kernels (gloo, all ranks on cuda:0): global advantage
-    moments per minibatch (rai_ppo_hparams.ext_moments), gradient all-reduce per step."""
+    moments per minibatch (rai_ppo_hparams.ext_moments), gradient all-reduce per step.  64 rows per
+    rank per step: batch_size 64 per rank ("per-rank") or the global 128 ("global")."""
     import torch
 
     _init(rank, world, port)
@@ -190,8 +199,10 @@ def wide_dp_worker(rank, world, port, q):
 
     dev = torch.device("cuda", 0)
     policy, r = wide_policy_and_rollout(make_wide_rank_data(rank, dev), dev)
-    algo = PPO(policy, dev, None, batch_size=64, n_epochs=2, learning_rate=3e-4, ent_coef=0.01)
-    algo.enable_data_parallel()
+    algo = PPO(policy, dev, None, batch_size=64 * (world if dp_batch == "global" else 1), n_epochs=2,
+               learning_rate=3e-4, ent_coef=0.01)
+    algo.enable_data_parallel(dp_batch=dp_batch)
+    assert algo.batch_size == 64
     stats, norms, _ = algo.update(r)
     assert algo._wide not in (None, False), "wide path not taken"
     q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
@@ -249,6 +260,34 @@ def mc_dp_worker(rank, world, port, q, after):
     algo.enable_data_parallel()
     stats, norms, _ = algo.update(r)
     q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+def batch_rule_worker(rank, world, port, q):
+    """PPO.enable_data_parallel's minibatch rules on CPU (gloo): per-rank keeps batch_size rows per
+    rank (global minibatch batch_size x world); global splits the YAML batch_size over the ranks and
+    rejects a batch that does not divide; weights are broadcast from rank 0."""
+    import torch
+
+    _init(rank, world, port)
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.ppo import PPO
+    import make_golden_networks as nets
+
+    out = {}
+    for rule, bs in (("per-rank", 256), ("global", 256), ("global", 255)):
+        torch.manual_seed(rank)  # different init per rank: enable_data_parallel must broadcast rank 0's
+        algo = PPO(nets.build("cartpole"), torch.device("cpu"), None, batch_size=bs)
+        try:
+            algo.enable_data_parallel(dp_batch=rule)
+            out[(rule, bs)] = (algo.batch_size, algo.global_batch_size, float(algo.flat.flat.double().sum()))
+        except ValueError as e:
+            out[(rule, bs)] = str(e)
+    q.put((rank, out))
     import torch.distributed as dist
 
     dist.destroy_process_group()

@@ -32,3 +32,24 @@ def test_global_advantage_moments_world2():
         o1, _ = (np.array(x) for x in outs[1][case])
         np.testing.assert_array_equal(o0, o1)  # identical on every rank
         np.testing.assert_allclose(o0, ref0, rtol=1e-5, atol=1e-6)
+
+
+def test_dp_batch_rules_world2():
+    import dp_worker
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.batch_rule_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        out = res[rank]
+        assert out[("per-rank", 256)][:2] == (256, 512)
+        assert out[("global", 256)][:2] == (128, 256)  # B / R rows per rank
+        assert "not divisible" in out[("global", 255)]
+    assert res[0][("global", 256)][2] == res[1][("global", 256)][2]  # identical weights after the broadcast

@@ -18,16 +18,28 @@ def _port():
     return p
 
 
+@pytest.mark.parametrize("dp_batch", ["global", "per-rank"])
 @pytest.mark.parametrize("xdp", ["1", "0"], ids=["in_kernel_xgmi_exchange", "per_step_loop"])
-def test_fused_dp_world2_matches_single_process_global_minibatches(xdp, monkeypatch):
+def test_fused_dp_world2_matches_single_process_global_minibatches(xdp, dp_batch, monkeypatch):
     """xdp=1: one launch per epoch per rank, gradients summed across the two processes inside
     the kernel through IPC-mapped regions (both ranks on this one GPU, running concurrently);
-    xdp=0: the per-step loop (grads kernel -> gloo all-reduce -> clip+Adam)."""
+    xdp=0: the per-step loop (grads kernel -> gloo all-reduce -> clip+Adam).
+    dp_batch="global" is SURVEY.md 8(e)'s rule (PPO(batch_size=256) on every rank, 128 rows per
+    rank per step): the update equals the single-process update at batch 256 over the ranks'
+    interleaved rollouts; "per-rank" gets there from batch_size=128 per rank."""
     monkeypatch.setenv("RAI_XDP", xdp)
-    _fused_dp_world2_check()
+    _fused_dp_world2_check(dp_batch=dp_batch)
 
 
-def _fused_dp_world2_check():
+def test_xdp_canary_failure_on_one_rank_falls_back_on_every_rank(monkeypatch):
+    """Rank 1's in-kernel exchange canary fails (RAI_XDP_INJECT_FAIL_RANK: it never launches, so
+    rank 0's canary times out waiting for it): both ranks must agree, release the mappings and
+    run the per-step loop — no hang, equal parameters, the single-process result."""
+    monkeypatch.setenv("RAI_XDP", "1")
+    _fused_dp_world2_check(dp_batch="global", inject_fail_rank=1)
+
+
+def _fused_dp_world2_check(dp_batch="per-rank", inject_fail_rank=None):
     import dp_worker
     import make_golden_networks as nets
     from rl_algo_impls_amd.ppo import PPO
@@ -36,7 +48,8 @@ def _fused_dp_world2_check():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=dp_worker.fused_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=dp_worker.fused_dp_worker, args=(r, 2, port, q, "gloo", dp_batch, inject_fail_rank))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = []
@@ -124,7 +137,8 @@ def test_native_rccl_epoch_loop_matches_python_loop_world1():
     np.testing.assert_allclose(pn, pg, rtol=1e-4, atol=1e-6)
 
 
-def test_wide_mlp_dp_world2_matches_single_process_global_minibatches():
+@pytest.mark.parametrize("dp_batch", ["global", "per-rank"])
+def test_wide_mlp_dp_world2_matches_single_process_global_minibatches(dp_batch):
     """HalfCheetah-class policy on the wide-MLP kernels, 2 ranks (gloo, both on cuda:0) with the
     identity permutation: rank r's minibatch i is its time steps [4i, 4i + 4) x 16 envs, so the
     global minibatch i is time steps [4i, 4i + 4) x all 32 envs of the concatenated rollout.  The
@@ -139,7 +153,7 @@ def test_wide_mlp_dp_world2_matches_single_process_global_minibatches():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=dp_worker.wide_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=dp_worker.wide_dp_worker, args=(r, 2, port, q, dp_batch)) for r in range(2)]
     for p in procs:
         p.start()
     res = []

@@ -1,0 +1,47 @@
+#!/bin/bash
+# C3 (Pong NatureCNN, 1024 envs x 128 steps) profile on the GPU box:
+#   1. kernel-trace stats of the bench run as shipped (graph-replayed update and rollout);
+#   2. PMC passes (FETCH_SIZE, WRITE_SIZE, MFMA busy) of ONE update at the same shape, with the update
+#      and rollout forwards run eagerly (RAI_GRAPHS=0 RAI_ROLLOUT_GRAPH=0): the same kernels, launched
+#      one by one.  rocprofv3's counter-collection callback crashed (SIGSEGV inside
+#      librocprofiler-sdk.so, on an HSA runtime thread) while the update's hipGraph was being replayed
+#      (r2b: gpurun_out/r2b/fetch_pong.log + diag/ maps), so counters are collected off-graph.
+# Each step has its own time limit; the script stops at the first step that does not exit 0.
+#   TAG=r2a bash tools/profile_pong.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-r2}
+OUT=gpurun_out/prof_pong_$TAG
+mkdir -p "$OUT"
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+  grep -v amdgpu.ids "$OUT/$name.log" | grep -v "^    @" | tail -4
+  [ $rc -eq 0 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
+}
+B="python3 bench.py --config pong --no-cpu-baseline --roofline-reps 20"
+if [ "${STATS:-1}" = 1 ]; then
+  run stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- $B --steps 2 --warmup 1
+  rm -f "$OUT/stats/run_kernel_trace.csv"
+fi
+export RAI_GRAPHS=0 RAI_ROLLOUT_GRAPH=0
+# a PMC pass serialises every dispatch (~125k in one update) and prints nothing for minutes: report
+# the growth of its counter CSV every 30 s (progress, not a keep-alive: each step keeps its own limit)
+( while sleep 30; do echo "$(date +%T) $(du -sb "$OUT" 2>/dev/null | cut -f1) bytes under $OUT" >> "$OUT/heartbeat.log"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+for pass in ${PASSES:-fetch write mfma}; do
+  case $pass in
+    fetch) ctr="FETCH_SIZE" ;;
+    write) ctr="WRITE_SIZE" ;;
+    mfma) ctr="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" ;;
+  esac
+  run "$pass" 420 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/$pass" -o run -- $B --steps 1 --warmup 0
+  f=$(ls "$OUT/$pass"/*counter_collection.csv | head -1)
+  run "${pass}_agg" 300 python3 tools/pmc_kernels.py "$f" "$OUT/${pass}_kernels.json" --delete
+done
+exit 0
