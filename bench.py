@@ -73,6 +73,9 @@ def parse():
                         "takes batch_size rows of its own rollout per optimizer step (global minibatch "
                         "batch_size x world; weak scaling); global = SURVEY 8(e): batch_size / world rows "
                         "per rank, so the global minibatch is the YAML batch_size")
+    p.add_argument("--deterministic", type=int, default=1, choices=[0, 1],
+                   help="torch.use_deterministic_algorithms + MIOpen deterministic solvers, as the reference's "
+                        "set_device_optimizations default (rl_algo_impls/runner/running_utils.py:161-166)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--roofline-reps", type=int, default=200)
@@ -209,6 +212,9 @@ def main():
         else:
             torch.distributed.init_process_group(backend)
     _lib.lib()
+    from rl_algo_impls_amd.running_utils import set_device_optimizations
+
+    set_device_optimizations(dev, use_deterministic_algorithms=bool(args.deterministic))
     if os.environ.get("RAI_CUDNN_BENCHMARK", "0") == "1":  # MIOpen find mode for the CNN convolutions
         torch.backends.cudnn.benchmark = True
 
@@ -360,6 +366,7 @@ def main():
                        "per_rank_batch": algo.batch_size,
                        "dp_batch": args.dp_batch, "env_partition": "split" if global_envs else "per-rank",
                        "n_epochs": algo_kw["n_epochs"], "batch_policy": args.batch_policy, "seq_len": T,
+                       "deterministic": bool(args.deterministic),
                        "parallelism": f"dp{world}"},
             "roofline": roofline,
             "roofline_latency": roof_lat,

@@ -145,6 +145,19 @@ int rai_bias_gelu_fwd(const float* x, const float* b, int64_t rows, int32_t C, f
 int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b, int64_t rows, int32_t C, float* dx,
                       void* stream);
 
+/* Conv / Linear bias + ReLU of the NatureCNN encoder (rl_algo_impls/shared/encoder/nature_cnn.py:10-53:
+ * Conv2d -> ReLU x3, then Linear -> ReLU) over NHWC (or (B, C) row-major) rows, C % 4 == 0, C / 4
+ * dividing 256.  Forward: out = relu(x + b[c]) (x = the bias-free conv / GEMM output).  Backward, one
+ * launch pair: dx = dy * (out > 0) (torch threshold_backward on the saved output) and the bias gradient
+ * db[c] = sum_rows dx[row, c], written (accumulate == 0) or added to db (accumulate != 0, e.g. straight
+ * into the flat .grad buffer).  The reduction order is fixed (deterministic).  workspace: at least
+ * rai_bias_relu_workspace_bytes(C) bytes, 16-B aligned (per-workgroup partial sums; no initial
+ * contents required); one workspace per concurrently running launch. */
+int64_t rai_bias_relu_workspace_bytes(int32_t C);
+int rai_bias_relu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream);
+int rai_bias_relu_bwd(const float* dy, const float* y, int64_t rows, int32_t C, float* dx, float* db,
+                      int32_t accumulate, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.
  * These live in HBM so a captured hipGraph replays against values the host
@@ -278,6 +291,29 @@ int rai_minibatch_advance(rai_minibatch_desc* desc, void* stream);
  * desc->mb) increments desc->mb and re-arms desc->arrivals. */
 int rai_gather_minibatch_next(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
                               const int64_t* row_bytes, int64_t batch_size, void* stream);
+
+/* Per-field output transform of the minibatch gather.
+ *   RAI_XFORM_COPY: the row's bytes are copied (as above).
+ *   RAI_XFORM_U8_CHW_TO_F32_HWC: the source row is `channels` (<= 4) planes of `hw` uint8 pixels
+ *     (hw % 4 == 0; row_bytes = channels * hw), the rollout's NCHW frames; dst receives hw x channels
+ *     float32 (NHWC, i.e. a channels_last (B, C, H, W) tensor, 16-B aligned) with
+ *     out = (float)u8 / divisor (IEEE division).  This is the NatureCNN input prescale
+ *     `obs.float() / range_size` of rl_algo_impls/shared/encoder/cnn.py:24-27 plus the channels_last
+ *     conversion, fused into the gather of rl_algo_impls/rollout/rollout.py:56-69.
+ * rai_gather_minibatch_x: rai_gather_minibatch (advance == 0) / _next (advance != 0) with one
+ * rai_gather_xform per field (xform NULL: all copies).  Errors: RAI_E_SHAPE for a transform whose
+ * shape or alignment does not fit, RAI_E_MODE for an unknown kind. */
+#define RAI_XFORM_COPY 0
+#define RAI_XFORM_U8_CHW_TO_F32_HWC 1
+typedef struct rai_gather_xform {
+  int32_t kind;
+  int32_t channels;
+  int64_t hw;
+  float divisor;
+  int32_t reserved;
+} rai_gather_xform;
+int rai_gather_minibatch_x(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst, const int64_t* row_bytes,
+                           const rai_gather_xform* xform, int64_t batch_size, int32_t advance, void* stream);
 
 /* --------------------------------------------------------------------------
  * Rollout post-head: sample actions from the policy head and write the

@@ -69,6 +69,22 @@ class MinibatchDesc(C.Structure):
     ]
 
 
+RAI_XFORM_COPY = 0
+RAI_XFORM_U8_CHW_TO_F32_HWC = 1
+
+
+class GatherXform(C.Structure):
+    """Mirror of rai_gather_xform (per-field output transform of the minibatch gather)."""
+
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("channels", C.c_int32),
+        ("hw", C.c_int64),
+        ("divisor", C.c_float),
+        ("reserved", C.c_int32),
+    ]
+
+
 class MlpWideDesc(C.Structure):
     """Mirror of rai_mlp_wide_desc."""
 
@@ -141,6 +157,10 @@ _SIGNATURES = {
     "rai_gather_minibatch": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_minibatch_advance": (C.c_int, [_vp, _vp]),
     "rai_gather_minibatch_next": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
+    "rai_gather_minibatch_x": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _i64, _i32, _vp]),
+    "rai_bias_relu_workspace_bytes": (_i64, [_i32]),
+    "rai_bias_relu_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "rai_bias_relu_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, [C.c_int64, C.c_int32]),
     "rai_mlp_ppo_grads": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _i32,
                                     _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),

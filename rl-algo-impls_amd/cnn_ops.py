@@ -1,0 +1,172 @@
+"""NatureCNN (config C3) layer epilogues on the GPU: conv / Linear -> bias + ReLU.
+
+The reference encoder (rl_algo_impls/shared/encoder/nature_cnn.py:10-53, cnn.py:24-72) is
+Conv2d -> ReLU x3, Flatten, Linear -> ReLU.  PyTorch-ROCm runs every layer as the MIOpen / hipBLASLt
+contraction plus a bias add and a clamp, and its backward as threshold_backward, a bias-gradient
+column sum and an accumulate of that gradient into .grad.  Here the contraction stays on
+MIOpen / hipBLASLt (MFMA), bias-free, and the epilogue is one HIP pass each way
+(rai_bias_relu_fwd / rai_bias_relu_bwd, csrc/se_block.hip):
+
+    forward    y = relu(conv(x, W) + b)             conv bias-free, then one pass
+    backward   dz = dy * (y > 0), db (+)= sum dz     one pass + a finalize, deterministic order
+
+Direct gradient accumulation.  Inside the trainer's update (`direct_grads(module)`), every
+parameter's .grad is a view into the flat gradient buffer (optim.FlatParams), zeroed by the
+optimizer step.  The bias gradient is then added by the backward kernel straight into that view,
+and the Linear weight gradient by a beta = 1 GEMM (W.grad.addmm_(dz^T, x)), instead of autograd
+materialising each gradient and launching an accumulate kernel per parameter.  Outside that
+context the Functions return their gradients to autograd like any module (torch.autograd.grad
+etc. see ordinary gradients).
+"""
+from __future__ import annotations
+
+import contextlib
+import threading
+from typing import Dict
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .dp_buckets import notify_grad_written
+
+_state = threading.local()
+
+
+@contextlib.contextmanager
+def direct_grads(enabled: bool = True):
+    """Within this context the fused epilogues accumulate parameter gradients in place (see the
+    module docstring).  The trainer enters it around its own forward + backward only."""
+    prev = getattr(_state, "direct", False)
+    _state.direct = enabled
+    try:
+        yield
+    finally:
+        _state.direct = prev
+
+
+def _direct(p: torch.Tensor) -> bool:
+    return getattr(_state, "direct", False) and p.grad is not None and p.grad.is_contiguous()
+
+
+class _Workspaces:
+    """Per-(layer, device) workspaces of rai_bias_relu_bwd (per-workgroup partial sums): one
+    allocation serves every eager call and graph replay of that layer."""
+
+    def __init__(self):
+        self._ws: Dict[tuple, torch.Tensor] = {}
+
+    def get(self, key, C: int, device) -> torch.Tensor:
+        k = (key, C, str(device))
+        ws = self._ws.get(k)
+        if ws is None:
+            # allocated outside any graph capture (a capture-time allocation would come from, and
+            # stay tied to, that graph's private pool); every graphed step has eager warm-up runs
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("cnn_ops: bias + ReLU workspace first requested inside a graph capture")
+            n = int(_lib.lib().rai_bias_relu_workspace_bytes(C))
+            ws = torch.empty(n, dtype=torch.uint8, device=device)
+            self._ws[k] = ws
+        return ws
+
+    def prewarm(self, key, C: int, device) -> None:
+        if not torch.cuda.is_current_stream_capturing():
+            self.get(key, C, device)
+
+
+_WS = _Workspaces()
+
+
+def _bias_relu_fwd(z: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    C = int(z.shape[1])
+    y = torch.empty_like(z)
+    _lib.check(_lib.lib().rai_bias_relu_fwd(z.data_ptr(), b.data_ptr(), z.numel() // C, C, y.data_ptr(),
+                                            _lib.stream_handle(z.device)), "rai_bias_relu_fwd")
+    return y
+
+
+def _bias_relu_bwd(dy: torch.Tensor, y: torch.Tensor, b: torch.Tensor, ws: torch.Tensor, direct: bool):
+    """(dz, db or None): db is added into b.grad when direct."""
+    C = int(y.shape[1])
+    dz = torch.empty_like(y)
+    db = b.grad if direct else torch.empty(C, dtype=torch.float32, device=y.device)
+    _lib.check(_lib.lib().rai_bias_relu_bwd(dy.data_ptr(), y.data_ptr(), y.numel() // C, C, dz.data_ptr(),
+                                            db.data_ptr(), 1 if direct else 0, ws.data_ptr(), ws.numel(),
+                                            _lib.stream_handle(y.device)), "rai_bias_relu_bwd")
+    return dz, (None if direct else db)
+
+
+class ConvBiasReLU(torch.autograd.Function):
+    """relu(conv2d(x, W) + b) on NHWC (channels_last) fp32 activations."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, key):
+        z = F.conv2d(x, w, None, stride, padding)
+        z = z.contiguous(memory_format=torch.channels_last)
+        y = _bias_relu_fwd(z, b)
+        ctx.save_for_backward(x, w, b, y)
+        ctx.conf = (stride, padding, key, _direct(b), _direct(w))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, y = ctx.saved_tensors
+        stride, padding, key, direct_b, direct_w = ctx.conf
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dz, db = _bias_relu_bwd(dy, y, b, _WS.get(key, int(y.shape[1]), y.device), direct_b)
+        need_dx = ctx.needs_input_grad[0]
+        dx, dw, _ = torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), _pair(padding), [1, 1],
+                                                        False, [0, 0], 1, [need_dx, True, False])
+        if direct_w:
+            w.grad.add_(dw)
+            dw = None
+            notify_grad_written(w)
+        return dx, dw, db, None, None, None
+
+
+class LinearBiasReLU(torch.autograd.Function):
+    """relu(x W^T + b) for (B, in) x: hipBLASLt GEMM, then the bias + ReLU pass."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, key):
+        z = torch.mm(x, w.t())
+        y = _bias_relu_fwd(z, b)
+        ctx.save_for_backward(x, w, b, y)
+        ctx.conf = (key, _direct(b), _direct(w))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, y = ctx.saved_tensors
+        key, direct_b, direct_w = ctx.conf
+        dz, db = _bias_relu_bwd(dy.contiguous(), y, b, _WS.get(key, int(y.shape[1]), y.device), direct_b)
+        dx = torch.mm(dz, w) if ctx.needs_input_grad[0] else None
+        if direct_w:
+            w.grad.addmm_(dz.t(), x)  # beta = 1: the GEMM accumulates into the flat gradient view
+            dw = None
+            notify_grad_written(w)  # data parallel: this layer's gradient bucket may go (dp_buckets)
+        else:
+            dw = torch.mm(dz.t(), x)
+        return dx, dw, db, None
+
+
+def _pair(v):
+    return list(v) if isinstance(v, (tuple, list)) else [v, v]
+
+
+def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """relu(conv(x)) for an NHWC fp32 GPU activation (fused epilogue), else the module path."""
+    if (x.is_cuda and x.dtype == torch.float32 and conv.bias is not None and conv.groups == 1
+            and tuple(conv.dilation) == (1, 1) and conv.padding_mode == "zeros" and isinstance(conv.padding, tuple)
+            and conv.out_channels % 4 == 0 and 256 % (conv.out_channels // 4) == 0):
+        _WS.prewarm(id(conv), conv.out_channels, x.device)
+        return ConvBiasReLU.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), id(conv))
+    return F.relu(conv(x))
+
+
+def linear_relu(lin: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and lin.bias is not None
+            and lin.out_features % 4 == 0 and 256 % (lin.out_features // 4) == 0):
+        _WS.prewarm(id(lin), lin.out_features, x.device)
+        return LinearBiasReLU.apply(x.contiguous(), lin.weight, lin.bias, id(lin))
+    return F.relu(lin(x))

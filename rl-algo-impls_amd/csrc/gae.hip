@@ -11,8 +11,8 @@
 //   (1) all 8 waves hold 8 rows each in registers and write the carry-independent
 //       part delta_t (+ next_nonterminal) to LDS,
 //   (2) wave 0 runs the serial carry recurrence (two dependent FP64 ops per row,
-//       operands batched out of LDS 16 rows at a time) while the other waves'
-//       loads of the NEXT tile are already in flight,
+//       operands batched out of LDS 4 rows at a time) while the NEXT tile's loads,
+//       issued one tile ahead (two tiles in flight from the start), are arriving,
 //   (3) every wave stores its rows of adv and returns (= adv + V, from registers).
 // So per tile the exposed latency is one HBM round trip shared by all 64 rows.
 // Exact mode keeps the reference's numpy precision sequence bit for bit:
@@ -162,7 +162,10 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
 #if GAE_DIAG & 8
   long long t_last = clock64();
 #endif
+  // two tiles in flight from the start: tile 1's loads are not left waiting behind tile 0's
+  // round trip (at C2's T = 128 that is every load of the launch up front)
   load(cur, 0);
+  if (!(GAE_DIAG & 4) && ntiles > 1) load(nxt, 1);
   Acc carry = (Acc)0;
   for (int tile = 0; tile < ntiles; ++tile) {
     const int64_t lo = T - (int64_t)(tile + 1) * GAE_TT;
@@ -177,8 +180,7 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
     GSTAMP(0);
     lds_barrier();
     GSTAMP(1);
-    // (2) next tile's loads go out while wave 0 runs the serial recurrence
-    if (!(GAE_DIAG & 4) && tile + 1 < ntiles) load(nxt, tile + 1);
+    // (2) wave 0 runs the serial recurrence while the next tile's loads are in flight
     if (!(GAE_DIAG & 1) && wave == 0 && sub == 0) {
       // The only serial work: carry = delta + coef*carry (two dependent FP64 ops per row),
       // operands batched out of LDS, carries written back in place.  Rows with t < 0 (only in
@@ -230,7 +232,10 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
       }
     }
     GSTAMP(4);
-    if (!(GAE_DIAG & 4) && tile + 1 < ntiles) cur = nxt;
+    if (!(GAE_DIAG & 4) && tile + 1 < ntiles) {
+      cur = nxt;
+      if (tile + 2 < ntiles) load(nxt, tile + 2);
+    }
     GSTAMP(5);
   }
 }

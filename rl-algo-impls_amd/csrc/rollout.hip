@@ -47,22 +47,36 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
 }
 
 // Minibatch gather driven by a device descriptor (graph replay: the launch is fixed, the
-// minibatch index advances on device).  Workgroup b owns rows b, b + G, ... and its 256 threads
-// stride the (row, unit) pairs of those rows over the concatenated units of all fields (16-, 4- or
-// 1-B units per field) with GM_BATCH loads in flight before the stores.  The grid is sized to ~256
-// pairs per workgroup, at most one per row and <= 1024, so few workgroups arrive on the advance
-// counter (a device-scope atomic on one address, serialised across the XCDs).
-// (The first version launched (rows x units / 256) x fields workgroups, each arriving on the one
-// counter and dividing u / units per element: 202 us per Pong minibatch, 7.2 MB of obs.)
+// minibatch index advances on device).  Workgroup b owns rows b, b + G, ... and its threads stride
+// the (row, unit) pairs of those rows over the concatenated units of all fields with GM_BATCH loads
+// in flight before the stores.  A unit is 16, 4 or 1 bytes of a copied field, or one QUAD of a frame
+// field (below).  The grid is at most one workgroup per row and <= 1024, so few workgroups arrive on
+// the advance counter (a device-scope atomic on one address, serialised across the XCDs); rows of
+// more than 256 units take 1024-thread workgroups so that a whole Pong row (1,764 frame quads) is
+// in flight at once instead of seven dependent 256-thread passes (43.8 us per Pong minibatch with
+// 256 threads; the first version, (rows x units / 256) x fields workgroups each arriving on the
+// counter, took 202 us).
+//
+// Frame fields (RAI_XFORM_U8_CHW_TO_F32_HWC): a source row of C <= 4 planes of HW uint8 pixels
+// (the rollout's NCHW frames) becomes HW x C float32 (NHWC, channels_last) with
+// out = (float)u8 / divisor: the NatureCNN input prescale obs.float() / range_size
+// (rl_algo_impls/shared/encoder/cnn.py:24-27) and the channels_last conversion fused into the
+// gather.  One unit = 4 consecutive pixels: C 4-byte loads (one per plane) and C float4 stores.
+// The division is IEEE-correct (hipcc's default), as the reference's CPU path divides; torch on a
+// GPU multiplies by the rounded reciprocal instead.
 struct MbDst {
   uint8_t* dst[RAI_MAX_FIELDS];
   int64_t units[RAI_MAX_FIELDS];
-  int32_t gran[RAI_MAX_FIELDS];
+  int32_t gran[RAI_MAX_FIELDS];  // 16 / 4 / 1: copy; 0: frame quads
+  int32_t planes[RAI_MAX_FIELDS];
+  int64_t hw[RAI_MAX_FIELDS];
+  float divisor[RAI_MAX_FIELDS];
   int32_t n_fields;
 };
 constexpr int GM_BATCH = 4;
-__global__ __launch_bounds__(256) void gather_minibatch_kernel(rai_minibatch_desc* __restrict__ d, const MbDst o,
-                                                               const int advance) {
+template <int NT>
+__global__ __launch_bounds__(NT) void gather_minibatch_kernel(rai_minibatch_desc* __restrict__ d, const MbDst o,
+                                                              const int advance) {
   const int64_t mb = d->mb, B = d->batch_size;
   const int64_t row0 = mb * B;
   const int rows = (int)min(B, d->n_rows - row0);
@@ -73,13 +87,13 @@ __global__ __launch_bounds__(256) void gather_minibatch_kernel(rai_minibatch_des
   const int G = (int)gridDim.x, b = (int)blockIdx.x;
   const int my_rows = rows > b ? (rows - b + G - 1) / G : 0;  // rows b, b + G, b + 2G, ...
   const int work = my_rows * total;  // < 2^31: checked at launch (batch_size x total)
-  for (int i0 = threadIdx.x; i0 < work; i0 += GM_BATCH * 256) {
+  for (int i0 = threadIdx.x; i0 < work; i0 += GM_BATCH * NT) {
     uint4 v[GM_BATCH];
-    int64_t so[GM_BATCH], doff[GM_BATCH];
+    int64_t doff[GM_BATCH];
     int fk[GM_BATCH];
 #pragma unroll
     for (int k = 0; k < GM_BATCH; ++k) {
-      const int i = i0 + k * 256;
+      const int i = i0 + k * NT;
       fk[k] = -1;
       if (i < work) {
         const int ri = (int)((unsigned)i / (unsigned)total);
@@ -89,21 +103,49 @@ __global__ __launch_bounds__(256) void gather_minibatch_kernel(rai_minibatch_des
         int f = 0;
         while (j >= (int)o.units[f]) j -= (int)o.units[f++];
         fk[k] = f;
-        so[k] = sr * o.units[f] + j;
-        doff[k] = r * o.units[f] + j;
         const uint8_t* src = static_cast<const uint8_t*>(d->src[f]);
-        if (o.gran[f] == 16) v[k] = reinterpret_cast<const uint4*>(src)[so[k]];
-        else if (o.gran[f] == 4) v[k].x = reinterpret_cast<const uint32_t*>(src)[so[k]];
-        else v[k].x = src[so[k]];
+        if (o.gran[f] == 0) {  // frame quad j of row sr: one word per plane
+          const int C = o.planes[f];
+          const int64_t hw4 = o.hw[f] >> 2;
+          const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src) + sr * C * hw4 + j;
+          v[k].x = s32[0];
+          v[k].y = C > 1 ? s32[hw4] : 0u;
+          v[k].z = C > 2 ? s32[2 * hw4] : 0u;
+          v[k].w = C > 3 ? s32[3 * hw4] : 0u;
+          doff[k] = (r * o.hw[f] + 4LL * j) * C;  // float index of the quad's first pixel
+        } else {
+          const int64_t so = sr * o.units[f] + j;
+          doff[k] = r * o.units[f] + j;
+          if (o.gran[f] == 16) v[k] = reinterpret_cast<const uint4*>(src)[so];
+          else if (o.gran[f] == 4) v[k].x = reinterpret_cast<const uint32_t*>(src)[so];
+          else v[k].x = src[so];
+        }
       }
     }
 #pragma unroll
     for (int k = 0; k < GM_BATCH; ++k) {
       const int f = fk[k];
-      if (f >= 0) {
-        if (o.gran[f] == 16) reinterpret_cast<uint4*>(o.dst[f])[doff[k]] = v[k];
-        else if (o.gran[f] == 4) reinterpret_cast<uint32_t*>(o.dst[f])[doff[k]] = v[k].x;
-        else o.dst[f][doff[k]] = (uint8_t)v[k].x;
+      if (f < 0) continue;
+      if (o.gran[f] == 0) {
+        const int C = o.planes[f];
+        const float div = o.divisor[f];
+        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        float4* out = reinterpret_cast<float4*>(reinterpret_cast<float*>(o.dst[f]) + doff[k]);
+        for (int q = 0; q < C; ++q) {  // float4 q holds elements m = 4q..4q+3 of (pixel p, plane c), m = p*C + c
+          float e[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int m = 4 * q + u, p = m / C, c = m - p * C;
+            e[u] = (float)((w[c] >> (8 * p)) & 0xffu) / div;
+          }
+          out[q] = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      } else if (o.gran[f] == 16) {
+        reinterpret_cast<uint4*>(o.dst[f])[doff[k]] = v[k];
+      } else if (o.gran[f] == 4) {
+        reinterpret_cast<uint32_t*>(o.dst[f])[doff[k]] = v[k].x;
+      } else {
+        o.dst[f][doff[k]] = (uint8_t)v[k].x;
       }
     }
   }
@@ -240,44 +282,73 @@ extern "C" int rai_gather_rows(int32_t n_fields, const void* const* src, void* c
 }
 
 static int gather_minibatch(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst, const int64_t* row_bytes,
-                            int64_t batch_size, int advance, void* stream) {
+                            const rai_gather_xform* xform, int64_t batch_size, int advance, void* stream) {
   if (n_fields < 1 || n_fields > RAI_MAX_FIELDS || batch_size < 1) return RAI_E_SHAPE;
   if (!desc || !dst || !row_bytes) return RAI_E_NULLPTR;
   MbDst o;
-  int64_t max_units = 1;
   for (int i = 0; i < n_fields; ++i) {
     if (!dst[i] || row_bytes[i] < 1) return RAI_E_NULLPTR;
-    const int gran = (row_bytes[i] % 16 == 0) ? 16 : ((row_bytes[i] % 4 == 0) ? 4 : 1);
     o.dst[i] = static_cast<uint8_t*>(dst[i]);
-    o.gran[i] = gran;
-    o.units[i] = row_bytes[i] / gran;
-    if (o.units[i] > max_units) max_units = o.units[i];
+    o.planes[i] = 0;
+    o.hw[i] = 0;
+    o.divisor[i] = 1.f;
+    const int kind = xform ? xform[i].kind : RAI_XFORM_COPY;
+    if (kind == RAI_XFORM_U8_CHW_TO_F32_HWC) {
+      const rai_gather_xform& x = xform[i];
+      // C <= 4 planes of HW pixels, HW % 4 == 0 (quads of 4-byte source words), 16-B aligned output
+      if (x.channels < 1 || x.channels > 4 || x.hw < 4 || x.hw % 4 || (int64_t)x.channels * x.hw != row_bytes[i] ||
+          !(x.divisor > 0.f) || ((uintptr_t)dst[i] & 15))
+        return RAI_E_SHAPE;
+      o.gran[i] = 0;
+      o.planes[i] = x.channels;
+      o.hw[i] = x.hw;
+      o.divisor[i] = x.divisor;
+      o.units[i] = x.hw / 4;
+    } else if (kind == RAI_XFORM_COPY) {
+      const int gran = (row_bytes[i] % 16 == 0) ? 16 : ((row_bytes[i] % 4 == 0) ? 4 : 1);
+      o.gran[i] = gran;
+      o.units[i] = row_bytes[i] / gran;
+    } else {
+      return RAI_E_MODE;
+    }
   }
   o.n_fields = n_fields;
-  (void)max_units;
-  // ~256 (row, unit) pairs per workgroup, at most one workgroup per row (and <= 1024): few
-  // workgroups arrive on the advance counter when rows are small (HalfCheetah: 64 x ~30 units)
   int64_t total = 0;
   for (int i = 0; i < n_fields; ++i) total += o.units[i];
   if (batch_size * total >= (1LL << 31)) return RAI_E_SHAPE;  // 32-bit (row, unit) indexing
-  int64_t blocks = (batch_size * total + 255) / 256;
+  // rows of more than 256 units: one 1024-thread workgroup per row (the row in flight at once);
+  // else ~256 (row, unit) pairs per 256-thread workgroup, at most one workgroup per row (<= 1024)
+  const bool wide = total > 256;
+  const int nt = wide ? 1024 : 256;
+  int64_t blocks = (batch_size * total + nt - 1) / nt;
   if (blocks > batch_size) blocks = batch_size;
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(gather_minibatch_kernel, dim3((unsigned)blocks), dim3(256), 0, rai_stream(stream), desc, o,
-                     advance);
+  if (wide)
+    hipLaunchKernelGGL(gather_minibatch_kernel<1024>, dim3((unsigned)blocks), dim3(1024), 0, rai_stream(stream), desc,
+                       o, advance);
+  else
+    hipLaunchKernelGGL(gather_minibatch_kernel<256>, dim3((unsigned)blocks), dim3(256), 0, rai_stream(stream), desc,
+                       o, advance);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }
 
 extern "C" int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
                                     const int64_t* row_bytes, int64_t batch_size, void* stream) {
-  return gather_minibatch(const_cast<rai_minibatch_desc*>(desc), n_fields, dst, row_bytes, batch_size, 0, stream);
+  return gather_minibatch(const_cast<rai_minibatch_desc*>(desc), n_fields, dst, row_bytes, nullptr, batch_size, 0,
+                          stream);
 }
 
 extern "C" int rai_gather_minibatch_next(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
                                          const int64_t* row_bytes, int64_t batch_size, void* stream) {
-  return gather_minibatch(desc, n_fields, dst, row_bytes, batch_size, 1, stream);
+  return gather_minibatch(desc, n_fields, dst, row_bytes, nullptr, batch_size, 1, stream);
+}
+
+extern "C" int rai_gather_minibatch_x(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
+                                      const int64_t* row_bytes, const rai_gather_xform* xform, int64_t batch_size,
+                                      int32_t advance, void* stream) {
+  return gather_minibatch(desc, n_fields, dst, row_bytes, xform, batch_size, advance ? 1 : 0, stream);
 }
 
 extern "C" int rai_minibatch_advance(rai_minibatch_desc* desc, void* stream) {

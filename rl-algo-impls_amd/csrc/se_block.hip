@@ -167,3 +167,158 @@ extern "C" int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }
+
+// ---- conv / linear bias + ReLU epilogue (NatureCNN, config C3) --------------------------------
+// The NatureCNN encoder (rl_algo_impls/shared/encoder/nature_cnn.py:10-53) is three conv -> ReLU
+// pairs and a Linear -> ReLU.  PyTorch runs each as conv, a bias add (broadcast over NHWC rows) and a
+// clamp; backward as threshold_backward, a column-sum reduction for the bias gradient and an
+// accumulate of that gradient into .grad: five launches per layer around the MIOpen / hipBLASLt
+// contraction.  Here, per layer:
+//   forward   one pass:  out = relu(x + b[c])                       (x: bias-free conv / GEMM output)
+//   backward  dx = dy * (out > 0) and db[c] (+)= sum_rows dx[row, c]: one pass over the rows plus a
+//             one-workgroup finalize of the per-workgroup column sums
+// The bias-gradient reduction is deterministic (fixed row runs per workgroup, fixed summation
+// orders).  relu(NaN) = NaN and dx = 0 where out <= 0, as torch's clamp_min / threshold_backward.
+namespace {
+constexpr int BR_THREADS = 256;
+constexpr int BR_MAX_BLOCKS = 1024;
+constexpr int BR_UNROLL = 4;      // rows in flight per lane before the first use
+constexpr int BR_ROWS_PER_LANE = 8;
+
+__global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_kernel(const f4* __restrict__ x, const float* __restrict__ b,
+                                                                  int C4, int64_t n4, f4* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)BR_THREADS + threadIdx.x; i < n4; i += (int64_t)gridDim.x * BR_THREADS) {
+    const f4 xv = x[i], bv = ld_bias4(b, (int)(i % C4));
+    f4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float t = xv[q] + bv[q];
+      o[q] = t < 0.f ? 0.f : t;
+    }
+    out[i] = o;
+  }
+}
+
+// Pass 1: workgroup w owns rows [w * rpb, (w + 1) * rpb); its threads are (row lane, float4 channel
+// group) pairs, each lane keeping BR_UNROLL rows' loads in flight; dx is stored and the workgroup's
+// column sums go to partial[w] (row lanes added in lane order).  Pass 2 (one workgroup): thread t
+// adds partials s, s + stripes, ... (s = t / C, fixed order) of channel t % C, then the stripes are
+// added in order through LDS -> db.  The kernel boundary orders the passes: no device-scope fences
+// or arrival counters (a last-workgroup-arrives variant paid an L2 writeback per workgroup).
+__global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __restrict__ dy, const f4* __restrict__ y,
+                                                                  int C4, int64_t rows, int64_t rows_per_block,
+                                                                  f4* __restrict__ dx, float* __restrict__ partial) {
+  __shared__ f4 part[BR_THREADS];
+  const int tid = threadIdx.x;
+  const int lanes = BR_THREADS / C4;  // row lanes; C4 divides 256
+  const int c4 = tid % C4, lane = tid / C4;
+  const int64_t r0 = blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0 + lane; r < r1; r += (int64_t)lanes * BR_UNROLL) {
+    f4 g[BR_UNROLL], yv[BR_UNROLL];
+#pragma unroll
+    for (int u = 0; u < BR_UNROLL; ++u) {
+      const int64_t rr = r + (int64_t)u * lanes;
+      const int64_t i = (rr < r1 ? rr : r) * C4 + c4;
+      g[u] = dy[i];
+      yv[u] = y[i];
+    }
+#pragma unroll
+    for (int u = 0; u < BR_UNROLL; ++u) {
+      const int64_t rr = r + (int64_t)u * lanes;
+      if (rr < r1) {
+        f4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = yv[u][q] <= 0.f ? 0.f : g[u][q];
+        dx[rr * C4 + c4] = o;
+        acc += o;
+      }
+    }
+  }
+  part[tid] = acc;
+  __syncthreads();
+  if (tid < C4) {
+    f4 t = part[tid];
+    for (int k = 1; k < lanes; ++k) t += part[tid + k * C4];
+    reinterpret_cast<f4*>(partial + (int64_t)blockIdx.x * 4 * C4)[tid] = t;
+  }
+}
+
+__global__ __launch_bounds__(BR_THREADS) void bias_grad_finalize_kernel(const float* __restrict__ partial, int nb, int C,
+                                                                       float* __restrict__ db, int accumulate) {
+  __shared__ float red[BR_THREADS];
+  const int tid = threadIdx.x;
+  if (C <= BR_THREADS) {
+    const int stripes = BR_THREADS / C, c = tid % C, s0 = tid / C;
+    float s = 0.f;
+    if (s0 < stripes)
+      for (int w = s0; w < nb; w += stripes) s += partial[(int64_t)w * C + c];
+    red[tid] = s;
+    __syncthreads();
+    if (tid < C) {
+      float t = red[tid];
+      for (int k = 1; k < stripes; ++k) t += red[tid + k * C];
+      db[tid] = accumulate ? db[tid] + t : t;
+    }
+  } else {
+    for (int c = tid; c < C; c += BR_THREADS) {
+      float t = 0.f;
+      for (int w = 0; w < nb; ++w) t += partial[(int64_t)w * C + c];
+      db[c] = accumulate ? db[c] + t : t;
+    }
+  }
+}
+
+bool br_shape_ok(int64_t rows, int32_t C) {
+  if (rows < 0 || C < 4 || C % 4) return false;
+  const int C4 = C / 4;
+  return C4 <= BR_THREADS && BR_THREADS % C4 == 0;
+}
+}  // namespace
+
+extern "C" int64_t rai_bias_relu_workspace_bytes(int32_t C) {
+  return (int64_t)BR_MAX_BLOCKS * (C > 0 ? C : 0) * 4;
+}
+
+extern "C" int rai_bias_relu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream) {
+  if (!br_shape_ok(rows, C)) return RAI_E_SHAPE;
+  if (rows == 0) return RAI_OK;
+  if (!x || !b || !out) return RAI_E_NULLPTR;
+  const int64_t n4 = rows * (C / 4);
+  hipLaunchKernelGGL(bias_relu_fwd_kernel, dim3((unsigned)ew_blocks(n4)), dim3(BR_THREADS), 0, rai_stream(stream),
+                     reinterpret_cast<const f4*>(x), b, C / 4, n4, reinterpret_cast<f4*>(out));
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_bias_relu_bwd(const float* dy, const float* y, int64_t rows, int32_t C, float* dx, float* db,
+                                 int32_t accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!br_shape_ok(rows, C)) return RAI_E_SHAPE;
+  if (!dy || !y || !dx || !db || !workspace) return RAI_E_NULLPTR;
+  if (workspace_bytes < rai_bias_relu_workspace_bytes(C) || ((uintptr_t)workspace & 15)) return RAI_E_WORKSPACE;
+  hipStream_t st = rai_stream(stream);
+  if (rows == 0) {
+    if (!accumulate) {
+      const hipError_t e = hipMemsetAsync(db, 0, (size_t)C * 4, st);
+      if (e != hipSuccess) return (int)e;
+    }
+    return RAI_OK;
+  }
+  const int C4 = C / 4, lanes = BR_THREADS / C4;
+  // ~BR_ROWS_PER_LANE rows per row lane, at most BR_MAX_BLOCKS workgroups
+  int64_t blocks = (rows + (int64_t)BR_ROWS_PER_LANE * lanes - 1) / ((int64_t)BR_ROWS_PER_LANE * lanes);
+  if (blocks > BR_MAX_BLOCKS) blocks = BR_MAX_BLOCKS;
+  if (blocks < 1) blocks = 1;
+  const int64_t rpb = (rows + blocks - 1) / blocks;
+  blocks = (rows + rpb - 1) / rpb;
+  float* partial = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(bias_relu_bwd_kernel, dim3((unsigned)blocks), dim3(BR_THREADS), 0, st,
+                     reinterpret_cast<const f4*>(dy), reinterpret_cast<const f4*>(y), C4, rows, rpb,
+                     reinterpret_cast<f4*>(dx), partial);
+  RAI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bias_grad_finalize_kernel, dim3(1), dim3(BR_THREADS), 0, st, partial, (int)blocks, C, db,
+                     accumulate);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

@@ -6,8 +6,9 @@ The reference runs one eager minibatch step per Python iteration (rl_algo_impls/
 cost exceeds their GPU time at these batch sizes.  Here the step is captured ONCE into a hipGraph
 (torch.cuda.CUDAGraph) and replayed for every minibatch of every epoch:
 
-    rai_gather_minibatch_next  rows perm[mb*B + i] of every rollout field -> static minibatch
-                           buffers; the last workgroup to finish advances mb (device-side counter)
+    rai_gather_minibatch_x rows perm[mb*B + i] of every rollout field -> static minibatch
+                           buffers (uint8 frames -> float32 / range_size, channels_last, for the
+                           NatureCNN); the last workgroup to finish advances mb (device counter)
     policy forward         PyTorch-ROCm (MIOpen / hipBLASLt), static inputs
     rai_ppo_loss           loss + dLoss/d(logp, entropy, v), stats row at state.stat_index
     autograd backward      into the flat .grad buffer
@@ -41,23 +42,18 @@ class MinibatchStepGraph:
     WARMUP = 2
 
     def __init__(self, device: torch.device, fields: List[torch.Tensor], batch_size: int,
-                 step: Callable[[List[torch.Tensor]], None]):
+                 step: Callable[[List[torch.Tensor]], None], xforms: Optional[list] = None):
         self.device = device
         self.B = int(batch_size)
         self.step = step
         self.row_bytes = [int(f[0].numel() * f.element_size()) for f in fields]
-        self.static = [torch.empty((self.B,) + tuple(f.shape[1:]), dtype=f.dtype, device=device) for f in fields]
+        self.xforms = xforms
+        self.static = static_buffers(fields, self.B, device, xforms)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.eager_runs = 0
 
     def gather(self, desc: torch.Tensor, bufs: List[torch.Tensor]) -> None:
-        n = len(bufs)
-        dst = (C.c_void_p * n)(*[b.data_ptr() for b in bufs])
-        rb = (C.c_int64 * n)(*self.row_bytes)
-        st = _lib.stream_handle(self.device)
-        L = _lib.lib()
-        _lib.check(L.rai_gather_minibatch_next(desc.data_ptr(), n, C.cast(dst, C.c_void_p), C.cast(rb, C.c_void_p),
-                                               int(bufs[0].shape[0]), st), "rai_gather_minibatch_next")
+        gather_next(self.device, desc, bufs, self.row_bytes, self.xforms)
 
     def _body(self, desc: torch.Tensor) -> None:
         self.gather(desc, self.static)
@@ -79,6 +75,37 @@ class MinibatchStepGraph:
         g.replay()  # the capture executed nothing: this replay is the minibatch
 
 
+def static_buffers(fields: List[torch.Tensor], rows: int, device, xforms: Optional[list]) -> List[torch.Tensor]:
+    """Minibatch destination buffers: the fields' own row shape and dtype, except a transformed
+    frame field (RAI_XFORM_U8_CHW_TO_F32_HWC), which is float32 channels_last."""
+    out = []
+    for i, f in enumerate(fields):
+        x = xforms[i] if xforms is not None else None
+        if x is not None and x.kind == _lib.RAI_XFORM_U8_CHW_TO_F32_HWC:
+            out.append(torch.empty((rows,) + tuple(f.shape[1:]), dtype=torch.float32, device=device,
+                                   memory_format=torch.channels_last))
+        else:
+            out.append(torch.empty((rows,) + tuple(f.shape[1:]), dtype=f.dtype, device=device))
+    return out
+
+
+def gather_next(device, desc: torch.Tensor, bufs: List[torch.Tensor], row_bytes: List[int],
+                xforms: Optional[list]) -> None:
+    """rai_gather_minibatch_x (advance): rows of the next minibatch into bufs."""
+    n = len(bufs)
+    dst = (C.c_void_p * n)(*[b.data_ptr() for b in bufs])
+    rb = (C.c_int64 * n)(*row_bytes)
+    xf = None
+    if xforms is not None:
+        arr = (_lib.GatherXform * n)()
+        for i, x in enumerate(xforms):
+            arr[i] = x if x is not None else _lib.GatherXform(kind=_lib.RAI_XFORM_COPY)
+        xf = C.cast(arr, C.c_void_p)
+    _lib.check(_lib.lib().rai_gather_minibatch_x(desc.data_ptr(), n, C.cast(dst, C.c_void_p), C.cast(rb, C.c_void_p),
+                                                 xf, int(bufs[0].shape[0]), 1, _lib.stream_handle(device)),
+               "rai_gather_minibatch_x")
+
+
 class GraphedUpdate:
     """Per-trainer cache of minibatch graphs and the device descriptor."""
 
@@ -90,8 +117,9 @@ class GraphedUpdate:
         self.perm: Optional[torch.Tensor] = None
         self._tail_bufs: Dict[Tuple, List[torch.Tensor]] = {}
 
-    def key(self, fields: List[torch.Tensor], B: int, tag) -> Tuple:
-        return (B, tag) + tuple((f.dtype, tuple(f.shape[1:])) for f in fields)
+    def key(self, fields: List[torch.Tensor], B: int, tag, xforms=None) -> Tuple:
+        xk = tuple((x.kind, x.channels, x.hw, x.divisor) if x is not None else None for x in xforms) if xforms else None
+        return (B, tag, xk) + tuple((f.dtype, tuple(f.shape[1:])) for f in fields)
 
     def set_rollout(self, fields: List[torch.Tensor], batch_size: int, shuffle: bool) -> None:
         n = int(fields[0].shape[0])
@@ -112,24 +140,21 @@ class GraphedUpdate:
             self.perm.copy_(perm, non_blocking=True)
         self.desc[_DESC_MB_OFFSET:_DESC_MB_OFFSET + 8].view(torch.int64).zero_()
 
-    def graph_for(self, fields: List[torch.Tensor], B: int, tag, step) -> MinibatchStepGraph:
-        k = self.key(fields, B, tag)
+    def graph_for(self, fields: List[torch.Tensor], B: int, tag, step, xforms=None) -> MinibatchStepGraph:
+        k = self.key(fields, B, tag, xforms)
         g = self.graphs.get(k)
         if g is None:
-            g = MinibatchStepGraph(self.device, fields, B, step)
+            g = MinibatchStepGraph(self.device, fields, B, step, xforms)
             self.graphs[k] = g
         g.step = step
         return g
 
-    def tail(self, fields: List[torch.Tensor], rows: int, step) -> None:
+    def tail(self, fields: List[torch.Tensor], rows: int, step, xforms=None) -> None:
         """Eager ragged last minibatch through the same device gather."""
-        k = self.key(fields, rows, "tail")
+        k = self.key(fields, rows, "tail", xforms)
         bufs = self._tail_bufs.get(k)
         if bufs is None:
-            bufs = [torch.empty((rows,) + tuple(f.shape[1:]), dtype=f.dtype, device=self.device) for f in fields]
+            bufs = static_buffers(fields, rows, self.device, xforms)
             self._tail_bufs[k] = bufs
-        helper = MinibatchStepGraph.__new__(MinibatchStepGraph)
-        helper.device = self.device
-        helper.row_bytes = [int(f[0].numel() * f.element_size()) for f in fields]
-        helper.gather(self.desc, bufs)
+        gather_next(self.device, self.desc, bufs, [int(f[0].numel() * f.element_size()) for f in fields], xforms)
         step(bufs)

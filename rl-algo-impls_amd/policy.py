@@ -42,6 +42,10 @@ F32_MIN = torch.finfo(torch.float32).min
 # minibatch gather and Categorical head: 1.611 vs 1.667 s per update (MIOpen's NHWC solvers, no
 # layout transposes, contiguous bias-gradient reductions).
 _CHANNELS_LAST = os.environ.get("RAI_CHANNELS_LAST", "1") == "1"
+# NatureCNN conv / Linear -> ReLU as bias-free contractions plus one-pass bias + ReLU epilogues
+# (cnn_ops.py), and the uint8 -> float / range_size prescale fused into the minibatch gather
+# (RAI_CNN_FUSED=0: the modules' own bias / ReLU kernels and the torch prescale)
+_FUSED_EPILOGUES = os.environ.get("RAI_CNN_FUSED", "1") == "1"
 
 
 class Step(NamedTuple):  # actor_critic.py:42-46
@@ -118,14 +122,49 @@ class NatureCnnEncoder(nn.Module):
             activation(),
         )
         self.out_dim = cnn_flatten_dim
+        self._relu = activation is nn.ReLU
+        # the divisor as a device scalar (non-persistent: not in the state_dict), see forward()
+        self.register_buffer("_range", torch.tensor(self.range_size, dtype=torch.float32), persistent=False)
 
-    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+    def obs_transform(self, obs: torch.Tensor):
+        """The rai_gather_xform that turns a gathered uint8 frame row into this encoder's input
+        (obs.float() / range_size, channels_last), or None when the fused path does not apply."""
+        from . import _lib
+
+        C, H, W = (int(d) for d in obs.shape[-3:])
+        if not (_CHANNELS_LAST and _FUSED_EPILOGUES and obs.is_cuda and obs.dtype == torch.uint8 and C <= 4
+                and (H * W) % 4 == 0):
+            return None
+        return _lib.GatherXform(kind=_lib.RAI_XFORM_U8_CHW_TO_F32_HWC, channels=C, hw=H * W,
+                                divisor=self.range_size)
+
+    def forward(self, obs: torch.Tensor, prepared: bool = False) -> torch.Tensor:
+        """prepared: obs is already obs.float() / range_size in channels_last (the minibatch gather's
+        RAI_XFORM_U8_CHW_TO_F32_HWC output)."""
         if obs.dim() == 3:
             obs = obs.unsqueeze(0)
-        x = obs.float() / self.range_size
+        if prepared:
+            x = obs
+        elif obs.is_cuda:
+            # IEEE division, as the reference's CPU path and the fused gather: torch divides a CUDA
+            # tensor by a Python scalar as a multiply by the rounded reciprocal
+            x = obs.float() / self._range
+        else:
+            x = obs.float() / self.range_size
         if _CHANNELS_LAST and x.is_cuda:
             x = x.contiguous(memory_format=torch.channels_last)
+            if _FUSED_EPILOGUES and self._relu:
+                return self._forward_fused(x)
         return self.fc(self.cnn(x))
+
+    def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
+        """Bias-free MIOpen convolutions / hipBLASLt GEMM with the bias + ReLU epilogues of
+        cnn_ops (same modules, same parameters, same state_dict)."""
+        from .cnn_ops import conv_relu, linear_relu
+
+        for i in (0, 2, 4):
+            x = conv_relu(self.cnn[i], x)
+        return linear_relu(self.fc[1], torch.flatten(x, 1))
 
 
 class Encoder(nn.Module):  # shared/encoder/encoder.py:25-73
@@ -152,7 +191,9 @@ class Encoder(nn.Module):  # shared/encoder/encoder.py:25-73
         else:
             raise NotImplementedError(f"Unsupported observation space: {obs_space}")
 
-    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+    def forward(self, obs: torch.Tensor, prepared: bool = False) -> torch.Tensor:
+        if self.kind == "cnn":
+            return self.feature_extractor(obs, prepared)
         if self.kind == "flat":
             if obs.dim() == 1:
                 obs = obs.unsqueeze(0)
@@ -271,8 +312,8 @@ class ConnectedTrioNetwork(nn.Module):
         self.pi_hidden_sizes = tuple(pi_hidden_sizes)
         self.v_hidden_sizes = tuple(v_hidden_sizes)
 
-    def forward(self, obs, action, action_masks=None):
-        enc = self._feature_extractor(obs)
+    def forward(self, obs, action, action_masks=None, obs_prepared: bool = False):
+        enc = self._feature_extractor(obs, obs_prepared)
         logp, ent = self._pi.logp_entropy(self._pi.params(enc), action, action_masks)
         return logp, ent, self._v(enc)
 
@@ -368,8 +409,18 @@ class ActorCritic(nn.Module):
     def is_discrete(self) -> bool:
         return not self.gridnet and isinstance(self.network._pi, CategoricalActorHead)
 
-    def forward(self, obs, action, action_masks=None) -> ACForward:
+    def forward(self, obs, action, action_masks=None, obs_prepared: bool = False) -> ACForward:
+        """obs_prepared: obs came through the minibatch gather's transform (obs_transform())"""
+        if obs_prepared:
+            return ACForward(*self.network(obs, action, action_masks, obs_prepared=True))
         return ACForward(*self.network(obs, action, action_masks))
+
+    def obs_transform(self, obs: torch.Tensor):
+        """The gather transform (rai_gather_xform) that prepares rollout obs rows for forward(...,
+        obs_prepared=True), or None (NatureCNN on uint8 frames only)."""
+        if self.gridnet or self.network._feature_extractor.kind != "cnn":
+            return None
+        return self.network._feature_extractor.feature_extractor.obs_transform(obs)
 
     def _as_tensor(self, a):
         return torch.as_tensor(a).to(self.device)

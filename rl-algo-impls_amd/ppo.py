@@ -530,9 +530,11 @@ class PPO:
         self._wide.check_pointers()
         return self._wide
 
-    def _minibatch_loss_grads(self, wide, obs, actions, masks, values, adv, ret, logprobs, K_box) -> None:
+    def _minibatch_loss_grads(self, wide, obs, actions, masks, values, adv, ret, logprobs, K_box,
+                              obs_prepared: bool = False) -> None:
         """Forward, fused loss and backward of one minibatch into the flat gradient buffer: the
-        wide-MLP kernels when available, else the PyTorch network + autograd."""
+        wide-MLP kernels when available, else the PyTorch network + autograd (NatureCNN layers
+        with the cnn_ops epilogues accumulating straight into the flat gradient views)."""
         if wide is not None and masks is None:
             B = int(obs.shape[0])
             outs = self._wide_out.get(B)
@@ -544,11 +546,17 @@ class PPO:
                                                    ret)
             wide.backward(obs, actions, d_logp, d_ent, d_v)
             return
-        logp, ent, v = self.policy(obs, actions, action_masks=masks)
-        if K_box[0] is None:
-            K_box[0] = value_columns(v)
-        d_logp, d_ent, d_v = launch_loss(self.blocks, logp, ent, v, logprobs, values, adv, ret, K_box[0])
-        torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
+        from .cnn_ops import direct_grads
+
+        with direct_grads(self.flat.flat.is_cuda):
+            if obs_prepared:
+                logp, ent, v = self.policy(obs, actions, action_masks=masks, obs_prepared=True)
+            else:
+                logp, ent, v = self.policy(obs, actions, action_masks=masks)
+            if K_box[0] is None:
+                K_box[0] = value_columns(v)
+            d_logp, d_ent, d_v = launch_loss(self.blocks, logp, ent, v, logprobs, values, adv, ret, K_box[0])
+            torch.autograd.backward([logp, ent, v], [d_logp, d_ent, d_v])
 
     def update(self, r) -> Tuple[np.ndarray, np.ndarray, int]:
         """All epochs x minibatches of one update, enqueued without host syncs;
@@ -649,16 +657,27 @@ class PPO:
         n = r.total_steps
         B = min(self.batch_size, n)
         n_full, tail = n // B, n % B
-        optim_in_step = not self.gradient_accumulation and not self.dp_enabled
+        # data parallel over our RCCL communicator: the gradient all-reduce is bucketed, overlapped
+        # with the backward on a side stream and captured with the step (dp_buckets.py)
+        buckets = self._grad_buckets() if not self.gradient_accumulation else None
+        optim_in_step = not self.gradient_accumulation and (not self.dp_enabled or buckets is not None)
         has_masks = r.action_masks is not None
         K_box = [None]
 
         wide = self._wide_step()
+        # NatureCNN on uint8 frames: the gather emits obs.float() / range_size in channels_last
+        xf = getattr(self.policy, "obs_transform", lambda o: None)(fields[0]) if wide is None else None
+        xforms = [xf] + [None] * (len(fields) - 1) if xf is not None else None
 
         def step(bufs):
             obs, actions, values, adv, ret, logprobs = bufs[:6]
             masks = bufs[6] if has_masks else None
-            self._minibatch_loss_grads(wide, obs, actions, masks, values, adv, ret, logprobs, K_box)
+            if buckets is not None:
+                buckets.begin()
+            self._minibatch_loss_grads(wide, obs, actions, masks, values, adv, ret, logprobs, K_box,
+                                       obs_prepared=xforms is not None)
+            if buckets is not None:
+                buckets.finish(scale=1.0 / self.world)
             if optim_in_step:
                 self.optimizer.step(blocks.state, blocks.norms, count=False)
 
@@ -673,10 +692,10 @@ class PPO:
         hp.ext_moments = ext.data_ptr() if ext is not None else None
         blocks.upload(hp, self.optimizer.step_count)
         # a graph bakes in every device pointer it touches: key it on the ones that can change
-        tag = (optim_in_step, wide is not None, blocks.stats.data_ptr(), blocks.norms.data_ptr(), blocks.hp.data_ptr(),
+        tag = (optim_in_step, wide is not None, buckets is not None, blocks.stats.data_ptr(), blocks.norms.data_ptr(), blocks.hp.data_ptr(),
                blocks.state.data_ptr(), self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
                self.optimizer.hp_dev.data_ptr())
-        g = gu.graph_for(fields, B, tag, step)
+        g = gu.graph_for(fields, B, tag, step, xforms)
         cur = torch.cuda.current_stream(self.device)
         gu.stream.wait_stream(cur)
         with torch.cuda.stream(gu.stream):
@@ -692,7 +711,7 @@ class PPO:
                         self._all_reduce(self.flat.grad, average=True)
                         self.optimizer.step(blocks.state, blocks.norms)
                 if tail:
-                    gu.tail(fields, tail, step)
+                    gu.tail(fields, tail, step, xforms)
                     if not optim_in_step and not self.gradient_accumulation:
                         self._all_reduce(self.flat.grad, average=True)
                         self.optimizer.step(blocks.state, blocks.norms)
@@ -704,6 +723,29 @@ class PPO:
         if optim_in_step:  # replays stepped the optimizer on device; keep the host count in sync
             self.optimizer.step_count += self.n_epochs * (n_full + (1 if tail else 0))
         return K
+
+    def _grad_buckets(self):
+        """GradBuckets for the bucketed, backward-overlapped all-reduce (dp_buckets.py) when data
+        parallel runs over our own RCCL communicator and the policy has a bucket layout (NatureCNN),
+        else None (one all-reduce of the whole flat gradient after the step).  RAI_DP_BUCKETS=0: off."""
+        if not self.dp_enabled or self._dp_comm is None or os.environ.get("RAI_DP_BUCKETS", "1") == "0":
+            return None
+        if getattr(self, "_buckets", None) is not None:
+            return self._buckets
+        from .dp_buckets import GradBuckets, nature_cnn_buckets
+
+        layout = nature_cnn_buckets(self.policy, self.flat)
+        if layout is None:
+            return None
+        bounds, triggers = layout
+        L, comm, dev = _lib.lib(), self._dp_comm, self.device
+
+        def allreduce(v: torch.Tensor) -> None:
+            _lib.check(L.rai_dp_allreduce_sum_f32(comm, v.data_ptr(), v.numel(), _lib.stream_handle(dev)),
+                       "rai_dp_allreduce_sum_f32")
+
+        self._buckets = GradBuckets(self.flat, bounds, triggers, allreduce, dev)
+        return self._buckets
 
     def _train_stats(self, stats: np.ndarray, norms: np.ndarray, K: int, nmb: int, explained_var: float):
         last = stats[-nmb:].astype(np.float64)  # only the last epoch's stats are kept (ppo.py:288-289)

@@ -1,0 +1,47 @@
+"""Run setup of a training process — drop-in for rl_algo_impls/runner/running_utils.py:161-184.
+
+The reference calls `set_seeds(seed)` then `set_device_optimizations(device, **device_hyperparams)`
+before it builds the policy (rai/runner/train.py:87,102); `use_deterministic_algorithms` defaults to
+True there (running_utils.py:164) and only the Lux YAML turns it off (ppo-LuxAI_S2.yml:4131).
+
+On MI355X the switch reaches every kernel of the update:
+  * this package's HIP kernels are deterministic by construction in both modes (fixed reduction
+    orders, no float atomics: the in-L2 / cross-GPU gradient exchanges sum partials in CU / rank
+    order, GAE is a serial chain per column);
+  * PyTorch-ROCm ops (the NatureCNN / squeeze-U-Net convolutions on MIOpen, hipBLASLt GEMMs,
+    index ops) follow torch.use_deterministic_algorithms, and torch.backends.cudnn.deterministic
+    restricts MIOpen to solvers whose reductions have a fixed order (the conv backward-weights
+    split-K solvers otherwise accumulate with atomics, which made two identical C3 updates differ in
+    the last bits, tests/test_gpu_pong.py).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+from typing import Optional
+
+import numpy as np
+import torch
+
+
+def set_device_optimizations(device: torch.device, set_float32_matmul_precision: Optional[str] = None,
+                             use_deterministic_algorithms: bool = True) -> None:
+    """running_utils.py:161-172."""
+    torch.use_deterministic_algorithms(use_deterministic_algorithms)
+    torch.backends.cudnn.deterministic = bool(use_deterministic_algorithms)
+    if torch.device(device).type == "cuda" and set_float32_matmul_precision:
+        logging.info(f"Setting torch.set_float32_matmul_precision to {set_float32_matmul_precision}")
+        torch.set_float32_matmul_precision(set_float32_matmul_precision)
+
+
+def set_seeds(seed: Optional[int]) -> None:
+    """running_utils.py:175-184 (the cuBLAS workspace variable is the reference's; hipBLASLt ignores it)."""
+    if seed is None:
+        return
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.backends.cudnn.benchmark = False
+    os.environ["CUBLAS_WORKSPACE_CONFIG"] = ":4096:8"
+    os.environ["TF_ENABLE_ONEDNN_OPTS"] = "0"

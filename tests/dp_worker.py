@@ -291,3 +291,51 @@ def batch_rule_worker(rank, world, port, q):
     import torch.distributed as dist
 
     dist.destroy_process_group()
+
+
+def cnn_dp_worker(rank, world, port, q, mode):
+    """NatureCNN (C3-shaped, 84x84 uint8 frames) graph-replayed update, world 1 on cuda:0.
+    mode "buckets": data parallel over our RCCL communicator with the bucketed all-reduce overlapped
+    with the backward and captured into the step's graph (dp_buckets.py); "flat": data parallel with
+    the whole-gradient all-reduce after each replay (RAI_DP_BUCKETS=0); "single": no data parallel."""
+    import numpy as np
+    import torch
+
+    if mode == "flat":
+        os.environ["RAI_DP_BUCKETS"] = "0"
+    if mode != "single":
+        _init(rank, world, port, "nccl")
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import DeviceRollout
+
+    torch.backends.cudnn.deterministic = True
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(5)
+    policy = ActorCritic(SyntheticVecEnv(2, "pong", seed=5), activation_fn="relu").to(dev)
+    g = torch.Generator().manual_seed(9)
+    T, N = 2, 256
+    t = lambda x: x.to(dev)
+    r = DeviceRollout(dev, t(torch.zeros(N, dtype=torch.uint8)), t(torch.randn(N, generator=g)),
+                      t(torch.randint(0, 256, (T, N, 4, 84, 84), generator=g, dtype=torch.uint8)),
+                      t(torch.randint(0, 6, (T, N), generator=g)), t(torch.randn(T, N, generator=g)),
+                      t((torch.rand(T, N, generator=g) < 0.05).to(torch.uint8)), t(torch.randn(T, N, generator=g)),
+                      t(-1.79 + 0.05 * torch.randn(T, N, generator=g)), None, 0.99, 0.95,
+                      perm_source=lambda n: torch.randperm(n, generator=torch.Generator().manual_seed(3)))
+    algo = PPO(policy, dev, None, batch_size=128, n_epochs=2, learning_rate=2.5e-4, clip_range=0.1, vf_coef=0.5,
+               ent_coef=0.01)
+    if mode != "single":
+        algo.enable_data_parallel()
+        assert algo._dp_comm is not None
+    stats, norms, _ = algo.update(r)
+    torch.cuda.synchronize()
+    assert (getattr(algo, "_buckets", None) is not None) == (mode == "buckets")
+    q.put((mode, algo.flat.flat.cpu().numpy(), np.asarray(stats), np.asarray(norms)))
+    if mode != "single":
+        import torch.distributed as dist
+
+        dist.destroy_process_group()

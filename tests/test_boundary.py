@@ -75,8 +75,10 @@ def test_policy_state_dict_keys_and_init_match_reference(name, golden):
 def test_registries_use_reference_names():
     from rl_algo_impls_amd import registry
 
-    assert set(registry.ALGOS) == {"ppo", "a2c"}
-    assert registry.DEFAULT_ROLLOUT_GENERATORS["ppo"].__name__ == "SyncStepRolloutGenerator"
+    # the reference's on-policy algorithms over the rollout hot path (running_utils.py:38-55)
+    assert set(registry.ALGOS) == {"ppo", "a2c", "acbc"}
+    for k in registry.ALGOS:
+        assert registry.DEFAULT_ROLLOUT_GENERATORS[k].__name__ == "SyncStepRolloutGenerator"
     assert registry.POLICIES["ppo"] is ActorCritic
 
 

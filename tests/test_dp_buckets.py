@@ -1,0 +1,44 @@
+"""GradBuckets (dp_buckets.py) host logic on CPU: bucket bounds of the NatureCNN policy, trigger
+order, every bucket reduced exactly once per step, the 1/world scale."""
+import torch
+
+from rl_algo_impls_amd.dp_buckets import GradBuckets, nature_cnn_buckets, notify_grad_written
+from rl_algo_impls_amd.envs import SyntheticVecEnv
+from rl_algo_impls_amd.optim import FlatParams
+from rl_algo_impls_amd.policy import ActorCritic
+
+
+def test_nature_cnn_bucket_layout_and_launch_order():
+    torch.manual_seed(0)
+    pol = ActorCritic(SyntheticVecEnv(2, "pong", seed=0), activation_fn="relu")
+    flat = FlatParams(pol, torch.device("cpu"))
+    bounds, triggers = nature_cnn_buckets(pol, flat)
+    fc_w = pol.network._feature_extractor.feature_extractor.fc[1].weight
+    names = [n for n, _ in pol.named_parameters()]
+    k = names.index("network._feature_extractor.feature_extractor.fc.1.weight")
+    assert bounds == [0, flat.offsets[k], flat.P]
+    assert triggers == {id(fc_w): 1}
+    # conv bucket 0.31 MB, fc + heads bucket 6.43 MB (6,750,876 B in total)
+    assert 4 * flat.P == 6750876
+    assert 4 * bounds[1] == 4 * (8192 + 32 + 32768 + 64 + 36864 + 64)
+
+    order = []
+
+    def allreduce(v):
+        order.append((v.data_ptr() - flat.grad.data_ptr()) // 4)
+        v.add_(1.0)  # "sum" with a second rank holding ones
+
+    gb = GradBuckets(flat, bounds, triggers, allreduce, torch.device("cpu"))
+    assert not gb.overlap  # CPU: no side stream; buckets are reduced at finish()
+    flat.grad.zero_()
+    gb.begin()
+    notify_grad_written(fc_w)
+    gb.finish(scale=0.5)
+    assert order == [bounds[1], 0]  # later layers first, each bucket once
+    assert torch.equal(flat.grad, torch.full_like(flat.grad, 0.5))
+
+
+def test_no_bucket_layout_for_mlp_policies():
+    torch.manual_seed(0)
+    pol = ActorCritic(SyntheticVecEnv(2, "cartpole", seed=0))
+    assert nature_cnn_buckets(pol, FlatParams(pol, torch.device("cpu"))) is None

@@ -228,3 +228,39 @@ def test_multicritic_dp_world2_matches_single_process_global_minibatches(after):
     np.testing.assert_allclose(n0, norms, rtol=1e-4)
     np.testing.assert_allclose(s0[:, :8], stats[:, :8], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=2e-6)
+
+
+def test_nature_cnn_bucketed_allreduce_world1_matches_single_process():
+    """C3's data-parallel step with the gradient all-reduce bucketed (fc + heads as soon as the fc
+    backward has written them, overlapping the convolutions' backward; the convolutions after) on
+    a side stream and captured into the step's hipGraph over our RCCL communicator (1-rank group on
+    this one GPU): the same update as the whole-gradient all-reduce after each replay and as the
+    single-process update (deterministic MIOpen solvers, so the three runs agree to fp32 rounding)."""
+    import queue
+    import time
+
+    import dp_worker
+
+    ctx = mp.get_context("spawn")
+    out = {}
+    for mode in ("buckets", "flat", "single"):
+        q = ctx.Queue()
+        p = ctx.Process(target=dp_worker.cnn_dp_worker, args=(0, 1, _port(), q, mode))
+        p.start()
+        deadline = time.time() + 240
+        while True:
+            try:
+                res = q.get(timeout=2)
+                break
+            except queue.Empty:
+                assert p.exitcode in (None, 0), f"{mode} worker exited with {p.exitcode}"
+                assert time.time() < deadline, f"{mode} worker did not report in time"
+        p.join(timeout=60)
+        assert p.exitcode == 0
+        out[res[0]] = res[1:]
+    pb, sb, nb = out["buckets"]
+    for other in ("flat", "single"):
+        po, so, no = out[other]
+        np.testing.assert_allclose(nb, no, rtol=1e-5)
+        np.testing.assert_allclose(sb[:, :6], so[:, :6], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(pb, po, rtol=1e-5, atol=1e-7)

@@ -419,3 +419,95 @@ def test_gather_minibatch_next_all_field_granularities(n, B, shuffle):
     torch.cuda.synchronize()
     d = _lib.MinibatchDesc.from_buffer_copy(bytes(gu.desc.cpu().numpy()))
     assert d.mb == nmb and d.arrivals == 0
+
+
+@pytest.mark.parametrize("C,H,W,n,B", [(4, 84, 84, 700, 256), (1, 12, 10, 300, 64), (3, 8, 8, 130, 64),
+                                       (2, 84, 84, 50, 32)])
+def test_gather_minibatch_frame_transform(C, H, W, n, B):
+    """rai_gather_minibatch_x with RAI_XFORM_U8_CHW_TO_F32_HWC on a uint8 frame field (the NatureCNN
+    prescale obs.float() / range_size of rl_algo_impls/shared/encoder/cnn.py:24-27 fused with the
+    channels_last conversion) next to copied fields: every minibatch's frames equal the CPU
+    reference's true division bit for bit, in channels_last layout; the copied fields equal the
+    index-gathered rows; the ragged tail and the device advance as for the plain gather."""
+    from rl_algo_impls_amd.graphs import GraphedUpdate, gather_next, static_buffers
+
+    g = torch.Generator(device="cpu").manual_seed(C * 1000 + n)
+    frames = torch.randint(0, 256, (n, C, H, W), generator=g, dtype=torch.uint8)
+    fields = [frames.to(DEV), torch.randint(0, 6, (n,), generator=g).to(DEV), torch.randn(n, generator=g).to(DEV)]
+    xf = _lib.GatherXform(kind=_lib.RAI_XFORM_U8_CHW_TO_F32_HWC, channels=C, hw=H * W, divisor=255.0)
+    xforms = [xf, None, None]
+    gu = GraphedUpdate(DEV)
+    gu.set_rollout(fields, B, True)
+    perm = torch.randperm(n, generator=g)
+    gu.start_epoch(perm.to(DEV))
+    row_bytes = [int(f[0].numel() * f.element_size()) for f in fields]
+    ref = frames.float() / 255.0  # the reference's CPU path: IEEE division
+    for mb in range((n + B - 1) // B):
+        rows = min(B, n - mb * B)
+        bufs = static_buffers(fields, B, DEV, xforms)
+        assert bufs[0].dtype == torch.float32 and bufs[0].is_contiguous(memory_format=torch.channels_last)
+        bufs[0].fill_(-1.0)
+        gather_next(DEV, gu.desc, bufs, row_bytes, xforms)
+        sel = perm[mb * B: mb * B + rows]
+        got = bufs[0][:rows].cpu()
+        assert torch.equal(got, ref[sel]), "frame transform differs from obs.float() / 255"
+        assert torch.equal(bufs[1][:rows].cpu(), fields[1][sel.to(DEV)].cpu())
+        assert torch.equal(bufs[2][:rows].cpu(), fields[2][sel.to(DEV)].cpu())
+        if rows < B:
+            assert (bufs[0][rows:] == -1.0).all()
+    torch.cuda.synchronize()
+    d = _lib.MinibatchDesc.from_buffer_copy(bytes(gu.desc.cpu().numpy()))
+    assert d.mb == (n + B - 1) // B and d.arrivals == 0
+
+
+def test_gather_minibatch_transform_rejects_bad_shapes():
+    import ctypes as C
+
+    from rl_algo_impls_amd.graphs import GraphedUpdate
+
+    fields = [torch.zeros(8, 5, 3, 3, dtype=torch.uint8, device=DEV)]  # 5 planes, hw = 9 (not % 4)
+    gu = GraphedUpdate(DEV)
+    gu.set_rollout(fields, 4, False)
+    gu.start_epoch(None)
+    out = torch.empty(4, 5, 3, 3, device=DEV)
+    dst = (C.c_void_p * 1)(out.data_ptr())
+    rb = (C.c_int64 * 1)(45)
+    for x in (_lib.GatherXform(kind=1, channels=5, hw=9, divisor=255.0),
+              _lib.GatherXform(kind=1, channels=4, hw=9, divisor=255.0), _lib.GatherXform(kind=7)):
+        arr = (_lib.GatherXform * 1)(x)
+        rc = _lib.lib().rai_gather_minibatch_x(gu.desc.data_ptr(), 1, C.cast(dst, C.c_void_p), C.cast(rb, C.c_void_p),
+                                               C.cast(arr, C.c_void_p), 4, 1, _lib.stream_handle(DEV))
+        assert rc in (-2, -3)
+
+
+@pytest.mark.parametrize("rows,C", [(256 * 400, 32), (256 * 81, 64), (256 * 49, 64), (256, 512), (3, 8), (1000, 1024)])
+def test_bias_relu_fwd_bwd_match_torch(rows, C):
+    """rai_bias_relu_fwd / _bwd (csrc/se_block.hip) against torch fp32: relu(x + b) and
+    threshold_backward bit for bit; the bias gradient (one fixed-order reduction) within fp32
+    summation tolerance of torch's column sum, written or accumulated, and identical run to run."""
+    g = torch.Generator(device="cpu").manual_seed(rows + C)
+    x = torch.randn(rows, C, generator=g).to(DEV)
+    b = torch.randn(C, generator=g).to(DEV)
+    dy = torch.randn(rows, C, generator=g).to(DEV)
+    x[0, :4] = float("nan")
+    L, st = _lib.lib(), _lib.stream_handle(DEV)
+    y = torch.empty_like(x)
+    _lib.check(L.rai_bias_relu_fwd(x.data_ptr(), b.data_ptr(), rows, C, y.data_ptr(), st), "fwd")
+    ref = torch.relu(x + b)
+    assert torch.equal(y.isnan(), ref.isnan())
+    assert torch.equal(torch.nan_to_num(y), torch.nan_to_num(ref))
+    y = torch.nan_to_num(y)
+    ws = torch.full((int(L.rai_bias_relu_workspace_bytes(C)),), 0x7f, dtype=torch.uint8, device=DEV)  # any contents
+    dbs = []
+    for acc in (0, 1, 0):
+        dx = torch.empty_like(x)
+        db = torch.full((C,), 0.5, device=DEV)
+        _lib.check(L.rai_bias_relu_bwd(dy.data_ptr(), y.data_ptr(), rows, C, dx.data_ptr(), db.data_ptr(), acc,
+                                       ws.data_ptr(), ws.numel(), st), "bwd")
+        dx_ref = torch.ops.aten.threshold_backward(dy, y, 0.0)
+        assert torch.equal(dx, dx_ref)
+        db_ref = dx_ref.double().sum(0)
+        np.testing.assert_allclose(db.double().cpu().numpy(), (db_ref + (0.5 if acc else 0.0)).cpu().numpy(),
+                                   rtol=1e-5, atol=2e-6 * rows ** 0.5)
+        dbs.append(db - (0.5 if acc else 0.0))
+    assert torch.equal(dbs[0], dbs[2])  # deterministic

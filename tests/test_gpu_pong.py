@@ -68,11 +68,15 @@ def _fixture_rollout(z, meta):
 
 
 @pytest.mark.parametrize("graphs", [True, False], ids=["graph_replay", "eager"])
-@pytest.mark.parametrize("channels_last", [True, False], ids=["nhwc", "nchw"])
-def test_pong_minibatch_steps_match_reference(channels_last, graphs, monkeypatch):
+@pytest.mark.parametrize("layout", ["nhwc_fused", "nhwc", "nchw"])
+def test_pong_minibatch_steps_match_reference(layout, graphs, monkeypatch):
+    """nhwc_fused (the default): frames prepared by the gather's uint8 -> float / 255 channels_last
+    transform (graph replay) and the cnn_ops bias + ReLU epilogues with in-place gradient
+    accumulation; nhwc: the modules' own kernels on channels_last; nchw: plain NCHW."""
     z = np.load(GOLDEN / "pong_steps.npz", allow_pickle=False)
     meta = json.loads(str(z["index"]))
-    monkeypatch.setattr(policy_mod, "_CHANNELS_LAST", channels_last)
+    monkeypatch.setattr(policy_mod, "_CHANNELS_LAST", layout != "nchw")
+    monkeypatch.setattr(policy_mod, "_FUSED_EPILOGUES", layout == "nhwc_fused")
     pol = _pong_policy(meta["shapes"])
     nets.load_flat(pol, pong_init([tuple(s) for s in meta["shapes"]], meta["init_seed"]))
     pol = pol.to(DEV)
@@ -85,6 +89,8 @@ def test_pong_minibatch_steps_match_reference(channels_last, graphs, monkeypatch
     torch.cuda.synchronize()
     if graphs:
         assert algo._graphed is not None and any(g.graph is not None for g in algo._graphed.graphs.values())
+        fused_gather = any(g.xforms is not None for g in algo._graphed.graphs.values())
+        assert fused_gather == (layout == "nhwc_fused")
     lr = float(kw["learning_rate"])
     # pre-clip gradient norms (each step clips to 0.5): fp32, different conv summation order
     np.testing.assert_allclose(norms, z["norms"], rtol=2e-4)
@@ -159,3 +165,46 @@ def test_pong_full_shape_update():
         np.testing.assert_allclose(pg, pe, rtol=1e-3, atol=2e-5)
     finally:
         torch.backends.cudnn.deterministic = det
+
+
+@pytest.mark.parametrize("deterministic", [True, False], ids=["deterministic", "default"])
+def test_c3_update_reproducibility(deterministic):
+    """The reference runs with torch.use_deterministic_algorithms(True) by default
+    (rl_algo_impls/runner/running_utils.py:161-166).  Under running_utils.set_device_optimizations
+    the same C3 update from the same weights, rollout and permutations is bitwise reproducible
+    (HIP kernels: fixed reduction orders; MIOpen / hipBLASLt: deterministic solvers).  Without it
+    the two runs agree within fp32 summation tolerance (MIOpen may pick split-K atomics)."""
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.running_utils import set_device_optimizations
+
+    prev = (torch.are_deterministic_algorithms_enabled(), torch.backends.cudnn.deterministic)
+    set_device_optimizations(DEV, use_deterministic_algorithms=deterministic)
+    try:
+        N, T = 64, 32
+        env = SyntheticVecEnv(N, "pong", seed=3)
+        torch.manual_seed(3)
+        pol = ActorCritic(env, activation_fn="relu").to(DEV)
+        gen = SyncStepRolloutGenerator(pol, env, n_steps=T, seed=3)
+        r = gen.rollout(gamma=0.99, gae_lambda=0.95)
+        p0 = torch.nn.utils.parameters_to_vector(pol.parameters()).detach().clone()
+        out = []
+        for _ in range(2):
+            torch.nn.utils.vector_to_parameters(p0, pol.parameters())
+            algo = PPO(pol, DEV, None, n_epochs=2, batch_size=256, learning_rate=2.5e-4, clip_range=0.1,
+                       vf_coef=0.5, ent_coef=0.01)
+            g = torch.Generator(device="cpu").manual_seed(11)
+            r._perm_source = lambda n: torch.randperm(n, generator=g)
+            stats, norms, _ = algo.update(r)
+            torch.cuda.synchronize()
+            out.append((algo.flat.flat.detach().cpu().numpy().copy(), norms.copy()))
+        (pa, na), (pb, nb) = out
+        if deterministic:
+            np.testing.assert_array_equal(pa, pb)
+            np.testing.assert_array_equal(na, nb)
+        else:
+            np.testing.assert_allclose(pa, pb, rtol=1e-4, atol=1e-6)
+            np.testing.assert_allclose(na, nb, rtol=1e-4)
+    finally:
+        torch.use_deterministic_algorithms(prev[0])
+        torch.backends.cudnn.deterministic = prev[1]

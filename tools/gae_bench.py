@@ -1,5 +1,6 @@
 """GAE kernel microbenchmark: algorithmic GB/s at the BASELINE shapes and in the
-bandwidth regime (HIP events on the launch stream)."""
+bandwidth regime (HIP events on the launch stream around back-to-back launches queued behind a
+spin, so the per-launch figure is kernel time plus the kernel-boundary gap)."""
 import sys
 from pathlib import Path
 
@@ -27,7 +28,11 @@ for (T, N, K) in [(128, 4096, 1), (512, 2048, 1), (128, 1024, 1), (512, 512, 3),
     for mode, name in ((EXACT, "exact"), (FAST, "fast")):
         for _ in range(5):
             compute_advantages_device(r, v, es, nes, nv, g, 0.95, mode=mode, advantages_out=adv, returns_out=ret)
-        reps = 50
+        reps = 200
+        torch.cuda.synchronize()
+        # park the stream behind a spin so every launch is queued before the GPU reaches it: the
+        # event pair then times back-to-back kernels, not the Python launch gap (as bench.py)
+        torch.cuda._sleep(50_000_000)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):

@@ -18,6 +18,6 @@ step() {  # name timeout cmd...
 }
 STEPS=${STEPS:-smoke,pytest,bench}
 [[ $STEPS == *smoke* ]] && step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *pytest* ]] && step pytest_gpu 900 python -m pytest tests -m gpu -q -x
+[[ $STEPS == *pytest* ]] && step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
 [[ $STEPS == *bench* ]] && step bench 900 python bench.py ${BENCH_ARGS:-}
 exit 0

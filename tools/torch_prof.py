@@ -25,6 +25,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--config", default="microrts")
 p.add_argument("--num-envs", type=int, default=64)
 p.add_argument("--rows", type=int, default=30)
+p.add_argument("--deterministic", type=int, default=0)
 args = p.parse_args()
 cfg = bench.CONFIGS[args.config]
 N, T = args.num_envs, cfg["n_steps"]
@@ -32,6 +33,9 @@ algo_kw = dict(cfg["algo"])
 if args.config == "microrts":
     algo_kw["batch_size"] = max(1, algo_kw["batch_size"] * N // cfg["num_envs"])
 dev = torch.device("cuda", 0)
+from rl_algo_impls_amd.running_utils import set_device_optimizations  # noqa: E402
+
+set_device_optimizations(dev, use_deterministic_algorithms=bool(args.deterministic))
 torch.manual_seed(1)
 env = SyntheticVecEnv(N, cfg["env"], seed=1)
 policy = ActorCritic(env, **cfg["policy"]).to(dev)
