@@ -73,9 +73,10 @@ def parse():
                         "takes batch_size rows of its own rollout per optimizer step (global minibatch "
                         "batch_size x world; weak scaling); global = SURVEY 8(e): batch_size / world rows "
                         "per rank, so the global minibatch is the YAML batch_size")
-    p.add_argument("--deterministic", type=int, default=1, choices=[0, 1],
-                   help="torch.use_deterministic_algorithms + MIOpen deterministic solvers, as the reference's "
-                        "set_device_optimizations default (rl_algo_impls/runner/running_utils.py:161-166)")
+    p.add_argument("--deterministic", type=int, default=0, choices=[0, 1],
+                   help="1: torch.use_deterministic_algorithms + MIOpen deterministic solvers (the reference's "
+                        "set_device_optimizations default, rl_algo_impls/runner/running_utils.py:161-166); off by "
+                        "default: ~100x slower C3 convolutions on MI355X (rl-algo-impls_amd/running_utils.py)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--roofline-reps", type=int, default=200)
@@ -307,12 +308,11 @@ def main():
     gae_us = e0.elapsed_time(e1) * 1e3 / args.roofline_reps
     workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
     pmc = {}
-    for name in ("r1g_pmc.json", "r1f_pmc.json", "r1e_pmc.json", "r1d_pmc.json", "r1c_pmc.json", "r1_pmc.json"):  # newest PMC summary holding this workload
-        pmc_path = ROOT / "profiles" / name
-        if pmc_path.exists():
-            pmc = json.loads(pmc_path.read_text()).get(workload, {})
-            if pmc:
-                break
+    # the newest PMC summary (profiles/r<round><letter>_pmc.json, tools/pmc_summary.py) holding this workload
+    for pmc_path in sorted((ROOT / "profiles").glob("r*_pmc.json"), reverse=True):
+        pmc = json.loads(pmc_path.read_text()).get(workload, {})
+        if pmc:
+            break
 
     def traffic(kernel):
         return pmc.get(kernel, {}).get("traffic_bytes_per_launch")
@@ -376,6 +376,9 @@ def main():
         if args.dp_rehearsal or world > 1:
             if algo._xdp is not None:
                 line["dp_path"] = "in-kernel cross-GPU exchange (IPC-mapped xGMI regions), one launch per epoch"
+            elif algo._dp_comm is not None and getattr(algo, "_buckets", None) is not None:
+                line["dp_path"] = ("bucketed RCCL all-reduce per optimizer step on a side stream, overlapped with "
+                                   "the backward, captured with the step's hipGraph")
             elif algo._dp_comm is not None:
                 line["dp_path"] = "native RCCL loop (all-reduce per optimizer step)"
             else:

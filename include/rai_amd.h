@@ -292,6 +292,27 @@ int rai_minibatch_advance(rai_minibatch_desc* desc, void* stream);
 int rai_gather_minibatch_next(rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
                               const int64_t* row_bytes, int64_t batch_size, void* stream);
 
+/* Actor-critic heads of the NatureCNN policy: a Categorical actor head Linear(D, A) and a critic head
+ * Linear(D, 1) over the encoder output enc (B, D), with the Categorical log-prob of `actions` and the
+ * entropy (rl_algo_impls/shared/actor/categorical.py:57-87, rl_algo_impls/shared/policy/critic.py:11-41,
+ * actor_critic_network/connected_trio.py:83-92; torch.distributions.Categorical arithmetic).
+ * Forward: logits_out (B, A) (kept for the backward), logp_out / entropy_out / v_out (B).
+ * Backward, two launches: from the upstream d_logp, d_entropy, d_v (B): d_enc (B, D) written, and the
+ * gradients of wpi (A, D), bpi (A), wv (D), bv (1) written (accumulate == 0) or added (accumulate != 0,
+ * e.g. into the flat .grad buffer).  A in 2..10 or 12; workspace >= rai_categorical_critic_heads_
+ * workspace_bytes(B, A).  Fixed reduction orders (deterministic). */
+int rai_categorical_critic_heads_fwd(const float* enc, const float* wpi, const float* bpi, const float* wv,
+                                     const float* bv, const int64_t* actions, int64_t B, int32_t D, int32_t A,
+                                     float* logits_out, float* logp_out, float* entropy_out, float* v_out,
+                                     void* stream);
+int64_t rai_categorical_critic_heads_workspace_bytes(int64_t B, int32_t A);
+int rai_categorical_critic_heads_bwd(const float* enc, const float* wpi, const float* bpi, const float* wv,
+                                     const float* bv, const int64_t* actions, const float* logits, int64_t B,
+                                     int32_t D, int32_t A, const float* d_logp, const float* d_entropy,
+                                     const float* d_v, float* d_enc, float* g_wpi, float* g_bpi, float* g_wv,
+                                     float* g_bv, int32_t accumulate, void* workspace, int64_t workspace_bytes,
+                                     void* stream);
+
 /* Per-field output transform of the minibatch gather.
  *   RAI_XFORM_COPY: the row's bytes are copied (as above).
  *   RAI_XFORM_U8_CHW_TO_F32_HWC: the source row is `channels` (<= 4) planes of `hw` uint8 pixels

@@ -159,6 +159,11 @@ _SIGNATURES = {
     "rai_gather_minibatch_next": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_gather_minibatch_x": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _i64, _i32, _vp]),
     "rai_bias_relu_workspace_bytes": (_i64, [_i32]),
+    "rai_categorical_critic_heads_fwd": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
+                                                   _vp]),
+    "rai_categorical_critic_heads_workspace_bytes": (_i64, [_i64, _i32]),
+    "rai_categorical_critic_heads_bwd": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp,
+                                                   _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_bias_relu_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "rai_bias_relu_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, [C.c_int64, C.c_int32]),

@@ -170,3 +170,70 @@ def linear_relu(lin: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
         _WS.prewarm(id(lin), lin.out_features, x.device)
         return LinearBiasReLU.apply(x.contiguous(), lin.weight, lin.bias, id(lin))
     return F.relu(lin(x))
+
+
+class CategoricalCriticHeads(torch.autograd.Function):
+    """(logp(a), entropy, v) of a Categorical actor head Linear(D, A) and a critic head Linear(D, 1)
+    over the encoder output (rai_categorical_critic_heads_fwd / _bwd, csrc/heads.hip): one launch
+    forward, two backward, in place of the heads' GEMMs, the Categorical kernels, the bias
+    reductions and the gradient accumulates."""
+
+    @staticmethod
+    def forward(ctx, enc, wpi, bpi, wv, bv, actions):
+        B, D = int(enc.shape[0]), int(enc.shape[1])
+        A = int(wpi.shape[0])
+        logits = torch.empty((B, A), dtype=torch.float32, device=enc.device)
+        logp = torch.empty(B, dtype=torch.float32, device=enc.device)
+        ent = torch.empty_like(logp)
+        v = torch.empty_like(logp)
+        _lib.check(_lib.lib().rai_categorical_critic_heads_fwd(
+            enc.data_ptr(), wpi.data_ptr(), bpi.data_ptr(), wv.data_ptr(), bv.data_ptr(), actions.data_ptr(), B, D, A,
+            logits.data_ptr(), logp.data_ptr(), ent.data_ptr(), v.data_ptr(), _lib.stream_handle(enc.device)),
+            "rai_categorical_critic_heads_fwd")
+        ctx.save_for_backward(enc, wpi, bpi, wv, bv, actions, logits)
+        ctx.direct = all(_direct(p) for p in (wpi, bpi, wv, bv))
+        ctx.mark_non_differentiable(logits)
+        return logp, ent, v
+
+    @staticmethod
+    def backward(ctx, d_logp, d_ent, d_v):
+        enc, wpi, bpi, wv, bv, actions, logits = ctx.saved_tensors
+        B, D, A = int(enc.shape[0]), int(enc.shape[1]), int(wpi.shape[0])
+        dev = enc.device
+        z = lambda t: t.contiguous() if t is not None else torch.zeros(B, dtype=torch.float32, device=dev)
+        d_logp, d_ent, d_v = z(d_logp), z(d_ent), z(d_v)
+        d_enc = torch.empty_like(enc)
+        if ctx.direct:
+            grads = (wpi.grad, bpi.grad, wv.grad, bv.grad)
+        else:
+            grads = tuple(torch.empty_like(p) for p in (wpi, bpi, wv, bv))
+        L = _lib.lib()
+        ws = torch.empty(int(L.rai_categorical_critic_heads_workspace_bytes(B, A)), dtype=torch.uint8, device=dev)
+        _lib.check(L.rai_categorical_critic_heads_bwd(
+            enc.data_ptr(), wpi.data_ptr(), bpi.data_ptr(), wv.data_ptr(), bv.data_ptr(), actions.data_ptr(),
+            logits.data_ptr(), B, D, A, d_logp.data_ptr(), d_ent.data_ptr(), d_v.data_ptr(), d_enc.data_ptr(),
+            *[g.data_ptr() for g in grads], 1 if ctx.direct else 0, ws.data_ptr(), ws.numel(),
+            _lib.stream_handle(dev)), "rai_categorical_critic_heads_bwd")
+        if ctx.direct:
+            return d_enc, None, None, None, None, None
+        return (d_enc,) + grads + (None,)
+
+
+def heads_fusable(network, enc: torch.Tensor, action_masks) -> bool:
+    """A ConnectedTrio network whose actor head is Categorical Linear(D, A) and critic head
+    Linear(D, 1), no hidden layers, no action masks, fp32 on the GPU (the NatureCNN policy)."""
+    from .policy import CategoricalActorHead
+
+    pi = network._pi
+    if not (enc.is_cuda and enc.dtype == torch.float32 and enc.dim() == 2 and action_masks is None
+            and isinstance(pi, CategoricalActorHead) and network.pi_hidden_sizes == () and network.v_hidden_sizes == ()):
+        return False
+    A = pi.act_dim
+    return (2 <= A <= 10 or A == 12) and isinstance(pi._fc[0], torch.nn.Linear)
+
+
+def categorical_critic_heads(network, enc: torch.Tensor, actions: torch.Tensor):
+    lin_pi = network._pi._fc[0]
+    lin_v = network._v._fc[0][0]
+    return CategoricalCriticHeads.apply(enc.contiguous(), lin_pi.weight, lin_pi.bias, lin_v.weight,
+                                        lin_v.bias, actions.long().contiguous())

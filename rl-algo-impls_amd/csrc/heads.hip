@@ -1,0 +1,279 @@
+// Actor-critic heads of the NatureCNN policy (config C3) on gfx950: a Categorical actor head and a
+// scalar critic head, both single Linear layers over the encoder output, plus the Categorical
+// log-prob / entropy.  Reference: rl_algo_impls/shared/actor/categorical.py:57-87
+// (CategoricalActorHead: Linear(512, A) logits, torch.distributions.Categorical log_prob and
+// entropy), rl_algo_impls/shared/policy/critic.py:11-41 (CriticHead: Linear(512, 1)), joined by
+// rl_algo_impls/shared/policy/actor_critic_network/connected_trio.py:83-92.
+//
+// PyTorch runs this as two hipBLASLt GEMMs with bias, a dozen Categorical kernels, and in the
+// backward two GEMMs for the weights, two for the input (then an add of the two input gradients),
+// two bias reductions and four accumulates into .grad: ~20 launches per minibatch of B = 256 rows
+// and 7 x 512 weights.  Here:
+//   forward   one launch:  logits = enc Wpi^T + bpi, v = enc Wv^T + bv, logp(a), entropy
+//                          (one wave per row, dot products as lane partials + a wave reduction)
+//   backward  two launches: (1) per row: dlogits from (d_logp, d_entropy), and
+//                          d_enc = dlogits Wpi + dv Wv;  (2) per 16-column slice of the weights:
+//                          dWpi, dWv summed over the rows in row order, biases by slice 0;
+//                          written or added (accumulate) into the caller's gradient buffers.
+// Categorical arithmetic follows torch.distributions.Categorical: logits normalised by logsumexp,
+// entropy = -sum(clamp(logits_n, min=finfo.min) * p).  Deterministic (fixed orders, no atomics).
+#include "common.h"
+
+namespace {
+
+constexpr int HD_THREADS = 256;  // 4 waves, one row each
+constexpr float HD_F32_MIN = -3.4028234663852886e38f;
+
+struct HeadsArgs {
+  const float* enc;    // (B, D)
+  const float* wpi;    // (A, D)
+  const float* bpi;    // (A)
+  const float* wv;     // (D)
+  const float* bv;     // (1)
+  const int64_t* act;  // (B)
+  int64_t B;
+  int D, A;
+};
+
+__device__ __forceinline__ float wave_reduce(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int A>
+__global__ __launch_bounds__(HD_THREADS) void heads_fwd_kernel(const HeadsArgs a, float* __restrict__ logits_out,
+                                                              float* __restrict__ logp, float* __restrict__ ent,
+                                                              float* __restrict__ v_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (HD_THREADS / 64) + (threadIdx.x >> 6);
+  if (b >= a.B) return;
+  const int D = a.D;
+  const float* e = a.enc + b * D;
+  float acc[A + 1];
+#pragma unroll
+  for (int o = 0; o <= A; ++o) acc[o] = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float x = e[d];
+#pragma unroll
+    for (int o = 0; o < A; ++o) acc[o] = fmaf(x, a.wpi[o * D + d], acc[o]);
+    acc[A] = fmaf(x, a.wv[d], acc[A]);
+  }
+  float z[A];
+#pragma unroll
+  for (int o = 0; o < A; ++o) z[o] = wave_reduce(acc[o]) + a.bpi[o];
+  const float v = wave_reduce(acc[A]) + a.bv[0];
+  if (lane == 0) {
+    float m = z[0];
+#pragma unroll
+    for (int o = 1; o < A; ++o) m = fmaxf(m, z[o]);
+    float se = 0.f;
+#pragma unroll
+    for (int o = 0; o < A; ++o) se += expf(z[o] - m);
+    const float lse = m + logf(se);
+    float H = 0.f;
+    const int act = (int)a.act[b];
+    float zact = z[0];
+#pragma unroll
+    for (int o = 0; o < A; ++o) {
+      const float n = z[o] - lse;
+      H -= fmaxf(n, HD_F32_MIN) * expf(n);
+      if (o == act) zact = z[o];
+      logits_out[b * A + o] = z[o];
+    }
+    logp[b] = zact - lse;
+    ent[b] = H;
+    v_out[b] = v;
+  }
+}
+
+// (1) per row: dlogits and d_enc; dlogits (B, A) and dv (B) stored for pass (2)
+template <int A>
+__global__ __launch_bounds__(HD_THREADS) void heads_bwd_rows_kernel(const HeadsArgs a, const float* __restrict__ logits,
+                                                                   const float* __restrict__ d_logp,
+                                                                   const float* __restrict__ d_ent,
+                                                                   const float* __restrict__ d_v,
+                                                                   float* __restrict__ dlogits, float* __restrict__ dvv,
+                                                                   float* __restrict__ d_enc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (HD_THREADS / 64) + (threadIdx.x >> 6);
+  if (b >= a.B) return;
+  float z[A];
+#pragma unroll
+  for (int o = 0; o < A; ++o) z[o] = logits[b * A + o];
+  float m = z[0];
+#pragma unroll
+  for (int o = 1; o < A; ++o) m = fmaxf(m, z[o]);
+  float se = 0.f;
+#pragma unroll
+  for (int o = 0; o < A; ++o) se += expf(z[o] - m);
+  const float lse = m + logf(se);
+  float H = 0.f;
+#pragma unroll
+  for (int o = 0; o < A; ++o) {
+    const float n = z[o] - lse;
+    H -= fmaxf(n, HD_F32_MIN) * expf(n);
+  }
+  const int act = (int)a.act[b];
+  const float gl = d_logp[b], ge = d_ent[b], gv = d_v[b];
+  float dq[A];
+#pragma unroll
+  for (int o = 0; o < A; ++o) {
+    const float n = z[o] - lse;
+    const float p = expf(n);
+    dq[o] = gl * ((o == act ? 1.f : 0.f) - p) + ge * (-p * (n + H));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int o = 0; o < A; ++o) dlogits[b * A + o] = dq[o];
+    dvv[b] = gv;
+  }
+  const int D = a.D;
+  for (int d = lane; d < D; d += 64) {
+    float s = gv * a.wv[d];
+#pragma unroll
+    for (int o = 0; o < A; ++o) s = fmaf(dq[o], a.wpi[o * D + d], s);
+    d_enc[b * D + d] = s;
+  }
+}
+
+// (2) weight gradients: workgroup j owns columns [16 j, 16 j + 16) of Wpi / Wv; its 256 threads are
+// 16 columns x 16 row lanes; each lane sums rows lane, lane + 16, ... (row order), then the 16 row
+// lanes are added in order through LDS.  Workgroup 0 also sums the bias gradients.
+template <int A>
+__global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const HeadsArgs a,
+                                                                      const float* __restrict__ dlogits,
+                                                                      const float* __restrict__ dvv,
+                                                                      float* __restrict__ g_wpi, float* __restrict__ g_bpi,
+                                                                      float* __restrict__ g_wv, float* __restrict__ g_bv,
+                                                                      int accumulate) {
+  __shared__ float red[A + 1][16][17];
+  const int tid = threadIdx.x, col = tid & 15, rl = tid >> 4;
+  const int d = blockIdx.x * 16 + col;
+  const int D = a.D;
+  const int64_t B = a.B;
+  float acc[A + 1];
+#pragma unroll
+  for (int o = 0; o <= A; ++o) acc[o] = 0.f;
+  if (d < D) {
+    for (int64_t b = rl; b < B; b += 16) {
+      const float x = a.enc[b * D + d];
+#pragma unroll
+      for (int o = 0; o < A; ++o) acc[o] = fmaf(dlogits[b * A + o], x, acc[o]);
+      acc[A] = fmaf(dvv[b], x, acc[A]);
+    }
+  }
+#pragma unroll
+  for (int o = 0; o <= A; ++o) red[o][rl][col] = acc[o];
+  __syncthreads();
+  if (tid < 16 * (A + 1)) {
+    const int o = tid >> 4, c = tid & 15;
+    const int dd = blockIdx.x * 16 + c;
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += red[o][r][c];
+    if (dd < D) {
+      float* dst = o < A ? g_wpi + o * D + dd : g_wv + dd;
+      *dst = accumulate ? *dst + s : s;
+    }
+  }
+  if (blockIdx.x == 0) {  // biases: 16 row lanes per output (rows lane, lane + 16, ...), lanes in order
+    __syncthreads();
+    const int o = tid >> 4, l = tid & 15;
+    float s = 0.f;
+    if (o <= A)
+      for (int64_t b = l; b < B; b += 16) s += o < A ? dlogits[b * A + o] : dvv[b];
+    if (o <= A) red[o][l][16] = s;
+    __syncthreads();
+    if (tid <= A) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t += red[tid][r][16];
+      float* dst = tid < A ? g_bpi + tid : g_bv;
+      *dst = accumulate ? *dst + t : t;
+    }
+  }
+}
+
+// 16 x (A + 1) threads of the weight pass cover the outputs: A <= 12 (Atari: 6; 18 would need a
+// second pass)
+bool a_ok(int A) { return (A >= 2 && A <= 10) || A == 12; }
+
+HeadsArgs make_args(const float* enc, const float* wpi, const float* bpi, const float* wv, const float* bv,
+                    const int64_t* actions, int64_t B, int32_t D, int32_t A) {
+  HeadsArgs a;
+  a.enc = enc;
+  a.wpi = wpi;
+  a.bpi = bpi;
+  a.wv = wv;
+  a.bv = bv;
+  a.act = actions;
+  a.B = B;
+  a.D = D;
+  a.A = A;
+  return a;
+}
+
+}  // namespace
+
+extern "C" int rai_categorical_critic_heads_fwd(const float* enc, const float* wpi, const float* bpi, const float* wv,
+                                                const float* bv, const int64_t* actions, int64_t B, int32_t D,
+                                                int32_t A, float* logits_out, float* logp_out, float* entropy_out,
+                                                float* v_out, void* stream) {
+  if (B < 0 || D < 1 || !a_ok(A)) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!enc || !wpi || !bpi || !wv || !bv || !actions || !logits_out || !logp_out || !entropy_out || !v_out)
+    return RAI_E_NULLPTR;
+  const HeadsArgs a = make_args(enc, wpi, bpi, wv, bv, actions, B, D, A);
+  const dim3 grid((unsigned)((B + 3) / 4));
+  hipStream_t st = rai_stream(stream);
+  switch (A) {
+#define RAI_HD_F(n) \
+  case n: hipLaunchKernelGGL(heads_fwd_kernel<n>, grid, dim3(HD_THREADS), 0, st, a, logits_out, logp_out, entropy_out, v_out); break;
+    RAI_HD_F(2) RAI_HD_F(3) RAI_HD_F(4) RAI_HD_F(5) RAI_HD_F(6) RAI_HD_F(7) RAI_HD_F(8) RAI_HD_F(9) RAI_HD_F(10)
+    RAI_HD_F(12)
+#undef RAI_HD_F
+    default: return RAI_E_SHAPE;
+  }
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int64_t rai_categorical_critic_heads_workspace_bytes(int64_t B, int32_t A) {
+  return B < 0 || A < 1 ? 0 : B * (int64_t)(A + 1) * 4;
+}
+
+extern "C" int rai_categorical_critic_heads_bwd(const float* enc, const float* wpi, const float* bpi, const float* wv,
+                                                const float* bv, const int64_t* actions, const float* logits,
+                                                int64_t B, int32_t D, int32_t A, const float* d_logp,
+                                                const float* d_entropy, const float* d_v, float* d_enc,
+                                                float* g_wpi, float* g_bpi, float* g_wv, float* g_bv,
+                                                int32_t accumulate, void* workspace, int64_t workspace_bytes,
+                                                void* stream) {
+  if (B < 0 || D < 1 || !a_ok(A)) return RAI_E_SHAPE;
+  if (!enc || !wpi || !bpi || !wv || !bv || !actions || !logits || !d_logp || !d_entropy || !d_v || !d_enc ||
+      !g_wpi || !g_bpi || !g_wv || !g_bv || !workspace)
+    return RAI_E_NULLPTR;
+  if (workspace_bytes < rai_categorical_critic_heads_workspace_bytes(B, A)) return RAI_E_WORKSPACE;
+  if (B == 0) return RAI_OK;
+  const HeadsArgs a = make_args(enc, wpi, bpi, wv, bv, actions, B, D, A);
+  float* dlogits = static_cast<float*>(workspace);
+  float* dvv = dlogits + B * A;
+  hipStream_t st = rai_stream(stream);
+  const dim3 grid1((unsigned)((B + 3) / 4)), grid2((unsigned)((D + 15) / 16));
+  switch (A) {
+#define RAI_HD_B(n)                                                                                          \
+  case n:                                                                                                    \
+    hipLaunchKernelGGL(heads_bwd_rows_kernel<n>, grid1, dim3(HD_THREADS), 0, st, a, logits, d_logp, d_entropy, \
+                       d_v, dlogits, dvv, d_enc);                                                            \
+    hipLaunchKernelGGL(heads_bwd_weights_kernel<n>, grid2, dim3(HD_THREADS), 0, st, a, dlogits, dvv, g_wpi,   \
+                       g_bpi, g_wv, g_bv, accumulate);                                                       \
+    break;
+    RAI_HD_B(2) RAI_HD_B(3) RAI_HD_B(4) RAI_HD_B(5) RAI_HD_B(6) RAI_HD_B(7) RAI_HD_B(8) RAI_HD_B(9) RAI_HD_B(10)
+    RAI_HD_B(12)
+#undef RAI_HD_B
+    default: return RAI_E_SHAPE;
+  }
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

@@ -183,7 +183,7 @@ namespace {
 constexpr int BR_THREADS = 256;
 constexpr int BR_MAX_BLOCKS = 1024;
 constexpr int BR_UNROLL = 4;      // rows in flight per lane before the first use
-constexpr int BR_ROWS_PER_LANE = 8;
+constexpr int BR_ROWS_PER_LANE = 16;  // conv1 at C3: 200 workgroups of 512 rows
 
 __global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_kernel(const f4* __restrict__ x, const float* __restrict__ b,
                                                                   int C4, int64_t n4, f4* __restrict__ out) {
@@ -251,10 +251,17 @@ __global__ __launch_bounds__(BR_THREADS) void bias_grad_finalize_kernel(const fl
   const int tid = threadIdx.x;
   if (C <= BR_THREADS) {
     const int stripes = BR_THREADS / C, c = tid % C, s0 = tid / C;
-    float s = 0.f;
-    if (s0 < stripes)
-      for (int w = s0; w < nb; w += stripes) s += partial[(int64_t)w * C + c];
-    red[tid] = s;
+    // four independent partial sums per thread (loads in flight), combined in a fixed order
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (s0 < stripes) {
+      int w = s0;
+      for (; w + 3 * stripes < nb; w += 4 * stripes) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s[u] += partial[(int64_t)(w + u * stripes) * C + c];
+      }
+      for (int u = 0; w < nb; w += stripes, ++u) s[u] += partial[(int64_t)w * C + c];
+    }
+    red[tid] = (s[0] + s[1]) + (s[2] + s[3]);
     __syncthreads();
     if (tid < C) {
       float t = red[tid];

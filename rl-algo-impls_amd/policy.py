@@ -314,6 +314,11 @@ class ConnectedTrioNetwork(nn.Module):
 
     def forward(self, obs, action, action_masks=None, obs_prepared: bool = False):
         enc = self._feature_extractor(obs, obs_prepared)
+        if _FUSED_EPILOGUES and self._feature_extractor.kind == "cnn":
+            from .cnn_ops import categorical_critic_heads, heads_fusable
+
+            if heads_fusable(self, enc, action_masks):  # one launch forward, two backward (csrc/heads.hip)
+                return categorical_critic_heads(self, enc, action)
         logp, ent = self._pi.logp_entropy(self._pi.params(enc), action, action_masks)
         return logp, ent, self._v(enc)
 

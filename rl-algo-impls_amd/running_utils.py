@@ -10,9 +10,19 @@ On MI355X the switch reaches every kernel of the update:
     order, GAE is a serial chain per column);
   * PyTorch-ROCm ops (the NatureCNN / squeeze-U-Net convolutions on MIOpen, hipBLASLt GEMMs,
     index ops) follow torch.use_deterministic_algorithms, and torch.backends.cudnn.deterministic
-    restricts MIOpen to solvers whose reductions have a fixed order (the conv backward-weights
-    split-K solvers otherwise accumulate with atomics, which made two identical C3 updates differ in
-    the last bits, tests/test_gpu_pong.py).
+    restricts MIOpen to solvers whose reductions have a fixed order (the implicit-GEMM backward
+    solvers otherwise split K and accumulate with atomics into zero-filled outputs).
+
+Measured cost on MI355X (C3, Pong NatureCNN, B = 256 minibatch step, graph-replayed): 0.554 ms per
+step by default, 56.8 ms with the deterministic solvers (tools/replay_timing.py, profiles/
+r2h_replay_timing.txt) — two orders of magnitude, so bench.py runs with --deterministic 0 and says
+so in its JSON line; the reproducibility test pins the deterministic mode itself.
+
+MIOpen records its solver choices per problem in a user database (~/.config/miopen): a
+deterministic run would leave its slow solvers there for later default runs of the same shapes.
+Deterministic mode therefore points MIOPEN_USER_DB_PATH (when the caller has not set it) at a
+database of its own; like every MIOpen setting it only takes effect if it is set before the first
+convolution of the process.
 """
 from __future__ import annotations
 
@@ -30,6 +40,9 @@ def set_device_optimizations(device: torch.device, set_float32_matmul_precision:
     """running_utils.py:161-172."""
     torch.use_deterministic_algorithms(use_deterministic_algorithms)
     torch.backends.cudnn.deterministic = bool(use_deterministic_algorithms)
+    if use_deterministic_algorithms and "MIOPEN_USER_DB_PATH" not in os.environ:
+        os.environ["MIOPEN_USER_DB_PATH"] = os.path.join(os.path.expanduser("~"), ".cache", "rl_algo_impls_amd",
+                                                         "miopen-deterministic")
     if torch.device(device).type == "cuda" and set_float32_matmul_precision:
         logging.info(f"Setting torch.set_float32_matmul_precision to {set_float32_matmul_precision}")
         torch.set_float32_matmul_precision(set_float32_matmul_precision)

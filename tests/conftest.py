@@ -1,5 +1,7 @@
 import json
+import os
 import sys
+import tempfile
 from pathlib import Path
 
 import numpy as np
@@ -7,6 +9,10 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
+# MIOpen records its solver choices per problem in a user database that outlives the process; the
+# tests switch MIOpen to its deterministic solvers (~100x slower at the C3 shapes), so they keep a
+# database of their own instead of leaving those choices to later runs on the same machine
+os.environ.setdefault("MIOPEN_USER_DB_PATH", tempfile.mkdtemp(prefix="rai-miopen-tests-"))
 sys.path.insert(0, str(ROOT / "oracle"))
 
 import _pkgload  # noqa: E402

@@ -339,3 +339,39 @@ def cnn_dp_worker(rank, world, port, q, mode):
         import torch.distributed as dist
 
         dist.destroy_process_group()
+
+
+def c3_repro_worker(q, deterministic):
+    """The same C3-shaped update twice from the same weights, rollout and permutations, under
+    running_utils.set_device_optimizations(use_deterministic_algorithms=deterministic)."""
+    import torch
+
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator
+    from rl_algo_impls_amd.running_utils import set_device_optimizations
+
+    dev = torch.device("cuda", 0)
+    set_device_optimizations(dev, use_deterministic_algorithms=deterministic)
+    N, T = 64, 32
+    env = SyntheticVecEnv(N, "pong", seed=3)
+    torch.manual_seed(3)
+    pol = ActorCritic(env, activation_fn="relu").to(dev)
+    gen = SyncStepRolloutGenerator(pol, env, n_steps=T, seed=3)
+    r = gen.rollout(gamma=0.99, gae_lambda=0.95)
+    p0 = torch.nn.utils.parameters_to_vector(pol.parameters()).detach().clone()
+    out = []
+    for _ in range(2):
+        torch.nn.utils.vector_to_parameters(p0, pol.parameters())
+        algo = PPO(pol, dev, None, n_epochs=2, batch_size=256, learning_rate=2.5e-4, clip_range=0.1, vf_coef=0.5,
+                   ent_coef=0.01)
+        g = torch.Generator(device="cpu").manual_seed(11)
+        r._perm_source = lambda n: torch.randperm(n, generator=g)
+        stats, norms, _ = algo.update(r)
+        torch.cuda.synchronize()
+        out.append((algo.flat.flat.detach().cpu().numpy().copy(), norms.copy()))
+    q.put(out)

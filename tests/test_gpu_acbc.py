@@ -75,7 +75,8 @@ def test_acbc_steps_match_reference(case):
     norms = algo.blocks.norms[:n_opt].cpu().numpy()
     np.testing.assert_allclose(norms, z[p + "norms"], rtol=2e-5)
     np.testing.assert_allclose(algo.flat.flat.cpu().numpy(), z[p + "params"][-1], rtol=1e-4, atol=2e-6)
-    np.testing.assert_allclose(algo.optimizer.state1.cpu().numpy(), z[p + "opt_state1"], rtol=1e-3, atol=1e-10)
+    m_ref = z[p + "opt_state1"]  # near-zero first moments differ by fp32 summation order: absolute floor
+    np.testing.assert_allclose(algo.optimizer.state1.cpu().numpy(), m_ref, rtol=1e-3, atol=1e-6 * np.abs(m_ref).max())
     ref = dict(meta["scalars"])
     for tag in ("losses/loss", "losses/pi_loss", "losses/v_loss", "losses/explained_var"):
         assert tag in rec.scalars, tag

@@ -168,43 +168,38 @@ def test_pong_full_shape_update():
 
 
 @pytest.mark.parametrize("deterministic", [True, False], ids=["deterministic", "default"])
-def test_c3_update_reproducibility(deterministic):
+def test_c3_update_reproducibility(deterministic, tmp_path, monkeypatch):
     """The reference runs with torch.use_deterministic_algorithms(True) by default
     (rl_algo_impls/runner/running_utils.py:161-166).  Under running_utils.set_device_optimizations
     the same C3 update from the same weights, rollout and permutations is bitwise reproducible
     (HIP kernels: fixed reduction orders; MIOpen / hipBLASLt: deterministic solvers).  Without it
-    the two runs agree within fp32 summation tolerance (MIOpen may pick split-K atomics)."""
-    from rl_algo_impls_amd.envs import SyntheticVecEnv
-    from rl_algo_impls_amd.policy import ActorCritic
-    from rl_algo_impls_amd.running_utils import set_device_optimizations
+    the two runs agree within fp32 summation tolerance (MIOpen may pick split-K atomics).
+    Each mode runs in a process of its own with its own MIOpen user database: MIOpen's recorded
+    solver choices outlive a process, and the deterministic ones are ~100x slower at these shapes."""
+    import multiprocessing as mp
+    import queue
+    import time
 
-    prev = (torch.are_deterministic_algorithms_enabled(), torch.backends.cudnn.deterministic)
-    set_device_optimizations(DEV, use_deterministic_algorithms=deterministic)
-    try:
-        N, T = 64, 32
-        env = SyntheticVecEnv(N, "pong", seed=3)
-        torch.manual_seed(3)
-        pol = ActorCritic(env, activation_fn="relu").to(DEV)
-        gen = SyncStepRolloutGenerator(pol, env, n_steps=T, seed=3)
-        r = gen.rollout(gamma=0.99, gae_lambda=0.95)
-        p0 = torch.nn.utils.parameters_to_vector(pol.parameters()).detach().clone()
-        out = []
-        for _ in range(2):
-            torch.nn.utils.vector_to_parameters(p0, pol.parameters())
-            algo = PPO(pol, DEV, None, n_epochs=2, batch_size=256, learning_rate=2.5e-4, clip_range=0.1,
-                       vf_coef=0.5, ent_coef=0.01)
-            g = torch.Generator(device="cpu").manual_seed(11)
-            r._perm_source = lambda n: torch.randperm(n, generator=g)
-            stats, norms, _ = algo.update(r)
-            torch.cuda.synchronize()
-            out.append((algo.flat.flat.detach().cpu().numpy().copy(), norms.copy()))
-        (pa, na), (pb, nb) = out
-        if deterministic:
-            np.testing.assert_array_equal(pa, pb)
-            np.testing.assert_array_equal(na, nb)
-        else:
-            np.testing.assert_allclose(pa, pb, rtol=1e-4, atol=1e-6)
-            np.testing.assert_allclose(na, nb, rtol=1e-4)
-    finally:
-        torch.use_deterministic_algorithms(prev[0])
-        torch.backends.cudnn.deterministic = prev[1]
+    import dp_worker
+
+    monkeypatch.setenv("MIOPEN_USER_DB_PATH", str(tmp_path))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=dp_worker.c3_repro_worker, args=(q, deterministic))
+    p.start()
+    deadline = time.time() + 240
+    while True:
+        try:
+            (pa, na), (pb, nb) = q.get(timeout=2)
+            break
+        except queue.Empty:
+            assert p.exitcode in (None, 0), f"worker exited with {p.exitcode}"
+            assert time.time() < deadline, "worker did not report in time"
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    if deterministic:
+        np.testing.assert_array_equal(pa, pb)
+        np.testing.assert_array_equal(na, nb)
+    else:
+        np.testing.assert_allclose(pa, pb, rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(na, nb, rtol=1e-4)
