@@ -60,6 +60,10 @@ CONFIGS = {
 }
 
 
+# algorithmic FLOPs per env step = rollout forward + n_epochs x (forward + backward)
+UPDATE_FLOPS = {"pong": 18.69e6 + 4 * 49.53e6, "halfcheetah": 0.283e6 + 20 * 0.832e6, "microrts": 954e6 + 2 * 2818e6}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -339,6 +343,17 @@ def main():
                     "traffic": traffic(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
         roof_lat = latency_roofline(G, ms, (T * N + algo.batch_size - 1) // algo.batch_size, kname)
+    elif args.config in UPDATE_FLOPS:
+        # no fused epoch kernel: the update's convolutions / GEMMs on MFMA (MIOpen, hipBLASLt) against
+        # the f32 MFMA peak, from SURVEY.md 8(d)'s algorithmic FLOPs per env step (rollout forward +
+        # n_epochs x forward/backward, torch.utils.flop_counter) and the measured update time;
+        # per-kernel MFMA-busy PMC in profiles/r2k_pong_mfma_pmc_kernels.json (C3)
+        fl = UPDATE_FLOPS[args.config] * T * N
+        tf = fl / (elapsed / args.steps) / 1e12
+        roofline = {"kernel": "whole update (MIOpen / hipBLASLt contractions + HIP epilogues)", "bound": "mfma",
+                    "achieved": round(tf, 3), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 4),
+                    "traffic": None, "flops_per_update": fl}
+        roof_lat = None
     else:
         roofline = roof_gae
         roof_lat = None
