@@ -46,7 +46,8 @@ class A2C:
         self.device = torch.device(device)
         self.tb_writer = tb_writer
         self.learning_rate = learning_rate
-        self.flat = FlatParams(policy, self.device)
+        cl = policy.channels_last_params() if self.device.type == "cuda" and hasattr(policy, "channels_last_params") else ()
+        self.flat = FlatParams(policy, self.device, channels_last=cl)
         if use_rms_prop:
             self.optimizer = FlatOptimizer(self.flat, FlatOptimizer.RMSPROP, lr=learning_rate, eps=rms_prop_eps,
                                            max_grad_norm=max_grad_norm)

@@ -55,7 +55,8 @@ class ACBC:
         self.device = torch.device(device)
         self.tb_writer = tb_writer
         self.learning_rate = learning_rate
-        self.flat = FlatParams(policy, self.device)
+        cl = policy.channels_last_params() if self.device.type == "cuda" and hasattr(policy, "channels_last_params") else ()
+        self.flat = FlatParams(policy, self.device, channels_last=cl)
         self.optimizer = FlatOptimizer(self.flat, FlatOptimizer.ADAM, lr=learning_rate, eps=1e-8,
                                        max_grad_norm=max_grad_norm)
         self.batch_size = batch_size

@@ -45,8 +45,13 @@ def direct_grads(enabled: bool = True):
         _state.direct = prev
 
 
-def _direct(p: torch.Tensor) -> bool:
-    return getattr(_state, "direct", False) and p.grad is not None and p.grad.is_contiguous()
+def _direct(p: torch.Tensor, raw: bool = False) -> bool:
+    """In-place accumulation applies: inside direct_grads() with a dense .grad (raw: a kernel writes
+    it through its data pointer, so it must also be contiguous; conv weights stored channels_last
+    are accumulated with Tensor.add_ instead)."""
+    g = p.grad
+    return getattr(_state, "direct", False) and g is not None and g.layout == torch.strided and (
+        not raw or g.is_contiguous())
 
 
 class _Workspaces:
@@ -105,7 +110,7 @@ class ConvBiasReLU(torch.autograd.Function):
         z = z.contiguous(memory_format=torch.channels_last)
         y = _bias_relu_fwd(z, b)
         ctx.save_for_backward(x, w, b, y)
-        ctx.conf = (stride, padding, key, _direct(b), _direct(w))
+        ctx.conf = (stride, padding, key, _direct(b, raw=True), _direct(w))
         return y
 
     @staticmethod
@@ -132,7 +137,7 @@ class LinearBiasReLU(torch.autograd.Function):
         z = torch.mm(x, w.t())
         y = _bias_relu_fwd(z, b)
         ctx.save_for_backward(x, w, b, y)
-        ctx.conf = (key, _direct(b), _direct(w))
+        ctx.conf = (key, _direct(b, raw=True), _direct(w))
         return y
 
     @staticmethod
@@ -191,7 +196,7 @@ class CategoricalCriticHeads(torch.autograd.Function):
             logits.data_ptr(), logp.data_ptr(), ent.data_ptr(), v.data_ptr(), _lib.stream_handle(enc.device)),
             "rai_categorical_critic_heads_fwd")
         ctx.save_for_backward(enc, wpi, bpi, wv, bv, actions, logits)
-        ctx.direct = all(_direct(p) for p in (wpi, bpi, wv, bv))
+        ctx.direct = all(_direct(p, raw=True) for p in (wpi, bpi, wv, bv))
         ctx.mark_non_differentiable(logits)
         return logp, ent, v
 

@@ -42,10 +42,11 @@ class MinibatchStepGraph:
     WARMUP = 2
 
     def __init__(self, device: torch.device, fields: List[torch.Tensor], batch_size: int,
-                 step: Callable[[List[torch.Tensor]], None], xforms: Optional[list] = None):
+                 xforms: Optional[list] = None):
+        # no reference to the step function (it closes over the trainer): the trainer owns the
+        # graphs, so dropping the trainer frees them at once instead of in a later cyclic GC pass
         self.device = device
         self.B = int(batch_size)
-        self.step = step
         self.row_bytes = [int(f[0].numel() * f.element_size()) for f in fields]
         self.xforms = xforms
         self.static = static_buffers(fields, self.B, device, xforms)
@@ -55,22 +56,23 @@ class MinibatchStepGraph:
     def gather(self, desc: torch.Tensor, bufs: List[torch.Tensor]) -> None:
         gather_next(self.device, desc, bufs, self.row_bytes, self.xforms)
 
-    def _body(self, desc: torch.Tensor) -> None:
+    def _body(self, desc: torch.Tensor, step: Callable[[List[torch.Tensor]], None]) -> None:
         self.gather(desc, self.static)
-        self.step(self.static)
+        step(self.static)
 
-    def run(self, desc: torch.Tensor, stream: torch.cuda.Stream) -> None:
-        """One minibatch on `stream` (the caller has made it current)."""
+    def run(self, desc: torch.Tensor, stream: torch.cuda.Stream, step: Callable[[List[torch.Tensor]], None]) -> None:
+        """One minibatch on `stream` (the caller has made it current); `step` runs the minibatch's
+        forward / loss / backward / optimizer on the static buffers (eager warm-up and capture)."""
         if self.graph is not None:
             self.graph.replay()
             return
         if self.eager_runs < self.WARMUP:
-            self._body(desc)
+            self._body(desc, step)
             self.eager_runs += 1
             return
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=stream):
-            self._body(desc)
+            self._body(desc, step)
         self.graph = g
         g.replay()  # the capture executed nothing: this replay is the minibatch
 
@@ -140,13 +142,12 @@ class GraphedUpdate:
             self.perm.copy_(perm, non_blocking=True)
         self.desc[_DESC_MB_OFFSET:_DESC_MB_OFFSET + 8].view(torch.int64).zero_()
 
-    def graph_for(self, fields: List[torch.Tensor], B: int, tag, step, xforms=None) -> MinibatchStepGraph:
+    def graph_for(self, fields: List[torch.Tensor], B: int, tag, xforms=None) -> MinibatchStepGraph:
         k = self.key(fields, B, tag, xforms)
         g = self.graphs.get(k)
         if g is None:
-            g = MinibatchStepGraph(self.device, fields, B, step, xforms)
+            g = MinibatchStepGraph(self.device, fields, B, xforms)
             self.graphs[k] = g
-        g.step = step
         return g
 
     def tail(self, fields: List[torch.Tensor], rows: int, step, xforms=None) -> None:

@@ -30,32 +30,61 @@ def struct_to_device(struct, device, out: Optional[torch.Tensor] = None) -> torc
 
 
 class FlatParams:
-    """Views every parameter of `module` into one flat fp32 buffer (+ flat grads)."""
+    """Views every parameter of `module` into one flat fp32 buffer (+ flat grads).
 
-    def __init__(self, module: torch.nn.Module, device: torch.device):
+    channels_last: parameters (4-D convolution weights) whose segment is laid out (K, kh, kw, C),
+    the parameter being a channels_last-strided view of it.  The NHWC MIOpen convolutions then take
+    the weight as stored (no per-call NCHW -> NHWC copy of the weight, forward and backward) and
+    the weight gradient they return accumulates with matching strides.  The logical tensors (and so
+    state_dict(), model.pth and optimizer.pt) are unchanged; vector() gives parameters() order."""
+
+    def __init__(self, module: torch.nn.Module, device: torch.device, channels_last=()):
         self.params: List[torch.nn.Parameter] = list(module.parameters())
         for p in self.params:
             if p.dtype != torch.float32:
                 raise TypeError("flat optimizer expects fp32 parameters")
+        cl = {id(p) for p in channels_last}
+        self.cl = [id(p) in cl and p.dim() == 4 for p in self.params]
+        self.shapes = [tuple(p.shape) for p in self.params]
         sizes = [p.numel() for p in self.params]
         self.P = int(sum(sizes))
         self.flat = torch.empty(self.P, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.P, dtype=torch.float32, device=device)
         off = 0
         self.offsets = []
+        for p, n in zip(self.params, sizes):
+            self.offsets.append(off)
+            off += n
         with torch.no_grad():
-            for p, n in zip(self.params, sizes):
-                self.flat[off:off + n].copy_(p.detach().reshape(-1))
-                p.data = self.flat[off:off + n].view_as(p)
-                p.grad = self.grad[off:off + n].view_as(p)
-                self.offsets.append(off)
-                off += n
+            for i, p in enumerate(self.params):
+                self.as_param(self.flat, i).copy_(p.detach())
+                p.data = self.as_param(self.flat, i)
+                p.grad = self.as_param(self.grad, i)
+
+    def as_param(self, buf: torch.Tensor, i: int) -> torch.Tensor:
+        """Parameter i's segment of a flat buffer (params, grads, optimizer moments) as a tensor of
+        the parameter's shape and layout."""
+        off, shp = self.offsets[i], self.shapes[i]
+        seg = buf[off:off + int(np.prod(shp))]
+        if self.cl[i]:
+            K, C, kh, kw = shp
+            return seg.view(K, kh, kw, C).permute(0, 3, 1, 2)
+        return seg.view(shp)
+
+    def vector(self, buf: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """A flat buffer in parameters() order with each parameter flattened row-major (what
+        torch.nn.utils.parameters_to_vector gives), whatever the segments' layout."""
+        buf = self.flat if buf is None else buf
+        if not any(self.cl):
+            return buf
+        return torch.cat([self.as_param(buf, i).reshape(-1) for i in range(len(self.params))])
 
     def check_views(self) -> None:
         for p, off in zip(self.params, self.offsets):
             assert p.data.data_ptr() == self.flat.data_ptr() + 4 * off, "parameter storage was replaced"
             assert p.grad is not None and p.grad.data_ptr() == self.grad.data_ptr() + 4 * off, (
                 "gradient storage was replaced (zero_grad(set_to_none=True)?)")
+            assert p.data.stride() == p.grad.stride(), "parameter / gradient layouts differ"
 
 
 class FlatOptimizer:
@@ -115,11 +144,12 @@ class FlatOptimizer:
             if self.step_count == 0:
                 continue
             s = {"step": torch.tensor(float(self.step_count))}
+            as_p = lambda buf: self.flat.as_param(buf, i).contiguous().clone()  # torch's layout
             if self.kind == self.ADAM:
-                s["exp_avg"] = self.state1[off:off + n].view_as(p).clone()
-                s["exp_avg_sq"] = self.state2[off:off + n].view_as(p).clone()
+                s["exp_avg"] = as_p(self.state1)
+                s["exp_avg_sq"] = as_p(self.state2)
             else:
-                s["square_avg"] = self.state1[off:off + n].view_as(p).clone()
+                s["square_avg"] = as_p(self.state1)
             state[i] = s
         if self.kind == self.ADAM:
             group = dict(lr=self.lr, betas=self.betas, eps=self.eps, weight_decay=0, amsgrad=False,
@@ -134,13 +164,13 @@ class FlatOptimizer:
         steps = set()
         for i, s in sd["state"].items():
             i = int(i)
-            off, p = self.flat.offsets[i], self.flat.params[i]
-            n = p.numel()
+            p = self.flat.params[i]
+            as_p = lambda buf: self.flat.as_param(buf, i)
             if self.kind == self.ADAM:
-                self.state1[off:off + n].copy_(s["exp_avg"].reshape(-1))
-                self.state2[off:off + n].copy_(s["exp_avg_sq"].reshape(-1))
+                as_p(self.state1).copy_(s["exp_avg"].reshape(p.shape))
+                as_p(self.state2).copy_(s["exp_avg_sq"].reshape(p.shape))
             else:
-                self.state1[off:off + n].copy_(s["square_avg"].reshape(-1))
+                as_p(self.state1).copy_(s["square_avg"].reshape(p.shape))
             steps.add(int(float(s["step"])))
         if len(steps) > 1:
             raise NotImplementedError("per-parameter step counts differ; flat optimizer needs one")

@@ -420,6 +420,14 @@ class ActorCritic(nn.Module):
             return ACForward(*self.network(obs, action, action_masks, obs_prepared=True))
         return ACForward(*self.network(obs, action, action_masks))
 
+    def channels_last_params(self) -> list:
+        """Parameters the flat buffer should store channels_last (optim.FlatParams): the NatureCNN
+        convolution weights when the activations are NHWC on the GPU."""
+        if self.gridnet or self.network._feature_extractor.kind != "cnn" or not _CHANNELS_LAST:
+            return []
+        cnn = self.network._feature_extractor.feature_extractor.cnn
+        return [cnn[i].weight for i in (0, 2, 4)]
+
     def obs_transform(self, obs: torch.Tensor):
         """The gather transform (rai_gather_xform) that prepares rollout obs rows for forward(...,
         obs_prepared=True), or None (NatureCNN on uint8 frames only)."""

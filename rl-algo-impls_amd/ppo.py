@@ -51,7 +51,8 @@ class PPO:
         self.device = torch.device(device)
         self.tb_writer = tb_writer
         self.learning_rate = learning_rate
-        self.flat = FlatParams(policy, self.device)
+        cl = policy.channels_last_params() if self.device.type == "cuda" and hasattr(policy, "channels_last_params") else ()
+        self.flat = FlatParams(policy, self.device, channels_last=cl)
         self.optimizer = FlatOptimizer(self.flat, FlatOptimizer.ADAM, lr=learning_rate, eps=1e-7,
                                        max_grad_norm=max_grad_norm)
         self.gamma = num_or_array(gamma)
@@ -695,7 +696,7 @@ class PPO:
         tag = (optim_in_step, wide is not None, buckets is not None, blocks.stats.data_ptr(), blocks.norms.data_ptr(), blocks.hp.data_ptr(),
                blocks.state.data_ptr(), self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
                self.optimizer.hp_dev.data_ptr())
-        g = gu.graph_for(fields, B, tag, step, xforms)
+        g = gu.graph_for(fields, B, tag, xforms)
         cur = torch.cuda.current_stream(self.device)
         gu.stream.wait_stream(cur)
         with torch.cuda.stream(gu.stream):
@@ -706,7 +707,7 @@ class PPO:
                     self._fill_epoch_moments(ext, e, fields[3][perm] if perm is not None else fields[3], nmb)
                 gu.start_epoch(perm)
                 for _ in range(n_full):
-                    g.run(gu.desc, gu.stream)
+                    g.run(gu.desc, gu.stream, step)
                     if not optim_in_step and not self.gradient_accumulation:
                         self._all_reduce(self.flat.grad, average=True)
                         self.optimizer.step(blocks.state, blocks.norms)

@@ -45,11 +45,11 @@ events = []
 orig_run = graphs.MinibatchStepGraph.run
 
 
-def timed_run(self, desc, stream):
+def timed_run(self, desc, stream, step):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     t0 = time.perf_counter()
-    orig_run(self, desc, stream)
+    orig_run(self, desc, stream, step)
     t1 = time.perf_counter()
     e1.record(stream)
     events.append((e0, e1, t1 - t0, self.graph is not None))
