@@ -148,11 +148,12 @@ int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b, int64_t r
 /* Conv / Linear bias + ReLU of the NatureCNN encoder (rl_algo_impls/shared/encoder/nature_cnn.py:10-53:
  * Conv2d -> ReLU x3, then Linear -> ReLU) over NHWC (or (B, C) row-major) rows, C % 4 == 0, C / 4
  * dividing 256.  Forward: out = relu(x + b[c]) (x = the bias-free conv / GEMM output).  Backward, one
- * launch pair: dx = dy * (out > 0) (torch threshold_backward on the saved output) and the bias gradient
+ * launch: dx = dy * (out > 0) (torch threshold_backward on the saved output) and the bias gradient
  * db[c] = sum_rows dx[row, c], written (accumulate == 0) or added to db (accumulate != 0, e.g. straight
- * into the flat .grad buffer).  The reduction order is fixed (deterministic).  workspace: at least
- * rai_bias_relu_workspace_bytes(C) bytes, 16-B aligned (per-workgroup partial sums; no initial
- * contents required); one workspace per concurrently running launch. */
+ * into the flat .grad buffer), in one launch (the last workgroup to arrive sums the per-workgroup
+ * partials).  The reduction order is fixed (deterministic).  workspace: at least
+ * rai_bias_relu_workspace_bytes(C) bytes, 16-B aligned, ZEROED before its first use (its arrival
+ * counter is re-armed by every launch); one workspace per concurrently running launch. */
 int64_t rai_bias_relu_workspace_bytes(int32_t C);
 int rai_bias_relu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream);
 int rai_bias_relu_bwd(const float* dy, const float* y, int64_t rows, int32_t C, float* dx, float* db,

@@ -8,7 +8,7 @@ MIOpen / hipBLASLt (MFMA), bias-free, and the epilogue is one HIP pass each way
 (rai_bias_relu_fwd / rai_bias_relu_bwd, csrc/se_block.hip):
 
     forward    y = relu(conv(x, W) + b)             conv bias-free, then one pass
-    backward   dz = dy * (y > 0), db (+)= sum dz     one pass + a finalize, deterministic order
+    backward   dz = dy * (y > 0), db (+)= sum dz     one launch, deterministic order
 
 Direct gradient accumulation.  Inside the trainer's update (`direct_grads(module)`), every
 parameter's .grad is a view into the flat gradient buffer (optim.FlatParams), zeroed by the
@@ -55,8 +55,9 @@ def _direct(p: torch.Tensor, raw: bool = False) -> bool:
 
 
 class _Workspaces:
-    """Per-(layer, device) workspaces of rai_bias_relu_bwd (per-workgroup partial sums): one
-    allocation serves every eager call and graph replay of that layer."""
+    """Zeroed per-(layer, device) workspaces of rai_bias_relu_bwd (per-workgroup partial sums and
+    an arrival counter the kernel re-arms): one allocation serves every eager call and graph replay
+    of that layer."""
 
     def __init__(self):
         self._ws: Dict[tuple, torch.Tensor] = {}
@@ -65,12 +66,12 @@ class _Workspaces:
         k = (key, C, str(device))
         ws = self._ws.get(k)
         if ws is None:
-            # allocated outside any graph capture (a capture-time allocation would come from, and
-            # stay tied to, that graph's private pool); every graphed step has eager warm-up runs
+            # zeroed by an eager memset: one recorded into a graph capture would not run before the
+            # first replay; every graphed step has eager warm-up runs that allocate it first
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("cnn_ops: bias + ReLU workspace first requested inside a graph capture")
             n = int(_lib.lib().rai_bias_relu_workspace_bytes(C))
-            ws = torch.empty(n, dtype=torch.uint8, device=device)
+            ws = torch.zeros(n, dtype=torch.uint8, device=device)
             self._ws[k] = ws
         return ws
 

@@ -20,6 +20,7 @@ namespace {
 
 constexpr int SE_THREADS = 256;
 using f4 = float __attribute__((ext_vector_type(4)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float gelu_f(float t) { return 0.5f * t * (1.f + erff(t * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_grad(float t) {
@@ -175,13 +176,13 @@ extern "C" int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b
 // accumulate of that gradient into .grad: five launches per layer around the MIOpen / hipBLASLt
 // contraction.  Here, per layer:
 //   forward   one pass:  out = relu(x + b[c])                       (x: bias-free conv / GEMM output)
-//   backward  dx = dy * (out > 0) and db[c] (+)= sum_rows dx[row, c]: one pass over the rows plus a
-//             one-workgroup finalize of the per-workgroup column sums
+//   backward  dx = dy * (out > 0) and db[c] (+)= sum_rows dx[row, c]: one pass over the rows whose
+//             last-arriving workgroup sums the per-workgroup column sums
 // The bias-gradient reduction is deterministic (fixed row runs per workgroup, fixed summation
 // orders).  relu(NaN) = NaN and dx = 0 where out <= 0, as torch's clamp_min / threshold_backward.
 namespace {
 constexpr int BR_THREADS = 256;
-constexpr int BR_MAX_BLOCKS = 1024;
+constexpr int BR_MAX_BLOCKS = 256;  // about one workgroup per CU (the hand-off's measured form)
 constexpr int BR_UNROLL = 4;      // rows in flight per lane before the first use
 constexpr int BR_ROWS_PER_LANE = 16;  // conv1 at C3: 200 workgroups of 512 rows
 
@@ -199,19 +200,35 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_kernel(const f4* __r
   }
 }
 
-// Pass 1: workgroup w owns rows [w * rpb, (w + 1) * rpb); its threads are (row lane, float4 channel
-// group) pairs, each lane keeping BR_UNROLL rows' loads in flight; dx is stored and the workgroup's
-// column sums go to partial[w] (row lanes added in lane order).  Pass 2 (one workgroup): thread t
-// adds partials s, s + stripes, ... (s = t / C, fixed order) of channel t % C, then the stripes are
-// added in order through LDS -> db.  The kernel boundary orders the passes: no device-scope fences
-// or arrival counters (a last-workgroup-arrives variant paid an L2 writeback per workgroup).
+// Workgroup w owns rows [w * rpb, (w + 1) * rpb); its threads are (row lane, float4 channel group)
+// pairs, each lane keeping BR_UNROLL rows' loads in flight; dx is stored and the workgroup's column
+// sums (row lanes added in lane order) go to partial[w].  The workgroup whose arrival comes last then
+// sums the partials: thread t adds partials s, s + stripes, ... (s = t / C, fixed order) of channel
+// t % C, then the stripes are added in order through LDS -> db.
+// Hand-off without fences (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms): the partials
+// are 16-B write-through (sc1) buffer stores drained by every storing wave (vmcnt(0)) before the
+// workgroup barrier and one agent-scope atomic add; the last arriver's waves read them with sc1 buffer
+// loads after a barrier.  (Two launches, the row pass then a one-workgroup finalize, cost a second
+// ~4.8 us launch per layer; a last-arriver variant with __threadfence() in every thread ~30 us.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t br_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+constexpr int BR_SC1 = 16;  // cache-policy operand: sc1 (write-through stores, L1-bypassing loads)
+
 __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __restrict__ dy, const f4* __restrict__ y,
                                                                   int C4, int64_t rows, int64_t rows_per_block,
-                                                                  f4* __restrict__ dx, float* __restrict__ partial) {
+                                                                  f4* __restrict__ dx, float* partial,
+                                                                  int* counter, float* __restrict__ db,
+                                                                  int accumulate) {
   __shared__ f4 part[BR_THREADS];
+  __shared__ float red[BR_THREADS];
+  __shared__ int last;
   const int tid = threadIdx.x;
   const int lanes = BR_THREADS / C4;  // row lanes; C4 divides 256
   const int c4 = tid % C4, lane = tid / C4;
+  const int C = 4 * C4;
+  const int nb = (int)gridDim.x;
+  const __amdgpu_buffer_rsrc_t prs = br_rsrc(partial, nb * C * 4);
   const int64_t r0 = blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
   f4 acc = f4{0.f, 0.f, 0.f, 0.f};
@@ -241,25 +258,26 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __r
   if (tid < C4) {
     f4 t = part[tid];
     for (int k = 1; k < lanes; ++k) t += part[tid + k * C4];
-    reinterpret_cast<f4*>(partial + (int64_t)blockIdx.x * 4 * C4)[tid] = t;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, t), prs, (blockIdx.x * C + 4 * tid) * 4, 0, BR_SC1);
   }
-}
-
-__global__ __launch_bounds__(BR_THREADS) void bias_grad_finalize_kernel(const float* __restrict__ partial, int nb, int C,
-                                                                       float* __restrict__ db, int accumulate) {
-  __shared__ float red[BR_THREADS];
-  const int tid = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  if (tid == 0) last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+  __syncthreads();
+  if (!last) return;
+  auto ld = [&](int w, int c) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prs, (w * C + c) * 4, 0, BR_SC1));
+  };
   if (C <= BR_THREADS) {
     const int stripes = BR_THREADS / C, c = tid % C, s0 = tid / C;
-    // four independent partial sums per thread (loads in flight), combined in a fixed order
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     if (s0 < stripes) {
       int w = s0;
       for (; w + 3 * stripes < nb; w += 4 * stripes) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) s[u] += partial[(int64_t)(w + u * stripes) * C + c];
+        for (int u = 0; u < 4; ++u) s[u] += ld(w + u * stripes, c);
       }
-      for (int u = 0; w < nb; w += stripes, ++u) s[u] += partial[(int64_t)w * C + c];
+      for (int u = 0; w < nb; w += stripes, ++u) s[u] += ld(w, c);
     }
     red[tid] = (s[0] + s[1]) + (s[2] + s[3]);
     __syncthreads();
@@ -271,10 +289,11 @@ __global__ __launch_bounds__(BR_THREADS) void bias_grad_finalize_kernel(const fl
   } else {
     for (int c = tid; c < C; c += BR_THREADS) {
       float t = 0.f;
-      for (int w = 0; w < nb; ++w) t += partial[(int64_t)w * C + c];
+      for (int w = 0; w < nb; ++w) t += ld(w, c);
       db[c] = accumulate ? db[c] + t : t;
     }
   }
+  if (tid == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
 }
 
 bool br_shape_ok(int64_t rows, int32_t C) {
@@ -285,7 +304,7 @@ bool br_shape_ok(int64_t rows, int32_t C) {
 }  // namespace
 
 extern "C" int64_t rai_bias_relu_workspace_bytes(int32_t C) {
-  return (int64_t)BR_MAX_BLOCKS * (C > 0 ? C : 0) * 4;
+  return (int64_t)BR_MAX_BLOCKS * (C > 0 ? C : 0) * 4 + 16;  // partials, then the arrival counter
 }
 
 extern "C" int rai_bias_relu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream) {
@@ -320,12 +339,10 @@ extern "C" int rai_bias_relu_bwd(const float* dy, const float* y, int64_t rows, 
   const int64_t rpb = (rows + blocks - 1) / blocks;
   blocks = (rows + rpb - 1) / rpb;
   float* partial = static_cast<float*>(workspace);
+  int* counter = reinterpret_cast<int*>(static_cast<uint8_t*>(workspace) + (int64_t)BR_MAX_BLOCKS * C * 4);
   hipLaunchKernelGGL(bias_relu_bwd_kernel, dim3((unsigned)blocks), dim3(BR_THREADS), 0, st,
                      reinterpret_cast<const f4*>(dy), reinterpret_cast<const f4*>(y), C4, rows, rpb,
-                     reinterpret_cast<f4*>(dx), partial);
-  RAI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bias_grad_finalize_kernel, dim3(1), dim3(BR_THREADS), 0, st, partial, (int)blocks, C, db,
-                     accumulate);
+                     reinterpret_cast<f4*>(dx), partial, counter, db, accumulate);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

@@ -497,7 +497,7 @@ def test_bias_relu_fwd_bwd_match_torch(rows, C):
     assert torch.equal(y.isnan(), ref.isnan())
     assert torch.equal(torch.nan_to_num(y), torch.nan_to_num(ref))
     y = torch.nan_to_num(y)
-    ws = torch.full((int(L.rai_bias_relu_workspace_bytes(C)),), 0x7f, dtype=torch.uint8, device=DEV)  # any contents
+    ws = torch.zeros(int(L.rai_bias_relu_workspace_bytes(C)), dtype=torch.uint8, device=DEV)
     dbs = []
     for acc in (0, 1, 0):
         dx = torch.empty_like(x)
@@ -511,3 +511,4 @@ def test_bias_relu_fwd_bwd_match_torch(rows, C):
                                    rtol=1e-5, atol=2e-6 * rows ** 0.5)
         dbs.append(db - (0.5 if acc else 0.0))
     assert torch.equal(dbs[0], dbs[2])  # deterministic
+    assert int(ws.view(torch.int32)[(ws.numel() - 16) // 4]) == 0  # the arrival counter, re-armed
