@@ -318,6 +318,31 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     gae_us = e0.elapsed_time(e1) * 1e3 / args.roofline_reps
+    # the same kernel in its bandwidth regime (SURVEY.md 8(d)'s (128, 2^20) microbench shape): the
+    # workload shape above is bound by the serial fp64 chain and launch latency, not by HBM
+    Tl, Nl = 128, 1 << 20
+    gl_ = torch.Generator(device=dev).manual_seed(3)
+    rl_, vl_ = (torch.randn((Tl, Nl), device=dev, generator=gl_) for _ in range(2))
+    esl = (torch.rand((Tl, Nl), device=dev, generator=gl_) < 0.01).to(torch.uint8)
+    nesl = torch.zeros(Nl, dtype=torch.uint8, device=dev)
+    nvl, advl, retl = torch.randn(Nl, device=dev, generator=gl_), torch.empty_like(rl_), torch.empty_like(rl_)
+    large = lambda: compute_advantages_device(rl_, vl_, esl, nesl, nvl, 0.99, 0.95, advantages_out=advl,
+                                              returns_out=retl)
+    for _ in range(3):
+        large()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(20):
+        large()
+    e1.record()
+    torch.cuda.synchronize()
+    large_us = e0.elapsed_time(e1) * 1e3 / 20
+    large_bytes = 16 * Tl * Nl + Tl * Nl + 5 * Nl
+    roof_gae_large = {"kernel": "gae_kernel<double, 64>", "shape": [Tl, Nl, 1], "bound": "hbm",
+                      "achieved": round(large_bytes / (large_us * 1e-6) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                      "frac": round(large_bytes / (large_us * 1e-6) / 1e9 / 8000.0, 4), "avg_us": round(large_us, 2),
+                      "bytes_per_launch": large_bytes}
+    del rl_, vl_, esl, advl, retl
     workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
     pmc = {}
     # the newest PMC summary (profiles/r<round><letter>_pmc.json, tools/pmc_summary.py) holding this workload
@@ -395,6 +420,7 @@ def main():
             "roofline": roofline,
             "roofline_latency": roof_lat,
             "roofline_gae": roof_gae,
+            "roofline_gae_bandwidth_regime": roof_gae_large,
             "cpu_baseline": cpu,
         }
         if args.dp_rehearsal or world > 1:

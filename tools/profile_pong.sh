@@ -1,11 +1,13 @@
 #!/bin/bash
 # C3 (Pong NatureCNN, 1024 envs x 128 steps) profile on the GPU box:
 #   1. kernel-trace stats of the bench run as shipped (graph-replayed update and rollout);
-#   2. PMC passes (FETCH_SIZE, WRITE_SIZE, MFMA busy) of ONE update at the same shape, with the update
-#      and rollout forwards run eagerly (RAI_GRAPHS=0 RAI_ROLLOUT_GRAPH=0): the same kernels, launched
-#      one by one.  rocprofv3's counter-collection callback crashed (SIGSEGV inside
-#      librocprofiler-sdk.so, on an HSA runtime thread) while the update's hipGraph was being replayed
-#      (r2b: gpurun_out/r2b/fetch_pong.log + diag/ maps), so counters are collected off-graph.
+#   2. the MFMA-busy PMC pass of ONE update at the same shape, with the update and rollout forwards
+#      run eagerly (RAI_GRAPHS=0 RAI_ROLLOUT_GRAPH=0: the same kernels, launched one by one) and the
+#      counters restricted to the contraction and epilogue kernels (--kernel-include-regex).
+#      Over the whole update rocprofv3 crashed: SIGSEGV in its counter callback during graph replay
+#      (round 1), HSA_STATUS_ERROR_INVALID_PACKET_FORMAT on a torch copy kernel eagerly (r2a).
+#      FETCH_SIZE / WRITE_SIZE still segfault restricted (inside MIOpen's convolution dispatch,
+#      profiles/r2o_pong_fetch_pmc_crash.txt): PASSES=fetch / write only to re-check that.
 # Each step has its own time limit; the script stops at the first step that does not exit 0.
 #   TAG=r2a bash tools/profile_pong.sh
 set -u
@@ -34,13 +36,15 @@ export RAI_GRAPHS=0 RAI_ROLLOUT_GRAPH=0
 ( while sleep 30; do echo "$(date +%T) $(du -sb "$OUT" 2>/dev/null | cut -f1) bytes under $OUT" >> "$OUT/heartbeat.log"; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-for pass in ${PASSES:-fetch write mfma}; do
+REGEX="igemm|Cijk|bias_relu|heads|gather_minibatch"
+for pass in ${PASSES:-mfma}; do
   case $pass in
     fetch) ctr="FETCH_SIZE" ;;
     write) ctr="WRITE_SIZE" ;;
     mfma) ctr="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" ;;
   esac
-  run "$pass" 420 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/$pass" -o run -- $B --steps 1 --warmup 0
+  run "$pass" 420 rocprofv3 --pmc $ctr --kernel-include-regex "$REGEX" --output-format csv -d "$OUT/$pass" -o run -- \
+      $B --steps 1 --warmup 0
   f=$(ls "$OUT/$pass"/*counter_collection.csv | head -1)
   run "${pass}_agg" 300 python3 tools/pmc_kernels.py "$f" "$OUT/${pass}_kernels.json" --delete
 done
