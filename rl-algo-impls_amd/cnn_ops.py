@@ -36,13 +36,50 @@ _state = threading.local()
 @contextlib.contextmanager
 def direct_grads(enabled: bool = True):
     """Within this context the fused epilogues accumulate parameter gradients in place (see the
-    module docstring).  The trainer enters it around its own forward + backward only."""
+    module docstring).  The trainer enters it around its own forward + backward only.
+
+    The convolution weight gradients come back from MIOpen as fresh tensors; their accumulates into
+    the flat gradient are deferred to the exit of this context and issued as ONE multi-tensor add
+    (torch._foreach_add_) instead of an add launch per layer.  The list is handed to the backward
+    through ctx (autograd runs CUDA backward nodes on its device thread, where this thread's
+    state is not visible)."""
     prev = getattr(_state, "direct", False)
+    prev_pending = getattr(_state, "pending", None)
     _state.direct = enabled
+    pending = _PendingGrads()
+    _state.pending = pending
+    ok = False
     try:
         yield
+        ok = True
     finally:
         _state.direct = prev
+        _state.pending = prev_pending
+        pending.close(flush=ok)
+
+
+class _PendingGrads:
+    """(weight, gradient) pairs awaiting their accumulate; a backward that runs after the context
+    has closed (forward inside it, backward outside) accumulates its own at once."""
+
+    def __init__(self):
+        self.items: list = []
+        self.closed = False
+
+    def add(self, w: torch.Tensor, dw: torch.Tensor) -> None:
+        if self.closed:
+            w.grad.add_(dw)
+            notify_grad_written(w)
+        else:
+            self.items.append((w, dw))
+
+    def close(self, flush: bool) -> None:
+        self.closed = True
+        items, self.items = self.items, []
+        if flush and items:
+            torch._foreach_add_([w.grad for w, _ in items], [dw for _, dw in items])
+            for w, _ in items:
+                notify_grad_written(w)
 
 
 def _direct(p: torch.Tensor, raw: bool = False) -> bool:
@@ -112,6 +149,7 @@ class ConvBiasReLU(torch.autograd.Function):
         y = _bias_relu_fwd(z, b)
         ctx.save_for_backward(x, w, b, y)
         ctx.conf = (stride, padding, key, _direct(b, raw=True), _direct(w))
+        ctx.pending = _state.pending if ctx.conf[4] else None
         return y
 
     @staticmethod
@@ -123,10 +161,9 @@ class ConvBiasReLU(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         dx, dw, _ = torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), _pair(padding), [1, 1],
                                                         False, [0, 0], 1, [need_dx, True, False])
-        if direct_w:
-            w.grad.add_(dw)
+        if direct_w:  # accumulated with the other layers' at direct_grads() exit
+            ctx.pending.add(w, dw)
             dw = None
-            notify_grad_written(w)
         return dx, dw, db, None, None, None
 
 

@@ -182,9 +182,10 @@ extern "C" int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b
 // orders).  relu(NaN) = NaN and dx = 0 where out <= 0, as torch's clamp_min / threshold_backward.
 namespace {
 constexpr int BR_THREADS = 256;
-constexpr int BR_MAX_BLOCKS = 256;  // about one workgroup per CU (the hand-off's measured form)
+constexpr int BR_MAX_BLOCKS = 512;  // two workgroups per CU
 constexpr int BR_UNROLL = 4;      // rows in flight per lane before the first use
-constexpr int BR_ROWS_PER_LANE = 16;  // conv1 at C3: 200 workgroups of 512 rows
+constexpr int BR_ROWS_PER_LANE = 8;  // conv1 at C3: 400 workgroups of 256 rows
+constexpr int BR_TAIL = 16;       // partial loads in flight per thread in the last arriver
 
 __global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_kernel(const f4* __restrict__ x, const float* __restrict__ b,
                                                                   int C4, int64_t n4, f4* __restrict__ out) {
@@ -202,9 +203,12 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_kernel(const f4* __r
 
 // Workgroup w owns rows [w * rpb, (w + 1) * rpb); its threads are (row lane, float4 channel group)
 // pairs, each lane keeping BR_UNROLL rows' loads in flight; dx is stored and the workgroup's column
-// sums (row lanes added in lane order) go to partial[w].  The workgroup whose arrival comes last then
-// sums the partials: thread t adds partials s, s + stripes, ... (s = t / C, fixed order) of channel
-// t % C, then the stripes are added in order through LDS -> db.
+// sums (a pairwise tree over the row lanes) go to partial[w].  The workgroup whose arrival comes last
+// then sums the partials: thread (lane, c4) adds partials lane, lane + lanes, ... of channel group c4
+// with BR_TAIL 16-B loads in flight, and the lanes are tree-summed again -> db.  Every order is fixed
+// by (rows, C), so db is deterministic.  (Round 2, first form: serial lane sums and 4-B tail loads
+// four in flight, 8-13 us per C3 layer against ~5 us for torch's threshold_backward alone;
+// tools/bias_relu_bench.py, profiles/r2t_bias_relu_bench.txt.)
 // Hand-off without fences (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms): the partials
 // are 16-B write-through (sc1) buffer stores drained by every storing wave (vmcnt(0)) before the
 // workgroup barrier and one agent-scope atomic add; the last arriver's waves read them with sc1 buffer
@@ -215,13 +219,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t br_rsrc(const void* p, int byt
 }
 constexpr int BR_SC1 = 16;  // cache-policy operand: sc1 (write-through stores, L1-bypassing loads)
 
+// part[lane * C4 + c4] (lanes a power of two) -> part[c4]: a pairwise tree over the lanes, the same
+// order on every launch.  Called with part written and the workgroup synchronised.
+__device__ __forceinline__ void lane_tree_sum(f4* part, int lane, int C4, int lanes) {
+  for (int h = lanes / 2; h >= 1; h /= 2) {
+    if (lane < h) part[threadIdx.x] += part[threadIdx.x + h * C4];
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __restrict__ dy, const f4* __restrict__ y,
                                                                   int C4, int64_t rows, int64_t rows_per_block,
                                                                   f4* __restrict__ dx, float* partial,
                                                                   int* counter, float* __restrict__ db,
                                                                   int accumulate) {
   __shared__ f4 part[BR_THREADS];
-  __shared__ float red[BR_THREADS];
   __shared__ int last;
   const int tid = threadIdx.x;
   const int lanes = BR_THREADS / C4;  // row lanes; C4 divides 256
@@ -255,43 +267,42 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __r
   }
   part[tid] = acc;
   __syncthreads();
-  if (tid < C4) {
-    f4 t = part[tid];
-    for (int k = 1; k < lanes; ++k) t += part[tid + k * C4];
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, t), prs, (blockIdx.x * C + 4 * tid) * 4, 0, BR_SC1);
-  }
+  lane_tree_sum(part, lane, C4, lanes);
+  if (tid < C4)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, part[tid]), prs, (blockIdx.x * C + 4 * tid) * 4, 0,
+                                           BR_SC1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
   __syncthreads();
   if (tid == 0) last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
   __syncthreads();
   if (!last) return;
-  auto ld = [&](int w, int c) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prs, (w * C + c) * 4, 0, BR_SC1));
-  };
-  if (C <= BR_THREADS) {
-    const int stripes = BR_THREADS / C, c = tid % C, s0 = tid / C;
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    if (s0 < stripes) {
-      int w = s0;
-      for (; w + 3 * stripes < nb; w += 4 * stripes) {
+  // the last arriver: thread (lane, c4) sums partials lane, lane + lanes, ... of channel group c4 with
+  // BR_TAIL loads in flight (one round for every C3 layer), then the lanes are tree-summed as above
+  f4 s[BR_TAIL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) s[u] += ld(w + u * stripes, c);
-      }
-      for (int u = 0; w < nb; w += stripes, ++u) s[u] += ld(w, c);
+  for (int u = 0; u < BR_TAIL; ++u) s[u] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int w0 = lane; w0 < nb; w0 += BR_TAIL * lanes) {
+    f4 v[BR_TAIL];
+#pragma unroll
+    for (int u = 0; u < BR_TAIL; ++u) {  // past nb: num_records bounds the resource, the load returns 0
+      const int w = w0 + u * lanes;
+      v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(prs, (w * C + 4 * c4) * 4, 0, BR_SC1));
     }
-    red[tid] = (s[0] + s[1]) + (s[2] + s[3]);
-    __syncthreads();
-    if (tid < C) {
-      float t = red[tid];
-      for (int k = 1; k < stripes; ++k) t += red[tid + k * C];
-      db[tid] = accumulate ? db[tid] + t : t;
-    }
-  } else {
-    for (int c = tid; c < C; c += BR_THREADS) {
-      float t = 0.f;
-      for (int w = 0; w < nb; ++w) t += ld(w, c);
-      db[c] = accumulate ? db[c] + t : t;
-    }
+#pragma unroll
+    for (int u = 0; u < BR_TAIL; ++u)
+      if (w0 + u * lanes < nb) s[u] += v[u];
+  }
+#pragma unroll
+  for (int h = BR_TAIL / 2; h >= 1; h /= 2)
+#pragma unroll
+    for (int u = 0; u < h; ++u) s[u] += s[u + h];
+  part[tid] = s[0];
+  __syncthreads();
+  lane_tree_sum(part, lane, C4, lanes);
+  if (tid < C4) {
+    const f4 t = part[tid];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) db[4 * tid + q] = accumulate ? db[4 * tid + q] + t[q] : t[q];
   }
   if (tid == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
 }

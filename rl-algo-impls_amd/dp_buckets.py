@@ -25,17 +25,25 @@ same buckets are summed after the backward instead.
 """
 from __future__ import annotations
 
-import threading
 from typing import Callable, Dict, List, Optional
 
 import torch
 
-_hooks = threading.local()
+
+class _Hooks:
+    """The armed trigger callback.  Process-wide, not thread-local: autograd runs the backward of
+    CUDA nodes on its per-device worker thread, not on the thread that called backward() (a
+    thread-local hook armed by begin() is invisible there, and every bucket then waited for
+    finish())."""
+    cb: Optional[Callable[[torch.Tensor], None]] = None
+
+
+_hooks = _Hooks()
 
 
 def notify_grad_written(param: torch.Tensor) -> None:
     """Called by the fused layer backwards (cnn_ops) right after they wrote `param`'s gradient."""
-    cb = getattr(_hooks, "cb", None)
+    cb = _hooks.cb
     if cb is not None:
         cb(param)
 
@@ -56,6 +64,7 @@ class GradBuckets:
         self.overlap = overlap and flat.grad.is_cuda
         self.side = torch.cuda.Stream(device) if self.overlap else None
         self.launched: List[bool] = []
+        self.early_launches = 0  # buckets launched by a trigger, i.e. inside the backward
 
     @property
     def n(self) -> int:
@@ -78,7 +87,8 @@ class GradBuckets:
 
     def _on_written(self, param: torch.Tensor) -> None:
         i = self.triggers.get(id(param))
-        if i is not None:
+        if i is not None and not self.launched[i]:
+            self.early_launches += 1
             self._launch(i)
 
     def begin(self) -> None:

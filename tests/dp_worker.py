@@ -334,6 +334,8 @@ def cnn_dp_worker(rank, world, port, q, mode):
     stats, norms, _ = algo.update(r)
     torch.cuda.synchronize()
     assert (getattr(algo, "_buckets", None) is not None) == (mode == "buckets")
+    if mode == "buckets":  # the fc + heads bucket went from inside the backward (autograd's device thread)
+        assert algo._buckets.early_launches > 0
     q.put((mode, algo.flat.flat.cpu().numpy(), np.asarray(stats), np.asarray(norms)))
     if mode != "single":
         import torch.distributed as dist
