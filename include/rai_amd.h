@@ -153,11 +153,21 @@ int rai_bias_gelu_bwd(const float* dy, const float* x, const float* b, int64_t r
  * into the flat .grad buffer), in one launch (the last workgroup to arrive sums the per-workgroup
  * partials).  The reduction order is fixed (deterministic).  workspace: at least
  * rai_bias_relu_workspace_bytes(C) bytes, 16-B aligned, ZEROED before its first use (its arrival
- * counter is re-armed by every launch); one workspace per concurrently running launch. */
+ * counters are re-armed by every launch); one workspace per concurrently running launch. */
 int64_t rai_bias_relu_workspace_bytes(int32_t C);
 int rai_bias_relu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream);
 int rai_bias_relu_bwd(const float* dy, const float* y, int64_t rows, int32_t C, float* dx, float* db,
                       int32_t accumulate, void* workspace, int64_t workspace_bytes, void* stream);
+/* The same pair for the layer whose output is flattened (NatureCNN conv3 -> nn.Flatten -> Linear,
+ * nature_cnn.py:41-53): x is the bias-free conv output in NHWC (B, HW, C); the forward writes
+ * out = relu(x + b) in the flattened NCHW order (B, C * HW) that nn.Flatten gives, the backward takes
+ * dy and y in that order and writes dx in NHWC (B, HW, C) for the convolution's backward, with db as
+ * rai_bias_relu_bwd (same workspace).  The two layout copies around the flatten disappear into the
+ * passes.  (C + 1) * HW <= 8192, C % 4 == 0, C / 4 dividing 256; dx 16-B aligned. */
+int rai_bias_relu_fwd_nchw(const float* x, const float* b, int64_t B, int32_t HW, int32_t C, float* out,
+                           void* stream);
+int rai_bias_relu_bwd_nchw(const float* dy, const float* y, int64_t B, int32_t HW, int32_t C, float* dx, float* db,
+                           int32_t accumulate, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.

@@ -166,6 +166,8 @@ _SIGNATURES = {
                                                    _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_bias_relu_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "rai_bias_relu_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
+    "rai_bias_relu_fwd_nchw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "rai_bias_relu_bwd_nchw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, [C.c_int64, C.c_int32]),
     "rai_mlp_ppo_grads": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _i32,
                                     _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),

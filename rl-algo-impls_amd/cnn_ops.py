@@ -128,6 +128,27 @@ def _bias_relu_fwd(z: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def _bias_relu_fwd_nchw(z: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """z (B, C, H, W) channels_last -> relu(z + b) flattened in NCHW order (B, C*H*W)."""
+    B, C, H, W = (int(v) for v in z.shape)
+    y = torch.empty((B, C * H * W), dtype=z.dtype, device=z.device)
+    _lib.check(_lib.lib().rai_bias_relu_fwd_nchw(z.data_ptr(), b.data_ptr(), B, H * W, C, y.data_ptr(),
+                                                 _lib.stream_handle(z.device)), "rai_bias_relu_fwd_nchw")
+    return y
+
+
+def _bias_relu_bwd_nchw(dy: torch.Tensor, y: torch.Tensor, b: torch.Tensor, ws: torch.Tensor, direct: bool,
+                        zshape):
+    """dy, y (B, C*H*W) in NCHW order -> (dz (B, C, H, W) channels_last, db or None)."""
+    B, C, H, W = zshape
+    dz = torch.empty(zshape, dtype=y.dtype, device=y.device, memory_format=torch.channels_last)
+    db = b.grad if direct else torch.empty(C, dtype=torch.float32, device=y.device)
+    _lib.check(_lib.lib().rai_bias_relu_bwd_nchw(dy.data_ptr(), y.data_ptr(), B, H * W, C, dz.data_ptr(),
+                                                 db.data_ptr(), 1 if direct else 0, ws.data_ptr(), ws.numel(),
+                                                 _lib.stream_handle(y.device)), "rai_bias_relu_bwd_nchw")
+    return dz, (None if direct else db)
+
+
 def _bias_relu_bwd(dy: torch.Tensor, y: torch.Tensor, b: torch.Tensor, ws: torch.Tensor, direct: bool):
     """(dz, db or None): db is added into b.grad when direct."""
     C = int(y.shape[1])
@@ -140,31 +161,36 @@ def _bias_relu_bwd(dy: torch.Tensor, y: torch.Tensor, b: torch.Tensor, ws: torch
 
 
 class ConvBiasReLU(torch.autograd.Function):
-    """relu(conv2d(x, W) + b) on NHWC (channels_last) fp32 activations."""
+    """relu(conv2d(x, W) + b) on NHWC (channels_last) fp32 activations; with flatten, returned as
+    torch.flatten(., 1) of it (NCHW order, (B, C*H*W)) by the transposing epilogue pair."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, key):
+    def forward(ctx, x, w, b, stride, padding, key, flatten=False):
         z = F.conv2d(x, w, None, stride, padding)
         z = z.contiguous(memory_format=torch.channels_last)
-        y = _bias_relu_fwd(z, b)
+        y = _bias_relu_fwd_nchw(z, b) if flatten else _bias_relu_fwd(z, b)
         ctx.save_for_backward(x, w, b, y)
-        ctx.conf = (stride, padding, key, _direct(b, raw=True), _direct(w))
+        ctx.conf = (stride, padding, key, _direct(b, raw=True), _direct(w), flatten, tuple(int(v) for v in z.shape))
         ctx.pending = _state.pending if ctx.conf[4] else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, b, y = ctx.saved_tensors
-        stride, padding, key, direct_b, direct_w = ctx.conf
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        dz, db = _bias_relu_bwd(dy, y, b, _WS.get(key, int(y.shape[1]), y.device), direct_b)
+        stride, padding, key, direct_b, direct_w, flatten, zshape = ctx.conf
+        ws = _WS.get(key, zshape[1], y.device)
+        if flatten:
+            dz, db = _bias_relu_bwd_nchw(dy.contiguous(), y, b, ws, direct_b, zshape)
+        else:
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            dz, db = _bias_relu_bwd(dy, y, b, ws, direct_b)
         need_dx = ctx.needs_input_grad[0]
         dx, dw, _ = torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), _pair(padding), [1, 1],
                                                         False, [0, 0], 1, [need_dx, True, False])
         if direct_w:  # accumulated with the other layers' at direct_grads() exit
             ctx.pending.add(w, dw)
             dw = None
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 class LinearBiasReLU(torch.autograd.Function):
@@ -197,14 +223,27 @@ def _pair(v):
     return list(v) if isinstance(v, (tuple, list)) else [v, v]
 
 
-def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """relu(conv(x)) for an NHWC fp32 GPU activation (fused epilogue), else the module path."""
-    if (x.is_cuda and x.dtype == torch.float32 and conv.bias is not None and conv.groups == 1
+_BRT_MAX_ELEMS = 8192  # csrc/se_block.hip BRT_MAX_ELEMS: (C + 1) * H * W of the transposing pair
+
+
+def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor, flatten: bool = False) -> torch.Tensor:
+    """relu(conv(x)) for an NHWC fp32 GPU activation (fused epilogue), else the module path.
+    flatten: return torch.flatten(relu(conv(x)), 1) (NCHW order), transposed inside the epilogue."""
+    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.bias is not None and conv.groups == 1
             and tuple(conv.dilation) == (1, 1) and conv.padding_mode == "zeros" and isinstance(conv.padding, tuple)
             and conv.out_channels % 4 == 0 and 256 % (conv.out_channels // 4) == 0):
+        if flatten:
+            hw = 1
+            for d in range(2):
+                hw *= (int(x.shape[2 + d]) + 2 * conv.padding[d] - conv.kernel_size[d]) // conv.stride[d] + 1
+            flatten = (conv.out_channels + 1) * hw <= _BRT_MAX_ELEMS
+            if not flatten:
+                return torch.flatten(conv_relu(conv, x), 1)
         _WS.prewarm(id(conv), conv.out_channels, x.device)
-        return ConvBiasReLU.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), id(conv))
-    return F.relu(conv(x))
+        return ConvBiasReLU.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), id(conv),
+                                  flatten)
+    y = F.relu(conv(x))
+    return torch.flatten(y, 1) if flatten else y
 
 
 def linear_relu(lin: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:

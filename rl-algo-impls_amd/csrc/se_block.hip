@@ -186,6 +186,8 @@ constexpr int BR_MAX_BLOCKS = 512;  // two workgroups per CU
 constexpr int BR_UNROLL = 4;      // rows in flight per lane before the first use
 constexpr int BR_ROWS_PER_LANE = 8;  // conv1 at C3: 400 workgroups of 256 rows
 constexpr int BR_TAIL = 16;       // partial loads in flight per thread in the last arriver
+constexpr int BR_CTR_STRIDE = 16;  // arrival counters 64 B apart: the top one, then 8 group counters
+constexpr int BR_CTR_BYTES = 9 * BR_CTR_STRIDE * 4;
 
 __global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_kernel(const f4* __restrict__ x, const float* __restrict__ b,
                                                                   int C4, int64_t n4, f4* __restrict__ out) {
@@ -211,8 +213,8 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_kernel(const f4* __r
 // tools/bias_relu_bench.py, profiles/r2t_bias_relu_bench.txt.)
 // Hand-off without fences (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms): the partials
 // are 16-B write-through (sc1) buffer stores drained by every storing wave (vmcnt(0)) before the
-// workgroup barrier and one agent-scope atomic add; the last arriver's waves read them with sc1 buffer
-// loads after a barrier.  (Two launches, the row pass then a one-workgroup finalize, cost a second
+// workgroup barrier and the agent-scope arrival atomics (group counter, then the top counter for the
+// last of a group); the last arriver's waves read them with sc1 buffer loads after a barrier.  (Two launches, the row pass then a one-workgroup finalize, cost a second
 // ~4.8 us launch per layer; a last-arriver variant with __threadfence() in every thread ~30 us.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t br_rsrc(const void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
@@ -228,6 +230,71 @@ __device__ __forceinline__ void lane_tree_sum(f4* part, int lane, int C4, int la
   }
 }
 
+// The end of every bias-gradient pass: this workgroup's column sums (thread tid < C4 holds channels
+// 4 tid .. 4 tid + 3 in wsum) go to partial[blockIdx.x] (write-through), the workgroup arrives on
+// the two-level counters, and the last arriver sums the nb partials in a fixed order into db
+// (db0: db as read at the kernel's start, for accumulate).
+__device__ __forceinline__ void br_finish(f4 wsum, f4* part, int* last, float* partial, int* counter, float* db,
+                                          const float* db0, int accumulate, int C4) {
+  const int tid = threadIdx.x, lanes = BR_THREADS / C4, c4 = tid % C4, lane = tid / C4, C = 4 * C4;
+  const int nb = (int)gridDim.x;
+  const __amdgpu_buffer_rsrc_t prs = br_rsrc(partial, nb * C * 4);
+  if (tid < C4)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, wsum), prs, (blockIdx.x * C + 4 * tid) * 4, 0,
+                                           BR_SC1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  // arrival in two levels: workgroup w counts in group w % 8 (same-address atomics serialise at
+  // ~10 ns each: one counter for 400 workgroups cost ~3.6 us), the last of each group in the top one
+  if (tid == 0) {
+    const int g = blockIdx.x & 7, gsize = (nb - g + 7) >> 3, ngroups = nb < 8 ? nb : 8;
+    int* cg = counter + BR_CTR_STRIDE * (1 + g);
+    *last = 0;
+    if (__hip_atomic_fetch_add(cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      *last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+    }
+  }
+  __syncthreads();
+  if (!*last) return;
+  // the last arriver: thread (lane, c4) sums partials lane, lane + lanes, ... of channel group c4 with
+  // BR_TAIL loads in flight (one round for every C3 layer), then the lanes are tree-summed
+  f4 s[BR_TAIL];
+#pragma unroll
+  for (int u = 0; u < BR_TAIL; ++u) s[u] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int w0 = lane; w0 < nb; w0 += BR_TAIL * lanes) {
+    f4 v[BR_TAIL];
+#pragma unroll
+    for (int u = 0; u < BR_TAIL; ++u) {  // past nb: num_records bounds the resource, the load returns 0
+      const int w = w0 + u * lanes;
+      v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(prs, (w * C + 4 * c4) * 4, 0, BR_SC1));
+    }
+#pragma unroll
+    for (int u = 0; u < BR_TAIL; ++u)
+      if (w0 + u * lanes < nb) s[u] += v[u];
+  }
+#pragma unroll
+  for (int h = BR_TAIL / 2; h >= 1; h /= 2)
+#pragma unroll
+    for (int u = 0; u < h; ++u) s[u] += s[u + h];
+  part[tid] = s[0];
+  __syncthreads();
+  lane_tree_sum(part, lane, C4, lanes);
+  if (tid < C4) {
+    const f4 t = part[tid];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) db[4 * tid + q] = accumulate ? db0[q] + t[q] : t[q];
+  }
+  if (tid == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+}
+
+__device__ __forceinline__ void br_load_db(const float* db, int accumulate, int C4, float* db0) {
+  if (accumulate && (int)threadIdx.x < C4) {  // db read now: the last arriver's update is then one store
+#pragma unroll
+    for (int q = 0; q < 4; ++q) db0[q] = db[4 * threadIdx.x + q];
+  }
+}
+
 __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __restrict__ dy, const f4* __restrict__ y,
                                                                   int C4, int64_t rows, int64_t rows_per_block,
                                                                   f4* __restrict__ dx, float* partial,
@@ -238,11 +305,10 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __r
   const int tid = threadIdx.x;
   const int lanes = BR_THREADS / C4;  // row lanes; C4 divides 256
   const int c4 = tid % C4, lane = tid / C4;
-  const int C = 4 * C4;
-  const int nb = (int)gridDim.x;
-  const __amdgpu_buffer_rsrc_t prs = br_rsrc(partial, nb * C * 4);
   const int64_t r0 = blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
+  float db0[4] = {0.f, 0.f, 0.f, 0.f};
+  br_load_db(db, accumulate, C4, db0);
   f4 acc = f4{0.f, 0.f, 0.f, 0.f};
   for (int64_t r = r0 + lane; r < r1; r += (int64_t)lanes * BR_UNROLL) {
     f4 g[BR_UNROLL], yv[BR_UNROLL];
@@ -268,43 +334,82 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_kernel(const f4* __r
   part[tid] = acc;
   __syncthreads();
   lane_tree_sum(part, lane, C4, lanes);
-  if (tid < C4)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, part[tid]), prs, (blockIdx.x * C + 4 * tid) * 4, 0,
-                                           BR_SC1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-  __syncthreads();
-  if (tid == 0) last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
-  __syncthreads();
-  if (!last) return;
-  // the last arriver: thread (lane, c4) sums partials lane, lane + lanes, ... of channel group c4 with
-  // BR_TAIL loads in flight (one round for every C3 layer), then the lanes are tree-summed as above
-  f4 s[BR_TAIL];
-#pragma unroll
-  for (int u = 0; u < BR_TAIL; ++u) s[u] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int w0 = lane; w0 < nb; w0 += BR_TAIL * lanes) {
-    f4 v[BR_TAIL];
-#pragma unroll
-    for (int u = 0; u < BR_TAIL; ++u) {  // past nb: num_records bounds the resource, the load returns 0
-      const int w = w0 + u * lanes;
-      v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(prs, (w * C + 4 * c4) * 4, 0, BR_SC1));
+  br_finish(part[tid], part, &last, partial, counter, db, db0, accumulate, C4);
+}
+
+// ---- the flattening layer's epilogue (NatureCNN conv3 -> Flatten -> Linear) ---------------------
+// nn.Flatten after a channels_last convolution flattens in NCHW order (c, h, w), so torch copies the
+// NHWC activation into that order before the fc GEMM and copies the fc's input gradient back to NHWC
+// for the convolution's backward: two layout copies per minibatch (19 us per C3 minibatch, r2x
+// stats).  These two kernels do the transposes inside the bias + ReLU passes instead:
+//   forward   out[b, c * HW + p] = relu(x[b, p, c] + bias[c])      (x NHWC, out flat NCHW)
+//   backward  dx[b, p, c] = y[b, c * HW + p] > 0 ? dy[b, c * HW + p] : 0   (dx NHWC), db as above
+// Workgroup w handles samples w, w + G, ...: the sample's HW x C plane is staged in LDS with rows of
+// C + 1 floats (the transposed reads walk 65-float strides: conflict-free) so that both the global
+// reads and the global writes are contiguous.  Needs (C + 1) * HW <= BRT_MAX_ELEMS.
+constexpr int BRT_MAX_ELEMS = 8192;  // (C + 1) * HW floats of LDS: 32 KB
+
+__global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_nchw_kernel(const float* __restrict__ x,
+                                                                       const float* __restrict__ b, int64_t B, int HW,
+                                                                       int C, float* __restrict__ out) {
+  __shared__ float t[BRT_MAX_ELEMS];
+  const int n = HW * C, ld = C + 1;
+  for (int64_t s = blockIdx.x; s < B; s += gridDim.x) {
+    const float* xs = x + s * n;
+    for (int m = threadIdx.x; m < n; m += BR_THREADS) {  // NHWC element m = p * C + c
+      const int p = m / C, c = m - p * C;
+      const float v = xs[m] + b[c];
+      t[p * ld + c] = v < 0.f ? 0.f : v;
     }
-#pragma unroll
-    for (int u = 0; u < BR_TAIL; ++u)
-      if (w0 + u * lanes < nb) s[u] += v[u];
+    __syncthreads();
+    float* os = out + s * n;
+    for (int e = threadIdx.x; e < n; e += BR_THREADS) {  // NCHW element e = c * HW + p
+      const int c = e / HW, p = e - c * HW;
+      os[e] = t[p * ld + c];
+    }
+    __syncthreads();
   }
-#pragma unroll
-  for (int h = BR_TAIL / 2; h >= 1; h /= 2)
-#pragma unroll
-    for (int u = 0; u < h; ++u) s[u] += s[u + h];
-  part[tid] = s[0];
-  __syncthreads();
-  lane_tree_sum(part, lane, C4, lanes);
-  if (tid < C4) {
-    const f4 t = part[tid];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) db[4 * tid + q] = accumulate ? db[4 * tid + q] + t[q] : t[q];
+}
+
+__global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_nchw_kernel(const float* __restrict__ dy,
+                                                                       const float* __restrict__ y, int64_t B, int HW,
+                                                                       int C, float* __restrict__ dx, float* partial,
+                                                                       int* counter, float* __restrict__ db,
+                                                                       int accumulate) {
+  __shared__ float t[BRT_MAX_ELEMS];
+  __shared__ f4 part[BR_THREADS];
+  __shared__ int last;
+  const int tid = threadIdx.x, C4 = C / 4, lanes = BR_THREADS / C4, c4 = tid % C4, lane = tid / C4;
+  const int n = HW * C, ld = C + 1;
+  float db0[4] = {0.f, 0.f, 0.f, 0.f};
+  br_load_db(db, accumulate, C4, db0);
+  f4 wsum = f4{0.f, 0.f, 0.f, 0.f};  // thread tid < C4: this workgroup's samples, in sample order
+  for (int64_t s = blockIdx.x; s < B; s += gridDim.x) {
+    const float* dys = dy + s * n;
+    const float* ys = y + s * n;
+    for (int e = tid; e < n; e += BR_THREADS) {  // NCHW element e = c * HW + p
+      const int c = e / HW, p = e - c * HW;
+      t[p * ld + c] = ys[e] <= 0.f ? 0.f : dys[e];
+    }
+    __syncthreads();
+    float* dxs = dx + s * n;
+    for (int m4 = tid; m4 < n / 4; m4 += BR_THREADS) {  // NHWC float4 m4: pixel p, channels 4 q .. 4 q + 3
+      const int p = m4 / C4, q = m4 - p * C4;
+      const float* r = t + p * ld + 4 * q;
+      reinterpret_cast<f4*>(dxs)[m4] = f4{r[0], r[1], r[2], r[3]};
+    }
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};  // thread (lane, c4): pixels lane, lane + lanes, ...
+    for (int p = lane; p < HW; p += lanes) {
+      const float* r = t + p * ld + 4 * c4;
+      acc += f4{r[0], r[1], r[2], r[3]};
+    }
+    part[tid] = acc;
+    __syncthreads();
+    lane_tree_sum(part, lane, C4, lanes);
+    if (tid < C4) wsum += part[tid];
+    __syncthreads();  // t and part are rewritten by the next sample
   }
-  if (tid == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+  br_finish(wsum, part, &last, partial, counter, db, db0, accumulate, C4);
 }
 
 bool br_shape_ok(int64_t rows, int32_t C) {
@@ -315,7 +420,7 @@ bool br_shape_ok(int64_t rows, int32_t C) {
 }  // namespace
 
 extern "C" int64_t rai_bias_relu_workspace_bytes(int32_t C) {
-  return (int64_t)BR_MAX_BLOCKS * (C > 0 ? C : 0) * 4 + 16;  // partials, then the arrival counter
+  return (int64_t)BR_MAX_BLOCKS * (C > 0 ? C : 0) * 4 + BR_CTR_BYTES;  // partials, then the arrival counters
 }
 
 extern "C" int rai_bias_relu_fwd(const float* x, const float* b, int64_t rows, int32_t C, float* out, void* stream) {
@@ -325,6 +430,46 @@ extern "C" int rai_bias_relu_fwd(const float* x, const float* b, int64_t rows, i
   const int64_t n4 = rows * (C / 4);
   hipLaunchKernelGGL(bias_relu_fwd_kernel, dim3((unsigned)ew_blocks(n4)), dim3(BR_THREADS), 0, rai_stream(stream),
                      reinterpret_cast<const f4*>(x), b, C / 4, n4, reinterpret_cast<f4*>(out));
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+static bool brt_shape_ok(int64_t B, int32_t HW, int32_t C) {
+  return B >= 0 && HW >= 1 && br_shape_ok(1, C) && (int64_t)(C + 1) * HW <= BRT_MAX_ELEMS;
+}
+
+extern "C" int rai_bias_relu_fwd_nchw(const float* x, const float* b, int64_t B, int32_t HW, int32_t C, float* out,
+                                      void* stream) {
+  if (!brt_shape_ok(B, HW, C)) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!x || !b || !out) return RAI_E_NULLPTR;
+  const int64_t blocks = B < 1024 ? B : 1024;
+  hipLaunchKernelGGL(bias_relu_fwd_nchw_kernel, dim3((unsigned)blocks), dim3(BR_THREADS), 0, rai_stream(stream), x, b,
+                     B, HW, C, out);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_bias_relu_bwd_nchw(const float* dy, const float* y, int64_t B, int32_t HW, int32_t C, float* dx,
+                                      float* db, int32_t accumulate, void* workspace, int64_t workspace_bytes,
+                                      void* stream) {
+  if (!brt_shape_ok(B, HW, C)) return RAI_E_SHAPE;
+  if (!dy || !y || !dx || !db || !workspace) return RAI_E_NULLPTR;
+  if (workspace_bytes < rai_bias_relu_workspace_bytes(C) || ((uintptr_t)workspace & 15) || ((uintptr_t)dx & 15))
+    return RAI_E_WORKSPACE;
+  hipStream_t st = rai_stream(stream);
+  if (B == 0) {
+    if (!accumulate) {
+      const hipError_t e = hipMemsetAsync(db, 0, (size_t)C * 4, st);
+      if (e != hipSuccess) return (int)e;
+    }
+    return RAI_OK;
+  }
+  const int64_t blocks = B < BR_MAX_BLOCKS ? B : BR_MAX_BLOCKS;
+  float* partial = static_cast<float*>(workspace);
+  int* counter = reinterpret_cast<int*>(static_cast<uint8_t*>(workspace) + (int64_t)BR_MAX_BLOCKS * C * 4);
+  hipLaunchKernelGGL(bias_relu_bwd_nchw_kernel, dim3((unsigned)blocks), dim3(BR_THREADS), 0, st, dy, y, B, HW, C, dx,
+                     partial, counter, db, accumulate);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

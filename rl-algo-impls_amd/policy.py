@@ -162,9 +162,10 @@ class NatureCnnEncoder(nn.Module):
         cnn_ops (same modules, same parameters, same state_dict)."""
         from .cnn_ops import conv_relu, linear_relu
 
-        for i in (0, 2, 4):
+        for i in (0, 2):
             x = conv_relu(self.cnn[i], x)
-        return linear_relu(self.fc[1], torch.flatten(x, 1))
+        # conv3's epilogue writes the flattened (NCHW-order) fc input itself: no layout copies
+        return linear_relu(self.fc[1], conv_relu(self.cnn[4], x, flatten=True))
 
 
 class Encoder(nn.Module):  # shared/encoder/encoder.py:25-73

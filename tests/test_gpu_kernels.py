@@ -511,4 +511,40 @@ def test_bias_relu_fwd_bwd_match_torch(rows, C):
                                    rtol=1e-5, atol=2e-6 * rows ** 0.5)
         dbs.append(db - (0.5 if acc else 0.0))
     assert torch.equal(dbs[0], dbs[2])  # deterministic
-    assert int(ws.view(torch.int32)[(ws.numel() - 16) // 4]) == 0  # the arrival counter, re-armed
+    assert bool((ws[-576:].view(torch.int32) == 0).all())  # the arrival counters, re-armed
+
+
+@pytest.mark.parametrize("B,H,W,C", [(256, 7, 7, 64), (1024, 7, 7, 64), (5, 3, 3, 8), (700, 2, 5, 32), (2, 7, 7, 128)])
+def test_bias_relu_nchw_pair_matches_torch_flatten(B, H, W, C):
+    """rai_bias_relu_fwd_nchw / _bwd_nchw (csrc/se_block.hip, NatureCNN conv3 -> Flatten): the forward
+    equals torch.flatten(relu(z + b), 1) of the channels_last conv output bit for bit; the backward
+    takes the flattened gradient, returns threshold_backward in NHWC bit for bit and the bias gradient
+    within fp32 summation tolerance (written, accumulated, deterministic, counters re-armed).
+    B = 700 / 1024 > 512 workgroups: several samples per workgroup."""
+    g = torch.Generator(device="cpu").manual_seed(B * 7 + C)
+    z = torch.randn(B, C, H, W, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(C, generator=g).to(DEV)
+    L, st = _lib.lib(), _lib.stream_handle(DEV)
+    y = torch.empty(B, C * H * W, device=DEV)
+    _lib.check(L.rai_bias_relu_fwd_nchw(z.data_ptr(), b.data_ptr(), B, H * W, C, y.data_ptr(), st), "fwd_nchw")
+    ref = torch.flatten(torch.relu(z + b.view(1, C, 1, 1)), 1)
+    assert torch.equal(y, ref)
+    dy = torch.randn(B, C * H * W, generator=g).to(DEV)
+    ws = torch.zeros(int(L.rai_bias_relu_workspace_bytes(C)), dtype=torch.uint8, device=DEV)
+    dx_ref = torch.ops.aten.threshold_backward(dy, y, 0.0).view(B, C, H, W)
+    dbs = []
+    for acc in (0, 1, 0):
+        dx = torch.empty(B, C, H, W, device=DEV, memory_format=torch.channels_last)
+        db = torch.full((C,), 0.5, device=DEV)
+        _lib.check(L.rai_bias_relu_bwd_nchw(dy.data_ptr(), y.data_ptr(), B, H * W, C, dx.data_ptr(), db.data_ptr(),
+                                            acc, ws.data_ptr(), ws.numel(), st), "bwd_nchw")
+        assert torch.equal(dx, dx_ref)
+        db_ref = dx_ref.double().sum((0, 2, 3))
+        np.testing.assert_allclose(db.double().cpu().numpy(), (db_ref + (0.5 if acc else 0.0)).cpu().numpy(),
+                                   rtol=1e-5, atol=2e-6 * (B * H * W) ** 0.5)
+        dbs.append(db - (0.5 if acc else 0.0))
+    assert torch.equal(dbs[0], dbs[2])
+    assert bool((ws[-576:].view(torch.int32) == 0).all())
+    # shapes the pair does not take: C not a multiple of 4, (C + 1) * HW over the LDS plane
+    assert L.rai_bias_relu_fwd_nchw(z.data_ptr(), b.data_ptr(), B, H * W, 6, y.data_ptr(), st) == -2
+    assert L.rai_bias_relu_fwd_nchw(z.data_ptr(), b.data_ptr(), 1, 4096, 64, y.data_ptr(), st) == -2

@@ -36,13 +36,13 @@ __global__ __launch_bounds__(T) void ew_kernel(const f4* dy, const f4* y, int64_
   }
 }
 
-template <int MODE, int UNROLL>  // MODE 0 pass, 1 counter, 2 full
-__global__ __launch_bounds__(T) void rows_kernel(const f4* __restrict__ dy, const f4* __restrict__ y, int C4,
+template <int MODE, int UNROLL, int NT = T, int TAIL = 16>  // MODE 0 pass, 1 counter, 2 full, 3 full two-level
+__global__ __launch_bounds__(NT) void rows_kernel(const f4* __restrict__ dy, const f4* __restrict__ y, int C4,
                                                  int64_t rows, int64_t rpb, f4* __restrict__ dx, float* partial,
                                                  int* counter, float* db) {
-  __shared__ f4 part[T];
+  __shared__ f4 part[NT];
   __shared__ int last;
-  const int tid = threadIdx.x, lanes = T / C4, c4 = tid % C4, lane = tid / C4, C = 4 * C4;
+  const int tid = threadIdx.x, lanes = NT / C4, c4 = tid % C4, lane = tid / C4, C = 4 * C4;
   const int nb = gridDim.x;
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(partial, 0, nb * C * 4, 0x00020000);
   const int64_t r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
@@ -79,13 +79,24 @@ __global__ __launch_bounds__(T) void rows_kernel(const f4* __restrict__ dy, cons
   if (MODE == 0) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+  if (MODE == 3) {  // counters 1..8 per group blockIdx % 8 (64 B apart), counter 0 the groups
+    if (tid == 0) {
+      const int g = blockIdx.x & 7, gsize = (nb - g + 7) >> 3, ng = nb < 8 ? nb : 8;
+      int* cg = counter + 16 * (1 + g);
+      last = 0;
+      if (__hip_atomic_fetch_add(cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+        __hip_atomic_store(cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+      }
+    }
+  } else if (tid == 0) {
+    last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+  }
   __syncthreads();
   if (MODE == 1 || !last) {
     if (MODE == 1 && last && tid == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  constexpr int TAIL = 16;
   f4 s[TAIL];
   for (int u = 0; u < TAIL; ++u) s[u] = f4{0.f, 0.f, 0.f, 0.f};
   for (int w0 = lane; w0 < nb; w0 += TAIL * lanes) {
@@ -144,8 +155,8 @@ int main() {
     CK(hipMalloc(&dx, n * 4));
     CK(hipMalloc(&part, 4096 * sh.C * 4));
     CK(hipMalloc(&db, sh.C * 4));
-    CK(hipMalloc(&counter, 16));
-    CK(hipMemset(counter, 0, 16));
+    CK(hipMalloc(&counter, 1024));
+    CK(hipMemset(counter, 0, 1024));
     CK(hipMemset(db, 0, sh.C * 4));
     std::vector<float> h(n);
     for (int64_t i = 0; i < n; ++i) h[i] = (float)((i * 2654435761u) % 1000) / 500.f - 1.f;
@@ -158,24 +169,30 @@ int main() {
     });
     std::printf("%s rows %lld C %d  (%.1f MB moved)  ew %.2f us\n", sh.name, (long long)sh.rows, sh.C, 3.0 * n * 4 / 1e6,
                 t_ew);
-    for (int rpl : {2, 4, 8, 16}) {
-      for (int maxb : {256, 512, 1024, 2048}) {
-        int64_t blocks = (sh.rows + (int64_t)rpl * lanes - 1) / ((int64_t)rpl * lanes);
-        if (blocks > maxb) blocks = maxb;
-        const int64_t rpb = (sh.rows + blocks - 1) / blocks;
-        blocks = (sh.rows + rpb - 1) / rpb;
-        if (blocks > 4096) continue;
-        auto L = [&](auto kern) {
-          return timeit([&] {
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(T), 0, 0, (const f4*)dy, (const f4*)y, C4, sh.rows,
-                               rpb, (f4*)dx, part, counter, db);
-          });
-        };
-        const float p4 = L(rows_kernel<0, 4>), c4v = L(rows_kernel<1, 4>), f4v = L(rows_kernel<2, 4>);
-        const float p2 = L(rows_kernel<0, 2>), f2 = L(rows_kernel<2, 2>);
-        std::printf("  rows/lane %2d maxb %4d -> %4lld wg: pass %6.2f counter %6.2f full %6.2f | unroll2 pass %6.2f "
-                    "full %6.2f us\n",
-                    rpl, maxb, (long long)blocks, p4, c4v, f4v, p2, f2);
+    for (int NTsel : {256, 1024}) {
+      const int nt = NTsel, lanes_nt = nt / C4;
+      for (int rpl : {4, 8}) {
+        for (int maxb : {128, 256, 512, 1024}) {
+          int64_t blocks = (sh.rows + (int64_t)rpl * lanes_nt - 1) / ((int64_t)rpl * lanes_nt);
+          if (blocks > maxb) blocks = maxb;
+          const int64_t rpb = (sh.rows + blocks - 1) / blocks;
+          blocks = (sh.rows + rpb - 1) / rpb;
+          auto L = [&](auto kern) {
+            return timeit([&] {
+              hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(nt), 0, 0, (const f4*)dy, (const f4*)y, C4,
+                                 sh.rows, rpb, (f4*)dx, part, counter, db);
+            });
+          };
+          float p, c, f, h;
+          if (nt == 256) {
+            p = L(rows_kernel<0, 4>), c = L(rows_kernel<1, 4>), f = L(rows_kernel<2, 4>), h = L(rows_kernel<3, 4>);
+          } else {
+            p = L(rows_kernel<0, 4, 1024, 8>), c = L(rows_kernel<1, 4, 1024, 8>), f = L(rows_kernel<2, 4, 1024, 8>),
+            h = L(rows_kernel<3, 4, 1024, 8>);
+          }
+          std::printf("  threads %4d rows/lane %2d maxb %4d -> %4lld wg: pass %6.2f counter %6.2f full %6.2f "
+                      "two-level %6.2f us\n", nt, rpl, maxb, (long long)blocks, p, c, f, h);
+        }
       }
     }
     CK(hipFree(dy));
