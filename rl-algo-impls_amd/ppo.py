@@ -484,10 +484,35 @@ class PPO:
         opt = self.optimizer
         L = _lib.lib()
         st = _lib.stream_handle(self.device)
-        for _ in range(self.n_epochs):
-            b = r.epoch_batch(shuffle=True)
-            assert b.logprobs is not None, "PPO needs rollout logprobs (include_logp=True)"
-            obs = b.obs if b.obs.dtype == torch.float32 else b.obs.float()
+        # Epoch k + 1's permutation and gather (a device randperm sort + one gather, ~0.5 ms) run on a
+        # side stream into the other of two permuted copies while epoch k's kernel (32 CUs) runs, so
+        # the 20 launches follow each other without them.  Same permutations: the generator's
+        # offsets are taken on the host in the same order.
+        cur = torch.cuda.current_stream(self.device)
+        two_slots = hasattr(r, "alloc_epoch_buffers")  # DeviceRollout; other rollouts: in order
+        side = self._epoch_prep_stream() if two_slots else cur
+        if two_slots:
+            for slot in (0, 1):
+                r.alloc_epoch_buffers(slot)
+            side.wait_stream(cur)  # the rollout, its GAE and the parameters are ready
+
+        def prep(k):
+            with torch.cuda.stream(side):
+                bk = r.epoch_batch(shuffle=True, slot=k % 2) if two_slots else r.epoch_batch(shuffle=True)
+                assert bk.logprobs is not None, "PPO needs rollout logprobs (include_logp=True)"
+                obs_k = bk.obs if bk.obs.dtype == torch.float32 else bk.obs.float()
+                obs_k = obs_k.contiguous()
+                if obs_k.data_ptr() != bk.obs.data_ptr():
+                    obs_k.record_stream(cur)
+                ready = torch.cuda.Event()
+                ready.record(side)
+            return bk, obs_k, ready
+
+        nxt = prep(0)
+        done: List[torch.cuda.Event] = []
+        for k in range(self.n_epochs):
+            b, obs, ready = nxt
+            cur.wait_event(ready)
             ev = None
             if self.kernel_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -505,6 +530,13 @@ class PPO:
                 ev[1].record()
                 self.kernel_events.append(ev)
             opt.step_count += nmb
+            done.append(torch.cuda.Event())
+            done[-1].record(cur)
+            if k + 1 < self.n_epochs:
+                if k >= 1 and two_slots:
+                    side.wait_event(done[k - 1])  # slot (k + 1) % 2 was read by epoch k - 1
+                nxt = prep(k + 1)
+        cur.wait_stream(side)
         host = torch.cat([blocks.stats[:n_steps].reshape(-1), blocks.norms[:n_steps],
                           blocks.state.view(torch.float32)]).cpu().numpy()
         stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE).copy()
@@ -514,6 +546,11 @@ class PPO:
             raise RuntimeError("rai_mlp_ppo_epoch: device-side exchange timed out (err flag set)")
         stats[:, 0] += float(self.vf_coef) * stats[:, 5]  # value term of the loss
         return stats, norms, 1
+
+    def _epoch_prep_stream(self) -> torch.cuda.Stream:
+        if getattr(self, "_prep_stream", None) is None:
+            self._prep_stream = torch.cuda.Stream(self.device)
+        return self._prep_stream
 
     def _wide_step(self):
         """The wide-MLP fused step for this policy, or None (structure / options not covered)."""

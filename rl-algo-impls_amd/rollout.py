@@ -156,7 +156,7 @@ class DeviceRollout(Rollout):
         self._perm_source = perm_source
         self._generator = generator
         self._flat: Optional[List[torch.Tensor]] = None
-        self._perm_buf: Optional[List[torch.Tensor]] = None
+        self._perm_bufs: Dict[int, List[torch.Tensor]] = {}
 
     # -- Rollout API ---------------------------------------------------------------------
     @property
@@ -209,15 +209,22 @@ class DeviceRollout(Rollout):
             return self._perm_source(self.total_steps).to(self.device)
         return torch.randperm(self.total_steps, device=self.device, generator=self._generator)
 
-    def epoch_batch(self, shuffle: bool = True) -> Batch:
+    def alloc_epoch_buffers(self, slot: int = 0) -> None:
+        """Allocate the permuted copy `slot` (on the current stream) ahead of an epoch_batch that
+        will run on another stream."""
+        if slot not in self._perm_bufs:
+            self._perm_bufs[slot] = [torch.empty_like(f) for f in self._flat_fields()]
+
+    def epoch_batch(self, shuffle: bool = True, slot: int = 0) -> Batch:
         """The whole rollout as one flat Batch, permuted for this epoch (one gather
-        kernel); minibatch i is rows [i*batch_size, (i+1)*batch_size)."""
+        kernel); minibatch i is rows [i*batch_size, (i+1)*batch_size).  slot selects the
+        permuted copy written (two slots: the next epoch's batch is prepared while the current
+        one is read)."""
         flat = self._flat_fields()
         if shuffle:
-            if self._perm_buf is None:
-                self._perm_buf = [torch.empty_like(f) for f in flat]
-            gather_rows(flat, self._perm_buf, self.permutation())
-            src = self._perm_buf
+            self.alloc_epoch_buffers(slot)
+            gather_rows(flat, self._perm_bufs[slot], self.permutation())
+            src = self._perm_bufs[slot]
         else:
             src = flat
         return self._batch_from(src, slice(0, self.total_steps))
