@@ -51,7 +51,7 @@ print(f"whole rollout {T} steps x {N} envs: {whole * 1e3:.1f} ms = {whole * 1e3 
 # phase split of the generic (non-fused, non-GridNet) step, synchronising after every phase
 net = policy.network
 ph = {k: [] for k in ("slot copies", "forward graph", "sample", "D2H act + sync", "env.step",
-                      "reward/done H2D", "stage obs (_stage_obs)")}
+                      "reward/done H2D", "stage obs (+ masks)")}
 policy.eval()
 with torch.no_grad():
     for s in range(args.steps):
@@ -60,11 +60,17 @@ with torch.no_grad():
         gen.obs[s_].copy_(gen.next_obs_dev)
         gen.episode_starts[s_].copy_(gen.next_episode_starts)
         sync(); t.append(time.perf_counter())
-        params, v = gen._policy_forward(net.dist_params_and_value)
+        if gen.action_masks is not None:
+            gen.action_masks[s_].copy_(gen.next_masks_dev)
+        if gen.gridnet:  # forward graph + GridNet sample in one phase, nothing in "sample"
+            gen._gridnet_step(s_)
+            sync(); t.append(time.perf_counter())
+        else:
+            params, v = gen._policy_forward(net.dist_params_and_value)
+            sync(); t.append(time.perf_counter())
+            gen._sample(params, v, s_)
         sync(); t.append(time.perf_counter())
-        gen._sample(params, v, s_)
-        sync(); t.append(time.perf_counter())
-        gen.h_act.copy_(gen.actions[s_], non_blocking=True)
+        gen.h_act.copy_(gen.actions[s_] if (gen.discrete or gen.gridnet) else gen.clamped, non_blocking=True)
         gen._act_ready.record()
         gen._act_ready.synchronize()
         t.append(time.perf_counter())
@@ -76,6 +82,7 @@ with torch.no_grad():
         gen.next_episode_starts.copy_(gen.h_done, non_blocking=True)
         sync(); t.append(time.perf_counter())
         gen._stage_obs(obs)
+        gen._stage_masks()
         sync(); t.append(time.perf_counter())
         for k, a, b in zip(ph, t[:-1], t[1:]):
             ph[k].append(b - a)
