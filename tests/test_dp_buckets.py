@@ -42,3 +42,52 @@ def test_no_bucket_layout_for_mlp_policies():
     torch.manual_seed(0)
     pol = ActorCritic(SyntheticVecEnv(2, "cartpole", seed=0))
     assert nature_cnn_buckets(pol, FlatParams(pol, torch.device("cpu"))) is None
+
+
+def test_trigger_hook_fires_from_another_thread():
+    """Autograd runs CUDA backward nodes on its per-device worker thread, not on the thread that
+    armed the buckets: the trigger hook is process-wide (a thread-local hook never fired there and
+    every bucket waited for finish())."""
+    import threading
+
+    from rl_algo_impls_amd import dp_buckets
+
+    seen = []
+    p = torch.zeros(3)
+    dp_buckets._hooks.cb = seen.append
+    try:
+        th = threading.Thread(target=notify_grad_written, args=(p,))
+        th.start()
+        th.join()
+    finally:
+        dp_buckets._hooks.cb = None
+    assert len(seen) == 1 and seen[0] is p
+    notify_grad_written(p)  # disarmed: nothing
+    assert len(seen) == 1
+
+
+def test_deferred_weight_gradient_accumulates():
+    """cnn_ops.direct_grads: the convolution weight gradients queued during the backward are added
+    by one multi-tensor add at the context's exit, in place into the (flat-buffer) .grad views; a
+    backward that runs after the context has closed adds its own at once; an exception inside the
+    context drops the queue."""
+    from rl_algo_impls_amd import cnn_ops
+
+    w1, w2 = torch.zeros(2, 3, requires_grad=True), torch.zeros(4, requires_grad=True)
+    w1.grad, w2.grad = torch.ones(2, 3), torch.ones(4)
+    with cnn_ops.direct_grads(True):
+        pending = cnn_ops._state.pending
+        pending.add(w1, torch.full((2, 3), 2.0))
+        pending.add(w2, torch.full((4,), 3.0))
+        assert torch.equal(w1.grad, torch.ones(2, 3))  # nothing added before the exit
+    assert torch.equal(w1.grad, torch.full((2, 3), 3.0)) and torch.equal(w2.grad, torch.full((4,), 4.0))
+    pending.add(w2, torch.full((4,), 1.0))  # closed: immediate
+    assert torch.equal(w2.grad, torch.full((4,), 5.0))
+    try:
+        with cnn_ops.direct_grads(True):
+            cnn_ops._state.pending.add(w2, torch.full((4,), 100.0))
+            raise RuntimeError("backward failed")
+    except RuntimeError:
+        pass
+    assert torch.equal(w2.grad, torch.full((4,), 5.0))
+    assert getattr(cnn_ops._state, "pending", None) is None and not getattr(cnn_ops._state, "direct", False)
