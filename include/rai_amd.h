@@ -294,6 +294,7 @@ typedef struct rai_minibatch_desc {
   int64_t mb;           /* next minibatch, advanced on device */
   int32_t n_fields;
   int32_t arrivals;     /* rai_gather_minibatch_next's block-arrival counter; 0 between launches */
+  int32_t group_arrivals[8 * 16]; /* its per-group counters (8 groups, 64 B apart); 0 between launches */
 } rai_minibatch_desc;
 int rai_gather_minibatch(const rai_minibatch_desc* desc, int32_t n_fields, void* const* dst,
                          const int64_t* row_bytes, int64_t batch_size, void* stream);

@@ -66,6 +66,7 @@ class MinibatchDesc(C.Structure):
         ("mb", C.c_int64),
         ("n_fields", C.c_int32),
         ("arrivals", C.c_int32),
+        ("group_arrivals", C.c_int32 * 128),
     ]
 
 

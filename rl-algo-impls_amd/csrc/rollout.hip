@@ -155,11 +155,20 @@ __global__ __launch_bounds__(NT) void gather_minibatch_kernel(rai_minibatch_desc
     // minibatch for the next launch (which sees it across the kernel boundary) and re-arm the
     // counter.  No fences: a __threadfence() here is an L2 write-back (buffer_wbl2) right after the
     // workgroup's 28 KB of output, 256 times a launch (26.3 us per C3 minibatch with them).
+    // Two-level arrival (same-address agent atomics serialise at ~10 ns each: 256 arrivals on one
+    // counter cost ~2.4 us): workgroup w counts in group w % 8, the last of a group in the top one.
     __syncthreads();
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(&d->arrivals, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-      __hip_atomic_store(&d->arrivals, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&d->mb, mb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      const int nb = (int)gridDim.x, w = (int)blockIdx.x;
+      const int grp = w & 7, gsize = (nb - grp + 7) >> 3, ngroups = nb < 8 ? nb : 8;
+      int* cg = &d->group_arrivals[16 * grp];
+      if (__hip_atomic_fetch_add(cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+        __hip_atomic_store(cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add(&d->arrivals, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1) {
+          __hip_atomic_store(&d->arrivals, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&d->mb, mb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
   }
 }
@@ -324,6 +333,8 @@ static int gather_minibatch(rai_minibatch_desc* desc, int32_t n_fields, void* co
   if (blocks > batch_size) blocks = batch_size;
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
+  // (two rows per workgroup measured 23.7 us per C3 minibatch, two and four workgroups per row
+  // 21.9 / 25.9 us, against 19.3 us for one workgroup per row: tools/gather_bench.py, profiles/r2zi_*)
   if (wide)
     hipLaunchKernelGGL(gather_minibatch_kernel<1024>, dim3((unsigned)blocks), dim3(1024), 0, rai_stream(stream), desc,
                        o, advance);

@@ -458,6 +458,7 @@ def test_gather_minibatch_frame_transform(C, H, W, n, B):
     torch.cuda.synchronize()
     d = _lib.MinibatchDesc.from_buffer_copy(bytes(gu.desc.cpu().numpy()))
     assert d.mb == (n + B - 1) // B and d.arrivals == 0
+    assert all(v == 0 for v in d.group_arrivals)  # the two-level arrival's group counters, re-armed
 
 
 def test_gather_minibatch_transform_rejects_bad_shapes():
