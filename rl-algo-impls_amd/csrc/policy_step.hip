@@ -87,17 +87,44 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// A network's weights, fetched into registers (every load issued before any LDS store: one global
+// round trip for the staging instead of one per element of a load -> ds_write loop), then stored.
 template <int INP>
-__device__ __forceinline__ void load_net(const NetPtrs& p, NetSmem<INP>& S, int IN, int tid) {
-  for (int e = tid; e < HID * INP; e += NT) {
-    const int j = e / INP, k = e % INP;
-    S.W1[j][k] = k < IN ? p.W1[j * IN + k] : 0.f;
+struct NetRegs {
+  static constexpr int W2PT = HID * HID / NT;             // 16 floats of W2 per thread
+  static constexpr int W1PT = (HID * INP + NT - 1) / NT;  // 1 (INP 4) or 2 (INP 8)
+  float w2[W2PT], w1[W1PT], b1, b2;
+};
+template <int INP>
+__device__ __forceinline__ NetRegs<INP> fetch_net(const NetPtrs& p, int IN, int tid) {
+  NetRegs<INP> r;
+#pragma unroll
+  for (int u = 0; u < NetRegs<INP>::W2PT; ++u) r.w2[u] = p.W2[tid + u * NT];
+#pragma unroll
+  for (int u = 0; u < NetRegs<INP>::W1PT; ++u) {
+    const int e = tid + u * NT, j = e / INP, k = e % INP;
+    r.w1[u] = (e < HID * INP && k < IN) ? p.W1[j * IN + k] : 0.f;
+  }
+  r.b1 = tid < HID ? p.b1[tid] : 0.f;
+  r.b2 = tid < HID ? p.b2[tid] : 0.f;
+  return r;
+}
+template <int INP>
+__device__ __forceinline__ void store_net(const NetRegs<INP>& r, NetSmem<INP>& S, int tid) {
+#pragma unroll
+  for (int u = 0; u < NetRegs<INP>::W2PT; ++u) {
+    const int e = tid + u * NT;
+    S.W2[e >> 6][e & 63] = r.w2[u];
+  }
+#pragma unroll
+  for (int u = 0; u < NetRegs<INP>::W1PT; ++u) {
+    const int e = tid + u * NT;
+    if (e < HID * INP) S.W1[e / INP][e % INP] = r.w1[u];
   }
   if (tid < HID) {
-    S.b1[tid] = p.b1[tid];
-    S.b2[tid] = p.b2[tid];
+    S.b1[tid] = r.b1;
+    S.b2[tid] = r.b2;
   }
-  for (int e = tid; e < HID * HID; e += NT) S.W2[e >> 6][e & 63] = p.W2[e];
 }
 
 // hidden activations h2[t][r] (row 4g + r of the wave's tile, column 16t + li) of one network
@@ -151,16 +178,40 @@ __global__ __launch_bounds__(NT) void mlp_policy_step_kernel(const StepArgs a) {
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
   const bool sample = a.actions != nullptr;
 
-  if (sample) load_net<INP>(a.pi, S.n[0], IN, tid);
-  load_net<INP>(a.v, S.n[1], IN, tid);
-  for (int e = tid; e < OUTP * HID; e += NT) S.W3a[e >> 6][e & 63] = (sample && (e >> 6) < NA) ? a.pi.W3[e] : 0.f;
-  if (tid < HID) S.W3v[tid] = a.v.W3[tid];
-  if (tid < 8) S.b3a[tid] = (sample && tid < NA) ? a.pi.b3[tid] : 0.f;
-  if (tid == 0) S.b3v = a.v.b3[0];
-  for (int e = tid; e < ROWS * INP; e += NT) {
-    const int r = e / INP, k = e % INP;
+  // every staging load of the launch in flight together: both networks, the output layers, the rows
+  const NetRegs<INP> rv = fetch_net<INP>(a.v, IN, tid);
+  NetRegs<INP> rp;
+  if (sample) rp = fetch_net<INP>(a.pi, IN, tid);
+  constexpr int W3PT = (OUTP * HID + NT - 1) / NT, XPT = (ROWS * INP + NT - 1) / NT;
+  float w3a[W3PT], xv[XPT];
+#pragma unroll
+  for (int u = 0; u < W3PT; ++u) {
+    const int e = tid + u * NT;
+    w3a[u] = (sample && e < OUTP * HID && (e >> 6) < NA) ? a.pi.W3[e] : 0.f;
+  }
+  const float w3v = tid < HID ? a.v.W3[tid] : 0.f;
+  const float b3a = (sample && tid < NA && tid < 8) ? a.pi.b3[tid] : 0.f;
+  const float b3v = tid == 0 ? a.v.b3[0] : 0.f;
+#pragma unroll
+  for (int u = 0; u < XPT; ++u) {
+    const int e = tid + u * NT, r = e / INP, k = e % INP;
     const int64_t row = row0 + r;
-    S.X[r][k] = (row < a.N && k < IN) ? a.obs[row * IN + k] : 0.f;
+    xv[u] = (e < ROWS * INP && row < a.N && k < IN) ? a.obs[row * IN + k] : 0.f;
+  }
+  store_net<INP>(rv, S.n[1], tid);
+  if (sample) store_net<INP>(rp, S.n[0], tid);
+#pragma unroll
+  for (int u = 0; u < W3PT; ++u) {
+    const int e = tid + u * NT;
+    if (e < OUTP * HID) S.W3a[e >> 6][e & 63] = w3a[u];
+  }
+  if (tid < HID) S.W3v[tid] = w3v;
+  if (tid < 8) S.b3a[tid] = b3a;
+  if (tid == 0) S.b3v = b3v;
+#pragma unroll
+  for (int u = 0; u < XPT; ++u) {
+    const int e = tid + u * NT;
+    if (e < ROWS * INP) S.X[e / INP][e % INP] = xv[u];
   }
   __syncthreads();
 

@@ -379,11 +379,19 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         self.values[s].copy_(v)
 
     def _layer_ptrs(self):
-        ps = [p.detach() for p in self.policy.parameters()]
+        """The two networks' six weight / bias pointers as ctypes arrays, rebuilt only when a
+        parameter's storage moved (the flat-buffer views keep theirs across updates)."""
+        ps = list(self.policy.parameters())
+        key = tuple(p.data_ptr() for p in ps)
+        cached = getattr(self, "_ptrs_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
         for p in ps:
             assert p.is_contiguous() and p.dtype == torch.float32
         arr = lambda xs: (C.c_void_p * 6)(*[x.data_ptr() for x in xs])
-        return arr(ps[:6]), arr(ps[6:12])
+        out = (arr(ps[:6]), arr(ps[6:12]))
+        self._ptrs_cache = (key, out)
+        return out
 
     def _fused_step(self, s: Optional[int]) -> None:
         """Actor + critic forward, sample and slot writes for env step s (s None: bootstrap values

@@ -62,7 +62,10 @@ with torch.no_grad():
         sync(); t.append(time.perf_counter())
         if gen.action_masks is not None:
             gen.action_masks[s_].copy_(gen.next_masks_dev)
-        if gen.gridnet:  # forward graph + GridNet sample in one phase, nothing in "sample"
+        if gen.fused_step is not None:  # CartPole class: forward + sample in one launch
+            gen._fused_step(s_)
+            sync(); t.append(time.perf_counter())
+        elif gen.gridnet:  # forward graph + GridNet sample in one phase, nothing in "sample"
             gen._gridnet_step(s_)
             sync(); t.append(time.perf_counter())
         else:
