@@ -107,7 +107,8 @@ class FlatOptimizer:
         self.param_groups = [dict(lr=lr)]
         self.step_count = 0
         self.hp_dev = torch.empty(C.sizeof(_lib.OptimHparams), dtype=torch.uint8, device=dev)
-        self.workspace = torch.empty(int(_lib.lib().rai_optim_workspace_bytes(flat.P)), dtype=torch.uint8,
+        # zero-filled once: the one-launch clip + Adam keeps monotonic arrival counters in it
+        self.workspace = torch.zeros(int(_lib.lib().rai_optim_workspace_bytes(flat.P)), dtype=torch.uint8,
                                      device=dev)
         self.sync_hparams()
 

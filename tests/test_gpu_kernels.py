@@ -235,6 +235,42 @@ def test_clip_adam_matches_torch_over_steps():
         assert sd["state"][0]["step"].item() == 5.0
 
 
+@pytest.mark.parametrize("P", [9155, 143_367, 1_690_003, 3_000_001])
+@pytest.mark.parametrize("kind", [0, 1])
+def test_clip_optim_one_launch_bit_identical_to_two_launch(P, kind, monkeypatch):
+    """The one-launch clip + Adam / RMSprop (in-kernel arrival barrier) against the two-launch form
+    (RAI_OPTIM_FUSED=0) over steps: parameters, both moments, the grad norms and the step counter
+    bitwise equal.  P: C2-sized, C4-sized, C3-sized (4 float4 per thread, scalar tail) and one past
+    the register budget (falls back to two launches)."""
+    from rl_algo_impls_amd.optim import FlatOptimizer, FlatParams
+
+    torch.manual_seed(1)
+    init = torch.randn(P)
+    runs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("RAI_OPTIM_FUSED", fused)
+        mod = torch.nn.ParameterList([torch.nn.Parameter(init.clone())]).to(DEV)
+        flat = FlatParams(mod, DEV)
+        opt = FlatOptimizer(flat, kind, lr=1e-3, eps=1e-7, max_grad_norm=0.5)
+        blocks = DeviceBlocks(DEV)
+        blocks.ensure_tables(1, 8)
+        blocks.upload(make_hparams(loss_kind=0, K=1), 0)
+        g = torch.Generator().manual_seed(7)
+        for step in range(6):
+            flat.grad.copy_((torch.randn(P, generator=g) * (0.01 if step % 2 else 3)).to(DEV))
+            opt.step(blocks.state, blocks.norms)
+        torch.cuda.synchronize()
+        st = blocks.state.cpu()
+        assert int(st[20:24].view(torch.int32)[0]) == 0  # no expired arrival wait
+        assert int(st[0:8].view(torch.int64)[0]) == 6
+        runs.append((flat.flat.cpu(), opt.state1.cpu(), None if opt.state2 is None else opt.state2.cpu(),
+                     blocks.norms[:6].cpu()))
+        assert float(flat.grad.abs().max()) == 0.0
+    for a, b in zip(runs[0], runs[1]):
+        if a is not None:
+            assert torch.equal(a, b)
+
+
 def test_optimizer_state_dict_loads_into_torch_adam():
     from rl_algo_impls_amd.optim import FlatOptimizer, FlatParams
 
