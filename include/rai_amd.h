@@ -256,9 +256,9 @@ int rai_ppo_loss(const float* new_logp, const float* entropy, int64_t n_entropy,
  * The total grad norm (pre-clip) is written to norms[state->norm_index++].
  * state->opt_step is incremented on device (bias corrections use it).
  * The workspace (rai_optim_workspace_bytes) must be zero-filled before its
- * first use and then serve one parameter buffer (fixed P): the one-launch form
- * keeps monotonic arrival counters in it.  RAI_OPTIM_FUSED=0 selects the
- * two-launch form (bit-identical results).
+ * first use and then serve one parameter buffer (fixed P): the opt-in
+ * one-launch form (RAI_OPTIM_FUSED=1, bit-identical results) keeps monotonic
+ * arrival counters in it.
  * ------------------------------------------------------------------------ */
 int64_t rai_optim_workspace_bytes(int64_t P);
 int rai_clip_optim_step(float* params, float* grads, float* state1, float* state2, int64_t P,

@@ -14,7 +14,7 @@
 //   K1 per-block partial sum of squares (fp64) -> workspace
 //   K2 every block re-reduces the partials in the same fixed order (identical
 //      result in every block), then scales, updates, and zeroes its slice.
-// One-launch form (clip_optim_fused_kernel, the default where it applies): the
+// One-launch form (clip_optim_fused_kernel, opt-in, RAI_OPTIM_FUSED=1): the
 // same two reductions around an in-kernel arrival barrier, bit-identical.
 // The step counter and grad-norm slot live in device memory (rai_train_state)
 // so a captured graph replays correctly.
@@ -162,13 +162,13 @@ __global__ __launch_bounds__(OPT_THREADS) void clip_optim_kernel(
   }
 }
 
-// One-launch form (the default when the buffers are 16-B aligned and every thread holds at most
+// One-launch form (opt-in; applies when the buffers are 16-B aligned and every thread holds at most
 // OPT_FUSED_K float4 of the gradient): each workgroup loads its float4s of g ONCE into registers,
 // forms the same per-thread / per-block fp64 partial as grad_sumsq_kernel (same element sets, same
 // summation order, same block count), publishes it write-through and arrives on two-level counters;
 // once every workgroup has arrived, each re-reduces the partials exactly as clip_optim_kernel does
 // and updates its register-held elements.  Results are bit-identical to the two-launch form; it saves
-// a launch and the second read of g (C4: sum of squares 4.7 + clip + Adam 5.6 us per minibatch).
+// a launch and the second read of g, but not time (see opt_fused_enabled).
 // The barrier needs every workgroup resident: the grid is at most OPT_MAX_BLOCKS = 2 per CU, and the
 // wait is bounded (state->err on expiry).  Counters are monotonic (u64, zero-filled workspace): a
 // workgroup's arrival value fixes its launch's generation, so no re-arming race.
@@ -339,9 +339,13 @@ extern "C" int64_t rai_optim_workspace_bytes(int64_t /*P*/) {
   return (int64_t)OPT_MAX_BLOCKS * sizeof(double) + OPT_CTR_BYTES;
 }
 
-static bool opt_fused_enabled() {  // RAI_OPTIM_FUSED=0 selects the two-launch form (A/B, parity tests)
+// RAI_OPTIM_FUSED=1 selects the one-launch form.  Off by default: measured no faster (C4: 9.93 us
+// against 4.7 + 5.6 us per minibatch, whole update 42.4k vs 43.3k env-steps/s; C3 137.6k vs 138.9k,
+// profiles/r2zs_optim_ab.txt): the in-kernel barrier (write-through publish, two arrival levels,
+// cross-XCD polling) costs what the launch boundary it replaces did.
+static bool opt_fused_enabled() {
   const char* e = getenv("RAI_OPTIM_FUSED");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 extern "C" int rai_clip_optim_step(float* params, float* grads, float* state1, float* state2,

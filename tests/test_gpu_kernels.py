@@ -238,8 +238,8 @@ def test_clip_adam_matches_torch_over_steps():
 @pytest.mark.parametrize("P", [9155, 143_367, 1_690_003, 3_000_001])
 @pytest.mark.parametrize("kind", [0, 1])
 def test_clip_optim_one_launch_bit_identical_to_two_launch(P, kind, monkeypatch):
-    """The one-launch clip + Adam / RMSprop (in-kernel arrival barrier) against the two-launch form
-    (RAI_OPTIM_FUSED=0) over steps: parameters, both moments, the grad norms and the step counter
+    """The one-launch clip + Adam / RMSprop (RAI_OPTIM_FUSED=1, in-kernel arrival barrier) against the
+    two-launch default (RAI_OPTIM_FUSED=0) over steps: parameters, both moments, the grad norms and the step counter
     bitwise equal.  P: C2-sized, C4-sized, C3-sized (4 float4 per thread, scalar tail) and one past
     the register budget (falls back to two launches)."""
     from rl_algo_impls_amd.optim import FlatOptimizer, FlatParams
