@@ -51,8 +51,8 @@ constexpr int M8_CNT2 = 2;
 // scratch (workspace) layout, bytes (sized for M8_GMAX; smaller G use a prefix of each region)
 constexpr int64_t M8_S1_BYTES = 2LL * 2 * M8_GMAX * WL_N * sizeof(float);  // [net][par][c][WL_N] partials
 constexpr int64_t M8_S2_OFF = M8_S1_BYTES;                                  // [net][par][WL_N] summed gradient
-constexpr int64_t M8_SQ_OFF = M8_S2_OFF + 2LL * 2 * WL_N * sizeof(float);   // [par][net][c] share |g|^2 (f64)
-constexpr int64_t M8_SCRATCH = M8_SQ_OFF + 2LL * 2 * M8_GMAX * sizeof(double);
+constexpr int64_t M8_SQ_OFF = M8_S2_OFF + 2LL * 2 * WL_N * sizeof(float);   // [par][net][c][wave] share |g|^2 (f64)
+constexpr int64_t M8_SCRATCH = M8_SQ_OFF + 2LL * 2 * M8_GMAX * M8_NW * sizeof(double);
 static_assert(2 * XDP_MAXW * M8_GMAX * 8 <= XDP_TEST_OFF, "xdp share flags");
 
 template <int OUTP, int G>
@@ -657,16 +657,18 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         for (int q = 0; q < 4; ++q) ss = __builtin_fma((double)s[q], (double)s[q], ss);
       }
       ss = wave_sum_v(ss);
-      if (lane == 0) S.st[0][w] = ss;  // (stats already published: reuse as scratch)
+      // each wave publishes its part of the share norm with the share itself, in the same drain (the
+      // readers add the four parts in wave order: the CU's norm is ((w0 + w1) + w2) + w3 as before,
+      // but without a second store -> drain round trip after a workgroup barrier)
+      if (lane == 0) {
+        const int so = (int)M8_SQ_OFF + (((par * 2 + net) * G + c) * M8_NW + w) * (int)sizeof(double);
+        const u4v pk = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){ss, 0.0});
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_shufflevector(pk, pk, 0, 1), srs, so, 0, 16);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (tid == 0) {
-      const double sq = ((S.st[0][0] + S.st[0][1]) + S.st[0][2]) + S.st[0][3];
-      const int so = (int)M8_SQ_OFF + ((par * 2 + net) * G + c) * (int)sizeof(double);
-      const u4v pk = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){sq, 0.0});
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_shufflevector(pk, pk, 0, 1), srs, so, 0, 16);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(&sync[M8_CNT2 + net], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!m8_wait2(sync, M8_CNT2, M8_CNT2 + 1, (unsigned long long)G * (mb + 1), MC_WAIT_LOCAL)) {
         atomicExch(a.err, 1);
@@ -686,13 +688,17 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         const int chl = min(tid + M8_NT * i, WL_CH - 1);
         gr[i] = as_f4(__builtin_amdgcn_raw_buffer_load_b128(srs, gbase + 16 * chl, 0, 16));
       }
-      // the 2G share norms (net-major, CU order), lane l holding number l; fixed-order wave sum
+      // the 2G share norms (net-major, CU order), lane l holding number l (its four wave parts added in
+      // wave order); fixed-order wave sum
+      static_assert(M8_NW == 4, "four wave parts per share norm");
       const int lq = min(lane, 2 * G - 1);
-      const auto d2 = __builtin_bit_cast(
-          double __attribute__((ext_vector_type(2))),
-          __builtin_amdgcn_raw_buffer_load_b128(
-              srs, (int)M8_SQ_OFF + (par * 2 * G + (lq & ~1)) * (int)sizeof(double), 0, 16));
-      const double tot = wave_sum_v(lane < 2 * G ? ((lq & 1) ? d2[1] : d2[0]) : 0.0);
+      const int sqo = (int)M8_SQ_OFF + (par * 2 * G + lq) * M8_NW * (int)sizeof(double);
+      const auto d2a = __builtin_bit_cast(double __attribute__((ext_vector_type(2))),
+                                          __builtin_amdgcn_raw_buffer_load_b128(srs, sqo, 0, 16));
+      const auto d2b = __builtin_bit_cast(double __attribute__((ext_vector_type(2))),
+                                          __builtin_amdgcn_raw_buffer_load_b128(srs, sqo + 16, 0, 16));
+      const double sq = ((d2a[0] + d2a[1]) + d2b[0]) + d2b[1];
+      const double tot = wave_sum_v(lane < 2 * G ? sq : 0.0);
       const float total_norm = (float)sqrt(tot);
       float coef = 1.f;
       if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
