@@ -592,6 +592,13 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
     __syncthreads();
     if (S.bail) break;
     STAMP(6);
+    // this step's Adam bias corrections (fp64 sqrt / divide) off the gradient's critical path: formed
+    // while the shares are summed and exchanged, used after the round-2 wait
+    pw1 *= beta1_d;
+    pw2 *= beta2_d;
+    const float inv_bc2_sqrt = 1.f / (float)sqrt(1.0 - pw2);
+    const float neg_step = (float)(-((double)lr / (1.0 - pw1)));
+    const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
     {
       RELANE();
       const int ch = c * SH + tid;
@@ -702,11 +709,6 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       const float total_norm = (float)sqrt(tot);
       float coef = 1.f;
       if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
-      pw1 *= beta1_d;
-      pw2 *= beta2_d;
-      const float inv_bc2_sqrt = 1.f / (float)sqrt(1.0 - pw2);
-      const float neg_step = (float)(-((double)lr / (1.0 - pw1)));
-      const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
 #pragma unroll
       for (int i = 0; i < MC_CPT; ++i) {
         const int ch = tid + M8_NT * i;
