@@ -7,11 +7,15 @@ n_epochs x minibatches of fused loss / backward / clip+Adam — exactly the regi
 the reference times as train/steps_per_second (rl_algo_impls/ppo/ppo.py:221,422-427).
 
     python bench.py [--gpus N --steps K --warmup W] [--config cartpole|pong|halfcheetah|microrts]
-                    [--batch-policy yaml|scaled]
+                    [--batch-policy yaml|scaled] [--env-partition split|per-rank] [--dp-batch global|per-rank]
 
-Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), each rank
-owns its own env group of num_envs envs and its own HBM rollout; gradients are
-all-reduced (RCCL) once per optimizer step.  Rank 0 prints ONE JSON line.
+Multi-GPU: one process per GPU (torch.distributed.run).  Default = SURVEY.md 8(d)/8(e): the config's
+num_envs is the GLOBAL env count, split over the ranks (rank r owns envs [r N/R, (r+1) N/R) with its
+own HBM rollout and local GAE), and every optimizer step's global minibatch is the YAML batch_size
+(batch_size / R rows per rank), so the update is the single-process update and the total work is
+fixed as R grows ("scaling": "strong").  --env-partition per-rank gives every rank num_envs envs
+(weak scaling).  Gradients are exchanged once per optimizer step (in-kernel over xGMI for the
+CartPole-class epoch kernel, RCCL otherwise).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -72,11 +76,15 @@ def parse():
     p.add_argument("--config", default="cartpole", choices=sorted(CONFIGS))
     p.add_argument("--batch-policy", default="yaml", choices=["yaml", "scaled"],
                    help="yaml: the YAML batch_size; scaled: batch = T*N/4 (4 minibatches/epoch)")
-    p.add_argument("--dp-batch", default="per-rank", choices=["per-rank", "global"],
-                   help="data-parallel minibatch rule, the same for every config: per-rank = every rank "
-                        "takes batch_size rows of its own rollout per optimizer step (global minibatch "
-                        "batch_size x world; weak scaling); global = SURVEY 8(e): batch_size / world rows "
-                        "per rank, so the global minibatch is the YAML batch_size")
+    p.add_argument("--dp-batch", default="global", choices=["global", "per-rank"],
+                   help="data-parallel minibatch rule, the same for every config: global (default) = SURVEY "
+                        "8(e): batch_size / world rows per rank, so the global minibatch is the YAML batch_size "
+                        "and the update equals the single-process one; per-rank = every rank takes batch_size "
+                        "rows of its own rollout per optimizer step (global minibatch batch_size x world)")
+    p.add_argument("--env-partition", default="split", choices=["split", "per-rank"],
+                   help="split (default) = SURVEY 8(d): the config's num_envs is global, each rank owns "
+                        "num_envs / world of them (total work fixed: strong scaling); per-rank = every rank "
+                        "owns num_envs envs (per-GPU work fixed: weak scaling)")
     p.add_argument("--deterministic", type=int, default=0, choices=[0, 1],
                    help="1: torch.use_deterministic_algorithms + MIOpen deterministic solvers (the reference's "
                         "set_device_optimizations default, rl_algo_impls/runner/running_utils.py:161-166); off by "
@@ -147,7 +155,10 @@ def cpu_baseline(args, N: int, T: int, algo_kw: dict) -> dict:
     sys.path.insert(0, str(ROOT / "oracle"))
     import cpu_trainer  # checker/baseline only
 
-    torch.set_num_threads(min(os.cpu_count() or 1, 16))  # the box's CPU share (16 per GPU)
+    # the host cores this process may use: the GPU box grants 16 threads per GPU (its OMP_NUM_THREADS /
+    # MAX_JOBS are 16), while os.cpu_count() reports the whole machine's CPUs, most of them not ours
+    share = int(os.environ.get("OMP_NUM_THREADS") or 16)
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, share)))
     kw = dict(n_steps=T, batch_size=algo_kw["batch_size"], n_epochs=algo_kw["n_epochs"])
     res = cpu_trainer.time_update(args.cpu_baseline_seconds, num_envs=N, **kw)
     # the same sampled fraction of a whole update 32x smaller, against that update timed whole
@@ -159,6 +170,8 @@ def cpu_baseline(args, N: int, T: int, algo_kw: dict) -> dict:
     err = est_small["update_s"] / full_small["update_s"] - 1.0
     return {"value": round(res["env_steps_per_s"], 1), "unit": "env-steps/s", "cores": res["threads"],
             "kind": "port", "cpu_model": cpu_model(),
+            "cores_note": ("threads = the box's per-GPU CPU share (OMP_NUM_THREADS, 16 on the GPU box); "
+                           "os.cpu_count() = %d counts the whole machine" % (os.cpu_count() or 0)),
             "sample": (f"full rollout {T}x{N} + numpy GAE + {res['minibatches_timed']} of "
                        f"{res['minibatches_total']} minibatch steps timed, update time extrapolated "
                        f"(oracle/cpu_trainer.py, torch CPU eager like the reference)"),
@@ -234,10 +247,12 @@ def main():
     cfg = CONFIGS[args.config]
     N, T = (args.num_envs or cfg["num_envs"]), cfg["n_steps"]
     algo_kw = dict(cfg["algo"])
-    # env partition: configs[3] / configs[4] are quoted as a global env count across the node (each rank
-    # owns N / world envs); configs[1] / configs[2] are single-GPU configs (each rank owns N envs)
-    global_envs = args.config in ("halfcheetah", "microrts")
-    if global_envs and world > 1:
+    # env partition (the same rule for every config): split = SURVEY 8(d)'s "global N fixed; per-GPU
+    # N = N/R" (each rank owns N / world envs); per-rank = every rank owns N envs
+    split = args.env_partition == "split"
+    if split and world > 1:
+        if N % world:
+            raise SystemExit(f"--env-partition split: num_envs {N} not divisible by {world}")
         N = N // world
     if args.config == "microrts" and args.num_envs:  # rehearsal at fewer envs: keep the YAML's minibatches
         algo_kw["batch_size"] = max(1, algo_kw["batch_size"] * N // cfg["num_envs"])
@@ -405,14 +420,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if split else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded host VecEnv with the config's obs/action shapes; random-init policy)",
             "config": {"workload": workload,
                        "global_batch": algo.global_batch_size if algo.dp_enabled else algo.batch_size,
                        "per_rank_batch": algo.batch_size,
-                       "dp_batch": args.dp_batch, "env_partition": "split" if global_envs else "per-rank",
+                       "dp_batch": args.dp_batch, "env_partition": args.env_partition,
+                       "global_num_envs": N * world,
                        "n_epochs": algo_kw["n_epochs"], "batch_policy": args.batch_policy, "seq_len": T,
                        "deterministic": bool(args.deterministic),
                        "miopen_find_mode": bool(torch.backends.cudnn.benchmark),

@@ -255,10 +255,8 @@ int rai_ppo_loss(const float* new_logp, const float* entropy, int64_t n_entropy,
  * buffer keeps its storage so parameter .grad views stay valid).
  * The total grad norm (pre-clip) is written to norms[state->norm_index++].
  * state->opt_step is incremented on device (bias corrections use it).
- * The workspace (rai_optim_workspace_bytes) must be zero-filled before its
- * first use and then serve one parameter buffer (fixed P): the opt-in
- * one-launch form (RAI_OPTIM_FUSED=1, bit-identical results) keeps monotonic
- * arrival counters in it.
+ * The workspace (rai_optim_workspace_bytes) holds the per-block fp64
+ * partial sums of squares; it is scratch for one call at a time per stream.
  * ------------------------------------------------------------------------ */
 int64_t rai_optim_workspace_bytes(int64_t P);
 int rai_clip_optim_step(float* params, float* grads, float* state1, float* state2, int64_t P,

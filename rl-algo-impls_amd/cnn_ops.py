@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import contextlib
 import threading
+import weakref
 from typing import Dict
 
 import torch
@@ -94,27 +95,30 @@ def _direct(p: torch.Tensor, raw: bool = False) -> bool:
 class _Workspaces:
     """Zeroed per-(layer, device) workspaces of rai_bias_relu_bwd (per-workgroup partial sums and
     an arrival counter the kernel re-arms): one allocation serves every eager call and graph replay
-    of that layer."""
+    of that layer.  Keyed weakly on the layer module itself, so a workspace is freed with its layer
+    and a later module can never alias it (an id() key could be recycled after collection)."""
 
     def __init__(self):
-        self._ws: Dict[tuple, torch.Tensor] = {}
+        self._ws: "weakref.WeakKeyDictionary[torch.nn.Module, Dict[tuple, torch.Tensor]]" = \
+            weakref.WeakKeyDictionary()
 
-    def get(self, key, C: int, device) -> torch.Tensor:
-        k = (key, C, str(device))
-        ws = self._ws.get(k)
+    def get(self, module: torch.nn.Module, C: int, device) -> torch.Tensor:
+        per = self._ws.setdefault(module, {})
+        k = (C, str(device))
+        ws = per.get(k)
         if ws is None:
             # zeroed by an eager memset: one recorded into a graph capture would not run before the
             # first replay; every graphed step has eager warm-up runs that allocate it first
-            if torch.cuda.is_current_stream_capturing():
+            if torch.device(device).type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("cnn_ops: bias + ReLU workspace first requested inside a graph capture")
             n = int(_lib.lib().rai_bias_relu_workspace_bytes(C))
             ws = torch.zeros(n, dtype=torch.uint8, device=device)
-            self._ws[k] = ws
+            per[k] = ws
         return ws
 
-    def prewarm(self, key, C: int, device) -> None:
-        if not torch.cuda.is_current_stream_capturing():
-            self.get(key, C, device)
+    def prewarm(self, module: torch.nn.Module, C: int, device) -> None:
+        if torch.device(device).type != "cuda" or not torch.cuda.is_current_stream_capturing():
+            self.get(module, C, device)
 
 
 _WS = _Workspaces()
@@ -239,8 +243,8 @@ def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor, flatten: bool = False) -> 
             flatten = (conv.out_channels + 1) * hw <= _BRT_MAX_ELEMS
             if not flatten:
                 return torch.flatten(conv_relu(conv, x), 1)
-        _WS.prewarm(id(conv), conv.out_channels, x.device)
-        return ConvBiasReLU.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), id(conv),
+        _WS.prewarm(conv, conv.out_channels, x.device)
+        return ConvBiasReLU.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), conv,
                                   flatten)
     y = F.relu(conv(x))
     return torch.flatten(y, 1) if flatten else y
@@ -249,8 +253,8 @@ def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor, flatten: bool = False) -> 
 def linear_relu(lin: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
     if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and lin.bias is not None
             and lin.out_features % 4 == 0 and 256 % (lin.out_features // 4) == 0):
-        _WS.prewarm(id(lin), lin.out_features, x.device)
-        return LinearBiasReLU.apply(x.contiguous(), lin.weight, lin.bias, id(lin))
+        _WS.prewarm(lin, lin.out_features, x.device)
+        return LinearBiasReLU.apply(x.contiguous(), lin.weight, lin.bias, lin)
     return F.relu(lin(x))
 
 

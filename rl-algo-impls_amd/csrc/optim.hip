@@ -14,8 +14,6 @@
 //   K1 per-block partial sum of squares (fp64) -> workspace
 //   K2 every block re-reduces the partials in the same fixed order (identical
 //      result in every block), then scales, updates, and zeroes its slice.
-// One-launch form (clip_optim_fused_kernel, opt-in, RAI_OPTIM_FUSED=1): the
-// same two reductions around an in-kernel arrival barrier, bit-identical.
 // The step counter and grad-norm slot live in device memory (rai_train_state)
 // so a captured graph replays correctly.
 #include "common.h"
@@ -162,168 +160,6 @@ __global__ __launch_bounds__(OPT_THREADS) void clip_optim_kernel(
   }
 }
 
-// One-launch form (opt-in; applies when the buffers are 16-B aligned and every thread holds at most
-// OPT_FUSED_K float4 of the gradient): each workgroup loads its float4s of g ONCE into registers,
-// forms the same per-thread / per-block fp64 partial as grad_sumsq_kernel (same element sets, same
-// summation order, same block count), publishes it write-through and arrives on two-level counters;
-// once every workgroup has arrived, each re-reduces the partials exactly as clip_optim_kernel does
-// and updates its register-held elements.  Results are bit-identical to the two-launch form; it saves
-// a launch and the second read of g, but not time (see opt_fused_enabled).
-// The barrier needs every workgroup resident: the grid is at most OPT_MAX_BLOCKS = 2 per CU, and the
-// wait is bounded (state->err on expiry).  Counters are monotonic (u64, zero-filled workspace): a
-// workgroup's arrival value fixes its launch's generation, so no re-arming race.
-constexpr int OPT_FUSED_K = 4;
-constexpr int OPT_CTR_STRIDE = 8;  // u64 counters 64 B apart: the top one, then 8 group counters
-constexpr int64_t OPT_CTR_BYTES = 9 * OPT_CTR_STRIDE * 8;
-constexpr int OPT_SC1 = 16;  // cache-policy operand: sc1 (write-through stores, L1-bypassing loads)
-typedef unsigned int opt_u2v __attribute__((ext_vector_type(2)));
-
-__global__ __launch_bounds__(OPT_THREADS) void clip_optim_fused_kernel(
-    float* __restrict__ p, float* __restrict__ g, float* __restrict__ s1, float* __restrict__ s2,
-    int64_t P, const rai_optim_hparams* __restrict__ hpp, rai_train_state* state, double* partial,
-    unsigned long long* ctr, float* norms, int max_norms) {
-  __shared__ double red[OPT_THREADS / 64];
-  const int nb = (int)gridDim.x;
-  const int64_t stride = (int64_t)nb * OPT_THREADS;
-  const int64_t gtid = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x;
-  const int64_t nv = P / 4;
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int64_t old_step = state->opt_step;  // drained by block_sum's barrier, before the arrival
-  float4 gv[OPT_FUSED_K];
-#pragma unroll
-  for (int k = 0; k < OPT_FUSED_K; ++k) {
-    const int64_t i = gtid + k * stride;
-    gv[k] = i < nv ? g4[i] : zero;
-  }
-  const int64_t it = nv * 4 + gtid;  // the scalar tail: < 4 elements, one per thread
-  const float gt = it < P ? g[it] : 0.f;
-  double s = 0.0;
-#pragma unroll
-  for (int k = 0; k < OPT_FUSED_K; ++k)
-    if (gtid + k * stride < nv) {
-      const float4 x = gv[k];
-      s += (double)x.x * x.x + (double)x.y * x.y + (double)x.z * x.z + (double)x.w * x.w;
-    }
-  if (it < P) s += (double)gt * gt;
-  double v[1] = {s};
-  block_sum<1>(v, red);
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(partial, 0, nb * 8, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(opt_u2v, v[0]), prs, blockIdx.x * 8, 0, OPT_SC1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long grp = blockIdx.x & 7, gsize = (nb - grp + 7) >> 3, ngroups = nb < 8 ? nb : 8;
-    const unsigned long long old =
-        __hip_atomic_fetch_add(&ctr[OPT_CTR_STRIDE * (1 + grp)], 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long gen = old / gsize;
-    if (old % gsize == gsize - 1)
-      __hip_atomic_fetch_add(&ctr[0], 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long want = (gen + 1) * ngroups;
-    const unsigned long long t0 = rai_clock();
-    ok = 1;
-    while (__hip_atomic_load(&ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      if (rai_expired(t0, RAI_SPIN_LOCAL)) {
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-  if (!ok) {  // a workgroup never arrived: flag it, leave the parameters untouched
-    if (threadIdx.x == 0) __hip_atomic_store(&state->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // identical fixed-order re-reduction in every block (clip_optim_kernel's order)
-  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(partial, 0, nb * 8, 0x00020000);
-  double t = 0.0;
-  for (int i = threadIdx.x; i < nb; i += OPT_THREADS)
-    t += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(prs, i * 8, 0, OPT_SC1));
-  v[0] = t;
-  block_sum<1>(v, red);
-  const rai_optim_hparams hp = *hpp;
-  const float total_norm = (float)sqrt(v[0]);
-  float coef = 1.f;
-  if (hp.max_grad_norm > 0.f) {
-    coef = hp.max_grad_norm / (total_norm + 1e-6f);
-    coef = fminf(coef, 1.f);
-  }
-  const int64_t step = old_step + 1;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // every workgroup has read old_step (it arrived)
-    state->opt_step = step;
-    const int ni = state->norm_index;
-    if (norms && ni < max_norms) norms[ni] = total_norm;
-    state->norm_index = ni + 1;
-  }
-  float c1, c2, c3, c4;
-  if (hp.kind == 0) {
-    const double bc1 = 1.0 - ipow(hp.beta1_d, step);
-    const double bc2 = 1.0 - ipow(hp.beta2_d, step);
-    c1 = (float)(1.0 - hp.beta1_d);
-    c2 = (float)(1.0 - hp.beta2_d);
-    c3 = (float)sqrt(bc2);
-    c4 = (float)(-((double)hp.lr / bc1));
-  } else {
-    c1 = (float)(1.0 - hp.beta1_d);
-    c2 = -hp.lr;
-    c3 = c4 = 0.f;
-  }
-  const bool adam = hp.kind == 0;
-  auto upd = [&](float graw, float& pp, float& m, float& vv) {
-    const float gi = graw * coef;
-    if (adam) {
-      m = m + c1 * (gi - m);
-      vv = vv * hp.beta2;
-      vv = vv + (c2 * gi) * gi;
-      const float denom = sqrtf(vv) / c3 + hp.eps;
-      pp = pp + c4 * (m / denom);
-    } else {
-      float sq = m * hp.alpha;
-      sq = sq + (c1 * gi) * gi;
-      const float avg = sqrtf(sq) + hp.eps;
-      pp = pp + c2 * (gi / avg);
-      m = sq;
-    }
-  };
-  float4* p4 = reinterpret_cast<float4*>(p);
-  float4* gw4 = reinterpret_cast<float4*>(g);
-  float4* m4 = reinterpret_cast<float4*>(s1);
-  float4* v4 = reinterpret_cast<float4*>(s2);
-  float4 pv[OPT_FUSED_K], mv[OPT_FUSED_K], vv4[OPT_FUSED_K];
-#pragma unroll
-  for (int k = 0; k < OPT_FUSED_K; ++k) {
-    const int64_t i = gtid + k * stride;
-    if (i < nv) {
-      pv[k] = p4[i];
-      mv[k] = m4[i];
-      vv4[k] = adam ? v4[i] : zero;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < OPT_FUSED_K; ++k) {
-    const int64_t i = gtid + k * stride;
-    if (i < nv) {
-      upd(gv[k].x, pv[k].x, mv[k].x, vv4[k].x);
-      upd(gv[k].y, pv[k].y, mv[k].y, vv4[k].y);
-      upd(gv[k].z, pv[k].z, mv[k].z, vv4[k].z);
-      upd(gv[k].w, pv[k].w, mv[k].w, vv4[k].w);
-      gw4[i] = zero;
-      p4[i] = pv[k];
-      m4[i] = mv[k];
-      if (adam) v4[i] = vv4[k];
-    }
-  }
-  if (it < P) {
-    float pp = p[it], m = s1[it], vv = adam ? s2[it] : 0.f;
-    g[it] = 0.f;
-    upd(gt, pp, m, vv);
-    p[it] = pp;
-    s1[it] = m;
-    if (adam) s2[it] = vv;
-  }
-}
-
 inline int opt_blocks(int64_t P) {
   int64_t b = (P + OPT_THREADS * 8 - 1) / (OPT_THREADS * 8);
   if (b < 1) b = 1;
@@ -333,19 +169,11 @@ inline int opt_blocks(int64_t P) {
 
 }  // namespace
 
-// Partials, then the fused form's arrival counters.  The workspace must be zero-filled before its
-// first use and then belongs to one parameter buffer (fixed P, hence a fixed grid).
+// The per-block fp64 partials.  Round 2's opt-in one-launch form (an in-kernel arrival barrier
+// over every workgroup) measured no faster (profiles/r2zs_optim_ab.txt) and could leave a partial
+// step when a workgroup was held off the GPU past its bounded wait; it was removed in round 3.
 extern "C" int64_t rai_optim_workspace_bytes(int64_t /*P*/) {
-  return (int64_t)OPT_MAX_BLOCKS * sizeof(double) + OPT_CTR_BYTES;
-}
-
-// RAI_OPTIM_FUSED=1 selects the one-launch form.  Off by default: measured no faster (C4: 9.93 us
-// against 4.7 + 5.6 us per minibatch, whole update 42.4k vs 43.3k env-steps/s; C3 137.6k vs 138.9k,
-// profiles/r2zs_optim_ab.txt): the in-kernel barrier (write-through publish, two arrival levels,
-// cross-XCD polling) costs what the launch boundary it replaces did.
-static bool opt_fused_enabled() {
-  const char* e = getenv("RAI_OPTIM_FUSED");
-  return e && e[0] == '1';
+  return (int64_t)OPT_MAX_BLOCKS * sizeof(double);
 }
 
 extern "C" int rai_clip_optim_step(float* params, float* grads, float* state1, float* state2,
@@ -361,15 +189,6 @@ extern "C" int rai_clip_optim_step(float* params, float* grads, float* state1, f
   const int aligned = ((uintptr_t)grads % 16) == 0;
   const int vec = aligned && ((uintptr_t)params % 16) == 0 && ((uintptr_t)state1 % 16) == 0 &&
                   ((uintptr_t)state2 % 16) == 0;
-  const int64_t per_thread = (P / 4 + (int64_t)blocks * OPT_THREADS - 1) / ((int64_t)blocks * OPT_THREADS);
-  if (vec && per_thread <= OPT_FUSED_K && opt_fused_enabled()) {
-    unsigned long long* ctr = reinterpret_cast<unsigned long long*>(
-        reinterpret_cast<char*>(workspace) + (int64_t)OPT_MAX_BLOCKS * sizeof(double));
-    hipLaunchKernelGGL(clip_optim_fused_kernel, dim3(blocks), dim3(OPT_THREADS), 0, rai_stream(stream), params,
-                       grads, state1, state2, P, hp, state, partial, ctr, norms, max_norms);
-    RAI_LAUNCH_CHECK();
-    return RAI_OK;
-  }
   hipLaunchKernelGGL(grad_sumsq_kernel, dim3(blocks), dim3(OPT_THREADS), 0, rai_stream(stream),
                      grads, P, aligned, partial, state);
   RAI_LAUNCH_CHECK();

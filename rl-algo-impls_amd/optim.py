@@ -107,7 +107,7 @@ class FlatOptimizer:
         self.param_groups = [dict(lr=lr)]
         self.step_count = 0
         self.hp_dev = torch.empty(C.sizeof(_lib.OptimHparams), dtype=torch.uint8, device=dev)
-        # zero-filled once: the one-launch clip + Adam keeps monotonic arrival counters in it
+        # the per-block partial sums of squares between the two launches
         self.workspace = torch.zeros(int(_lib.lib().rai_optim_workspace_bytes(flat.P)), dtype=torch.uint8,
                                      device=dev)
         self.sync_hparams()

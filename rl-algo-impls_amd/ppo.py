@@ -94,6 +94,8 @@ class PPO:
         self.dp_enabled = False  # enable_data_parallel() called (any world size, incl. 1-rank rehearsal)
         self.dp_batch = "per-rank"
         self.global_batch_size = batch_size
+        self._yaml_batch_size = batch_size  # enable_data_parallel derives the per-rank size from it
+        self._buckets = None
 
     # -- data parallel (one process per GPU) ------------------------------------------------
     def enable_data_parallel(self, group=None, native_dp: bool = True, xdp: Optional[bool] = None,
@@ -121,15 +123,22 @@ class PPO:
         if dp_batch not in ("per-rank", "global"):
             raise ValueError(f"dp_batch must be 'per-rank' or 'global', not {dp_batch!r}")
         self.dp_batch = dp_batch
-        self.global_batch_size = self.batch_size * self.world
+        # idempotent: derived from the YAML batch_size every call, never from a previous division
+        yaml_bs = self._yaml_batch_size
+        self.batch_size = yaml_bs
+        self.global_batch_size = yaml_bs * self.world
         if dp_batch == "global":
-            if self.batch_size % self.world:
-                raise ValueError(f"dp_batch='global': batch_size {self.batch_size} is not divisible by the "
+            if yaml_bs % self.world:
+                raise ValueError(f"dp_batch='global': batch_size {yaml_bs} is not divisible by the "
                                  f"world size {self.world}")
-            self.global_batch_size = self.batch_size
-            self.batch_size //= self.world
+            self.global_batch_size = yaml_bs
+            self.batch_size = yaml_bs // self.world
         self._dp_comm = None
         self._xdp = None
+        # the bucketed all-reduce closes over the communicator, and the captured minibatch-step
+        # graphs over the buckets: both are rebuilt against the new communicator
+        self._buckets = None
+        self._graphed = None
         if xdp is None:
             xdp = os.environ.get("RAI_XDP", "1") != "0"
         spec = self.fused_mlp_spec()
@@ -768,7 +777,7 @@ class PPO:
         else None (one all-reduce of the whole flat gradient after the step).  RAI_DP_BUCKETS=0: off."""
         if not self.dp_enabled or self._dp_comm is None or os.environ.get("RAI_DP_BUCKETS", "1") == "0":
             return None
-        if getattr(self, "_buckets", None) is not None:
+        if self._buckets is not None:
             return self._buckets
         from .dp_buckets import GradBuckets, nature_cnn_buckets
 

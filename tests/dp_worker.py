@@ -287,6 +287,13 @@ def batch_rule_worker(rank, world, port, q):
             out[(rule, bs)] = (algo.batch_size, algo.global_batch_size, float(algo.flat.flat.double().sum()))
         except ValueError as e:
             out[(rule, bs)] = str(e)
+    # idempotent: a second call (or a switch of rule) derives from the YAML batch_size again
+    algo = PPO(nets.build("cartpole"), torch.device("cpu"), None, batch_size=256)
+    sizes = []
+    for rule in ("global", "global", "per-rank", "global"):
+        algo.enable_data_parallel(dp_batch=rule)
+        sizes.append((algo.batch_size, algo.global_batch_size))
+    out["repeat"] = sizes
     q.put((rank, out))
     import torch.distributed as dist
 
@@ -377,3 +384,63 @@ def c3_repro_worker(q, deterministic):
         torch.cuda.synchronize()
         out.append((algo.flat.flat.detach().cpu().numpy().copy(), norms.copy()))
     q.put(out)
+
+
+SPLIT_T, SPLIT_N = 16, 64
+
+
+def split_rollout_tensors(seed=21):
+    """One (T, N) CartPole-shaped rollout (inputs of GAE and the update), identical wherever it is
+    built: the env group of N envs that bench.py --env-partition split divides over the ranks."""
+    import torch
+
+    g = torch.Generator().manual_seed(seed)
+    T, N = SPLIT_T, SPLIT_N
+    return dict(obs=torch.randn(T, N, 4, generator=g), act=torch.randint(0, 2, (T, N), generator=g),
+                rew=torch.randn(T, N, generator=g), starts=(torch.rand(T, N, generator=g) < 0.05).to(torch.uint8),
+                vals=torch.randn(T, N, generator=g), logp=-0.69 + 0.05 * torch.randn(T, N, generator=g),
+                nstarts=(torch.rand(N, generator=g) < 0.05).to(torch.uint8), nvals=torch.randn(N, generator=g))
+
+
+def split_device_rollout(d, cols, dev, perm):
+    """DeviceRollout (GAE on the device) over env columns `cols` of the rollout, epoch permutation
+    `perm` every epoch."""
+    from rl_algo_impls_amd.rollout import DeviceRollout
+
+    t = lambda x: x[:, cols].contiguous().to(dev)
+    return DeviceRollout(dev, d["nstarts"][cols].contiguous().to(dev), d["nvals"][cols].contiguous().to(dev),
+                         t(d["obs"]), t(d["act"]), t(d["rew"]), t(d["starts"]), t(d["vals"]), t(d["logp"]), None,
+                         0.98, 0.8, perm_source=lambda n: perm.clone())
+
+
+SPLIT_KW = dict(batch_size=256, n_epochs=2, learning_rate=3e-3, clip_range=0.2, ent_coef=0.01, gamma=0.98,
+                gae_lambda=0.8)
+
+
+def split_worker(rank, world, port, q):
+    """bench.py --env-partition split --dp-batch global on the C2 path: rank r owns env columns
+    [r N/R, (r+1) N/R) of ONE env group, runs its own GAE on the device and takes batch_size / R rows
+    per optimizer step through the fused epoch kernel with the in-kernel exchange (identity epoch
+    permutation, so the parent can rebuild the global minibatches)."""
+    import torch
+
+    _init(rank, world, port)
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.ppo import PPO
+    import make_golden_networks as nets
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    algo = PPO(nets.build("cartpole").to(dev), dev, None, **SPLIT_KW)
+    algo.enable_data_parallel(dp_batch="global")
+    assert algo.batch_size == SPLIT_KW["batch_size"] // world and algo.fused_mlp_spec() is not None
+    n = SPLIT_N // world
+    cols = torch.arange(rank * n, (rank + 1) * n)
+    r = split_device_rollout(split_rollout_tensors(), cols, dev, torch.arange(SPLIT_T * n))
+    stats, norms, _ = algo.update(r)
+    q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms, algo._xdp is not None))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()

@@ -91,3 +91,22 @@ def test_clamp_actions_reference_vectors():
     np.testing.assert_array_equal(clamp_actions(np.array([-1.5, 0, 1.5]), space, False), np.array([-1, 0, 1]))
     space = Box(low=-3, high=2, shape=(1,))
     np.testing.assert_array_equal(clamp_actions(np.array([-1, 0, 1]), space, True), np.array([-3, -0.5, 2]))
+
+
+def test_bias_relu_workspaces_are_freed_with_their_layer():
+    """cnn_ops keys the bias + ReLU backward workspaces weakly on the layer module: one workspace per
+    (layer, channels, device), reused on every call, dropped when the layer is collected (so a later
+    layer can never alias a dead layer's workspace, as an id() key could)."""
+    import gc
+
+    from rl_algo_impls_amd import cnn_ops
+
+    ws = cnn_ops._Workspaces()
+    a, b = torch.nn.Linear(4, 8), torch.nn.Linear(4, 8)
+    wa = ws.get(a, 8, torch.device("cpu"))
+    assert ws.get(a, 8, torch.device("cpu")) is wa
+    assert ws.get(b, 8, torch.device("cpu")) is not wa
+    assert int(wa.numel()) == int(_lib.lib().rai_bias_relu_workspace_bytes(8)) and not wa.any()
+    del a
+    gc.collect()
+    assert len(ws._ws) == 1

@@ -52,4 +52,5 @@ def test_dp_batch_rules_world2():
         assert out[("per-rank", 256)][:2] == (256, 512)
         assert out[("global", 256)][:2] == (128, 256)  # B / R rows per rank
         assert "not divisible" in out[("global", 255)]
+        assert out["repeat"] == [(128, 256), (128, 256), (256, 512), (128, 256)]
     assert res[0][("global", 256)][2] == res[1][("global", 256)][2]  # identical weights after the broadcast

@@ -264,3 +264,55 @@ def test_nature_cnn_bucketed_allreduce_world1_matches_single_process():
         np.testing.assert_allclose(nb, no, rtol=1e-5)
         np.testing.assert_allclose(sb[:, :6], so[:, :6], rtol=1e-5, atol=1e-7)
         np.testing.assert_allclose(pb, po, rtol=1e-5, atol=1e-7)
+
+
+def test_env_partition_split_world2_matches_single_process_c2():
+    """bench.py's default multi-GPU rule (SURVEY.md 8(d) "global N fixed; per-GPU N = N/R" with
+    8(e)'s global minibatch): 2 ranks (gloo, both on cuda:0, in-kernel exchange) each own half the
+    env columns of ONE 16 x 64 CartPole-shaped rollout, compute their GAE on the device and take
+    128 of the 256 rows of each optimizer step.  Reference: the single-process update over the whole
+    rollout (GAE over all 64 columns) whose epoch permutation lists, for minibatch i, rank 0's rows
+    [128 i, 128 i + 128) and then rank 1's, as (t, n) of the concatenated env group."""
+    import queue
+    import time
+
+    import dp_worker
+    import make_golden_networks as nets
+    from rl_algo_impls_amd.ppo import PPO
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.split_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    deadline = time.time() + 240
+    while len(res) < 2:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"rank exited with {dead}"
+            assert time.time() < deadline, "ranks did not report in time"
+    res.sort(key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, s0, n0, x0), (_, p1, s1, n1, x1) = res
+    assert x0 and x1, "the in-kernel exchange was not used"
+    np.testing.assert_array_equal(p0, p1)
+
+    T, N, half, b = dp_worker.SPLIT_T, dp_worker.SPLIT_N, dp_worker.SPLIT_N // 2, 128
+    local = torch.arange(T * half)  # rank-local flat row -> (t, n) of the whole env group
+    to_global = [(local // half) * N + (local % half) + r * half for r in range(2)]
+    perm = torch.cat([torch.cat([to_global[0][i * b:(i + 1) * b], to_global[1][i * b:(i + 1) * b]])
+                      for i in range(T * half // b)])
+    dev = torch.device("cuda", 0)
+    r = dp_worker.split_device_rollout(dp_worker.split_rollout_tensors(), torch.arange(N), dev, perm)
+    torch.manual_seed(0)
+    algo = PPO(nets.build("cartpole").to(dev), dev, None, **dp_worker.SPLIT_KW)
+    stats, norms, _ = algo.update(r)
+    np.testing.assert_allclose(n0, norms, rtol=1e-4)
+    np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)

@@ -237,38 +237,46 @@ def test_clip_adam_matches_torch_over_steps():
 
 @pytest.mark.parametrize("P", [9155, 143_367, 1_690_003, 3_000_001])
 @pytest.mark.parametrize("kind", [0, 1])
-def test_clip_optim_one_launch_bit_identical_to_two_launch(P, kind, monkeypatch):
-    """The one-launch clip + Adam / RMSprop (RAI_OPTIM_FUSED=1, in-kernel arrival barrier) against the
-    two-launch default (RAI_OPTIM_FUSED=0) over steps: parameters, both moments, the grad norms and the step counter
-    bitwise equal.  P: C2-sized, C4-sized, C3-sized (4 float4 per thread, scalar tail) and one past
-    the register budget (falls back to two launches)."""
+def test_clip_optim_matches_torch_at_config_sizes(P, kind):
+    """clip_grad_norm_ + Adam(eps=1e-7) / RMSprop(alpha=0.99, eps=1e-5) over six steps of alternating
+    large and small gradients (clipping on and off) against torch.optim on the same device, at the
+    C2, C4 and C3 parameter counts and one past them (float4 body + scalar tail): parameters, both
+    moments and the pre-clip norms within fp32 tolerance (rl_algo_impls/ppo/ppo.py:441-447,
+    rl_algo_impls/a2c/a2c.py:45-50,202-205), and the flat gradient zeroed."""
     from rl_algo_impls_amd.optim import FlatOptimizer, FlatParams
 
     torch.manual_seed(1)
     init = torch.randn(P)
-    runs = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("RAI_OPTIM_FUSED", fused)
-        mod = torch.nn.ParameterList([torch.nn.Parameter(init.clone())]).to(DEV)
-        flat = FlatParams(mod, DEV)
-        opt = FlatOptimizer(flat, kind, lr=1e-3, eps=1e-7, max_grad_norm=0.5)
-        blocks = DeviceBlocks(DEV)
-        blocks.ensure_tables(1, 8)
-        blocks.upload(make_hparams(loss_kind=0, K=1), 0)
-        g = torch.Generator().manual_seed(7)
-        for step in range(6):
-            flat.grad.copy_((torch.randn(P, generator=g) * (0.01 if step % 2 else 3)).to(DEV))
-            opt.step(blocks.state, blocks.norms)
-        torch.cuda.synchronize()
-        st = blocks.state.cpu()
-        assert int(st[20:24].view(torch.int32)[0]) == 0  # no expired arrival wait
-        assert int(st[0:8].view(torch.int64)[0]) == 6
-        runs.append((flat.flat.cpu(), opt.state1.cpu(), None if opt.state2 is None else opt.state2.cpu(),
-                     blocks.norms[:6].cpu()))
-        assert float(flat.grad.abs().max()) == 0.0
-    for a, b in zip(runs[0], runs[1]):
-        if a is not None:
-            assert torch.equal(a, b)
+    mod = torch.nn.ParameterList([torch.nn.Parameter(init.clone())]).to(DEV)
+    flat = FlatParams(mod, DEV)
+    eps = 1e-7 if kind == 0 else 1e-5
+    opt = FlatOptimizer(flat, kind, lr=1e-3, eps=eps, max_grad_norm=0.5)
+    ref_p = torch.nn.Parameter(init.clone().to(DEV))
+    ref = (torch.optim.Adam([ref_p], lr=1e-3, eps=eps) if kind == 0 else
+           torch.optim.RMSprop([ref_p], lr=1e-3, alpha=0.99, eps=eps))
+    blocks = DeviceBlocks(DEV)
+    blocks.ensure_tables(1, 8)
+    blocks.upload(make_hparams(loss_kind=0, K=1), 0)
+    g = torch.Generator().manual_seed(7)
+    ref_norms = []
+    for step in range(6):
+        grad = (torch.randn(P, generator=g) * (0.01 if step % 2 else 3)).to(DEV)
+        flat.grad.copy_(grad)
+        opt.step(blocks.state, blocks.norms)
+        ref_p.grad = grad.clone()
+        ref_norms.append(float(torch.nn.utils.clip_grad_norm_([ref_p], 0.5)))
+        ref.step()
+    torch.cuda.synchronize()
+    assert int(blocks.state.cpu()[0:8].view(torch.int64)[0]) == 6
+    np.testing.assert_allclose(blocks.norms[:6].cpu().numpy(), ref_norms, rtol=1e-5)
+    np.testing.assert_allclose(flat.flat.cpu().numpy(), ref_p.detach().cpu().numpy(), rtol=1e-4, atol=2e-6)
+    st = ref.state[ref_p]
+    np.testing.assert_allclose(opt.state1.cpu().numpy(),
+                               (st["exp_avg"] if kind == 0 else st["square_avg"]).cpu().numpy(),
+                               rtol=1e-4, atol=1e-9)
+    if kind == 0:
+        np.testing.assert_allclose(opt.state2.cpu().numpy(), st["exp_avg_sq"].cpu().numpy(), rtol=1e-4, atol=1e-12)
+    assert float(flat.grad.abs().max()) == 0.0
 
 
 def test_optimizer_state_dict_loads_into_torch_adam():

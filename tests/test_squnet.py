@@ -240,3 +240,109 @@ def test_conv_bias_gelu_vs_pytorch(transpose):
     np.testing.assert_allclose(out.detach().cpu().numpy(), ref_out.detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
     for a, b_ in zip(got, ref):
         np.testing.assert_allclose(a.cpu().numpy(), b_.cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.fixture(scope="module")
+def case128():
+    return np.load(GOLDEN / "squnet128_case.npz", allow_pickle=False)
+
+
+def test_c5_width128_seeded_init(case128):
+    """The C5 network at its own width (channels_per_level [128]*3, critic_channels 64) initialises
+    like the reference from the same seed: per-tensor sum and sum of squares (float64 over the fp32
+    values) equal for the default-initialised layers, within 1e-6 relative for orthogonal_ ones (the
+    reference's own values at width 128 are in tests/golden/squnet128_case.npz)."""
+    seed, width, _ = (int(x) for x in case128["meta"])
+    net = _net(width, critic_channels=64, seed=seed)
+    sd = net.state_dict()
+    assert list(sd.keys()) == [str(k) for k in case128["keys"]]
+    assert sum(v.numel() for v in sd.values()) == 5458513
+    for (k, v), ref in zip(sd.items(), case128["init_moments"]):
+        got = np.array([v.double().sum().item(), (v.double() ** 2).sum().item()])
+        if k.startswith("backbone.") or k.endswith(".bias"):
+            np.testing.assert_array_equal(got, ref, err_msg=k)
+        else:
+            np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6 * np.sqrt(ref[1]), err_msg=k)
+
+
+@pytest.mark.gpu
+def test_c5_width128_forward_backward_vs_reference(case128):
+    """Forward (MIOpen channels_last backbone at 128 channels, fused GridNet head) and the autograd
+    gradients of sum(wl*logp + we*entropy + wv.v) at B=2 against the reference's CPU run of the
+    same seeded C5 network.  The fixture keeps per-tensor gradient moments, so the bounds are the
+    ones the width-16/32 element-wise tolerance (atol 2e-4 + 2e-3 max|g|) implies for them: the
+    norm within sqrt(n) times it and 1 % relative, the sum within n times it."""
+    dev = torch.device("cuda", 0)
+    seed, width, _ = (int(x) for x in case128["meta"])
+    net = _net(width, critic_channels=64, seed=seed).to(dev)
+    t = lambda k: torch.tensor(case128[k], device=dev)
+    logp, ent, v = net(t("obs"), t("actions"), action_masks=t("masks"))
+    np.testing.assert_allclose(logp.detach().cpu().numpy(), case128["logp"], rtol=1e-4, atol=2e-3)
+    np.testing.assert_allclose(ent.detach().cpu().numpy(), case128["entropy"], rtol=1e-4, atol=2e-3)
+    np.testing.assert_allclose(v.detach().cpu().numpy(), case128["v"], rtol=1e-4, atol=1e-5)
+    ((t("wl") * logp).sum() + (t("we") * ent).sum() + (t("wv") * v).sum()).backward()
+    names = [str(n) for n in case128["grad_names"]]
+    params = dict(net.named_parameters())
+    assert list(params) == names
+    for n, (rsum, rsq, rmax) in zip(names, case128["grad_moments"]):
+        g = params[n].grad.double()
+        el = 2e-4 + 2e-3 * rmax
+        norm, rnorm = float(g.norm()), float(np.sqrt(rsq))
+        assert abs(norm - rnorm) <= min(np.sqrt(g.numel()) * el, 1e-2 * rnorm + 1e-6), (n, norm, rnorm)
+        assert abs(float(g.sum()) - rsum) <= g.numel() * el, (n, float(g.sum()), rsum)
+
+
+@pytest.mark.gpu
+def test_c5_full_width_update():
+    """C5 at its own width on the product path: the squnet-d16-128 policy (5,458,513 parameters,
+    channels_last MIOpen backbone, fused GridNet head and SE epilogues), a 64-env x 24-step rollout
+    through the GridNet sampler (C5's 64 envs per GPU), then one update at the per-GPU minibatch
+    B = 768 (6,144 / 8 ranks) with the C5 hyperparameters (ppo-Microrts.yml:511-565, first schedule
+    phase): gradient accumulation, K = 3 critics, multi_reward_weights, per-critic vf_coef, vf
+    halving, 2 epochs.  Checks: finite stats and grad norms; Adam's per-step bound (|dp| <= ~lr per
+    optimizer step); most parameters move; and, under MIOpen's deterministic solvers, the update is
+    bitwise reproducible from the same weights, rollout and permutations.  (Gradient accumulation
+    runs the minibatches eagerly: there is no graph-replayed variant of this update to compare.)"""
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator
+
+    dev = torch.device("cuda", 0)
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        torch.manual_seed(1)
+        env = SyntheticVecEnv(64, kind="microrts", seed=1, obs_pool=2)
+        pol = ActorCritic(env, actor_head_style="squeeze_unet", channels_per_level=[128, 128, 128],
+                          **{k: v for k, v in C5_KW.items() if k != "init_layers_orthogonal"}).to(dev)
+        assert sum(p.numel() for p in pol.parameters()) == 5458513
+        kw = dict(batch_size=768, n_epochs=2, gamma=[0.99, 0.999, 0.999], gae_lambda=[0.95, 0.99, 0.99],
+                  clip_range=0.1, clip_range_vf=None, ppo2_vf_coef_halving=True, max_grad_norm=0.5,
+                  gradient_accumulation=True, multi_reward_weights=[0.8, 0.01, 0.19], vf_coef=[0.5, 0.1, 0.2],
+                  ent_coef=0.01, learning_rate=1e-4)
+        gen = SyncStepRolloutGenerator(pol, env, n_steps=24, seed=1)
+        r = gen.rollout(gamma=kw["gamma"], gae_lambda=kw["gae_lambda"])
+        assert tuple(r.values.shape) == (24, 64, 3) and bool(torch.isfinite(r.advantages).all())
+        p0 = torch.nn.utils.parameters_to_vector(pol.parameters()).detach().clone()
+        runs = []
+        for _ in range(2):
+            torch.nn.utils.vector_to_parameters(p0, pol.parameters())
+            algo = PPO(pol, dev, None, **kw)
+            g = torch.Generator(device="cpu").manual_seed(5)
+            r._perm_source = lambda n: torch.randperm(n, generator=g)
+            stats, norms, K = algo.update(r)
+            torch.cuda.synchronize()
+            runs.append((algo.flat.vector().detach().cpu().numpy().copy(), stats.copy(), norms.copy(),
+                         algo.optimizer.step_count, K))
+        (pa, sa, na, ca, K), (pb, sb, nb, cb, _) = runs
+        assert K == 3 and ca == cb == 2  # one optimizer step per epoch under gradient accumulation
+        assert np.isfinite(sa).all() and np.isfinite(na).all() and (na > 0).all()
+        dp = np.abs(pa - p0.cpu().numpy())
+        assert dp.max() <= 1.01 * kw["learning_rate"] * ca * 3.2
+        assert (dp > 0).mean() > 0.9
+        np.testing.assert_array_equal(pa, pb)
+        np.testing.assert_array_equal(na, nb)
+        np.testing.assert_array_equal(sa, sb)
+    finally:
+        torch.backends.cudnn.deterministic = det
