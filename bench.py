@@ -375,7 +375,23 @@ def main():
     roof_gae = {"kernel": gae_name, "bound": "hbm", "achieved": round(gae_bytes / (gae_us * 1e-6) / 1e9, 1),
                 "peak": 8000.0, "unit": "GB/s", "frac": round(gae_bytes / (gae_us * 1e-6) / 1e9 / 8000.0, 4),
                 "traffic": traffic(gae_name), "avg_us": round(gae_us, 3), "bytes_per_launch": gae_bytes}
-    if epoch_ms:
+    if epoch_ms and args.config == "halfcheetah":
+        # dominant kernel: the persistent wide-MLP epoch (rai_mlp_wide_epoch, csrc/mlp_wide_epoch.hip):
+        # one launch = every minibatch step of one epoch = T*N samples of forward+backward at SURVEY.md
+        # 8(d)'s 0.832 MFLOP/sample (HalfCheetah MLP, torch.utils.flop_counter), f32 MFMA peak
+        flops = 0.832e6 * T * N
+        ms = float(np.mean(epoch_ms))
+        tf = flops / (ms * 1e-3) / 1e12
+        head = 1  # Gaussian
+        kname = "mlp_wide_epoch_kernel<%d>" % head
+        roofline = {"kernel": kname + " (rai_mlp_wide_epoch, 16 CUs per network)", "bound": "mfma",
+                    "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
+                    "traffic": traffic(kname), "avg_ms": round(ms, 3), "flops_per_launch": flops,
+                    "launches_timed": len(epoch_ms)}
+        steps_per_launch = (T * N + algo.batch_size - 1) // algo.batch_size
+        roof_lat = {"kernel": kname, "bound": "latency", "achieved": round(ms * 1e3 / steps_per_launch, 3),
+                    "unit": "us per dependent optimizer step", "steps_per_launch": steps_per_launch}
+    elif epoch_ms:
         # dominant kernel: one fused PPO epoch per launch = T*N samples of forward+backward at
         # SURVEY.md 8(d)'s 52,352 FLOP/sample (CartPole MLP, torch.utils.flop_counter), f32 MFMA peak
         flops = 52352.0 * T * N

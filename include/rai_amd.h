@@ -467,6 +467,25 @@ int rai_mlp_wide_forward_loss(const rai_mlp_wide_desc* desc, const float* obs, c
 int rai_mlp_wide_backward(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,
                           const float* d_logp, const float* d_entropy, const float* d_v, void* workspace,
                           int64_t workspace_bytes, void* stream);
+/* One whole PPO epoch for the wide MLP actor-critic in ONE launch (persistent kernel,
+ * csrc/mlp_wide_epoch.hip): for every minibatch of batch_size (<= 64) consecutive rows of the
+ * epoch's permuted rollout copy, the forward, head log-prob / entropy, the clipped-surrogate /
+ * value / entropy loss, the backward, clip_grad_norm_ and Adam -- replaces the per-minibatch loop
+ * of rl_algo_impls/ppo/ppo.py:290-411 (forward + loss + backward + optimizer_step at :441-447).
+ * The parameters (desc->w / log_std: views of the flat buffer `params`, P floats) and the Adam
+ * moments (exp_avg / exp_avg_sq, same layout) are read at the start and written back at the end;
+ * gradients never reach HBM (desc->g is unused).  Stats rows / grad norms / state as
+ * rai_mlp_ppo_epoch (stats[0] excludes the value term: the host adds vf_coef * stats[5]).
+ * Options outside K = 1, Adam, no gradient accumulation / kl_cutoff / multi-reward weights
+ * are not covered (the caller keeps the per-minibatch path).  workspace:
+ * rai_mlp_wide_epoch_workspace_bytes (its counters are reset by the call). */
+int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden);
+int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq, int64_t P,
+                       const float* obs, const void* actions, const float* old_logp, const float* old_values,
+                       const float* advantages, const float* returns, int64_t n_rows, int32_t batch_size,
+                       const rai_ppo_hparams* hp, const rai_optim_hparams* ohp, rai_train_state* state,
+                       float* stats, int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
+                       int64_t workspace_bytes, void* stream);
 
 /* --------------------------------------------------------------------------
  * Data-parallel runtime: one process per GPU, an RCCL

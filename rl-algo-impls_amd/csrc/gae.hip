@@ -254,6 +254,95 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
   }
 }
 
+// Bandwidth regime (C >= GAE_STREAM_MIN_C columns): one thread owns 4 consecutive columns and walks
+// T backwards on its own -- 16-B loads of r and V and 16-B stores of adv and returns (the tiled
+// kernel above moves 4 B per lane per instruction), four independent carry chains per lane, and no
+// LDS or workgroup barrier.  Rows are processed in chunks of D with the next chunk's loads in
+// flight.  Per column the arithmetic and its order are the tiled kernel's (gae_delta, the select
+// coefficient, the fp64 carry), so exact mode stays bit-identical to the reference.
+constexpr int GAE_STREAM_NT = 256;
+constexpr int64_t GAE_STREAM_MIN_C = 1LL << 18;
+
+template <typename Acc, int D, bool K1>
+__global__ __launch_bounds__(GAE_STREAM_NT) void gae_stream_kernel(const GaeArgs a) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int64_t C = a.C, N = a.N, T = a.T;
+  const int64_t c0 = 4 * ((int64_t)blockIdx.x * GAE_STREAM_NT + threadIdx.x);
+  if (c0 >= C) return;
+  const int K = a.K;
+  const bool gvec = a.gamma_is_vector != 0;
+  float g32[4];
+  double g64[4];
+  Acc gl[4];
+  int64_t env[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t c = c0 + i;
+    env[i] = K1 ? c : c / K;
+    const int k = K1 ? 0 : (int)(c - env[i] * K);
+    g32[i] = a.gamma32[k];
+    g64[i] = a.gamma[k];
+    gl[i] = (sizeof(Acc) == 8) ? (Acc)a.gl[k] : (Acc)a.gl32[k];
+  }
+  const float* __restrict__ rewards = a.rewards;
+  const float* __restrict__ values = a.values;
+  const uint8_t* __restrict__ es = a.es;
+  auto load_e = [&](const uint8_t* row, uint8_t (&e)[4]) {
+    if (K1) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(row + c0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) e[i] = (uint8_t)(w >> (8 * i));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) e[i] = row[env[i]];
+    }
+  };
+  f4v vprev = *reinterpret_cast<const f4v*>(a.next_values + c0);
+  uint8_t eprev[4];
+  load_e(a.next_es, eprev);
+  Acc carry[4] = {(Acc)0, (Acc)0, (Acc)0, (Acc)0};
+  struct Chunk {
+    f4v r[D], v[D];
+    uint8_t e[D][4];
+  };
+  auto load_chunk = [&](Chunk& ch, int64_t top) {  // rows top, top - 1, ..., clamped at 0
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int64_t t = top - i < 0 ? 0 : top - i;
+      ch.r[i] = *reinterpret_cast<const f4v*>(rewards + t * C + c0);
+      ch.v[i] = *reinterpret_cast<const f4v*>(values + t * C + c0);
+      load_e(es + t * N, ch.e[i]);
+    }
+  };
+  Chunk cur, nxt;
+  load_chunk(cur, T - 1);
+  const int64_t nch = (T + D - 1) / D;
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    const int64_t top = T - 1 - ch * D;
+    if (ch + 1 < nch) load_chunk(nxt, top - D);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int64_t t = top - i;
+      if (t < 0) break;
+      f4v adv4, ret4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const Acc dl = gae_delta<Acc>(cur.r[i][q], cur.v[i][q], vprev[q], eprev[q], gvec, g32[q], g64[q]);
+        const Acc cf = eprev[q] ? (Acc)0 : gl[q];
+        carry[q] = dl + cf * carry[q];
+        adv4[q] = (float)carry[q];
+        ret4[q] = adv4[q] + cur.v[i][q];
+      }
+      *reinterpret_cast<f4v*>(a.adv + t * C + c0) = adv4;
+      if (a.ret) *reinterpret_cast<f4v*>(a.ret + t * C + c0) = ret4;
+      vprev = cur.v[i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) eprev[q] = cur.e[i][q];
+    }
+    cur = nxt;
+  }
+}
+
 }  // namespace
 
 extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t* episode_starts,
@@ -288,6 +377,34 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
     a.gamma32[k] = (float)gamma[kk];
     a.gl32[k] = (float)a.gl[k];
   }
+  hipStream_t st = rai_stream(stream);
+  // bandwidth regime: the 4-columns-per-lane streaming kernel (16-B accesses need C % 4 == 0 and
+  // 16-B aligned float buffers; the K = 1 start bytes are read 4 at a time: N % 4 == 0)
+  const bool aligned16 = ((uintptr_t)rewards | (uintptr_t)values | (uintptr_t)next_values | (uintptr_t)adv_out |
+                          (uintptr_t)(returns_out ? returns_out : adv_out)) % 16 == 0;
+  const char* sf = getenv("RAI_GAE_STREAM");  // diagnostics: 0 forces the tiled kernel
+  if (a.C >= GAE_STREAM_MIN_C && a.C % 4 == 0 && aligned16 && !(sf && sf[0] == '0')) {
+    const bool k1 = K == 1 && N % 4 == 0 && (uintptr_t)episode_starts % 4 == 0 &&
+                    (uintptr_t)next_episode_starts % 4 == 0;
+    const dim3 grid((unsigned)((a.C / 4 + GAE_STREAM_NT - 1) / GAE_STREAM_NT)), block(GAE_STREAM_NT);
+    const char* sd = getenv("RAI_GAE_STREAM_D");  // diagnostics: rows in flight per chunk (4 or 8)
+    const bool d4 = sd && sd[0] == '4';
+#define RAI_GAE_STREAM_LAUNCH(ACC, DD)                                                               \
+  do {                                                                                               \
+    if (k1) hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, true>), grid, block, 0, st, a);          \
+    else hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, false>), grid, block, 0, st, a);            \
+  } while (0)
+    if (mode == RAI_GAE_EXACT) {
+      if (d4) RAI_GAE_STREAM_LAUNCH(double, 4);
+      else RAI_GAE_STREAM_LAUNCH(double, 8);
+    } else {
+      if (d4) RAI_GAE_STREAM_LAUNCH(float, 4);
+      else RAI_GAE_STREAM_LAUNCH(float, 8);
+    }
+#undef RAI_GAE_STREAM_LAUNCH
+    RAI_LAUNCH_CHECK();
+    return RAI_OK;
+  }
   // columns per block: the widest of 64 / 32 / 16 that still gives >= 256 blocks (one per CU)
   int cols = 64;
   if (const char* f = getenv("RAI_GAE_COLS")) cols = atoi(f);  // diagnostics (tools/gae_bench.py)
@@ -295,7 +412,6 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
   if (cols != 16 && cols != 32) cols = 64;
   const int64_t blocks = (a.C + cols - 1) / cols;
   const dim3 grid((unsigned)blocks), block(GAE_WAVES * 64);
-  hipStream_t st = rai_stream(stream);
   if (mode == RAI_GAE_EXACT) {
     if (cols == 16) hipLaunchKernelGGL((gae_kernel<double, 16>), grid, block, 0, st, a);
     else if (cols == 32) hipLaunchKernelGGL((gae_kernel<double, 32>), grid, block, 0, st, a);

@@ -1,0 +1,865 @@
+// Persistent PPO epoch for wide MLP actor-critics on gfx950 (HalfCheetah class: separate
+// [in -> H -> H -> out] actor and critic, H <= 256 in 16-unit slices, Gaussian or Categorical
+// head).  ONE launch runs every minibatch step of an epoch of rl_algo_impls/ppo/ppo.py:290-411:
+// forward, head log-prob / entropy, the clipped-surrogate / value / entropy loss, the backward,
+// clip_grad_norm_ and Adam(eps) -- where the per-minibatch path (mlp_wide.hip + rai_ppo_loss +
+// rai_clip_optim_step) is a chain of 8 dependent launches per optimizer step.
+//
+// Layout: each network runs on G = H / 16 workgroups (one per CU; the grid is launched 8 G wide
+// and only blocks b % 8 == 0 (actor) / == 1 (critic) work, so each network's workgroups share one
+// XCD's L2 -- placement is a speed choice only, the hand-offs below are placement-independent).
+// Workgroup j OWNS hidden units [16 j, 16 j + 16) of both hidden layers and keeps in LDS, updated
+// by its own Adam every step: W1 rows j, b1 j, W2 rows j (for the forward), W2 columns j (for the
+// backward dH1 = dZ2 W2), b2 j, W3 columns j, and copies of b3 / log_std.  Its Adam moments live
+// in registers.  A W2 element is thus held by its row owner and its column owner; both compute its
+// gradient with the same MFMA tile code on the same operands in the same order (we_dw2_tile), so
+// the two copies stay bitwise equal.
+//
+// One optimizer step = four hand-offs through L2 (16-B write-through (sc1) stores, every storing
+// wave drained, one agent-scope arrival per workgroup on a monotonic counter, sc1 loads after the
+// poll -- MI355X_MICROARCH.md "Valid forms", row 1):
+//   A  H1[:, j] published; every workgroup of the network gathers H1 (B x H)
+//   B  output-layer partials H2[:, j] W3[:, j]^T published; every workgroup sums them in slice
+//      order and runs the head + loss for all rows (identical everywhere), then dZ2[:, j]
+//   C  dZ2[:, j] published (dW2 rows j computed while it lands); every workgroup gathers dZ2 and
+//      forms dW2 columns j, dH1[:, j], dZ1, dW1 rows j
+//   D  (both networks) each workgroup's share of the squared gradient norm; every workgroup sums
+//      the 2 G shares in a fixed order (clip_grad_norm_ over all parameters, bit-identical on every
+//      workgroup) and applies clip + Adam to what it owns.
+// Every spin is bounded and sets state->err.  Numerics: fp32 like the reference, exact-f32 MFMA
+// (v_mfma_f32_16x16x4f32), IEEE Adam as rai_clip_optim_step; parity to fp32 tolerance against the
+// per-minibatch path (tests/test_gpu_trainer.py).
+#include "common.h"
+
+namespace {
+
+constexpr int WE_NT = 256;                  // threads per workgroup (4 waves)
+constexpr int WE_SL = 16;                   // hidden units per workgroup
+constexpr int WE_B = 64;                    // max minibatch rows (4 row tiles of 16)
+constexpr int WE_HMAX = RAI_WIDE_MAX_H;     // 256
+constexpr int WE_GMAX = WE_HMAX / WE_SL;    // 16
+constexpr int WE_HP = WE_HMAX + 4;          // LDS row stride of H-long rows (16-B aligned)
+constexpr int WE_INMAX = RAI_WIDE_MAX_IN;   // 64
+constexpr int WE_XLD = WE_INMAX + 4;        // LDS row stride of obs rows
+constexpr int WE_OUTM = RAI_WIDE_MAX_OUT;   // 8
+constexpr int WE_SP = WE_SL + 1;            // padded stride of [rows][16] slices
+constexpr int WE_NSMALL = 2 * WE_SL + WE_OUTM * WE_SL + 2 * WE_OUTM;  // b1 j, b2 j, W3 cols j, b3, log_std
+constexpr int WE_SC1 = 16;                  // buffer cache policy: sc1
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+
+// workspace layout (bytes)
+constexpr int64_t WE_CTR_STRIDE = 128;                                  // one counter per 128-B line
+constexpr int64_t WE_CTR_BYTES = 8 * WE_CTR_STRIDE;                     // A0 A1 B0 B1 C0 C1 D
+constexpr int64_t WE_ACT_SLOT = (int64_t)WE_B * WE_HMAX * 4;            // one [64][H] f32 slot
+constexpr int64_t WE_H1_OFF = WE_CTR_BYTES;                             // [net][par] H1 slots
+constexpr int64_t WE_Z2_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dZ2 slots
+constexpr int64_t WE_P_SLOT = (int64_t)WE_GMAX * WE_B * WE_OUTM * 4;    // [slice][64][8] f32
+constexpr int64_t WE_P_OFF = WE_Z2_OFF + 4 * WE_ACT_SLOT;               // [net][par] partial slots
+constexpr int64_t WE_N_OFF = WE_P_OFF + 4 * WE_P_SLOT;                  // [par][net][slice] f64
+constexpr int64_t WE_WS_BYTES = WE_N_OFF + 2 * 2 * WE_GMAX * 8;
+enum { WE_CA = 0, WE_CB = 2, WE_CC = 4, WE_CD = 6 };
+
+struct WeArgs {
+  rai_mlp_wide_desc d;
+  float* params;       // flat parameter buffer (desc.w point into it)
+  float* exp_avg;      // Adam state, same layout as params
+  float* exp_avg_sq;
+  const float* obs;    // (n_rows, in) of the epoch's permuted copy
+  const void* actions; // Gaussian (n_rows, out) f32; Categorical (n_rows,) i64
+  const float* old_logp;
+  const float* old_values;
+  const float* adv;
+  const float* ret;
+  int64_t n_rows;
+  int32_t batch;
+  const rai_ppo_hparams* hp;
+  const rai_optim_hparams* ohp;
+  rai_train_state* state;
+  float* stats;
+  int32_t max_stats;
+  float* norms;
+  int32_t max_norms;
+  unsigned char* ws;
+};
+
+struct WeSmem {
+  float Act[WE_B][WE_HP];     // H1 of the minibatch (all columns), later dZ2
+  float W2r[WE_SL][WE_HP];    // W2[16 j + i][:]
+  float W2c[WE_SL][WE_HP];    // W2[:][16 j + i] (transposed)
+  float Xs[WE_B][WE_XLD];     // minibatch observations (zero-padded)
+  float W1j[WE_SL][WE_XLD];   // W1[16 j + i][:]
+  float H1j[WE_B][WE_SP];
+  float H2j[WE_B][WE_SP];
+  float Z2j[WE_B][WE_SP];
+  float Z1j[WE_B][WE_SP];
+  float dOut[WE_B][WE_OUTM];
+  float dls[WE_B][WE_OUTM];
+  float small[WE_NSMALL];     // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
+  double red[4][8];
+  float adv_mean, adv_den;
+  int bail;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t we_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float we_act(int act, float z) { return act ? fmaxf(z, 0.f) : tanhf(z); }
+__device__ __forceinline__ float we_actd(int act, float h) { return act ? (h > 0.f ? 1.f : 0.f) : (1.f - h * h); }
+
+__device__ __forceinline__ float we_vf_loss(int fn, float x) {
+#pragma clang fp contract(off)
+  if (fn == 0) return x * x;
+  const float z = fabsf(x);
+  return z < 1.f ? 0.5f * z * z : (z - 0.5f);
+}
+__device__ __forceinline__ float we_vf_grad(int fn, float x) {
+#pragma clang fp contract(off)
+  if (fn == 0) return 2.f * x;
+  return x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x);
+}
+
+// 16 x 16 tile of  Rows[16 tiles rows][k] . Cols[16][k]^T  over k in [0, H) (LDS, ld WE_HP), as
+// mlp_wide.hip's tile_dot: lane group g takes the contiguous quarter [g H/4, (g+1) H/4).
+__device__ __forceinline__ f4 we_tile_dot(const float* rows, const float* cols, int H, int lane) {
+  const int li = lane & 15, g = lane >> 4, KQ = H >> 2;
+  const float* ra = rows + li * WE_HP + g * KQ;
+  const float* cb = cols + li * WE_HP + g * KQ;
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int kk = 0; kk < KQ; kk += 4) {
+    const f4 av = *reinterpret_cast<const f4*>(ra + kk);
+    const f4 bv = *reinterpret_cast<const f4*>(cb + kk);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc1, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+
+// dW2 tile: D[i][jj] = sum over the 64 minibatch rows k of A[k][i] * Bm[k][jj], k = 4 kk + g, one
+// accumulator chain.  The row owner calls it with A = its dZ2 slice, Bm = H1 columns; the column
+// owner with A = dZ2 columns, Bm = its H1 slice: the same products in the same order, so both
+// copies of a W2 element receive the same gradient bits.
+__device__ __forceinline__ f4 we_dw2_tile(const float* A, int lda, const float* Bm, int ldb, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < WE_B / 4; ++kk) {
+    const int k = 4 * kk + g;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[k * lda + li], Bm[k * ldb + li], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void adam_ieee(float& p, float& m, float& v, float g, float c1, float c2, float beta2,
+                                          float c3, float c4, float eps) {
+#pragma clang fp contract(off)
+  m = m + c1 * (g - m);
+  v = v * beta2;
+  v = v + (c2 * g) * g;
+  const float denom = sqrtf(v) / c3 + eps;
+  p = p + c4 * (m / denom);
+}
+
+// arrive on counter `ci` after every wave's stores drained (caller: s_waitcnt vmcnt(0) in every
+// storing wave, then this); lane 0 polls until ctr[ci] >= want (and ctr[ci2] >= want2).
+__device__ __forceinline__ bool we_arrive_wait(unsigned long long* ctr, int ci, unsigned long long want, int ci2,
+                                               unsigned long long want2, rai_train_state* state, int& bail) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(&ctr[ci * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = rai_clock();
+    while (__hip_atomic_load(&ctr[ci * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want ||
+           (ci2 >= 0 &&
+            __hip_atomic_load(&ctr[ci2 * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want2)) {
+      if (rai_expired(t0, RAI_SPIN_LOCAL)) {
+        __hip_atomic_store(&state->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bail = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  return !bail;
+}
+
+template <int HEAD>  // 0 Categorical, 1 Gaussian
+__device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j) {
+  const rai_mlp_wide_desc& d = a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int H = d.hidden, G = H / WE_SL, IN = d.in_dim, IN4 = (IN + 3) & ~3;
+  const int O = net == 0 ? d.out_pi : 1;
+  const int act = d.activation;
+  const rai_ppo_hparams& hp = *a.hp;
+  const rai_optim_hparams& ohp = *a.ohp;
+  unsigned long long* ctr = reinterpret_cast<unsigned long long*>(a.ws);
+  const __amdgpu_buffer_rsrc_t wrs = we_rsrc(a.ws, WE_WS_BYTES);
+  const float* const* W = d.w[net];
+  const int64_t pbase_off = 0;
+  (void)pbase_off;
+  auto foff = [&](const float* p) -> int64_t { return p - a.params; };  // offset in the flat buffer
+
+  // ---- parameters -> LDS, Adam moments -> registers -------------------------------------------
+  for (int e = tid; e < WE_SL * WE_XLD; e += WE_NT) {
+    const int i = e / WE_XLD, k = e - i * WE_XLD;
+    S.W1j[i][k] = k < IN ? W[0][(int64_t)(WE_SL * j + i) * IN + k] : 0.f;
+  }
+  for (int e = tid; e < WE_SL * H; e += WE_NT) {
+    const int i = e / H, k = e - i * H;
+    S.W2r[i][k] = W[2][(int64_t)(WE_SL * j + i) * H + k];
+    S.W2c[i][k] = W[2][(int64_t)k * H + WE_SL * j + i];
+  }
+  // small parameters: index e -> (tensor, element) in the flat buffer (-1: padding)
+  auto small_flat = [&](int e) -> int64_t {
+    if (e < WE_SL) return foff(W[1]) + WE_SL * j + e;                         // b1
+    e -= WE_SL;
+    if (e < WE_SL) return foff(W[3]) + WE_SL * j + e;                         // b2
+    e -= WE_SL;
+    if (e < WE_OUTM * WE_SL) {                                                 // W3[o][16 j + c]
+      const int o = e / WE_SL, c = e - o * WE_SL;
+      return o < O ? foff(W[4]) + (int64_t)o * H + WE_SL * j + c : -1;
+    }
+    e -= WE_OUTM * WE_SL;
+    if (e < WE_OUTM) return e < O ? foff(W[5]) + e : -1;                     // b3
+    e -= WE_OUTM;
+    return (net == 0 && HEAD == 1 && e < O) ? foff(d.log_std) + e : -1;       // log_std
+  };
+  float m_s = 0.f, v_s = 0.f;
+  int64_t fs = -1;
+  if (tid < WE_NSMALL) {
+    fs = small_flat(tid);
+    S.small[tid] = fs >= 0 ? a.params[fs] : 0.f;
+    m_s = fs >= 0 ? a.exp_avg[fs] : 0.f;
+    v_s = fs >= 0 ? a.exp_avg_sq[fs] : 0.f;
+  }
+  // W2 row slice: wave w holds column tiles 4 w + t (t < 4) of row tile j: lane element (t, r) =
+  // W2[16 j + 4 g + r][16 (4 w + t) + li]; column slice: row tiles 4 w + t of column tile j: lane
+  // element (t, r) = W2[16 (4 w + t) + 4 g + r][16 j + li].  Tiles beyond H are inactive.
+  float m_r[4][4], v_r[4][4], m_c[4][4], v_c[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ct = 4 * w + t;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool on = ct < G;
+      const int64_t fr = foff(W[2]) + (int64_t)(WE_SL * j + 4 * g + r) * H + WE_SL * ct + li;
+      const int64_t fc = foff(W[2]) + (int64_t)(WE_SL * ct + 4 * g + r) * H + WE_SL * j + li;
+      m_r[t][r] = on ? a.exp_avg[fr] : 0.f;
+      v_r[t][r] = on ? a.exp_avg_sq[fr] : 0.f;
+      m_c[t][r] = on ? a.exp_avg[fc] : 0.f;
+      v_c[t][r] = on ? a.exp_avg_sq[fc] : 0.f;
+    }
+  }
+  // W1 rows j: wave w holds column tile w: lane element r = W1[16 j + 4 g + r][16 w + li]
+  float m_1[4], v_1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int col = WE_SL * w + li;
+    const int64_t f = foff(W[0]) + (int64_t)(WE_SL * j + 4 * g + r) * IN + col;
+    m_1[r] = col < IN ? a.exp_avg[f] : 0.f;
+    v_1[r] = col < IN ? a.exp_avg_sq[f] : 0.f;
+  }
+
+  const int B = a.batch;
+  const int64_t n_rows = a.n_rows;
+  const int nmb = (int)((n_rows + B - 1) / B);
+  const int64_t step0 = a.state->opt_step;
+  const int stat0 = a.state->stat_index;
+  const int norm0 = a.state->norm_index;
+  const float beta2 = ohp.beta2, eps = ohp.eps, lr = ohp.lr;
+  const double beta1_d = ohp.beta1_d, beta2_d = ohp.beta2_d;
+  const float c1 = (float)(1.0 - beta1_d), c2 = (float)(1.0 - beta2_d);
+  double pw1 = ipow(beta1_d, step0), pw2 = ipow(beta2_d, step0);
+  if (tid == 0) S.bail = 0;
+  __syncthreads();
+
+  for (int mb = 0; mb < nmb; ++mb) {
+    const int par = mb & 1;
+    const int64_t row0 = (int64_t)mb * B;
+    const int rows = (int)min((int64_t)B, n_rows - row0);
+    const unsigned long long want = (unsigned long long)G * (mb + 1);
+    // ---- observations of the minibatch -> LDS (zero rows / columns beyond the data) ----------
+    for (int e = tid; e < WE_B * IN4; e += WE_NT) {
+      const int r = e / IN4, k = e - r * IN4;
+      S.Xs[r][k] = (r < rows && k < IN) ? a.obs[(row0 + r) * IN + k] : 0.f;
+    }
+    lds_barrier();
+    // ============ fwd1: H1[:, j] = act(X W1[j]^T + b1[j]); wave w: row tile w =============
+    {
+      f4 z = {0.f, 0.f, 0.f, 0.f};
+      for (int kk = 0; kk < IN4 / 4; ++kk) {
+        const int k = 4 * kk + g;
+        z = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Xs[16 * w + li][k], S.W1j[li][k], z, 0, 0, 0);
+      }
+      const float bj = S.small[li];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S.H1j[16 * w + 4 * g + r][li] = we_act(act, z[r] + bj);
+    }
+    lds_barrier();
+    {  // publish H1[:, j]: row tid >> 2, columns 4 (tid & 3) ..
+      const int r = tid >> 2, q = tid & 3;
+      const f4 v = {S.H1j[r][4 * q], S.H1j[r][4 * q + 1], S.H1j[r][4 * q + 2], S.H1j[r][4 * q + 3]};
+      const int64_t off = WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT + ((int64_t)r * H + WE_SL * j + 4 * q) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), wrs, (int)off, 0, WE_SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!we_arrive_wait(ctr, WE_CA + net, want, -1, 0, a.state, S.bail)) break;
+    {  // gather H1 (B x H) -> Act
+      const int n4 = WE_B * H / 4, per_row = H / 4;
+      const int64_t base = WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
+      f4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = min(tid + WE_NT * u, n4 - 1);
+        v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)(base + 16 * (int64_t)i), 0, WE_SC1));
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = tid + WE_NT * u;
+        if (i < n4) {
+          const int r = i / per_row, c = (i - r * per_row) * 4;
+          *reinterpret_cast<f4*>(&S.Act[r][c]) = v[u];
+        }
+      }
+    }
+    lds_barrier();
+    // ============ fwd2: H2[:, j] = act(H1 W2[j]^T + b2[j]); wave w: row tile w =============
+    {
+      const f4 z = we_tile_dot(&S.Act[16 * w][0], &S.W2r[0][0], H, lane);
+      const float bj = S.small[WE_SL + li];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S.H2j[16 * w + 4 * g + r][li] = we_act(act, z[r] + bj);
+    }
+    lds_barrier();
+    {  // output-layer partials over the slice: P[row][o] = sum_c H2[row][c] W3[o][16 j + c]
+      if (tid < WE_B * 2) {
+        const int r = tid >> 1, o0 = 4 * (tid & 1);
+        f4 p = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int o = o0 + q;
+          float s = 0.f;
+          if (o < O) {
+#pragma unroll
+            for (int c = 0; c < WE_SL; ++c) s += S.H2j[r][c] * S.small[2 * WE_SL + o * WE_SL + c];
+          }
+          p[q] = s;
+        }
+        const int64_t off = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT + (((int64_t)j * WE_B + r) * WE_OUTM + o0) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, p), wrs, (int)off, 0, WE_SC1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!we_arrive_wait(ctr, WE_CB + net, want, -1, 0, a.state, S.bail)) break;
+    // ============ head + loss, all rows (identical on every workgroup of the network) ========
+    if (w == 0) {
+      const int r = lane;
+      const bool valid = r < rows;
+      const int64_t gr = row0 + (valid ? r : 0);
+      float out[WE_OUTM];
+      {
+        const int64_t base = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT;
+        f4 pa[WE_GMAX], pb[WE_GMAX];
+#pragma unroll
+        for (int s = 0; s < WE_GMAX; ++s) {
+          const int ss = min(s, G - 1);
+          const int64_t off = base + (((int64_t)ss * WE_B + r) * WE_OUTM) * 4;
+          pa[s] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)off, 0, WE_SC1));
+          pb[s] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)off + 16, 0, WE_SC1));
+        }
+#pragma unroll
+        for (int o = 0; o < WE_OUTM; ++o) {
+          float acc = 0.f;
+#pragma unroll
+          for (int s = 0; s < WE_GMAX; ++s)
+            if (s < G) acc += o < 4 ? pa[s][o] : pb[s][o - 4];
+          out[o] = o < O ? acc + S.small[2 * WE_SL + WE_OUTM * WE_SL + o] : 0.f;
+        }
+      }
+      float dout[WE_OUTM], dl[WE_OUTM];
+#pragma unroll
+      for (int o = 0; o < WE_OUTM; ++o) dout[o] = dl[o] = 0.f;
+      // statistics: [0] sum min(s1, s2) | loss, [1] sum kl | vclipped, [2] clipped, [3] entropy
+      double st[4] = {0.0, 0.0, 0.0, 0.0};
+      const float invB = 1.f / (float)rows;
+      if (net == 0) {
+#pragma clang fp contract(off)
+        // advantage moments over the minibatch (two passes, fp64 sums; ppo.py:313-316)
+        const float x = valid ? a.adv[gr] : 0.f;
+        float A = x;
+        if (hp.normalize_advantage || hp.standardize_advantage) {
+          const double s1 = wave_sum(valid ? (double)x : 0.0);
+          const float mean = (float)(s1 / (double)rows);
+          const double dv = (double)x - (double)mean;
+          const double s2 = wave_sum(valid ? dv * dv : 0.0);
+          const float den = (float)sqrt(s2 / (double)(rows - 1)) + 1e-8f;
+          A = hp.normalize_advantage ? (x - mean) / den : x / den;
+        }
+        float lp = 0.f, ent = 0.f;  // log-prob of the action, entropy (summed over dims)
+        if (HEAD == 1) {
+          const float* av = static_cast<const float*>(a.actions) + gr * O;
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o)
+            if (o < O) {
+              const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + o]);
+              const float var = scale * scale;
+              const float log_scale = logf(scale);
+              const float xo = av[o] - out[o];
+              lp += -(xo * xo) / (2.f * var) - log_scale - 0.91893853320467274f;
+              ent += 1.4189385332046727f + log_scale;
+            }
+        } else {
+          const int64_t ai = static_cast<const int64_t*>(a.actions)[gr];
+          float mx = out[0];
+#pragma unroll
+          for (int o = 1; o < WE_OUTM; ++o)
+            if (o < O) mx = fmaxf(mx, out[o]);
+          float se = 0.f;
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o)
+            if (o < O) se += expf(out[o] - mx);
+          const float lse = mx + logf(se);
+          float h = 0.f;
+          float za = out[0];
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o)
+            if (o < O) {
+              const float l = out[o] - lse;
+              h -= fmaxf(l, -3.4028234663852886e38f) * expf(l);
+              if (o == (ai >= 0 && ai < O ? ai : 0)) za = out[o];
+            }
+          lp = za - lse;
+          ent = h;
+        }
+        const float logratio = lp - a.old_logp[gr];
+        const float ratio = expf(logratio);
+        const float lo = 1.f - hp.clip_range, hi = 1.f + hp.clip_range;
+        const float cr = fminf(fmaxf(ratio, lo), hi);
+        const float s1 = ratio * A, s2 = cr * A;
+        const float g_pi = -invB;
+        float g1, g2;
+        if (s1 < s2) { g1 = g_pi; g2 = 0.f; }
+        else if (s1 > s2) { g1 = 0.f; g2 = g_pi; }
+        else { g1 = g_pi * 0.5f; g2 = g_pi * 0.5f; }
+        const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float d_logp = valid ? (g1 * A + (g2 * A) * in_clip) * ratio : 0.f;
+        const float n_ent = (float)(HEAD == 1 ? rows * O : rows);
+        const float d_ent = valid ? -hp.ent_coef / n_ent : 0.f;
+        if (HEAD == 1) {
+          const float* av = static_cast<const float*>(a.actions) + gr * O;
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o)
+            if (o < O) {
+              const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + o]);
+              const float var = scale * scale;
+              const float xo = av[o] - out[o];
+              dout[o] = d_logp * (xo / var);
+              dl[o] = d_logp * ((xo * xo) / var - 1.f) + d_ent;
+            }
+        } else {
+          const int64_t ai = static_cast<const int64_t*>(a.actions)[gr];
+          float mx = out[0];
+#pragma unroll
+          for (int o = 1; o < WE_OUTM; ++o)
+            if (o < O) mx = fmaxf(mx, out[o]);
+          float se = 0.f;
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o)
+            if (o < O) se += expf(out[o] - mx);
+          const float lse = mx + logf(se);
+          float h = 0.f;
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o)
+            if (o < O) {
+              const float l = out[o] - lse;
+              h -= l * expf(l);
+            }
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o)
+            if (o < O) {
+              const float l = out[o] - lse, p = expf(l);
+              dout[o] = d_logp * ((o == ai ? 1.f : 0.f) - p) - d_ent * p * (l + h);
+            }
+        }
+        if (valid) {
+          st[0] = (double)fminf(s1, s2);
+          st[1] = (double)((ratio - 1.f) - logratio);
+          st[2] = (fabsf(ratio - 1.f) > hp.clip_range) ? 1.0 : 0.0;
+          st[3] = (double)ent;
+        }
+      } else {
+#pragma clang fp contract(off)
+        const float v = out[0], R = a.ret[gr];
+        const float halve = hp.ppo2_vf_coef_halving ? 0.5f : 1.f;
+        const float gl = (hp.vf_coef[0] * halve) * invB;
+        const int vfn = hp.vf_loss_fn;
+        float l = we_vf_loss(vfn, v - R), dv;
+        float vcf = 0.f;
+        if (hp.has_clip_range_vf) {
+          const float vc_ = hp.clip_range_vf, vo = a.old_values[gr];
+          const float dvo = v - vo;
+          const float vcl = vo + fminf(fmaxf(dvo, -vc_), vc_);
+          const float l2 = we_vf_loss(vfn, vcl - R);
+          float w1, w2;
+          if (l > l2) { w1 = gl; w2 = 0.f; }
+          else if (l < l2) { w1 = 0.f; w2 = gl; }
+          else { w1 = gl * 0.5f; w2 = gl * 0.5f; }
+          const float inv = (dvo >= -vc_ && dvo <= vc_) ? 1.f : 0.f;
+          dv = w1 * we_vf_grad(vfn, v - R) + (w2 * we_vf_grad(vfn, vcl - R)) * inv;
+          vcf = (fabsf(v - vo) > vc_) ? 1.f : 0.f;
+          l = fmaxf(l, l2);
+        } else {
+          dv = gl * we_vf_grad(vfn, v - R);
+        }
+        dout[0] = valid ? dv : 0.f;
+        if (valid) {
+          st[0] = (double)l;
+          st[1] = (double)vcf;
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < WE_OUTM; ++o) {
+        S.dOut[r][o] = dout[o];
+        S.dls[r][o] = dl[o];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st[i] = wave_sum(st[i]);
+      if (j == 0 && lane == 0 && a.stats) {
+        const int srow = stat0 + mb;
+        if (srow < a.max_stats) {
+          float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
+          const double Bd = (double)rows;
+          if (net == 0) {
+            const float pi_loss = (float)(-st[0] / Bd);
+            const float ent_loss = (float)(-st[3] / (double)(HEAD == 1 ? rows * O : rows));
+            row[0] = pi_loss + hp.ent_coef * ent_loss;  // the host adds vf_coef * v_loss
+            row[1] = pi_loss;
+            row[2] = ent_loss;
+            row[3] = (float)(st[1] / Bd);
+            row[4] = (float)(st[2] / Bd);
+          } else {
+            row[5] = (float)(st[0] / Bd) * (hp.ppo2_vf_coef_halving ? 0.5f : 1.f);
+            row[5 + RAI_MAX_K] = hp.has_clip_range_vf ? (float)(st[1] / Bd) : 0.f;
+          }
+        }
+      }
+    }
+    lds_barrier();
+    // ============ bwd2 (local): dZ2[:, j], publish; dW2 rows j; small gradients ===============
+    {
+      const int r = tid >> 2, q = tid & 3;
+      f4 z;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = 4 * q + u;
+        float dh = 0.f;
+#pragma unroll
+        for (int o = 0; o < WE_OUTM; ++o)
+          if (o < O) dh += S.dOut[r][o] * S.small[2 * WE_SL + o * WE_SL + c];
+        z[u] = dh * we_actd(act, S.H2j[r][c]);
+        S.Z2j[r][c] = z[u];
+      }
+      const int64_t off = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT + ((int64_t)r * H + WE_SL * j + 4 * q) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, z), wrs, (int)off, 0, WE_SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    // while dZ2 lands: small-parameter gradients and dW2 rows j (H1 still in Act)
+    float g_s = 0.f;
+    if (tid < WE_NSMALL && fs >= 0) {
+      int e = tid;
+      if (e >= WE_SL) {  // b1 j is formed after dZ1 (below)
+        e -= WE_SL;
+        if (e < WE_SL) {  // db2
+          for (int r = 0; r < WE_B; ++r) g_s += S.Z2j[r][e];
+        } else if ((e -= WE_SL) < WE_OUTM * WE_SL) {  // dW3[o][16 j + c]
+          const int o = e / WE_SL, c = e - o * WE_SL;
+          for (int r = 0; r < WE_B; ++r) g_s += S.dOut[r][o] * S.H2j[r][c];
+        } else if ((e -= WE_OUTM * WE_SL) < WE_OUTM) {  // db3
+          for (int r = 0; r < WE_B; ++r) g_s += S.dOut[r][e];
+        } else {  // dlog_std
+          e -= WE_OUTM;
+          for (int r = 0; r < WE_B; ++r) g_s += S.dls[r][e];
+        }
+      }
+    }
+    f4 g_r[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ct = 4 * w + t;
+      g_r[t] = ct < G ? we_dw2_tile(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * ct], WE_HP, lane) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    // wait for every workgroup's dZ2 slice
+    if (tid == 0) {
+      const unsigned long long t0 = rai_clock();
+      while (__hip_atomic_load(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+             want) {
+        if (rai_expired(t0, RAI_SPIN_LOCAL)) {
+          __hip_atomic_store(&a.state->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          S.bail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();  // also: every wave is done reading H1 from Act
+    if (S.bail) break;
+    {  // gather dZ2 (B x H) -> Act
+      const int n4 = WE_B * H / 4, per_row = H / 4;
+      const int64_t base = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
+      f4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = min(tid + WE_NT * u, n4 - 1);
+        v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)(base + 16 * (int64_t)i), 0, WE_SC1));
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = tid + WE_NT * u;
+        if (i < n4) {
+          const int r = i / per_row, c = (i - r * per_row) * 4;
+          *reinterpret_cast<f4*>(&S.Act[r][c]) = v[u];
+        }
+      }
+    }
+    lds_barrier();
+    // ============ bwd1: dW2 columns j, dH1[:, j] -> dZ1, dW1 rows j, db1 j ====================
+    f4 g_c[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int rt = 4 * w + t;
+      g_c[t] = rt < G ? we_dw2_tile(&S.Act[0][WE_SL * rt], WE_HP, &S.H1j[0][0], WE_SP, lane) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    {
+      const f4 z = we_tile_dot(&S.Act[16 * w][0], &S.W2c[0][0], H, lane);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * w + 4 * g + r;
+        S.Z1j[row][li] = z[r] * we_actd(act, S.H1j[row][li]);
+      }
+    }
+    lds_barrier();
+    f4 g_1 = {0.f, 0.f, 0.f, 0.f};  // dW1[16 j + 4 g + r][16 w + li]
+    if (WE_SL * w < IN) {
+      const int li_c = WE_SL * w + li;
+      for (int kk = 0; kk < WE_B / 4; ++kk) {
+        const int k = 4 * kk + g;
+        g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Z1j[k][li], li_c < WE_XLD ? S.Xs[k][min(li_c, WE_XLD - 1)] : 0.f,
+                                                   g_1, 0, 0, 0);
+      }
+    }
+    if (tid < WE_SL) {
+      for (int r = 0; r < WE_B; ++r) g_s += S.Z1j[r][tid];  // db1
+    }
+    // ============ D: this workgroup's share of |g|^2, then clip_grad_norm_ + Adam =============
+    {
+      double ss = 0.0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss += (double)g_r[t][r] * (double)g_r[t][r];
+      if (WE_SL * w + li < IN) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss += (double)g_1[r] * (double)g_1[r];
+      }
+      // b3 and log_std are counted once, by workgroup 0
+      const bool count_small = tid < WE_NSMALL && fs >= 0 &&
+                               (tid < 2 * WE_SL + WE_OUTM * WE_SL || j == 0);
+      if (count_small) ss += (double)g_s * (double)g_s;
+      ss = wave_sum(ss);
+      if (lane == 0) S.red[0][w] = ss;
+      __syncthreads();
+      if (tid == 0) {
+        const double tot = ((S.red[0][0] + S.red[0][1]) + S.red[0][2]) + S.red[0][3];
+        const int64_t off = WE_N_OFF + ((int64_t)(par * 2 + net) * WE_GMAX + j) * 8;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, tot), wrs, (int)off, 0, WE_SC1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    if (!we_arrive_wait(ctr, WE_CD, 2 * want, -1, 0, a.state, S.bail)) break;
+    {
+      // the 2 G shares, net-major then slice order: lane l < 2 G loads share l; fixed-order wave sum
+      const int l = lane < 2 * G ? lane : 0;
+      const int nn = l / G, jj = l - nn * G;
+      const int64_t off = WE_N_OFF + ((int64_t)(par * 2 + nn) * WE_GMAX + jj) * 8;
+      const double sh = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wrs, (int)off, 0, WE_SC1));
+      const double tot = wave_sum(lane < 2 * G ? sh : 0.0);
+      const float total_norm = (float)sqrt(tot);
+      float coef = 1.f;
+      if (ohp.max_grad_norm > 0.f) coef = fminf(ohp.max_grad_norm / (total_norm + 1e-6f), 1.f);
+      if (net == 0 && j == 0 && tid == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;
+      pw1 *= beta1_d;
+      pw2 *= beta2_d;
+      const double bc1 = 1.0 - pw1, bc2 = 1.0 - pw2;
+      const float c3 = (float)sqrt(bc2), c4 = (float)(-((double)lr / bc1));
+      // W2 row slice
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int ct = 4 * w + t;
+        if (ct < G) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float& p = S.W2r[4 * g + r][WE_SL * ct + li];
+            float pv = p;
+            adam_ieee(pv, m_r[t][r], v_r[t][r], g_r[t][r] * coef, c1, c2, beta2, c3, c4, eps);
+            p = pv;
+          }
+        }
+      }
+      // W2 column slice (the same elements' other copy)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int rt = 4 * w + t;
+        if (rt < G) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float& p = S.W2c[li][WE_SL * rt + 4 * g + r];
+            float pv = p;
+            adam_ieee(pv, m_c[t][r], v_c[t][r], g_c[t][r] * coef, c1, c2, beta2, c3, c4, eps);
+            p = pv;
+          }
+        }
+      }
+      if (WE_SL * w + li < IN) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float& p = S.W1j[4 * g + r][WE_SL * w + li];
+          float pv = p;
+          adam_ieee(pv, m_1[r], v_1[r], g_1[r] * coef, c1, c2, beta2, c3, c4, eps);
+          p = pv;
+        }
+      }
+      if (tid < WE_NSMALL && fs >= 0) {
+        float pv = S.small[tid];
+        adam_ieee(pv, m_s, v_s, g_s * coef, c1, c2, beta2, c3, c4, eps);
+        S.small[tid] = pv;
+      }
+    }
+    lds_barrier();
+  }
+
+  // ---- write back what this workgroup owns: parameters and Adam moments ----------------------
+  if (!S.bail) {
+    for (int e = tid; e < WE_SL * IN; e += WE_NT) {
+      const int i = e / IN, k = e - i * IN;
+      a.params[foff(W[0]) + (int64_t)(WE_SL * j + i) * IN + k] = S.W1j[i][k];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = WE_SL * w + li;
+      if (col < IN) {
+        const int64_t f = foff(W[0]) + (int64_t)(WE_SL * j + 4 * g + r) * IN + col;
+        a.exp_avg[f] = m_1[r];
+        a.exp_avg_sq[f] = v_1[r];
+      }
+    }
+    for (int e = tid; e < WE_SL * H; e += WE_NT) {
+      const int i = e / H, k = e - i * H;
+      a.params[foff(W[2]) + (int64_t)(WE_SL * j + i) * H + k] = S.W2r[i][k];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ct = 4 * w + t;
+      if (ct < G) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t f = foff(W[2]) + (int64_t)(WE_SL * j + 4 * g + r) * H + WE_SL * ct + li;
+          a.exp_avg[f] = m_r[t][r];
+          a.exp_avg_sq[f] = v_r[t][r];
+        }
+      }
+    }
+    // small parameters: b3 / log_std copies are identical everywhere; workgroup 0 writes them
+    if (tid < WE_NSMALL && fs >= 0 && (tid < 2 * WE_SL + WE_OUTM * WE_SL || j == 0)) {
+      a.params[fs] = S.small[tid];
+      a.exp_avg[fs] = m_s;
+      a.exp_avg_sq[fs] = v_s;
+    }
+  }
+  if (net == 0 && j == 0 && tid == 0 && !S.bail) {
+    a.state->stat_index = stat0 + nmb;
+    a.state->opt_step = step0 + nmb;
+    a.state->norm_index = norm0 + nmb;
+  }
+}
+
+template <int HEAD>
+__global__ __launch_bounds__(WE_NT) void mlp_wide_epoch_kernel(const WeArgs a) {
+  static_assert(sizeof(WeSmem) <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[sizeof(WeSmem)];
+  const int b = blockIdx.x, grp = b & 7, j = b >> 3;
+  if (grp >= 2) return;  // two XCDs' worth of blocks work (locality, not correctness)
+  we_epoch<HEAD>(a, *reinterpret_cast<WeSmem*>(smem_raw), grp, j);
+}
+
+}  // namespace
+
+extern "C" int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden) {
+  (void)hidden;
+  return WE_WS_BYTES;
+}
+
+extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq,
+                                  int64_t P, const float* obs, const void* actions, const float* old_logp,
+                                  const float* old_values, const float* advantages, const float* returns,
+                                  int64_t n_rows, int32_t batch_size, const rai_ppo_hparams* hp,
+                                  const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
+                                  int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
+                                  int64_t workspace_bytes, void* stream) {
+  if (!desc || !params || !exp_avg || !exp_avg_sq || !obs || !actions || !old_logp || !old_values || !advantages ||
+      !returns || !hp || !ohp || !state || !workspace)
+    return RAI_E_NULLPTR;
+  if (workspace_bytes < WE_WS_BYTES) return RAI_E_WORKSPACE;
+  if (n_rows < 2 || batch_size < 2 || batch_size > WE_B) return RAI_E_SHAPE;
+  if (n_rows % batch_size == 1) return RAI_E_SHAPE;  // a 1-row minibatch has no unbiased std
+  const int H = desc->hidden;
+  if (H < WE_SL || H > WE_HMAX || H % WE_SL != 0) return RAI_E_UNSUPPORTED;
+  if (desc->in_dim < 1 || desc->in_dim > WE_INMAX || desc->out_pi < 1 || desc->out_pi > WE_OUTM)
+    return RAI_E_UNSUPPORTED;
+  if (desc->head != 0 && desc->head != 1) return RAI_E_MODE;
+  if (desc->head == 1 && !desc->log_std) return RAI_E_NULLPTR;
+  if (desc->accumulate) return RAI_E_UNSUPPORTED;
+  for (int n = 0; n < 2; ++n)
+    for (int i = 0; i < 6; ++i) {
+      if (!desc->w[n][i]) return RAI_E_NULLPTR;
+      if (desc->w[n][i] < params || desc->w[n][i] >= params + P) return RAI_E_SHAPE;  // views of the flat buffer
+    }
+  if (desc->head == 1 && (desc->log_std < params || desc->log_std >= params + P)) return RAI_E_SHAPE;
+  WeArgs a{};
+  a.d = *desc;
+  a.params = params;
+  a.exp_avg = exp_avg;
+  a.exp_avg_sq = exp_avg_sq;
+  a.obs = obs;
+  a.actions = actions;
+  a.old_logp = old_logp;
+  a.old_values = old_values;
+  a.adv = advantages;
+  a.ret = returns;
+  a.n_rows = n_rows;
+  a.batch = batch_size;
+  a.hp = hp;
+  a.ohp = ohp;
+  a.state = state;
+  a.stats = stats;
+  a.max_stats = max_stats;
+  a.norms = norms;
+  a.max_norms = max_norms;
+  a.ws = static_cast<unsigned char*>(workspace);
+  hipStream_t s = rai_stream(stream);
+  const hipError_t e = hipMemsetAsync(workspace, 0, WE_CTR_BYTES, s);  // monotonic counters start at 0
+  if (e != hipSuccess) return (int)e;
+  const dim3 grid(8 * (H / WE_SL));
+  if (desc->head == 1) hipLaunchKernelGGL(mlp_wide_epoch_kernel<1>, grid, dim3(WE_NT), 0, s, a);
+  else hipLaunchKernelGGL(mlp_wide_epoch_kernel<0>, grid, dim3(WE_NT), 0, s, a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}

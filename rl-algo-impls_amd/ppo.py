@@ -15,6 +15,7 @@ flat parameter buffer.  No host synchronisation until the update ends.
 """
 from __future__ import annotations
 
+import ctypes as C
 import gc
 import logging
 import os
@@ -556,6 +557,94 @@ class PPO:
         stats[:, 0] += float(self.vf_coef) * stats[:, 5]  # value term of the loss
         return stats, norms, 1
 
+    def _wide_epoch_step(self, r):
+        """The WideStep (descriptor) when the whole epoch can run as ONE persistent launch
+        (rai_mlp_wide_epoch): a wide-MLP policy with K = 1, Adam, minibatches of 2..64 rows, no
+        gradient accumulation / kl_cutoff / multi-reward weights / vf_weights, single process.
+        RAI_WIDE_EPOCH=0 keeps the graph-replayed per-minibatch path."""
+        if os.environ.get("RAI_WIDE_EPOCH", "1") == "0" or not hasattr(r, "epoch_batch") or self.dp_enabled:
+            return None
+        if (self.gradient_accumulation or self.kl_cutoff is not None or self.multi_reward_weights is not None
+                or self.vf_weights is not None or self.normalize_advantages_after_scaling
+                or np.ndim(self.vf_coef) > 0 or self.optimizer.kind != self.optimizer.ADAM):
+            return None
+        if not (2 <= self.batch_size <= 64) or r.total_steps < 2 or r.total_steps % self.batch_size == 1:
+            return None
+        return self._wide_step()
+
+    def _update_wide_epoch(self, r, wide) -> Tuple[np.ndarray, np.ndarray, int]:
+        """One rai_mlp_wide_epoch launch per epoch over the epoch's permuted rollout copy; epoch
+        k + 1's permutation and gather are prepared on a side stream while epoch k runs (as
+        _update_fused)."""
+        nmb = r.num_minibatches(self.batch_size)
+        n_steps = self.n_epochs * nmb
+        blocks = self.blocks
+        blocks.ensure_tables(n_steps, n_steps)
+        blocks.upload(self._hparams(1, nmb), self.optimizer.step_count)
+        opt = self.optimizer
+        L = _lib.lib()
+        st = _lib.stream_handle(self.device)
+        if getattr(self, "_we_ws", None) is None:
+            self._we_ws = torch.zeros(int(L.rai_mlp_wide_epoch_workspace_bytes(wide.spec["hidden"])),
+                                      dtype=torch.uint8, device=self.device)
+        cur = torch.cuda.current_stream(self.device)
+        two_slots = hasattr(r, "alloc_epoch_buffers")
+        side = self._epoch_prep_stream() if two_slots else cur
+        if two_slots:
+            for slot in (0, 1):
+                r.alloc_epoch_buffers(slot)
+            side.wait_stream(cur)
+
+        def prep(k):
+            with torch.cuda.stream(side):
+                bk = r.epoch_batch(shuffle=True, slot=k % 2) if two_slots else r.epoch_batch(shuffle=True)
+                assert bk.logprobs is not None, "PPO needs rollout logprobs (include_logp=True)"
+                obs_k = bk.obs if bk.obs.dtype == torch.float32 else bk.obs.float()
+                obs_k = obs_k.contiguous()
+                if obs_k.data_ptr() != bk.obs.data_ptr():
+                    obs_k.record_stream(cur)
+                ready = torch.cuda.Event()
+                ready.record(side)
+            return bk, obs_k, ready
+
+        f = self.flat
+        nxt = prep(0)
+        done: List[torch.cuda.Event] = []
+        for k in range(self.n_epochs):
+            b, obs, ready = nxt
+            cur.wait_event(ready)
+            ev = None
+            if self.kernel_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            rc = L.rai_mlp_wide_epoch(
+                C.byref(wide.desc), f.flat.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), f.P,
+                obs.data_ptr(), b.actions.contiguous().data_ptr(), b.logprobs.data_ptr(), b.values.data_ptr(),
+                b.advantages.data_ptr(), b.returns.data_ptr(), r.total_steps, self.batch_size, blocks.hp.data_ptr(),
+                opt.hp_dev.data_ptr(), blocks.state.data_ptr(), blocks.stats.data_ptr(), int(blocks.stats.shape[0]),
+                blocks.norms.data_ptr(), int(blocks.norms.shape[0]), self._we_ws.data_ptr(), self._we_ws.numel(), st)
+            _lib.check(rc, "rai_mlp_wide_epoch")
+            if ev is not None:
+                ev[1].record()
+                self.kernel_events.append(ev)
+            opt.step_count += nmb
+            done.append(torch.cuda.Event())
+            done[-1].record(cur)
+            if k + 1 < self.n_epochs:
+                if k >= 1 and two_slots:
+                    side.wait_event(done[k - 1])
+                nxt = prep(k + 1)
+        cur.wait_stream(side)
+        host = torch.cat([blocks.stats[:n_steps].reshape(-1), blocks.norms[:n_steps],
+                          blocks.state.view(torch.float32)]).cpu().numpy()
+        stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE).copy()
+        norms = host[n_steps * _lib.RAI_STAT_STRIDE: n_steps * _lib.RAI_STAT_STRIDE + n_steps]
+        state = host[n_steps * _lib.RAI_STAT_STRIDE + n_steps:].view(np.int32)
+        if state[5] != 0:
+            raise RuntimeError("rai_mlp_wide_epoch: a device-side hand-off timed out (err flag set)")
+        stats[:, 0] += float(self.vf_coef) * stats[:, 5]  # value term of the loss
+        return stats, norms, 1
+
     def _epoch_prep_stream(self) -> torch.cuda.Stream:
         if getattr(self, "_prep_stream", None) is None:
             self._prep_stream = torch.cuda.Stream(self.device)
@@ -611,6 +700,9 @@ class PPO:
         spec = self.fused_mlp_spec() if hasattr(r, "epoch_batch") else None
         if spec is not None:
             return self._update_fused_dp(r, spec) if self.dp_enabled else self._update_fused(r, spec)
+        wide_epoch = self._wide_epoch_step(r)
+        if wide_epoch is not None:
+            return self._update_wide_epoch(r, wide_epoch)
         nmb = r.num_minibatches(self.batch_size)
         n_steps = self.n_epochs * nmb
         n_norms = self.n_epochs if self.gradient_accumulation else n_steps

@@ -39,7 +39,11 @@ def test_gae_golden_returns_fused(gae_cases):
 
 
 @pytest.mark.parametrize("T,N,K,dens", [(128, 4096, 1, 0.005), (512, 2048, 1, 0.001), (37, 999, 3, 0.05),
-                                        (128, 65536, 1, 0.005)])
+                                        (128, 65536, 1, 0.005),
+                                        # the 4-columns-per-lane streaming kernel (C >= 2^18, C % 4 == 0):
+                                        # K = 1 (start bytes read 4 at a time), K = 3 vector gamma, and T
+                                        # not a multiple of its 8-row chunks
+                                        (19, 1 << 18, 1, 0.02), (13, 87384, 3, 0.05), (8, 262148, 1, 1.0)])
 def test_gae_full_size_exact_vs_c_oracle(T, N, K, dens):
     rng = np.random.default_rng(T * N + K)
     shp = (T, N) if K == 1 else (T, N, K)
@@ -54,6 +58,28 @@ def test_gae_full_size_exact_vs_c_oracle(T, N, K, dens):
                                          want_returns=True)
     np.testing.assert_array_equal(adv.cpu().numpy(), adv_ref)
     np.testing.assert_array_equal(ret.cpu().numpy(), ret_ref)
+
+
+@pytest.mark.parametrize("D", ["8", "4"])
+def test_gae_stream_kernel_rows_in_flight_variants(D, monkeypatch):
+    """Both chunk depths of the streaming GAE kernel (RAI_GAE_STREAM_D) and the tiled kernel forced on
+    the same large input (RAI_GAE_STREAM=0) give the C oracle's bits."""
+    rng = np.random.default_rng(41)
+    T, N = 21, 1 << 18
+    r = rng.standard_normal((T, N), dtype=np.float32)
+    v = rng.standard_normal((T, N), dtype=np.float32)
+    es = rng.random((T, N)) < 0.03
+    nes = rng.random(N) < 0.03
+    nv = rng.standard_normal(N, dtype=np.float32)
+    adv_ref, ret_ref = oracle.gae_c(r, v, es, nes, nv, 0.98, 0.8)
+    for stream in ("1", "0"):
+        monkeypatch.setenv("RAI_GAE_STREAM_D", D)
+        monkeypatch.setenv("RAI_GAE_STREAM", stream)
+        adv, ret = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), 0.98, 0.8, want_returns=True)
+        np.testing.assert_array_equal(adv.cpu().numpy(), adv_ref)
+        np.testing.assert_array_equal(ret.cpu().numpy(), ret_ref)
+    fast, _ = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), 0.98, 0.8, mode=FAST)
+    np.testing.assert_allclose(fast.cpu().numpy(), adv_ref, rtol=1e-5, atol=1e-5)
 
 
 def test_gae_fast_mode_tolerance():

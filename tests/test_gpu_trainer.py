@@ -44,6 +44,16 @@ class FixedDeviceRollout:
         return float(1 - torch.var(y - p, unbiased=False) / torch.var(y, unbiased=False))
 
 
+class EpochFixedRollout(FixedDeviceRollout):
+    """The fixed minibatches as one epoch copy in order (no shuffle): the whole-epoch kernels
+    (rai_mlp_wide_epoch) take minibatch i as rows [i B, (i + 1) B) of it."""
+
+    def epoch_batch(self, shuffle=True):
+        cat = lambda f: torch.cat([getattr(b, f) for b in self.batches]).contiguous()
+        return Batch(cat("obs"), cat("logprobs"), cat("actions"), None, None, cat("values"), cat("advantages"),
+                     cat("returns"))
+
+
 def _device_batches(z, name, n, with_logp=True):
     out = []
     for i in range(n):
@@ -54,13 +64,17 @@ def _device_batches(z, name, n, with_logp=True):
     return out
 
 
-@pytest.mark.parametrize("wide", [True, False], ids=["wide_kernels", "pytorch_network"])
+@pytest.mark.parametrize("wide", [True, False, "epoch"], ids=["wide_kernels", "pytorch_network", "wide_epoch"])
 @pytest.mark.parametrize("name", ["cp_default", "cp_vclip_ent", "cp_gradacc", "cp_klcut", "hc_gauss", "mc_mrw",
                                   "mc_after", "mc_huber_w"])
 def test_ppo_minibatch_steps_match_reference(golden, name, wide):
     """Per-minibatch path against the reference's PPO steps.  The MLP cases (cp_*, hc_gauss: 64-wide
     actor/critic) run through the fused wide-MLP kernels (mlp_wide.py) or the PyTorch network +
-    autograd; the multi-critic cases (mc_*) always take the PyTorch network."""
+    autograd; the multi-critic cases (mc_*) always take the PyTorch network.  wide_epoch: the same
+    minibatches as ONE whole-epoch launch (rai_mlp_wide_epoch, csrc/mlp_wide_epoch.hip) where its
+    scope covers the case (hc_gauss: B = 64, Gaussian head, Adam, no gradient accumulation)."""
+    if wide == "epoch" and name != "hc_gauss":
+        pytest.skip("outside rai_mlp_wide_epoch's scope (B > 64, gradient accumulation, kl_cutoff or K > 1)")
     z = golden("ppo_steps.npz")
     meta = json.loads(str(z["index"]))[name]
     policy = nets.build(meta["policy"])
@@ -68,9 +82,11 @@ def test_ppo_minibatch_steps_match_reference(golden, name, wide):
     policy = policy.to(DEV)
     kw = dict(meta["kw"])
     algo = PPO(policy, DEV, Recorder(), n_epochs=1, **kw)
-    algo.use_wide = wide
-    r = FixedDeviceRollout(_device_batches(z, name, meta["n"]))
+    algo.use_wide = bool(wide)
+    bs = _device_batches(z, name, meta["n"])
+    r = EpochFixedRollout(bs) if wide == "epoch" else FixedDeviceRollout(bs)
     stats, norms, K = algo.update(r)
+    assert (getattr(algo, "_we_ws", None) is not None) == (wide == "epoch"), "whole-epoch kernel path"
     ref_params = z[f"{name}/params"]
     got = algo.flat.flat.cpu().numpy()
     # Adam's first steps normalise g/|g|; tolerance covers fp32 reduction-order
@@ -483,14 +499,22 @@ def _graphed_vs_eager(kind, T, N, bs, extra):
     ("halfcheetah", 128, "tanh", dict(clip_range_vf=0.2)),
     ("cartpole", 256, "tanh", dict(ent_coef=0.01)),                        # Categorical head, 256 wide
     ("halfcheetah", 64, "relu", dict(gradient_accumulation=True)),         # accumulate mode
+    ("halfcheetah", 192, "relu", dict(N=25, clip_range_vf=0.1)),           # 400 rows: ragged tail of 16
 ])
-def test_wide_mlp_kernels_match_pytorch_path(kind, hidden, act, extra):
-    """Fused wide-MLP forward/backward (graph-replayed) vs the PyTorch network + autograd (eager)
-    on the same minibatches: two updates x 3 epochs, fp32 tolerance (different reduction order)."""
+@pytest.mark.parametrize("epoch", ["1", "0"], ids=["whole_epoch_kernel", "per_minibatch_kernels"])
+def test_wide_mlp_kernels_match_pytorch_path(kind, hidden, act, extra, epoch, monkeypatch):
+    """Fused wide-MLP path vs the PyTorch network + autograd (eager) on the same minibatches: two
+    updates x 3 epochs, fp32 tolerance (different reduction order).  whole_epoch_kernel: one
+    rai_mlp_wide_epoch launch per epoch (where its scope covers the options; gradient accumulation
+    keeps the per-minibatch kernels); per_minibatch_kernels (RAI_WIDE_EPOCH=0): the graph-replayed
+    wide-MLP kernels + rai_ppo_loss + rai_clip_optim_step."""
     from rl_algo_impls_amd.envs import SyntheticVecEnv
     from rl_algo_impls_amd.policy import ActorCritic
 
-    T, N, bs = 16, 24, 64  # 384 rows: 6 minibatches
+    monkeypatch.setenv("RAI_WIDE_EPOCH", epoch)
+
+    extra = dict(extra)
+    T, N, bs = 16, extra.pop("N", 24), 64  # 384 rows: 6 minibatches
     res = []
     for wide in (True, False):
         torch.manual_seed(7)
@@ -515,9 +539,10 @@ def test_wide_mlp_kernels_match_pytorch_path(kind, hidden, act, extra):
                           0.99, 0.95, perm_source=lambda n: torch.randperm(n, generator=perm_g))
         out = [algo.update(r)[:2] for _ in range(2)]
         torch.cuda.synchronize()
-        res.append((algo.flat.flat.cpu().numpy(), out, algo._wide))
-    (p_w, o_w, w), (p_t, o_t, _) = res
+        res.append((algo.flat.flat.cpu().numpy(), out, algo._wide, getattr(algo, "_we_ws", None) is not None))
+    (p_w, o_w, w, we), (p_t, o_t, _, _) = res
     assert w not in (None, False), "wide path not taken"
+    assert we == (epoch == "1" and not extra.get("gradient_accumulation")), "whole-epoch kernel use"
     np.testing.assert_allclose(p_w, p_t, rtol=1e-4, atol=2e-6)
     for (s_w, n_w), (s_t, n_t) in zip(o_w, o_t):
         np.testing.assert_allclose(s_w[:, :6], s_t[:, :6], rtol=1e-4, atol=1e-6)
