@@ -63,7 +63,8 @@ struct SmemM8 {
   unsigned long long t_last;
 #endif
   double pw[2];
-  double st[4][4];   // per-tile loss statistics (the first wave of each tile); round 2: share |g|^2
+  double st[4][4];   // round 2: share |g|^2
+  float strow[Geo::RC][4];  // per-row loss statistics, reduced off the critical path (round-1 wait)
   int bail;
   float db3p[Geo::NTILE][OUTP];
   float Wt[WL_N];    // weights
@@ -367,7 +368,6 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
     // ============ loss (both halves, identical), dZ2 on own columns ============
     float pw3[CT][OUTP], pb2[CT];
     float dq[OUTP];
-    float st[4] = {0.f, 0.f, 0.f, 0.f};
     {
       RELANE();
       const int T_ = w / WPT, hf_ = w % WPT;
@@ -382,13 +382,11 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         z[o] = zs + S.Wt[WL_B3 + o];
         dq[o] = 0.f;
       }
-      if (RG + g * 4 + q < rows) {
-        float sr[4];
-        ppo_row_loss<OUTP, ACTOR>(z, lh, c_act, c_a, c_b, amean, aden, dq, sr);
-        if (li < 4 && hf_ == 0) {
+      float sr[4] = {0.f, 0.f, 0.f, 0.f};
+      if (RG + g * 4 + q < rows) ppo_row_loss<OUTP, ACTOR>(z, lh, c_act, c_a, c_b, amean, aden, dq, sr);
+      if (li < 4 && hf_ == 0) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) st[i] = sr[i];
-        }
+        for (int i = 0; i < 4; ++i) S.strow[lr_][i] = sr[i];
       }
       float dr[4][OUTP];
 #pragma unroll
@@ -487,11 +485,6 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
           const float t3 = wave_sum_v(li < 4 ? dq[o] : 0.f);
           if (lane == 0) S.db3p[T_][o] = t3;
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const double t = wave_sum_v((double)st[i]);
-          if (lane == 0) S.st[T_][i] = t;
-        }
       }
     }
     lds_barrier();
@@ -565,20 +558,6 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
           __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), srs, sbase + 16 * ch, 0, 16);
         }
       }
-      if (tid == 0) {  // this CU's loss statistics (tile order); CU 0 turns them into rows at the end
-        double sv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          sv[i] = S.st[0][i];
-#pragma unroll
-          for (int q = 1; q < NTILE; ++q) sv[i] += S.st[q][i];
-        }
-        const u4v p0 = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){sv[0], sv[1]});
-        const u4v p1 = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){sv[2], sv[3]});
-        const int so = ((net * nmb + mb) * G + c) * 32;
-        __builtin_amdgcn_raw_buffer_store_b128(p0, str, so, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(p1, str, so + 16, 0, 16);
-      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
     }
     __syncthreads();
@@ -588,6 +567,21 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         atomicExch(a.err, 1);
         S.bail = 1;
       }
+    } else if (w == 1) {
+      // while wave 0 waits for the other CUs: this CU's loss statistics (fp64 sums over its rows in
+      // row order of the lanes); CU 0 turns them into rows at the end.  Off the gradient's path.
+      const int ln = tid & 63;
+      double sv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sv[i] = wave_sum_v(ln < RC ? (double)S.strow[ln < RC ? ln : 0][i] : 0.0);
+      if (ln == 0) {
+        const u4v p0 = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){sv[0], sv[1]});
+        const u4v p1 = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){sv[2], sv[3]});
+        const int so = ((net * nmb + mb) * G + c) * 32;
+        __builtin_amdgcn_raw_buffer_store_b128(p0, str, so, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(p1, str, so + 16, 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (S.bail) break;

@@ -97,6 +97,7 @@ struct WeSmem {
   float Z1j[WE_B][WE_SP];
   float dOut[WE_B][WE_OUTM];
   float dls[WE_B][WE_OUTM];
+  float Pw[4][WE_B][WE_OUTM];  // per-wave sums of 4 slices' output partials
   float small[WE_NSMALL];     // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
   double red[4][8];
   float adv_mean, adv_den;
@@ -279,16 +280,61 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   if (tid == 0) S.bail = 0;
   __syncthreads();
 
+  // the next minibatch's inputs are loaded into registers one step ahead: its observations (all
+  // threads) and, for wave 0 (lane = row), the per-row loss inputs
+  constexpr int XU = (WE_B * WE_INMAX + WE_NT - 1) / WE_NT;
+  float xr[XU];
+  float pa[WE_OUTM], p_lpold = 0.f, p_adv = 0.f, p_ret = 0.f, p_vold = 0.f;
+  int64_t p_ai = 0;
+  auto prefetch = [&](int m) {
+    const int64_t r0 = (int64_t)m * B;
+    const int rws = (int)min((int64_t)B, n_rows - r0);
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int e = tid + WE_NT * u;
+      const int r = e / IN4, k = e - r * IN4;
+      const bool ok = e < WE_B * IN4 && r < rws && k < IN;
+      const float x = a.obs[ok ? (r0 + r) * IN + k : 0];
+      xr[u] = ok ? x : 0.f;
+    }
+    if (w == 0) {
+      const bool ok = lane < rws;
+      const int64_t gr = r0 + (ok ? lane : 0);
+      if (net == 0) {
+        if (HEAD == 1) {
+          const float* av = static_cast<const float*>(a.actions) + gr * O;
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o) pa[o] = av[o < O ? o : 0];
+        } else {
+          p_ai = static_cast<const int64_t*>(a.actions)[gr];
+        }
+        p_lpold = a.old_logp[gr];
+        p_adv = a.adv[gr];
+      } else {
+        p_ret = a.ret[gr];
+        p_vold = a.old_values[gr];
+      }
+    }
+  };
+  if (nmb > 0) prefetch(0);
+
   for (int mb = 0; mb < nmb; ++mb) {
     const int par = mb & 1;
     const int64_t row0 = (int64_t)mb * B;
     const int rows = (int)min((int64_t)B, n_rows - row0);
     const unsigned long long want = (unsigned long long)G * (mb + 1);
     // ---- observations of the minibatch -> LDS (zero rows / columns beyond the data) ----------
-    for (int e = tid; e < WE_B * IN4; e += WE_NT) {
-      const int r = e / IN4, k = e - r * IN4;
-      S.Xs[r][k] = (r < rows && k < IN) ? a.obs[(row0 + r) * IN + k] : 0.f;
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int e = tid + WE_NT * u;
+      if (e < WE_B * IN4) S.Xs[e / IN4][e % IN4] = xr[u];
     }
+    float c_act[WE_OUTM];
+#pragma unroll
+    for (int o = 0; o < WE_OUTM; ++o) c_act[o] = pa[o];
+    const int64_t c_ai = p_ai;
+    const float c_lpold = p_lpold, c_adv = p_adv, c_ret = p_ret, c_vold = p_vold;
+    if (mb + 1 < nmb) prefetch(mb + 1);
     lds_barrier();
     // ============ fwd1: H1[:, j] = act(X W1[j]^T + b1[j]); wave w: row tile w =============
     {
@@ -358,29 +404,36 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
     if (!we_arrive_wait(ctr, WE_CB + net, want, -1, 0, a.state, S.bail)) break;
     // ============ head + loss, all rows (identical on every workgroup of the network) ========
+    {  // slice partials: wave w sums slices [4 w, 4 w + 4) for row = lane (loads issued together)
+      const int64_t base = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT;
+      f4 qa[4], qb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ss = min(4 * w + u, G - 1);
+        const int64_t off = base + (((int64_t)ss * WE_B + lane) * WE_OUTM) * 4;
+        qa[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)off, 0, WE_SC1));
+        qb[u] = O > 4 ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)off + 16, 0, WE_SC1))
+                      : f4{0.f, 0.f, 0.f, 0.f};
+      }
+      f4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (4 * w + u < G) {
+          sa += qa[u];
+          sb += qb[u];
+        }
+      *reinterpret_cast<f4*>(&S.Pw[w][lane][0]) = sa;
+      *reinterpret_cast<f4*>(&S.Pw[w][lane][4]) = sb;
+    }
+    lds_barrier();
     if (w == 0) {
       const int r = lane;
       const bool valid = r < rows;
-      const int64_t gr = row0 + (valid ? r : 0);
       float out[WE_OUTM];
-      {
-        const int64_t base = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT;
-        f4 pa[WE_GMAX], pb[WE_GMAX];
 #pragma unroll
-        for (int s = 0; s < WE_GMAX; ++s) {
-          const int ss = min(s, G - 1);
-          const int64_t off = base + (((int64_t)ss * WE_B + r) * WE_OUTM) * 4;
-          pa[s] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)off, 0, WE_SC1));
-          pb[s] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)off + 16, 0, WE_SC1));
-        }
-#pragma unroll
-        for (int o = 0; o < WE_OUTM; ++o) {
-          float acc = 0.f;
-#pragma unroll
-          for (int s = 0; s < WE_GMAX; ++s)
-            if (s < G) acc += o < 4 ? pa[s][o] : pb[s][o - 4];
-          out[o] = o < O ? acc + S.small[2 * WE_SL + WE_OUTM * WE_SL + o] : 0.f;
-        }
+      for (int o = 0; o < WE_OUTM; ++o) {
+        const float acc = ((S.Pw[0][r][o] + S.Pw[1][r][o]) + S.Pw[2][r][o]) + S.Pw[3][r][o];
+        out[o] = o < O ? acc + S.small[2 * WE_SL + WE_OUTM * WE_SL + o] : 0.f;
       }
       float dout[WE_OUTM], dl[WE_OUTM];
 #pragma unroll
@@ -391,7 +444,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       if (net == 0) {
 #pragma clang fp contract(off)
         // advantage moments over the minibatch (two passes, fp64 sums; ppo.py:313-316)
-        const float x = valid ? a.adv[gr] : 0.f;
+        const float x = valid ? c_adv : 0.f;
         float A = x;
         if (hp.normalize_advantage || hp.standardize_advantage) {
           const double s1 = wave_sum(valid ? (double)x : 0.0);
@@ -403,19 +456,18 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         }
         float lp = 0.f, ent = 0.f;  // log-prob of the action, entropy (summed over dims)
         if (HEAD == 1) {
-          const float* av = static_cast<const float*>(a.actions) + gr * O;
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o)
             if (o < O) {
               const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + o]);
               const float var = scale * scale;
               const float log_scale = logf(scale);
-              const float xo = av[o] - out[o];
+              const float xo = c_act[o] - out[o];
               lp += -(xo * xo) / (2.f * var) - log_scale - 0.91893853320467274f;
               ent += 1.4189385332046727f + log_scale;
             }
         } else {
-          const int64_t ai = static_cast<const int64_t*>(a.actions)[gr];
+          const int64_t ai = c_ai;
           float mx = out[0];
 #pragma unroll
           for (int o = 1; o < WE_OUTM; ++o)
@@ -437,7 +489,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
           lp = za - lse;
           ent = h;
         }
-        const float logratio = lp - a.old_logp[gr];
+        const float logratio = lp - c_lpold;
         const float ratio = expf(logratio);
         const float lo = 1.f - hp.clip_range, hi = 1.f + hp.clip_range;
         const float cr = fminf(fmaxf(ratio, lo), hi);
@@ -452,18 +504,17 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         const float n_ent = (float)(HEAD == 1 ? rows * O : rows);
         const float d_ent = valid ? -hp.ent_coef / n_ent : 0.f;
         if (HEAD == 1) {
-          const float* av = static_cast<const float*>(a.actions) + gr * O;
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o)
             if (o < O) {
               const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + o]);
               const float var = scale * scale;
-              const float xo = av[o] - out[o];
+              const float xo = c_act[o] - out[o];
               dout[o] = d_logp * (xo / var);
               dl[o] = d_logp * ((xo * xo) / var - 1.f) + d_ent;
             }
         } else {
-          const int64_t ai = static_cast<const int64_t*>(a.actions)[gr];
+          const int64_t ai = c_ai;
           float mx = out[0];
 #pragma unroll
           for (int o = 1; o < WE_OUTM; ++o)
@@ -495,14 +546,14 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         }
       } else {
 #pragma clang fp contract(off)
-        const float v = out[0], R = a.ret[gr];
+        const float v = out[0], R = c_ret;
         const float halve = hp.ppo2_vf_coef_halving ? 0.5f : 1.f;
         const float gl = (hp.vf_coef[0] * halve) * invB;
         const int vfn = hp.vf_loss_fn;
         float l = we_vf_loss(vfn, v - R), dv;
         float vcf = 0.f;
         if (hp.has_clip_range_vf) {
-          const float vc_ = hp.clip_range_vf, vo = a.old_values[gr];
+          const float vc_ = hp.clip_range_vf, vo = c_vold;
           const float dvo = v - vo;
           const float vcl = vo + fminf(fmaxf(dvo, -vc_), vc_);
           const float l2 = we_vf_loss(vfn, vcl - R);

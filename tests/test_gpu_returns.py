@@ -84,10 +84,36 @@ def _device_run(cfg, seed):
                           len(eps)])
             return True
 
-    algo.learn(c["n_timesteps"], gen, callbacks=[ht, Record()])
+    # PPO.learn's loop (rl_algo_impls/ppo/ppo.py:192-212) without its per-update gc.collect()
+    steps, cbs = 0, [ht, Record()]
+    while steps < c["n_timesteps"]:
+        steps, go = algo.learn_epoch(steps, c["n_timesteps"], gen, cbs)
+        if not go:
+            break
     st = evaluate(CartPoleVecEnv(8, seed=seed + 1000), policy, REF["eval_episodes"], deterministic=True,
                   print_returns=False)
     return curve, float(st.score.mean)
+
+
+_RUNS = {}
+
+
+def _device_result(cfg, seed):
+    if (cfg, seed) not in _RUNS:
+        _RUNS[(cfg, seed)] = _device_run(cfg, seed)
+    return _RUNS[(cfg, seed)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", ["yaml_8x32", "c1_8x128"])
+def test_device_training_run(cfg, seed):
+    """One seeded device training run on the reference's env and hyperparameters (kept for the band
+    test below): one rolling-mean point per update, finite, within CartPole-v1's [0, 500]."""
+    curve, ev = _device_result(cfg, seed)
+    assert len(curve) == len(REF["runs"][cfg][str(seed)]["curve"])
+    vals = np.array([p[1] for p in curve])
+    assert np.isfinite(vals).all() and vals.min() >= 0 and vals.max() <= 500 and 0 <= ev <= 500
 
 
 @pytest.mark.gpu
@@ -105,7 +131,7 @@ def test_episode_return_matches_reference(cfg):
     r_fin, r_auc, r_eval = _ref(cfg)
     fins, aucs, evals = [], [], []
     for seed in (1, 2, 3, 4, 5):
-        curve, ev = _device_run(cfg, seed)
+        curve, ev = _device_result(cfg, seed)
         assert len(curve) == len(REF["runs"][cfg][str(seed)]["curve"])
         fins.append(curve[-1][1])
         aucs.append(np.mean([p[1] for p in curve]))

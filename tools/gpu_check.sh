@@ -18,6 +18,8 @@ step() {  # name timeout cmd...
 }
 STEPS=${STEPS:-smoke,pytest,bench}
 [[ $STEPS == *smoke* ]] && step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *pytest* ]] && step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+if [[ -n ${PYTEST_K:-} ]]; then KARGS=(-k "$PYTEST_K"); else KARGS=(); fi
+[[ $STEPS == *pytest* ]] && step pytest_gpu 1000 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -v --timeout 300 --timeout-method thread "${KARGS[@]}" ${PYTEST_ARGS:-}
 [[ $STEPS == *bench* ]] && step bench 900 python bench.py ${BENCH_ARGS:-}
+[[ $STEPS == *gaebench* ]] && step gaebench 300 python tools/gae_bench.py
 exit 0

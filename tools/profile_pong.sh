@@ -26,6 +26,9 @@ run() {  # name timeout cmd...
   [ $rc -eq 0 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
 }
 B="python3 bench.py --config pong --no-cpu-baseline --roofline-reps 20"
+# DIAG=1: bench.py dumps /proc/self/maps at each stage and Python stacks on a fatal signal into
+# $OUT/diag (RAI_DIAG_DIR), so a native crash's PCs map to a library and offset (tools/map_pcs.py)
+[ "${DIAG:-0}" = 1 ] && export RAI_DIAG_DIR="$OUT/diag"
 if [ "${STATS:-1}" = 1 ]; then
   run stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- $B --steps 2 --warmup 1
   rm -f "$OUT/stats/run_kernel_trace.csv"
