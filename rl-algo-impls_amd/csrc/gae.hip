@@ -263,11 +263,11 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
 constexpr int GAE_STREAM_NT = 256;
 constexpr int64_t GAE_STREAM_MIN_C = 1LL << 18;
 
-template <typename Acc, int D, bool K1>
-__global__ __launch_bounds__(GAE_STREAM_NT) void gae_stream_kernel(const GaeArgs a) {
+template <typename Acc, int D, bool K1, int NT>
+__global__ __launch_bounds__(NT) void gae_stream_kernel(const GaeArgs a) {
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int64_t C = a.C, N = a.N, T = a.T;
-  const int64_t c0 = 4 * ((int64_t)blockIdx.x * GAE_STREAM_NT + threadIdx.x);
+  const int64_t c0 = 4 * ((int64_t)blockIdx.x * NT + threadIdx.x);
   if (c0 >= C) return;
   const int K = a.K;
   const bool gvec = a.gamma_is_vector != 0;
@@ -386,20 +386,32 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
   if (a.C >= GAE_STREAM_MIN_C && a.C % 4 == 0 && aligned16 && !(sf && sf[0] == '0')) {
     const bool k1 = K == 1 && N % 4 == 0 && (uintptr_t)episode_starts % 4 == 0 &&
                     (uintptr_t)next_episode_starts % 4 == 0;
-    const dim3 grid((unsigned)((a.C / 4 + GAE_STREAM_NT - 1) / GAE_STREAM_NT)), block(GAE_STREAM_NT);
-    const char* sd = getenv("RAI_GAE_STREAM_D");  // diagnostics: rows in flight per chunk (4 or 8)
+    // diagnostics: rows in flight per chunk (RAI_GAE_STREAM_D = 4 or 8) and threads per block
+    // (RAI_GAE_STREAM_NT = 256 or 1024: 4 KB or 16 KB of each row per block)
+    const char* sd = getenv("RAI_GAE_STREAM_D");
+    const char* sn = getenv("RAI_GAE_STREAM_NT");
     const bool d4 = sd && sd[0] == '4';
-#define RAI_GAE_STREAM_LAUNCH(ACC, DD)                                                               \
+    int nt = GAE_STREAM_NT;
+    if (sn && atoi(sn) == 512) nt = 512;
+    if (sn && atoi(sn) == 1024 && k1) nt = 1024;  // K > 1 spills at 128 VGPRs
+    const dim3 grid((unsigned)((a.C / 4 + nt - 1) / nt)), block(nt);
+#define RAI_GAE_STREAM_LAUNCH(ACC, DD, NTT)                                                          \
   do {                                                                                               \
-    if (k1) hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, true>), grid, block, 0, st, a);          \
-    else hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, false>), grid, block, 0, st, a);            \
+    if (k1) hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, true, NTT>), grid, block, 0, st, a);     \
+    else hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, false, NTT>), grid, block, 0, st, a);       \
   } while (0)
-    if (mode == RAI_GAE_EXACT) {
-      if (d4) RAI_GAE_STREAM_LAUNCH(double, 4);
-      else RAI_GAE_STREAM_LAUNCH(double, 8);
+    if (nt == 1024) {  // 128 VGPRs per lane at 4 waves per SIMD: 4 rows in flight
+      if (mode == RAI_GAE_EXACT) hipLaunchKernelGGL((gae_stream_kernel<double, 4, true, 1024>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((gae_stream_kernel<float, 4, true, 1024>), grid, block, 0, st, a);
+    } else if (nt == 512) {  // 256 VGPRs per lane at 2 waves per SIMD: 8 rows in flight
+      if (mode == RAI_GAE_EXACT) RAI_GAE_STREAM_LAUNCH(double, 8, 512);
+      else RAI_GAE_STREAM_LAUNCH(float, 8, 512);
+    } else if (mode == RAI_GAE_EXACT) {
+      if (d4) RAI_GAE_STREAM_LAUNCH(double, 4, 256);
+      else RAI_GAE_STREAM_LAUNCH(double, 8, 256);
     } else {
-      if (d4) RAI_GAE_STREAM_LAUNCH(float, 4);
-      else RAI_GAE_STREAM_LAUNCH(float, 8);
+      if (d4) RAI_GAE_STREAM_LAUNCH(float, 4, 256);
+      else RAI_GAE_STREAM_LAUNCH(float, 8, 256);
     }
 #undef RAI_GAE_STREAM_LAUNCH
     RAI_LAUNCH_CHECK();

@@ -27,8 +27,8 @@
 //      the 2 G shares in a fixed order (clip_grad_norm_ over all parameters, bit-identical on every
 //      workgroup) and applies clip + Adam to what it owns.
 // Every spin is bounded and sets state->err.  Numerics: fp32 like the reference, exact-f32 MFMA
-// (v_mfma_f32_16x16x4f32), IEEE Adam as rai_clip_optim_step; parity to fp32 tolerance against the
-// per-minibatch path (tests/test_gpu_trainer.py).
+// (v_mfma_f32_16x16x4f32), Adam with the hardware sqrt / rcp (as the CartPole epoch kernel); parity
+// to fp32 tolerance against the per-minibatch path and the reference (tests/test_gpu_trainer.py).
 #include "common.h"
 
 namespace {
@@ -104,6 +104,24 @@ struct WeSmem {
   int bail;
 };
 
+#ifdef RAI_STAMPS
+// diagnostic build only (lib/librai_amd_stamps.so, tools/wide_stamps.py): per-phase shader-clock ticks
+// of workgroup 0 of each network, accumulated over launches
+__device__ unsigned long long g_we_stamps[2][16];
+#define WSTAMP(i)                                                             \
+  do {                                                                        \
+    if (j == 0 && threadIdx.x == 0) {                                         \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();            \
+      st_acc[i] += t_ - t_last;                                               \
+      t_last = t_;                                                            \
+    }                                                                         \
+  } while (0)
+#else
+#define WSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t we_rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
@@ -155,14 +173,28 @@ __device__ __forceinline__ f4 we_dw2_tile(const float* A, int lda, const float* 
   return acc;
 }
 
-__device__ __forceinline__ void adam_ieee(float& p, float& m, float& v, float g, float c1, float c2, float beta2,
-                                          float c3, float c4, float eps) {
-#pragma clang fp contract(off)
+// sum over the 64 minibatch rows of f(r), as four interleaved partial sums (rows r = q mod 4) added
+// in a fixed order: four independent dependency chains instead of one, identical on every workgroup
+template <typename F>
+__device__ __forceinline__ float we_rowsum(F f) {
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < WE_B; r += 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += f(r + q);
+  }
+  return ((acc[0] + acc[1]) + acc[2]) + acc[3];
+}
+
+// Adam with the hardware square root and reciprocal (as the CartPole epoch kernel's
+// adam_update_fast): a few ulps from torch's IEEE sequence, far inside the fp32 tolerances
+__device__ __forceinline__ void adam_fast(float& p, float& m, float& v, float g, float c1, float c2, float beta2,
+                                          float inv_c3, float c4, float eps) {
   m = m + c1 * (g - m);
   v = v * beta2;
   v = v + (c2 * g) * g;
-  const float denom = sqrtf(v) / c3 + eps;
-  p = p + c4 * (m / denom);
+  const float denom = __builtin_amdgcn_sqrtf(v) * inv_c3 + eps;
+  p = p + c4 * (m * __builtin_amdgcn_rcpf(denom));
 }
 
 // arrive on counter `ci` after every wave's stores drained (caller: s_waitcnt vmcnt(0) in every
@@ -317,6 +349,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
   };
   if (nmb > 0) prefetch(0);
+#ifdef RAI_STAMPS
+  unsigned long long st_acc[16] = {0}, t_last = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int mb = 0; mb < nmb; ++mb) {
     const int par = mb & 1;
@@ -334,7 +369,6 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     for (int o = 0; o < WE_OUTM; ++o) c_act[o] = pa[o];
     const int64_t c_ai = p_ai;
     const float c_lpold = p_lpold, c_adv = p_adv, c_ret = p_ret, c_vold = p_vold;
-    if (mb + 1 < nmb) prefetch(mb + 1);
     lds_barrier();
     // ============ fwd1: H1[:, j] = act(X W1[j]^T + b1[j]); wave w: row tile w =============
     {
@@ -355,7 +389,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), wrs, (int)off, 0, WE_SC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    WSTAMP(0);
     if (!we_arrive_wait(ctr, WE_CA + net, want, -1, 0, a.state, S.bail)) break;
+    WSTAMP(1);
     {  // gather H1 (B x H) -> Act
       const int n4 = WE_B * H / 4, per_row = H / 4;
       const int64_t base = WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
@@ -402,7 +438,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    WSTAMP(2);
     if (!we_arrive_wait(ctr, WE_CB + net, want, -1, 0, a.state, S.bail)) break;
+    WSTAMP(3);
     // ============ head + loss, all rows (identical on every workgroup of the network) ========
     {  // slice partials: wave w sums slices [4 w, 4 w + 4) for row = lane (loads issued together)
       const int64_t base = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT;
@@ -455,13 +493,22 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
           A = hp.normalize_advantage ? (x - mean) / den : x / den;
         }
         float lp = 0.f, ent = 0.f;  // log-prob of the action, entropy (summed over dims)
+        // Normal(mu, exp(log_std)) per-dimension constants, formed once per step
+        float gvar[WE_OUTM], glsc[WE_OUTM];
+        if (HEAD == 1) {
+#pragma unroll
+          for (int o = 0; o < WE_OUTM; ++o) {
+            const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + (o < O ? o : 0)]);
+            gvar[o] = scale * scale;
+            glsc[o] = logf(scale);
+          }
+        }
         if (HEAD == 1) {
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o)
             if (o < O) {
-              const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + o]);
-              const float var = scale * scale;
-              const float log_scale = logf(scale);
+              const float var = gvar[o];
+              const float log_scale = glsc[o];
               const float xo = c_act[o] - out[o];
               lp += -(xo * xo) / (2.f * var) - log_scale - 0.91893853320467274f;
               ent += 1.4189385332046727f + log_scale;
@@ -507,8 +554,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o)
             if (o < O) {
-              const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + o]);
-              const float var = scale * scale;
+              const float var = gvar[o];
               const float xo = c_act[o] - out[o];
               dout[o] = d_logp * (xo / var);
               dl[o] = d_logp * ((xo * xo) / var - 1.f) + d_ent;
@@ -602,6 +648,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
+    WSTAMP(4);
     // ============ bwd2 (local): dZ2[:, j], publish; dW2 rows j; small gradients ===============
     {
       const int r = tid >> 2, q = tid & 3;
@@ -623,6 +670,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
+    WSTAMP(5);
     // while dZ2 lands: small-parameter gradients and dW2 rows j (H1 still in Act)
     float g_s = 0.f;
     if (tid < WE_NSMALL && fs >= 0) {
@@ -630,15 +678,15 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       if (e >= WE_SL) {  // b1 j is formed after dZ1 (below)
         e -= WE_SL;
         if (e < WE_SL) {  // db2
-          for (int r = 0; r < WE_B; ++r) g_s += S.Z2j[r][e];
+          g_s = we_rowsum([&](int r) { return S.Z2j[r][e]; });
         } else if ((e -= WE_SL) < WE_OUTM * WE_SL) {  // dW3[o][16 j + c]
           const int o = e / WE_SL, c = e - o * WE_SL;
-          for (int r = 0; r < WE_B; ++r) g_s += S.dOut[r][o] * S.H2j[r][c];
+          g_s = we_rowsum([&](int r) { return S.dOut[r][o] * S.H2j[r][c]; });
         } else if ((e -= WE_OUTM * WE_SL) < WE_OUTM) {  // db3
-          for (int r = 0; r < WE_B; ++r) g_s += S.dOut[r][e];
+          g_s = we_rowsum([&](int r) { return S.dOut[r][e]; });
         } else {  // dlog_std
           e -= WE_OUTM;
-          for (int r = 0; r < WE_B; ++r) g_s += S.dls[r][e];
+          g_s = we_rowsum([&](int r) { return S.dls[r][e]; });
         }
       }
     }
@@ -648,6 +696,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       const int ct = 4 * w + t;
       g_r[t] = ct < G ? we_dw2_tile(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * ct], WE_HP, lane) : f4{0.f, 0.f, 0.f, 0.f};
     }
+    WSTAMP(6);
     // wait for every workgroup's dZ2 slice
     if (tid == 0) {
       const unsigned long long t0 = rai_clock();
@@ -663,6 +712,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
     __syncthreads();  // also: every wave is done reading H1 from Act
     if (S.bail) break;
+    WSTAMP(7);
     {  // gather dZ2 (B x H) -> Act
       const int n4 = WE_B * H / 4, per_row = H / 4;
       const int64_t base = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
@@ -708,7 +758,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     if (tid < WE_SL) {
-      for (int r = 0; r < WE_B; ++r) g_s += S.Z1j[r][tid];  // db1
+      g_s = we_rowsum([&](int r) { return S.Z1j[r][tid]; });  // db1
     }
     // ============ D: this workgroup's share of |g|^2, then clip_grad_norm_ + Adam =============
     {
@@ -735,7 +785,12 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
+    // the next minibatch's inputs, issued after this step's last store drain: they land during the
+    // D wait and Adam, before the next drain (vmcnt counts loads and stores together)
+    if (mb + 1 < nmb) prefetch(mb + 1);
+    WSTAMP(8);
     if (!we_arrive_wait(ctr, WE_CD, 2 * want, -1, 0, a.state, S.bail)) break;
+    WSTAMP(9);
     {
       // the 2 G shares, net-major then slice order: lane l < 2 G loads share l; fixed-order wave sum
       const int l = lane < 2 * G ? lane : 0;
@@ -750,7 +805,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       pw1 *= beta1_d;
       pw2 *= beta2_d;
       const double bc1 = 1.0 - pw1, bc2 = 1.0 - pw2;
-      const float c3 = (float)sqrt(bc2), c4 = (float)(-((double)lr / bc1));
+      const float inv_c3 = 1.f / (float)sqrt(bc2), c4 = (float)(-((double)lr / bc1));
       // W2 row slice
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -760,7 +815,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
           for (int r = 0; r < 4; ++r) {
             float& p = S.W2r[4 * g + r][WE_SL * ct + li];
             float pv = p;
-            adam_ieee(pv, m_r[t][r], v_r[t][r], g_r[t][r] * coef, c1, c2, beta2, c3, c4, eps);
+            adam_fast(pv, m_r[t][r], v_r[t][r], g_r[t][r] * coef, c1, c2, beta2, inv_c3, c4, eps);
             p = pv;
           }
         }
@@ -774,7 +829,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
           for (int r = 0; r < 4; ++r) {
             float& p = S.W2c[li][WE_SL * rt + 4 * g + r];
             float pv = p;
-            adam_ieee(pv, m_c[t][r], v_c[t][r], g_c[t][r] * coef, c1, c2, beta2, c3, c4, eps);
+            adam_fast(pv, m_c[t][r], v_c[t][r], g_c[t][r] * coef, c1, c2, beta2, inv_c3, c4, eps);
             p = pv;
           }
         }
@@ -784,18 +839,23 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         for (int r = 0; r < 4; ++r) {
           float& p = S.W1j[4 * g + r][WE_SL * w + li];
           float pv = p;
-          adam_ieee(pv, m_1[r], v_1[r], g_1[r] * coef, c1, c2, beta2, c3, c4, eps);
+          adam_fast(pv, m_1[r], v_1[r], g_1[r] * coef, c1, c2, beta2, inv_c3, c4, eps);
           p = pv;
         }
       }
       if (tid < WE_NSMALL && fs >= 0) {
         float pv = S.small[tid];
-        adam_ieee(pv, m_s, v_s, g_s * coef, c1, c2, beta2, c3, c4, eps);
+        adam_fast(pv, m_s, v_s, g_s * coef, c1, c2, beta2, inv_c3, c4, eps);
         S.small[tid] = pv;
       }
     }
     lds_barrier();
+    WSTAMP(10);
   }
+#ifdef RAI_STAMPS
+  if (j == 0 && tid == 0)
+    for (int i = 0; i < 16; ++i) atomicAdd(&g_we_stamps[net][i], st_acc[i]);
+#endif
 
   // ---- write back what this workgroup owns: parameters and Adam moments ----------------------
   if (!S.bail) {
@@ -852,6 +912,12 @@ __global__ __launch_bounds__(WE_NT) void mlp_wide_epoch_kernel(const WeArgs a) {
 }
 
 }  // namespace
+
+#ifdef RAI_STAMPS
+extern "C" int rai_wide_epoch_debug_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_we_stamps), sizeof(g_we_stamps));
+}
+#endif
 
 extern "C" int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden) {
   (void)hidden;

@@ -60,8 +60,8 @@ def test_gae_full_size_exact_vs_c_oracle(T, N, K, dens):
     np.testing.assert_array_equal(ret.cpu().numpy(), ret_ref)
 
 
-@pytest.mark.parametrize("D", ["8", "4"])
-def test_gae_stream_kernel_rows_in_flight_variants(D, monkeypatch):
+@pytest.mark.parametrize("D,NT", [("8", "256"), ("4", "256"), ("8", "512"), ("4", "1024")])
+def test_gae_stream_kernel_rows_in_flight_variants(D, NT, monkeypatch):
     """Both chunk depths of the streaming GAE kernel (RAI_GAE_STREAM_D) and the tiled kernel forced on
     the same large input (RAI_GAE_STREAM=0) give the C oracle's bits."""
     rng = np.random.default_rng(41)
@@ -74,6 +74,7 @@ def test_gae_stream_kernel_rows_in_flight_variants(D, monkeypatch):
     adv_ref, ret_ref = oracle.gae_c(r, v, es, nes, nv, 0.98, 0.8)
     for stream in ("1", "0"):
         monkeypatch.setenv("RAI_GAE_STREAM_D", D)
+        monkeypatch.setenv("RAI_GAE_STREAM_NT", NT)
         monkeypatch.setenv("RAI_GAE_STREAM", stream)
         adv, ret = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), 0.98, 0.8, want_returns=True)
         np.testing.assert_array_equal(adv.cpu().numpy(), adv_ref)

@@ -15,6 +15,7 @@ written in each test.  Runs are deterministic per seed on the device (fused epoc
 sampler), so a pass is reproducible.
 """
 import json
+import os
 
 import numpy as np
 import pytest
@@ -140,6 +141,13 @@ def test_episode_return_matches_reference(cfg):
     msg = f"device finals {fins.round(1)} auc {aucs.round(1)} eval {evals.round(1)}; " \
           f"reference finals {r_fin.round(1)} auc {r_auc.round(1)} eval {r_eval.round(1)}"
     print(msg)
+    rep = os.environ.get("RAI_TEST_REPORT_DIR")
+    if rep:  # the GPU runs keep the comparison (tools/gpu_check.sh)
+        os.makedirs(rep, exist_ok=True)
+        with open(os.path.join(rep, f"returns_{cfg}.json"), "w") as f:
+            json.dump(dict(device_final=fins.tolist(), device_auc=aucs.tolist(), device_eval=evals.tolist(),
+                           reference_final=r_fin.tolist(), reference_auc=r_auc.tolist(),
+                           reference_eval=r_eval.tolist()), f)
     assert abs(fins.mean() - r_fin.mean()) <= 40, msg
     assert (fins >= r_fin.min() - 25).sum() >= 3, msg
     assert abs(aucs.mean() / r_auc.mean() - 1) <= 0.15, msg

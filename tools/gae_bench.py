@@ -13,8 +13,21 @@ import _pkgload  # noqa: E402
 _pkgload.load()
 from rl_algo_impls_amd.gae import EXACT, FAST, compute_advantages_device  # noqa: E402
 
+import os  # noqa: E402
+
 dev = torch.device("cuda", 0)
-for (T, N, K) in [(128, 4096, 1), (512, 2048, 1), (128, 1024, 1), (512, 512, 3), (128, 1 << 20, 1), (512, 1 << 18, 3)]:
+# kernel variants for the bandwidth-regime shapes: the tiled kernel (RAI_GAE_STREAM=0) and the
+# streaming kernel at 8 / 4 rows in flight per chunk (RAI_GAE_STREAM_D); GAE_BENCH_VARIANTS=0: default only
+VARIANTS = [("default", {})]
+if os.environ.get("GAE_BENCH_VARIANTS", "1") != "0":
+    VARIANTS += [("tiled", {"RAI_GAE_STREAM": "0"}), ("stream_d8", {"RAI_GAE_STREAM_D": "8"}),
+                 ("stream_d4", {"RAI_GAE_STREAM_D": "4"}), ("stream_512", {"RAI_GAE_STREAM_NT": "512"}),
+                 ("stream_1k", {"RAI_GAE_STREAM_NT": "1024"})]
+CASES = [(128, 4096, 1), (512, 2048, 1), (128, 1024, 1), (512, 512, 3), (128, 1 << 20, 1), (512, 1 << 18, 3)]
+for (T, N, K, vname, venv) in [c + v for c in CASES for v in (VARIANTS if c[1] >= (1 << 18) else VARIANTS[:1])]:
+    for k in ("RAI_GAE_STREAM", "RAI_GAE_STREAM_D", "RAI_GAE_STREAM_NT"):
+        os.environ.pop(k, None)
+    os.environ.update(venv)
     shp = (T, N) if K == 1 else (T, N, K)
     r = torch.randn(shp, device=dev)
     v = torch.randn(shp, device=dev)
@@ -40,5 +53,5 @@ for (T, N, K) in [(128, 4096, 1), (512, 2048, 1), (128, 1024, 1), (512, 512, 3),
         e1.record()
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps
-        print(f"T={T:4d} N={N:8d} K={K} {name:5s}: {us:9.2f} us  {byts / us / 1e3:8.1f} GB/s  "
+        print(f"T={T:4d} N={N:8d} K={K} {vname:9s} {name:5s}: {us:9.2f} us  {byts / us / 1e3:8.1f} GB/s  "
               f"({100 * byts / us / 1e3 / 8000:.1f}% of 8 TB/s)", flush=True)

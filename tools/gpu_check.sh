@@ -6,6 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export RAI_TEST_REPORT_DIR=gpurun_out/reports
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "== $name: $*" | tee -a gpurun_out/steps.log
