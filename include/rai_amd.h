@@ -456,6 +456,12 @@ int64_t rai_mlp_wide_workspace_bytes(int64_t B, int32_t hidden);
 int rai_mlp_wide_forward(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,
                          float* logp_out, float* entropy_out, float* v_out, void* workspace,
                          int64_t workspace_bytes, void* stream);
+/* Rollout forward of the wide MLP (rl_algo_impls/shared/policy/actor_critic.py:306-318 up to the
+ * distribution): params_out (B, out_pi) = the Gaussian mean or the Categorical logits, v_out (B) the
+ * critic value, for the sampler (rai_gaussian_sample / rai_categorical_sample).  3 launches instead
+ * of the PyTorch module's GEMMs and elementwise kernels; desc->g is not used. */
+int rai_mlp_wide_dist_params(const rai_mlp_wide_desc* desc, const float* obs, int64_t B, float* params_out,
+                             float* v_out, void* workspace, int64_t workspace_bytes, void* stream);
 /* rai_mlp_wide_forward followed by rai_ppo_loss (K = 1) with the head and the loss in ONE
  * workgroup launch: same arguments as the two calls, same results (the loss body is shared). */
 int rai_mlp_wide_forward_loss(const rai_mlp_wide_desc* desc, const float* obs, const void* actions, int64_t B,

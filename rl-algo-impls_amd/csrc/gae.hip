@@ -391,9 +391,13 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
     const char* sd = getenv("RAI_GAE_STREAM_D");
     const char* sn = getenv("RAI_GAE_STREAM_NT");
     const bool d4 = sd && sd[0] == '4';
-    int nt = GAE_STREAM_NT;
+    // default: K = 1 -> 1024 threads (16 KB of every row per block; 128 x 2^20: 446-449 us against
+    // 455-482 at 256 threads, profiles/r3b_gae_bench.txt); K > 1 -> 256 threads, 8 rows in flight
+    // (the 1024-thread form spills there)
+    int nt = k1 ? 1024 : GAE_STREAM_NT;
+    if (sn && atoi(sn) == 256) nt = 256;
     if (sn && atoi(sn) == 512) nt = 512;
-    if (sn && atoi(sn) == 1024 && k1) nt = 1024;  // K > 1 spills at 128 VGPRs
+    if (sn && atoi(sn) == 1024 && k1) nt = 1024;
     const dim3 grid((unsigned)((a.C / 4 + nt - 1) / nt)), block(nt);
 #define RAI_GAE_STREAM_LAUNCH(ACC, DD, NTT)                                                          \
   do {                                                                                               \

@@ -298,6 +298,27 @@ __device__ __forceinline__ void wide_head_body(const WideArgs& a) {
 
 __global__ __launch_bounds__(WT) void wide_head_kernel(const WideArgs a) { wide_head_body(a); }
 
+// Rollout head: the actor's distribution parameters (Gaussian mean or Categorical logits, (B, out)
+// contiguous) and the critic's value, the slice partials summed in slice order as wide_head_body;
+// one thread per (row, output), no log-prob (the sampler draws the action from these).
+__global__ __launch_bounds__(WT) void wide_head_params_kernel(const WideArgs a, float* params_out) {
+  const rai_mlp_wide_desc& d = a.d;
+  const int H = d.hidden, B = a.B, S = H / SL, A = d.out_pi;
+  const WideWs wp = ws_of(a.ws, 0, B, H), wv = ws_of(a.ws, 1, B, H);
+  const int per = A + 1;
+  for (int i = blockIdx.x * WT + threadIdx.x; i < B * per; i += gridDim.x * WT) {
+    const int b = i / per, o = i - b * per;
+    const bool critic = o == A;
+    const float* P = critic ? wv.P : wp.P;
+    const int oo = critic ? 0 : o;
+    float acc = 0.f;
+    for (int q = 0; q < S; ++q) acc += P[((int64_t)q * B + b) * OUTM + oo];
+    const float val = acc + (critic ? d.w[1][5][0] : d.w[0][5][o]);
+    if (critic) a.v[b] = val;
+    else params_out[(int64_t)b * A + o] = val;
+  }
+}
+
 #include "loss_body.h"
 
 // Head + PPO loss in one workgroup: the head's logp / entropy / v rows go to global memory and,
@@ -547,6 +568,25 @@ extern "C" int rai_mlp_wide_forward(const rai_mlp_wide_desc* desc, const float* 
   hipLaunchKernelGGL(wide_fwd2_kernel, grid, dim3(WT), 0, st, a);
   RAI_LAUNCH_CHECK();
   hipLaunchKernelGGL(wide_head_kernel, dim3(1), dim3(WT), 0, st, a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+extern "C" int rai_mlp_wide_dist_params(const rai_mlp_wide_desc* desc, const float* obs, int64_t B, float* params_out,
+                                        float* v_out, void* workspace, int64_t workspace_bytes, void* stream) {
+  int rc = check(desc, B, obs, workspace, workspace_bytes);
+  if (rc != RAI_OK) return rc;
+  if (!params_out || !v_out) return RAI_E_NULLPTR;
+  WideArgs a = make_args(desc, obs, B, workspace);
+  a.v = v_out;
+  const dim3 grid(desc->hidden / SL, 2);
+  hipStream_t st = rai_stream(stream);
+  hipLaunchKernelGGL(wide_fwd1_kernel, grid, dim3(WT), 0, st, a);
+  RAI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(wide_fwd2_kernel, grid, dim3(WT), 0, st, a);
+  RAI_LAUNCH_CHECK();
+  const int nb = (int)((B * (desc->out_pi + 1) + WT - 1) / WT);
+  hipLaunchKernelGGL(wide_head_params_kernel, dim3(nb), dim3(WT), 0, st, a, params_out);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

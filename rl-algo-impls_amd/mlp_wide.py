@@ -143,3 +143,50 @@ class WideStep:
                                               d_ent.data_ptr(), d_v.data_ptr(), ws.data_ptr(), ws.numel() * 4,
                                               _lib.stream_handle(self.device))
         _lib.check(rc, "rai_mlp_wide_backward")
+
+
+class WideRolloutForward:
+    """Rollout forward of a wide-MLP policy (rai_mlp_wide_dist_params): the actor's distribution
+    parameters (Gaussian mean / Categorical logits) and the critic value for a fixed batch of B
+    observations, into static buffers (capturable into the rollout's step graph).  Weight pointers
+    only; the descriptor is rebuilt if a parameter's storage moved (FlatParams re-views them once,
+    when the trainer is built)."""
+
+    def __init__(self, policy, device: torch.device, B: int):
+        spec = wide_mlp_spec(policy)
+        if spec is None:
+            raise ValueError("policy does not have the wide-MLP structure")
+        if not 1 <= B <= _lib.RAI_WIDE_MAX_B:
+            raise ValueError(f"rollout batch {B} outside 1..{_lib.RAI_WIDE_MAX_B}")
+        self.spec, self.device, self.B = spec, device, B
+        self._params = [p for l in spec["pi"] + spec["v"] for p in (l.weight, l.bias)]
+        self._key = None
+        nbytes = int(_lib.lib().rai_mlp_wide_workspace_bytes(B, spec["hidden"]))
+        self.ws = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+        self.params_out = torch.empty((B, spec["out"]), dtype=torch.float32, device=device)
+        self.v_out = torch.empty((B,), dtype=torch.float32, device=device)
+
+    def _desc(self):
+        key = tuple(p.data_ptr() for p in self._params)
+        if key != self._key:
+            for p in self._params:
+                assert p.is_contiguous() and p.dtype == torch.float32
+            d = _lib.MlpWideDesc()
+            for n in range(2):
+                for i in range(6):
+                    d.w[n][i] = self._params[6 * n + i].data_ptr()
+            d.in_dim, d.hidden, d.out_pi = self.spec["in_dim"], self.spec["hidden"], self.spec["out"]
+            d.head, d.activation = self.spec["head"], self.spec["activation"]
+            if self.spec["head"] == 1:
+                d.log_std = self.spec["log_std"].data_ptr()
+            self.desc, self._key = d, key
+        return self.desc
+
+    def __call__(self, obs: torch.Tensor):
+        obs = obs if obs.dtype == torch.float32 else obs.float()
+        rc = _lib.lib().rai_mlp_wide_dist_params(C.byref(self._desc()), obs.contiguous().data_ptr(), self.B,
+                                                 self.params_out.data_ptr(), self.v_out.data_ptr(),
+                                                 self.ws.data_ptr(), self.ws.numel() * 4,
+                                                 _lib.stream_handle(self.device))
+        _lib.check(rc, "rai_mlp_wide_dist_params")
+        return self.params_out, self.v_out

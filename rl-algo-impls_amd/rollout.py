@@ -335,6 +335,15 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         spec = mlp_actor_critic_spec(policy)
         if spec is not None and self.discrete and self.obs_dtype == torch.float32 and len(obs_space.shape) == 1:
             self.fused_step = spec
+        # wide-MLP policies (HalfCheetah class): the rollout forward as rai_mlp_wide_dist_params (3
+        # launches) instead of the PyTorch module; RAI_ROLLOUT_WIDE=0 keeps the module
+        self._wide_fwd = None
+        if (self.fused_step is None and not self.gridnet and self.device.type == "cuda"
+                and os.environ.get("RAI_ROLLOUT_WIDE", "1") != "0" and len(obs_space.shape) == 1):
+            from .mlp_wide import WideRolloutForward, wide_mlp_spec
+
+            if wide_mlp_spec(policy) is not None and N <= _lib.RAI_WIDE_MAX_B:
+                self._wide_fwd = WideRolloutForward(policy, dev, N)
         obs, _ = vec_env.reset()
         self._stage_obs(obs)
         self._stage_masks()
@@ -464,7 +473,8 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             elif self.gridnet:
                 self._gridnet_step(s)
             else:
-                params, v = self._policy_forward(net.dist_params_and_value)
+                params, v = self._policy_forward(self._wide_fwd if self._wide_fwd is not None
+                                                 else net.dist_params_and_value)
                 self._sample(params, v, s)
             src = self.actions[s] if (self.discrete or self.gridnet) else self.clamped
             self.h_act.copy_(src, non_blocking=True)

@@ -60,7 +60,7 @@ def test_gae_full_size_exact_vs_c_oracle(T, N, K, dens):
     np.testing.assert_array_equal(ret.cpu().numpy(), ret_ref)
 
 
-@pytest.mark.parametrize("D,NT", [("8", "256"), ("4", "256"), ("8", "512"), ("4", "1024")])
+@pytest.mark.parametrize("D,NT", [("8", "256"), ("4", "256"), ("8", "512"), ("4", "1024"), ("8", "default")])
 def test_gae_stream_kernel_rows_in_flight_variants(D, NT, monkeypatch):
     """Both chunk depths of the streaming GAE kernel (RAI_GAE_STREAM_D) and the tiled kernel forced on
     the same large input (RAI_GAE_STREAM=0) give the C oracle's bits."""
