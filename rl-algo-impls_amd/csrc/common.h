@@ -51,6 +51,52 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// The same sums without LDS round trips (each __shfl_xor is a ds_bpermute, ~100+ cycles in a dependent
+// chain): lanes pair up by DPP -- xor 1 and xor 2 (quad_perm), the 8-lane half mirror, the 16-lane row
+// mirror -- then gfx950's v_permlane16_swap / v_permlane32_swap add the rows' and halves' sums.  Each
+// step adds two commuted operands, so every lane ends with the same bits; the association differs from
+// wave_sum's (pairing 1, 2, 4, 8, 16, 32 instead of 32 .. 1).  Requires all 64 lanes active.
+template <int CTRL>
+__device__ __forceinline__ int rai_dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += __int_as_float(rai_dpp<0xB1>(__float_as_int(v)));   // quad_perm [1,0,3,2]
+  v += __int_as_float(rai_dpp<0x4E>(__float_as_int(v)));   // quad_perm [2,3,0,1]
+  v += __int_as_float(rai_dpp<0x141>(__float_as_int(v)));  // row_half_mirror
+  v += __int_as_float(rai_dpp<0x140>(__float_as_int(v)));  // row_mirror
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double rai_dpp_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)rai_dpp<CTRL>((int)(unsigned)u);
+  const unsigned hi = (unsigned)rai_dpp<CTRL>((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double rai_swap_sum_d(double v, bool half32) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const auto l = half32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = half32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double a = __longlong_as_double((long long)(((unsigned long long)h[0] << 32) | l[0]));
+  const double b = __longlong_as_double((long long)(((unsigned long long)h[1] << 32) | l[1]));
+  return a + b;
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += rai_dpp_d<0xB1>(v);
+  v += rai_dpp_d<0x4E>(v);
+  v += rai_dpp_d<0x141>(v);
+  v += rai_dpp_d<0x140>(v);
+  v = rai_swap_sum_d(v, false);
+  return rai_swap_sum_d(v, true);
+}
+
 // Block-wide sum of NV values per thread; every thread receives the totals.
 // scratch: >= NV * (blockDim/64) doubles of LDS.
 template <int NV>

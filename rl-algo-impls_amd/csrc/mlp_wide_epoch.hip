@@ -42,7 +42,7 @@ constexpr int WE_HP = WE_HMAX + 4;          // LDS row stride of H-long rows (16
 constexpr int WE_INMAX = RAI_WIDE_MAX_IN;   // 64
 constexpr int WE_XLD = WE_INMAX + 4;        // LDS row stride of obs rows
 constexpr int WE_OUTM = RAI_WIDE_MAX_OUT;   // 8
-constexpr int WE_SP = WE_SL + 1;            // padded stride of [rows][16] slices
+constexpr int WE_SP = WE_SL + 4;            // stride of [rows][16] slices: 16-B rows, 4 rows = 16 banks
 constexpr int WE_NSMALL = 2 * WE_SL + WE_OUTM * WE_SL + 2 * WE_OUTM;  // b1 j, b2 j, W3 cols j, b3, log_std
 constexpr int WE_SC1 = 16;                  // buffer cache policy: sc1
 
@@ -59,7 +59,8 @@ constexpr int64_t WE_Z2_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net]
 constexpr int64_t WE_P_SLOT = (int64_t)WE_GMAX * WE_B * WE_OUTM * 4;    // [slice][64][8] f32
 constexpr int64_t WE_P_OFF = WE_Z2_OFF + 4 * WE_ACT_SLOT;               // [net][par] partial slots
 constexpr int64_t WE_N_OFF = WE_P_OFF + 4 * WE_P_SLOT;                  // [par][net][slice] f64
-constexpr int64_t WE_WS_BYTES = WE_N_OFF + 2 * 2 * WE_GMAX * 8;
+constexpr int64_t WE_ADV_OFF = WE_N_OFF + 2 * 2 * WE_GMAX * 8;        // (n_rows) normalized advantages
+inline int64_t we_ws_bytes(int64_t n_rows) { return WE_ADV_OFF + ((n_rows * 4 + 255) & ~(int64_t)255); }
 enum { WE_CA = 0, WE_CB = 2, WE_CC = 4, WE_CD = 6 };
 
 struct WeArgs {
@@ -89,7 +90,7 @@ struct WeSmem {
   float Act[WE_B][WE_HP];     // H1 of the minibatch (all columns), later dZ2
   float W2r[WE_SL][WE_HP];    // W2[16 j + i][:]
   float W2c[WE_SL][WE_HP];    // W2[:][16 j + i] (transposed)
-  float Xs[WE_B][WE_XLD];     // minibatch observations (zero-padded)
+  float Xl[WE_B * WE_INMAX + 4];  // minibatch observations, row stride IN (a linear copy; zero tail)
   float W1j[WE_SL][WE_XLD];   // W1[16 j + i][:]
   float H1j[WE_B][WE_SP];
   float H2j[WE_B][WE_SP];
@@ -99,6 +100,9 @@ struct WeSmem {
   float dls[WE_B][WE_OUTM];
   float Pw[4][WE_B][WE_OUTM];  // per-wave sums of 4 slices' output partials
   float small[WE_NSMALL];     // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
+  double st[4][WE_B];         // per-row loss statistics, reduced off the critical path (D wait)
+  float gvar[WE_OUTM], glsc[WE_OUTM], entc;  // Gaussian variance, log scale, per-row entropy
+  float adamc[2];             // this step's Adam bias-correction constants (formed during the D wait)
   double red[4][8];
   float adv_mean, adv_den;
   int bail;
@@ -140,37 +144,107 @@ __device__ __forceinline__ float we_vf_grad(int fn, float x) {
   return x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x);
 }
 
-// 16 x 16 tile of  Rows[16 tiles rows][k] . Cols[16][k]^T  over k in [0, H) (LDS, ld WE_HP), as
-// mlp_wide.hip's tile_dot: lane group g takes the contiguous quarter [g H/4, (g+1) H/4).
+// 16 x 16 tile of  Rows[16 tiles rows][k] . Cols[16][k]^T  over k in [0, H) (LDS, ld WE_HP): lane
+// group g takes the contiguous quarter [g H/4, (g+1) H/4), four accumulator chains (one per f4
+// component).  For the common widths (KQ = H / 4 a compile-time constant) the loop is unrolled and
+// the next 16-B operands are read while the current four MFMAs issue.
+template <int KQ>
+__device__ __forceinline__ f4 we_tile_dot_k(const float* ra, const float* cb) {
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+  f4 av = *reinterpret_cast<const f4*>(ra), bv = *reinterpret_cast<const f4*>(cb);
+#pragma unroll
+  for (int kk = 0; kk < KQ; kk += 4) {
+    f4 an = av, bn = bv;
+    if (kk + 4 < KQ) {
+      an = *reinterpret_cast<const f4*>(ra + kk + 4);
+      bn = *reinterpret_cast<const f4*>(cb + kk + 4);
+    }
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc3, 0, 0, 0);
+    if (kk + 4 < KQ) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS reads of the next step
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // this step's MFMAs
+    }
+    av = an;
+    bv = bn;
+  }
+  return (acc0 + acc1) + (acc2 + acc3);
+}
 __device__ __forceinline__ f4 we_tile_dot(const float* rows, const float* cols, int H, int lane) {
   const int li = lane & 15, g = lane >> 4, KQ = H >> 2;
   const float* ra = rows + li * WE_HP + g * KQ;
   const float* cb = cols + li * WE_HP + g * KQ;
-  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (H == 256) return we_tile_dot_k<64>(ra, cb);
+  if (H == 128) return we_tile_dot_k<32>(ra, cb);
+  if (H == 64) return we_tile_dot_k<16>(ra, cb);
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
   for (int kk = 0; kk < KQ; kk += 4) {
     const f4 av = *reinterpret_cast<const f4*>(ra + kk);
     const f4 bv = *reinterpret_cast<const f4*>(cb + kk);
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
     acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc3, 0, 0, 0);
   }
-  return acc0 + acc1;
+  return (acc0 + acc1) + (acc2 + acc3);
 }
 
-// dW2 tile: D[i][jj] = sum over the 64 minibatch rows k of A[k][i] * Bm[k][jj], k = 4 kk + g, one
-// accumulator chain.  The row owner calls it with A = its dZ2 slice, Bm = H1 columns; the column
-// owner with A = dZ2 columns, Bm = its H1 slice: the same products in the same order, so both
-// copies of a W2 element receive the same gradient bits.
-__device__ __forceinline__ f4 we_dw2_tile(const float* A, int lda, const float* Bm, int ldb, int lane) {
+// Minibatch row fed by lane group g to the kk-th MFMA of a row-reduction: rows come in blocks of 8,
+// two MFMAs per block, lane groups g = 0..3 taking offsets 0, 4, 2, 6 (+1 in the odd MFMA).  The two
+// lane groups of one ds_read_b32 half-wave (g, g + 1) then read rows 4 apart: with a row stride of
+// 4 (mod 32) dwords (WE_HP, WE_XLD, WE_SP) they sit 16 banks apart -- no bank conflicts.
+__device__ __forceinline__ int we_krow(int kk, int g) {
+  return 8 * (kk >> 1) + (kk & 1) + ((g & 1) << 2) + ((g >> 1) << 1);
+}
+
+// Four dW2 tiles t = 0..3: D_t[i][jj] = sum over the 64 minibatch rows k of A[k][t as + i] *
+// Bm[k][t bs + jj], k = we_krow(kk, g), one accumulator chain per tile, the four chains interleaved
+// (each kk step reads the shared operand once).  The row owner calls it with A = its dZ2 slice (as = 0),
+// Bm = H1 columns 16 (4 w + t) (bs = 16); the column owner with A = dZ2 columns 16 (4 w + t)
+// (as = 16), Bm = its H1 slice (bs = 0): the same products in the same order, so both copies of a W2
+// element receive the same gradient bits.  Tiles past H read in-bounds stale LDS; callers mask them.
+template <int as, int bs>
+__device__ __forceinline__ void we_dw2_tiles4(const float* A, int lda, const float* Bm, int ldb, int lane, f4 out[4]) {
   const int li = lane & 15, g = lane >> 4;
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float* a0 = A + we_krow(0, g) * lda + li;
+  const float* b0 = Bm + we_krow(0, g) * ldb + li;
+  f4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  // operands one kk step ahead: step kk + 1's reads issue before step kk's MFMAs
+  float av[4], bv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    av[t] = a0[t * as];
+    bv[t] = b0[t * bs];
+  }
 #pragma unroll
   for (int kk = 0; kk < WE_B / 4; ++kk) {
-    const int k = 4 * kk + g;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[k * lda + li], Bm[k * ldb + li], acc, 0, 0, 0);
+    const int dk = 8 * ((kk + 1) >> 1) + ((kk + 1) & 1);  // we_krow(kk + 1, g) - we_krow(0, g)
+    float an[4], bn[4];
+    if (kk + 1 < WE_B / 4) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        an[t] = a0[dk * lda + t * as];
+        bn[t] = b0[dk * ldb + t * bs];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc[t], 0, 0, 0);
+    if (kk + 1 < WE_B / 4) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // DS reads of step kk + 1
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMAs of step kk
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        av[t] = an[t];
+        bv[t] = bn[t];
+      }
+    }
   }
-  return acc;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) out[t] = acc[t];
 }
 
 // sum over the 64 minibatch rows of f(r), as four interleaved partial sums (rows r = q mod 4) added
@@ -198,16 +272,17 @@ __device__ __forceinline__ void adam_fast(float& p, float& m, float& v, float g,
 }
 
 // arrive on counter `ci` after every wave's stores drained (caller: s_waitcnt vmcnt(0) in every
-// storing wave, then this); lane 0 polls until ctr[ci] >= want (and ctr[ci2] >= want2).
-__device__ __forceinline__ bool we_arrive_wait(unsigned long long* ctr, int ci, unsigned long long want, int ci2,
-                                               unsigned long long want2, rai_train_state* state, int& bail) {
+// storing wave, then this); lane 0 polls until ctr[ci] >= want.
+// Wave 1 runs `side` (work off the critical path: LDS in, LDS / plain global out) while lane 0 polls.
+template <typename F>
+__device__ __forceinline__ bool we_arrive_wait(unsigned long long* ctr, int ci, unsigned long long want,
+                                               rai_train_state* state, int& bail, int w, F side) {
   __syncthreads();
+  if (w == 1) side();
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(&ctr[ci * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = rai_clock();
-    while (__hip_atomic_load(&ctr[ci * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want ||
-           (ci2 >= 0 &&
-            __hip_atomic_load(&ctr[ci2 * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want2)) {
+    while (__hip_atomic_load(&ctr[ci * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
       if (rai_expired(t0, RAI_SPIN_LOCAL)) {
         __hip_atomic_store(&state->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bail = 1;
@@ -232,7 +307,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   const rai_ppo_hparams& hp = *a.hp;
   const rai_optim_hparams& ohp = *a.ohp;
   unsigned long long* ctr = reinterpret_cast<unsigned long long*>(a.ws);
-  const __amdgpu_buffer_rsrc_t wrs = we_rsrc(a.ws, WE_WS_BYTES);
+  const __amdgpu_buffer_rsrc_t wrs = we_rsrc(a.ws, WE_ADV_OFF);  // the exchange region
   const float* const* W = d.w[net];
   const int64_t pbase_off = 0;
   (void)pbase_off;
@@ -310,6 +385,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   const float c1 = (float)(1.0 - beta1_d), c2 = (float)(1.0 - beta2_d);
   double pw1 = ipow(beta1_d, step0), pw2 = ipow(beta2_d, step0);
   if (tid == 0) S.bail = 0;
+  if (tid < 4) S.Xl[WE_B * WE_INMAX + tid] = 0.f;
   __syncthreads();
 
   // the next minibatch's inputs are loaded into registers one step ahead: its observations (all
@@ -322,11 +398,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     const int64_t r0 = (int64_t)m * B;
     const int rws = (int)min((int64_t)B, n_rows - r0);
 #pragma unroll
-    for (int u = 0; u < XU; ++u) {
+    for (int u = 0; u < XU; ++u) {  // the minibatch's rows are contiguous: a linear copy
       const int e = tid + WE_NT * u;
-      const int r = e / IN4, k = e - r * IN4;
-      const bool ok = e < WE_B * IN4 && r < rws && k < IN;
-      const float x = a.obs[ok ? (r0 + r) * IN + k : 0];
+      const bool ok = e < rws * IN;
+      const float x = a.obs[r0 * IN + (ok ? e : 0)];
       xr[u] = ok ? x : 0.f;
     }
     if (w == 0) {
@@ -360,22 +435,68 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     const unsigned long long want = (unsigned long long)G * (mb + 1);
     // ---- observations of the minibatch -> LDS (zero rows / columns beyond the data) ----------
 #pragma unroll
-    for (int u = 0; u < XU; ++u) {
-      const int e = tid + WE_NT * u;
-      if (e < WE_B * IN4) S.Xs[e / IN4][e % IN4] = xr[u];
-    }
+    for (int u = 0; u < XU; ++u) S.Xl[tid + WE_NT * u] = xr[u];
     float c_act[WE_OUTM];
 #pragma unroll
     for (int o = 0; o < WE_OUTM; ++o) c_act[o] = pa[o];
     const int64_t c_ai = p_ai;
-    const float c_lpold = p_lpold, c_adv = p_adv, c_ret = p_ret, c_vold = p_vold;
+    const float c_lpold = p_lpold, c_ret = p_ret, c_vold = p_vold;
+    const float c_adv = p_adv;
     lds_barrier();
+    // wave 1 during the A wait: the Gaussian head's per-step constants of Normal(mu, exp(log_std)) --
+    // variance, log scale (lane o) and the per-row entropy summed over dims in order
+    auto side_a = [&]() {
+      if (net != 0 || HEAD != 1) return;
+      const float* ls = &S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM];
+      const float scale = expf(ls[lane < O ? lane : 0]);
+      const float lsc = logf(scale);
+      if (lane < WE_OUTM) {
+        S.gvar[lane] = scale * scale;
+        S.glsc[lane] = lsc;
+      }
+      float ent = 0.f;
+      for (int o = 0; o < O; ++o)
+        ent += 1.4189385332046727f + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lsc), o));
+      if (lane == 0) S.entc = ent;
+    };
+    // wave 1 during the D wait: the minibatch's loss statistics (per-row values left in S.st)
+    auto side_d = [&]() {
+      pw1 *= beta1_d;
+      pw2 *= beta2_d;
+      if (lane == 0) {
+        S.adamc[0] = 1.f / (float)sqrt(1.0 - pw2);
+        S.adamc[1] = (float)(-((double)lr / (1.0 - pw1)));
+      }
+      double st[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st[i] = wave_sum_dpp(S.st[i][lane]);
+      if (j == 0 && lane == 0 && a.stats) {
+        const int srow = stat0 + mb;
+        if (srow < a.max_stats) {
+          float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
+          const double Bd = (double)rows;
+          if (net == 0) {
+            const float pi_loss = (float)(-st[0] / Bd);
+            const float ent_loss = (float)(-st[3] / (double)(HEAD == 1 ? rows * O : rows));
+            row[0] = pi_loss + hp.ent_coef * ent_loss;  // the host adds vf_coef * v_loss
+            row[1] = pi_loss;
+            row[2] = ent_loss;
+            row[3] = (float)(st[1] / Bd);
+            row[4] = (float)(st[2] / Bd);
+          } else {
+            row[5] = (float)(st[0] / Bd) * (hp.ppo2_vf_coef_halving ? 0.5f : 1.f);
+            row[5 + RAI_MAX_K] = hp.has_clip_range_vf ? (float)(st[1] / Bd) : 0.f;
+          }
+        }
+      }
+    };
     // ============ fwd1: H1[:, j] = act(X W1[j]^T + b1[j]); wave w: row tile w =============
     {
       f4 z = {0.f, 0.f, 0.f, 0.f};
       for (int kk = 0; kk < IN4 / 4; ++kk) {
         const int k = 4 * kk + g;
-        z = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Xs[16 * w + li][k], S.W1j[li][k], z, 0, 0, 0);
+        // k in [IN, IN4) reads the next row (or the zero tail) against W1j's zero padding
+        z = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Xl[(16 * w + li) * IN + k], S.W1j[li][k], z, 0, 0, 0);
       }
       const float bj = S.small[li];
 #pragma unroll
@@ -390,7 +511,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     WSTAMP(0);
-    if (!we_arrive_wait(ctr, WE_CA + net, want, -1, 0, a.state, S.bail)) break;
+    if (!we_arrive_wait(ctr, WE_CA + net, want, a.state, S.bail, w, side_a)) break;
     WSTAMP(1);
     {  // gather H1 (B x H) -> Act
       const int n4 = WE_B * H / 4, per_row = H / 4;
@@ -411,6 +532,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
+    WSTAMP(2);
     // ============ fwd2: H2[:, j] = act(H1 W2[j]^T + b2[j]); wave w: row tile w =============
     {
       const f4 z = we_tile_dot(&S.Act[16 * w][0], &S.W2r[0][0], H, lane);
@@ -438,9 +560,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    WSTAMP(2);
-    if (!we_arrive_wait(ctr, WE_CB + net, want, -1, 0, a.state, S.bail)) break;
     WSTAMP(3);
+    if (!we_arrive_wait(ctr, WE_CB + net, want, a.state, S.bail, w, [] {})) break;
+    WSTAMP(4);
     // ============ head + loss, all rows (identical on every workgroup of the network) ========
     {  // slice partials: wave w sums slices [4 w, 4 w + 4) for row = lane (loads issued together)
       const int64_t base = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT;
@@ -464,6 +586,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       *reinterpret_cast<f4*>(&S.Pw[w][lane][4]) = sb;
     }
     lds_barrier();
+    WSTAMP(5);
     if (w == 0) {
       const int r = lane;
       const bool valid = r < rows;
@@ -477,42 +600,24 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma unroll
       for (int o = 0; o < WE_OUTM; ++o) dout[o] = dl[o] = 0.f;
       // statistics: [0] sum min(s1, s2) | loss, [1] sum kl | vclipped, [2] clipped, [3] entropy
-      double st[4] = {0.0, 0.0, 0.0, 0.0};
+      double st[4] = {0.0, 0.0, 0.0, 0.0};  // per row; summed by side_d
       const float invB = 1.f / (float)rows;
       if (net == 0) {
 #pragma clang fp contract(off)
-        // advantage moments over the minibatch (two passes, fp64 sums; ppo.py:313-316)
-        const float x = valid ? c_adv : 0.f;
-        float A = x;
-        if (hp.normalize_advantage || hp.standardize_advantage) {
-          const double s1 = wave_sum(valid ? (double)x : 0.0);
-          const float mean = (float)(s1 / (double)rows);
-          const double dv = (double)x - (double)mean;
-          const double s2 = wave_sum(valid ? dv * dv : 0.0);
-          const float den = (float)sqrt(s2 / (double)(rows - 1)) + 1e-8f;
-          A = hp.normalize_advantage ? (x - mean) / den : x / den;
-        }
+        const float A = c_adv;  // normalized per minibatch by we_adv_norm_kernel before the epoch
         float lp = 0.f, ent = 0.f;  // log-prob of the action, entropy (summed over dims)
-        // Normal(mu, exp(log_std)) per-dimension constants, formed once per step
-        float gvar[WE_OUTM], glsc[WE_OUTM];
+        float gvar[WE_OUTM];
         if (HEAD == 1) {
 #pragma unroll
-          for (int o = 0; o < WE_OUTM; ++o) {
-            const float scale = expf(S.small[2 * WE_SL + WE_OUTM * WE_SL + WE_OUTM + (o < O ? o : 0)]);
-            gvar[o] = scale * scale;
-            glsc[o] = logf(scale);
-          }
-        }
-        if (HEAD == 1) {
+          for (int o = 0; o < WE_OUTM; ++o) gvar[o] = S.gvar[o];
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o)
             if (o < O) {
               const float var = gvar[o];
-              const float log_scale = glsc[o];
               const float xo = c_act[o] - out[o];
-              lp += -(xo * xo) / (2.f * var) - log_scale - 0.91893853320467274f;
-              ent += 1.4189385332046727f + log_scale;
+              lp += -(xo * xo) / (2.f * var) - S.glsc[o] - 0.91893853320467274f;
             }
+          ent = S.entc;
         } else {
           const int64_t ai = c_ai;
           float mx = out[0];
@@ -626,29 +731,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         S.dls[r][o] = dl[o];
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) st[i] = wave_sum(st[i]);
-      if (j == 0 && lane == 0 && a.stats) {
-        const int srow = stat0 + mb;
-        if (srow < a.max_stats) {
-          float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
-          const double Bd = (double)rows;
-          if (net == 0) {
-            const float pi_loss = (float)(-st[0] / Bd);
-            const float ent_loss = (float)(-st[3] / (double)(HEAD == 1 ? rows * O : rows));
-            row[0] = pi_loss + hp.ent_coef * ent_loss;  // the host adds vf_coef * v_loss
-            row[1] = pi_loss;
-            row[2] = ent_loss;
-            row[3] = (float)(st[1] / Bd);
-            row[4] = (float)(st[2] / Bd);
-          } else {
-            row[5] = (float)(st[0] / Bd) * (hp.ppo2_vf_coef_halving ? 0.5f : 1.f);
-            row[5 + RAI_MAX_K] = hp.has_clip_range_vf ? (float)(st[1] / Bd) : 0.f;
-          }
-        }
-      }
+      for (int i = 0; i < 4; ++i) S.st[i][r] = st[i];
     }
     lds_barrier();
-    WSTAMP(4);
+    WSTAMP(6);
     // ============ bwd2 (local): dZ2[:, j], publish; dW2 rows j; small gradients ===============
     {
       const int r = tid >> 2, q = tid & 3;
@@ -670,7 +756,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
-    WSTAMP(5);
+    WSTAMP(7);
     // while dZ2 lands: small-parameter gradients and dW2 rows j (H1 still in Act)
     float g_s = 0.f;
     if (tid < WE_NSMALL && fs >= 0) {
@@ -691,12 +777,11 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     f4 g_r[4];
+    we_dw2_tiles4<0, WE_SL>(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * 4 * w], WE_HP, lane, g_r);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int ct = 4 * w + t;
-      g_r[t] = ct < G ? we_dw2_tile(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * ct], WE_HP, lane) : f4{0.f, 0.f, 0.f, 0.f};
-    }
-    WSTAMP(6);
+    for (int t = 0; t < 4; ++t)
+      if (4 * w + t >= G) g_r[t] = f4{0.f, 0.f, 0.f, 0.f};
+    WSTAMP(8);
     // wait for every workgroup's dZ2 slice
     if (tid == 0) {
       const unsigned long long t0 = rai_clock();
@@ -712,7 +797,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
     __syncthreads();  // also: every wave is done reading H1 from Act
     if (S.bail) break;
-    WSTAMP(7);
+    WSTAMP(9);
     {  // gather dZ2 (B x H) -> Act
       const int n4 = WE_B * H / 4, per_row = H / 4;
       const int64_t base = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
@@ -732,13 +817,14 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
+    WSTAMP(10);
     // ============ bwd1: dW2 columns j, dH1[:, j] -> dZ1, dW1 rows j, db1 j ====================
     f4 g_c[4];
+    we_dw2_tiles4<WE_SL, 0>(&S.Act[0][WE_SL * 4 * w], WE_HP, &S.H1j[0][0], WE_SP, lane, g_c);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int rt = 4 * w + t;
-      g_c[t] = rt < G ? we_dw2_tile(&S.Act[0][WE_SL * rt], WE_HP, &S.H1j[0][0], WE_SP, lane) : f4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int t = 0; t < 4; ++t)
+      if (4 * w + t >= G) g_c[t] = f4{0.f, 0.f, 0.f, 0.f};
+    WSTAMP(11);
     {
       const f4 z = we_tile_dot(&S.Act[16 * w][0], &S.W2c[0][0], H, lane);
 #pragma unroll
@@ -748,12 +834,14 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
+    WSTAMP(12);
     f4 g_1 = {0.f, 0.f, 0.f, 0.f};  // dW1[16 j + 4 g + r][16 w + li]
     if (WE_SL * w < IN) {
       const int li_c = WE_SL * w + li;
+#pragma unroll
       for (int kk = 0; kk < WE_B / 4; ++kk) {
-        const int k = 4 * kk + g;
-        g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Z1j[k][li], li_c < WE_XLD ? S.Xs[k][min(li_c, WE_XLD - 1)] : 0.f,
+        const int k = we_krow(kk, g);
+        g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Z1j[k][li], S.Xl[k * IN + min(li_c, IN - 1)],
                                                    g_1, 0, 0, 0);
       }
     }
@@ -775,7 +863,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       const bool count_small = tid < WE_NSMALL && fs >= 0 &&
                                (tid < 2 * WE_SL + WE_OUTM * WE_SL || j == 0);
       if (count_small) ss += (double)g_s * (double)g_s;
-      ss = wave_sum(ss);
+      ss = wave_sum_dpp(ss);
       if (lane == 0) S.red[0][w] = ss;
       __syncthreads();
       if (tid == 0) {
@@ -788,24 +876,21 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     // the next minibatch's inputs, issued after this step's last store drain: they land during the
     // D wait and Adam, before the next drain (vmcnt counts loads and stores together)
     if (mb + 1 < nmb) prefetch(mb + 1);
-    WSTAMP(8);
-    if (!we_arrive_wait(ctr, WE_CD, 2 * want, -1, 0, a.state, S.bail)) break;
-    WSTAMP(9);
+    WSTAMP(13);
+    if (!we_arrive_wait(ctr, WE_CD, 2 * want, a.state, S.bail, w, side_d)) break;
+    WSTAMP(14);
     {
       // the 2 G shares, net-major then slice order: lane l < 2 G loads share l; fixed-order wave sum
       const int l = lane < 2 * G ? lane : 0;
       const int nn = l / G, jj = l - nn * G;
       const int64_t off = WE_N_OFF + ((int64_t)(par * 2 + nn) * WE_GMAX + jj) * 8;
       const double sh = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wrs, (int)off, 0, WE_SC1));
-      const double tot = wave_sum(lane < 2 * G ? sh : 0.0);
+      const double tot = wave_sum_dpp(lane < 2 * G ? sh : 0.0);
       const float total_norm = (float)sqrt(tot);
       float coef = 1.f;
       if (ohp.max_grad_norm > 0.f) coef = fminf(ohp.max_grad_norm / (total_norm + 1e-6f), 1.f);
       if (net == 0 && j == 0 && tid == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;
-      pw1 *= beta1_d;
-      pw2 *= beta2_d;
-      const double bc1 = 1.0 - pw1, bc2 = 1.0 - pw2;
-      const float inv_c3 = 1.f / (float)sqrt(bc2), c4 = (float)(-((double)lr / bc1));
+      const float inv_c3 = S.adamc[0], c4 = S.adamc[1];
       // W2 row slice
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -850,7 +935,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
-    WSTAMP(10);
+    WSTAMP(15);
   }
 #ifdef RAI_STAMPS
   if (j == 0 && tid == 0)
@@ -902,6 +987,33 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   }
 }
 
+// Per-minibatch advantage normalization of the epoch's permuted rows (ppo.py:313-316: mean and the
+// unbiased std over the minibatch, fp64 two-pass sums), one wave per minibatch, before the epoch:
+// it depends on no parameter, so the epoch kernel reads the normalized values instead of forming
+// them on its critical path.  Without normalization the values are copied.
+__global__ __launch_bounds__(256) void we_adv_norm_kernel(const float* adv, int64_t n_rows, int B,
+                                                          const rai_ppo_hparams* hpp, float* out) {
+#pragma clang fp contract(off)
+  const int64_t mb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = mb * B;
+  if (r0 >= n_rows) return;  // wave-uniform
+  const rai_ppo_hparams& hp = *hpp;
+  const int rows = (int)min((int64_t)B, n_rows - r0);
+  const bool valid = lane < rows;
+  const float x = valid ? adv[r0 + lane] : 0.f;
+  float A = x;
+  if (hp.normalize_advantage || hp.standardize_advantage) {
+    const double s1 = wave_sum_dpp(valid ? (double)x : 0.0);
+    const float mean = (float)(s1 / (double)rows);
+    const double dv = (double)x - (double)mean;
+    const double s2 = wave_sum_dpp(valid ? dv * dv : 0.0);
+    const float den = (float)sqrt(s2 / (double)(rows - 1)) + 1e-8f;
+    A = hp.normalize_advantage ? (x - mean) / den : x / den;
+  }
+  if (valid) out[r0 + lane] = A;
+}
+
 template <int HEAD>
 __global__ __launch_bounds__(WE_NT) void mlp_wide_epoch_kernel(const WeArgs a) {
   static_assert(sizeof(WeSmem) <= 160 * 1024, "LDS budget");
@@ -919,9 +1031,9 @@ extern "C" int rai_wide_epoch_debug_stamps(unsigned long long* host_out) {
 }
 #endif
 
-extern "C" int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden) {
+extern "C" int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden, int64_t n_rows) {
   (void)hidden;
-  return WE_WS_BYTES;
+  return n_rows < 0 ? -1 : we_ws_bytes(n_rows);
 }
 
 extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq,
@@ -934,8 +1046,8 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   if (!desc || !params || !exp_avg || !exp_avg_sq || !obs || !actions || !old_logp || !old_values || !advantages ||
       !returns || !hp || !ohp || !state || !workspace)
     return RAI_E_NULLPTR;
-  if (workspace_bytes < WE_WS_BYTES) return RAI_E_WORKSPACE;
   if (n_rows < 2 || batch_size < 2 || batch_size > WE_B) return RAI_E_SHAPE;
+  if (workspace_bytes < we_ws_bytes(n_rows)) return RAI_E_WORKSPACE;
   if (n_rows % batch_size == 1) return RAI_E_SHAPE;  // a 1-row minibatch has no unbiased std
   const int H = desc->hidden;
   if (H < WE_SL || H > WE_HMAX || H % WE_SL != 0) return RAI_E_UNSUPPORTED;
@@ -959,7 +1071,7 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   a.actions = actions;
   a.old_logp = old_logp;
   a.old_values = old_values;
-  a.adv = advantages;
+  a.adv = reinterpret_cast<const float*>(static_cast<unsigned char*>(workspace) + WE_ADV_OFF);
   a.ret = returns;
   a.n_rows = n_rows;
   a.batch = batch_size;
@@ -974,6 +1086,10 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   hipStream_t s = rai_stream(stream);
   const hipError_t e = hipMemsetAsync(workspace, 0, WE_CTR_BYTES, s);  // monotonic counters start at 0
   if (e != hipSuccess) return (int)e;
+  const int64_t nmb = (n_rows + batch_size - 1) / batch_size;
+  hipLaunchKernelGGL(we_adv_norm_kernel, dim3((unsigned)((nmb + 3) / 4)), dim3(256), 0, s, advantages, n_rows,
+                     (int)batch_size, hp, const_cast<float*>(a.adv));
+  RAI_LAUNCH_CHECK();
   const dim3 grid(8 * (H / WE_SL));
   if (desc->head == 1) hipLaunchKernelGGL(mlp_wide_epoch_kernel<1>, grid, dim3(WE_NT), 0, s, a);
   else hipLaunchKernelGGL(mlp_wide_epoch_kernel<0>, grid, dim3(WE_NT), 0, s, a);

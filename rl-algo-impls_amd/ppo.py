@@ -584,9 +584,9 @@ class PPO:
         opt = self.optimizer
         L = _lib.lib()
         st = _lib.stream_handle(self.device)
-        if getattr(self, "_we_ws", None) is None:
-            self._we_ws = torch.zeros(int(L.rai_mlp_wide_epoch_workspace_bytes(wide.spec["hidden"])),
-                                      dtype=torch.uint8, device=self.device)
+        ws_bytes = int(L.rai_mlp_wide_epoch_workspace_bytes(wide.spec["hidden"], r.total_steps))
+        if getattr(self, "_we_ws", None) is None or self._we_ws.numel() < ws_bytes:
+            self._we_ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
         cur = torch.cuda.current_stream(self.device)
         two_slots = hasattr(r, "alloc_epoch_buffers")
         side = self._epoch_prep_stream() if two_slots else cur

@@ -22,9 +22,10 @@ from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
 from rl_algo_impls_amd.ppo import PPO  # noqa: E402
 from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 
-NAMES = ["X + fwd1 + publish H1", "A wait", "gather H1 + fwd2 + publish P", "B wait", "head + loss",
-         "bwd2 dZ2 + publish", "small grads + dW2 rows", "C wait", "gather dZ2 + dW2 cols + dH1 + dW1 + norm",
-         "D wait", "clip + Adam"]
+NAMES = ["X + fwd1 + publish H1", "A wait (wave 1: advantage norm)", "gather H1", "fwd2 + partials + publish P",
+         "B wait", "load partials", "head + loss (wave 0)", "bwd2 dZ2 + publish", "small grads + dW2 rows",
+         "C wait", "gather dZ2", "dW2 cols", "dH1 + dZ1", "dW1 + db1 + norm share", "D wait (wave 1: stats)",
+         "clip + Adam"]
 lib = _lib.lib()
 fn = getattr(lib, "rai_wide_epoch_debug_stamps")
 fn.restype = C.c_int
