@@ -101,8 +101,9 @@ struct WeSmem {
   float Pw[4][WE_B][WE_OUTM];  // per-wave sums of 4 slices' output partials
   float small[WE_NSMALL];     // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
   double st[4][WE_B];         // per-row loss statistics, reduced off the critical path (D wait)
-  float gvar[WE_OUTM], glsc[WE_OUTM], entc;  // Gaussian variance, log scale, per-row entropy
+  float ginv[WE_OUTM], glsc[WE_OUTM], entc;  // Gaussian 1 / variance, log scale, per-row entropy
   float adamc[2];             // this step's Adam bias-correction constants (formed during the D wait)
+  float db1[WE_SL];           // db1 j (wave 3)
   double red[4][8];
   float adv_mean, adv_den;
   int bail;
@@ -111,7 +112,7 @@ struct WeSmem {
 #ifdef RAI_STAMPS
 // diagnostic build only (lib/librai_amd_stamps.so, tools/wide_stamps.py): per-phase shader-clock ticks
 // of workgroup 0 of each network, accumulated over launches
-__device__ unsigned long long g_we_stamps[2][16];
+__device__ unsigned long long g_we_stamps[2][24];
 #define WSTAMP(i)                                                             \
   do {                                                                        \
     if (j == 0 && threadIdx.x == 0) {                                         \
@@ -425,7 +426,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   };
   if (nmb > 0) prefetch(0);
 #ifdef RAI_STAMPS
-  unsigned long long st_acc[16] = {0}, t_last = __builtin_amdgcn_s_memtime();
+  unsigned long long st_acc[24] = {0}, t_last = __builtin_amdgcn_s_memtime();
 #endif
 
   for (int mb = 0; mb < nmb; ++mb) {
@@ -451,7 +452,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       const float scale = expf(ls[lane < O ? lane : 0]);
       const float lsc = logf(scale);
       if (lane < WE_OUTM) {
-        S.gvar[lane] = scale * scale;
+        S.ginv[lane] = 1.f / (scale * scale);
         S.glsc[lane] = lsc;
       }
       float ent = 0.f;
@@ -541,6 +542,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       for (int r = 0; r < 4; ++r) S.H2j[16 * w + 4 * g + r][li] = we_act(act, z[r] + bj);
     }
     lds_barrier();
+    WSTAMP(3);
     {  // output-layer partials over the slice: P[row][o] = sum_c H2[row][c] W3[o][16 j + c]
       if (tid < WE_B * 2) {
         const int r = tid >> 1, o0 = 4 * (tid & 1);
@@ -560,9 +562,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    WSTAMP(3);
-    if (!we_arrive_wait(ctr, WE_CB + net, want, a.state, S.bail, w, [] {})) break;
     WSTAMP(4);
+    if (!we_arrive_wait(ctr, WE_CB + net, want, a.state, S.bail, w, [] {})) break;
+    WSTAMP(5);
     // ============ head + loss, all rows (identical on every workgroup of the network) ========
     {  // slice partials: wave w sums slices [4 w, 4 w + 4) for row = lane (loads issued together)
       const int64_t base = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT;
@@ -586,7 +588,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       *reinterpret_cast<f4*>(&S.Pw[w][lane][4]) = sb;
     }
     lds_barrier();
-    WSTAMP(5);
+    WSTAMP(6);
     if (w == 0) {
       const int r = lane;
       const bool valid = r < rows;
@@ -606,16 +608,17 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma clang fp contract(off)
         const float A = c_adv;  // normalized per minibatch by we_adv_norm_kernel before the epoch
         float lp = 0.f, ent = 0.f;  // log-prob of the action, entropy (summed over dims)
-        float gvar[WE_OUTM];
+        // Normal.log_prob's divisions by var and 2 var as products with the per-step reciprocal
+        // (within an ulp of torch's quotients)
+        float ginv[WE_OUTM];
         if (HEAD == 1) {
 #pragma unroll
-          for (int o = 0; o < WE_OUTM; ++o) gvar[o] = S.gvar[o];
+          for (int o = 0; o < WE_OUTM; ++o) ginv[o] = S.ginv[o];
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o)
             if (o < O) {
-              const float var = gvar[o];
               const float xo = c_act[o] - out[o];
-              lp += -(xo * xo) / (2.f * var) - S.glsc[o] - 0.91893853320467274f;
+              lp += -(xo * xo) * (0.5f * ginv[o]) - S.glsc[o] - 0.91893853320467274f;
             }
           ent = S.entc;
         } else {
@@ -659,10 +662,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o)
             if (o < O) {
-              const float var = gvar[o];
               const float xo = c_act[o] - out[o];
-              dout[o] = d_logp * (xo / var);
-              dl[o] = d_logp * ((xo * xo) / var - 1.f) + d_ent;
+              dout[o] = d_logp * (xo * ginv[o]);
+              dl[o] = d_logp * ((xo * xo) * ginv[o] - 1.f) + d_ent;
             }
         } else {
           const int64_t ai = c_ai;
@@ -725,6 +727,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
           st[1] = (double)vcf;
         }
       }
+      WSTAMP(7);
 #pragma unroll
       for (int o = 0; o < WE_OUTM; ++o) {
         S.dOut[r][o] = dout[o];
@@ -734,7 +737,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       for (int i = 0; i < 4; ++i) S.st[i][r] = st[i];
     }
     lds_barrier();
-    WSTAMP(6);
+    WSTAMP(8);
     // ============ bwd2 (local): dZ2[:, j], publish; dW2 rows j; small gradients ===============
     {
       const int r = tid >> 2, q = tid & 3;
@@ -756,7 +759,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
-    WSTAMP(7);
+    WSTAMP(9);
     // while dZ2 lands: small-parameter gradients and dW2 rows j (H1 still in Act)
     float g_s = 0.f;
     if (tid < WE_NSMALL && fs >= 0) {
@@ -776,12 +779,13 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         }
       }
     }
+    WSTAMP(10);
     f4 g_r[4];
     we_dw2_tiles4<0, WE_SL>(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * 4 * w], WE_HP, lane, g_r);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       if (4 * w + t >= G) g_r[t] = f4{0.f, 0.f, 0.f, 0.f};
-    WSTAMP(8);
+    WSTAMP(11);
     // wait for every workgroup's dZ2 slice
     if (tid == 0) {
       const unsigned long long t0 = rai_clock();
@@ -797,7 +801,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
     __syncthreads();  // also: every wave is done reading H1 from Act
     if (S.bail) break;
-    WSTAMP(9);
+    WSTAMP(12);
     {  // gather dZ2 (B x H) -> Act
       const int n4 = WE_B * H / 4, per_row = H / 4;
       const int64_t base = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
@@ -817,14 +821,14 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
-    WSTAMP(10);
+    WSTAMP(13);
     // ============ bwd1: dW2 columns j, dH1[:, j] -> dZ1, dW1 rows j, db1 j ====================
     f4 g_c[4];
     we_dw2_tiles4<WE_SL, 0>(&S.Act[0][WE_SL * 4 * w], WE_HP, &S.H1j[0][0], WE_SP, lane, g_c);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       if (4 * w + t >= G) g_c[t] = f4{0.f, 0.f, 0.f, 0.f};
-    WSTAMP(11);
+    WSTAMP(14);
     {
       const f4 z = we_tile_dot(&S.Act[16 * w][0], &S.W2c[0][0], H, lane);
 #pragma unroll
@@ -834,20 +838,55 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
-    WSTAMP(12);
+    WSTAMP(15);
     f4 g_1 = {0.f, 0.f, 0.f, 0.f};  // dW1[16 j + 4 g + r][16 w + li]
     if (WE_SL * w < IN) {
-      const int li_c = WE_SL * w + li;
+      // two accumulator chains (even / odd kk), operands read one step ahead
+      const float* za = &S.Z1j[we_krow(0, g)][li];
+      const float* xa = &S.Xl[we_krow(0, g) * IN + min(WE_SL * w + li, IN - 1)];
+      f4 g_1b = {0.f, 0.f, 0.f, 0.f};
+      float zv = za[0], xv = xa[0];
 #pragma unroll
       for (int kk = 0; kk < WE_B / 4; ++kk) {
-        const int k = we_krow(kk, g);
-        g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Z1j[k][li], S.Xl[k * IN + min(li_c, IN - 1)],
-                                                   g_1, 0, 0, 0);
+        const int dk = 8 * ((kk + 1) >> 1) + ((kk + 1) & 1);
+        float zn = zv, xn = xv;
+        if (kk + 1 < WE_B / 4) {
+          zn = za[dk * WE_SP];
+          xn = xa[dk * IN];
+        }
+        if (kk & 1) g_1b = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, xv, g_1b, 0, 0, 0);
+        else g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, xv, g_1, 0, 0, 0);
+        if (kk + 1 < WE_B / 4) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        zv = zn;
+        xv = xn;
+      }
+      g_1 += g_1b;
+    }
+    WSTAMP(16);
+    // db1 (wave 3, all lanes): lane (c = lane & 15, q = lane >> 4) sums rows [16 q, 16 q + 16) of
+    // column c in four chains; the quarters are added by the row / half swaps
+    float db1_sq = 0.f;
+    if (w == 3) {
+      const int c = lane & 15, q = lane >> 4;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; r += 4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += S.Z1j[16 * q + r + u][c];
+      float v = ((acc[0] + acc[1]) + acc[2]) + acc[3];
+      const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+      const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+      if (lane < WE_SL) {
+        S.db1[lane] = v;
+        db1_sq = v;  // its square joins wave 3's norm share
       }
     }
-    if (tid < WE_SL) {
-      g_s = we_rowsum([&](int r) { return S.Z1j[r][tid]; });  // db1
-    }
+    WSTAMP(17);
     // ============ D: this workgroup's share of |g|^2, then clip_grad_norm_ + Adam =============
     {
       double ss = 0.0;
@@ -862,7 +901,8 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       // b3 and log_std are counted once, by workgroup 0
       const bool count_small = tid < WE_NSMALL && fs >= 0 &&
                                (tid < 2 * WE_SL + WE_OUTM * WE_SL || j == 0);
-      if (count_small) ss += (double)g_s * (double)g_s;
+      if (count_small && tid >= WE_SL) ss += (double)g_s * (double)g_s;  // db1: wave 3 below
+      ss += (double)db1_sq * (double)db1_sq;
       ss = wave_sum_dpp(ss);
       if (lane == 0) S.red[0][w] = ss;
       __syncthreads();
@@ -873,12 +913,13 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
+    WSTAMP(18);
     // the next minibatch's inputs, issued after this step's last store drain: they land during the
     // D wait and Adam, before the next drain (vmcnt counts loads and stores together)
     if (mb + 1 < nmb) prefetch(mb + 1);
-    WSTAMP(13);
+    WSTAMP(19);
     if (!we_arrive_wait(ctr, WE_CD, 2 * want, a.state, S.bail, w, side_d)) break;
-    WSTAMP(14);
+    WSTAMP(20);
     {
       // the 2 G shares, net-major then slice order: lane l < 2 G loads share l; fixed-order wave sum
       const int l = lane < 2 * G ? lane : 0;
@@ -930,16 +971,16 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
       if (tid < WE_NSMALL && fs >= 0) {
         float pv = S.small[tid];
-        adam_fast(pv, m_s, v_s, g_s * coef, c1, c2, beta2, inv_c3, c4, eps);
+        adam_fast(pv, m_s, v_s, (tid < WE_SL ? S.db1[tid] : g_s) * coef, c1, c2, beta2, inv_c3, c4, eps);
         S.small[tid] = pv;
       }
     }
     lds_barrier();
-    WSTAMP(15);
+    WSTAMP(21);
   }
 #ifdef RAI_STAMPS
   if (j == 0 && tid == 0)
-    for (int i = 0; i < 16; ++i) atomicAdd(&g_we_stamps[net][i], st_acc[i]);
+    for (int i = 0; i < 24; ++i) atomicAdd(&g_we_stamps[net][i], st_acc[i]);
 #endif
 
   // ---- write back what this workgroup owns: parameters and Adam moments ----------------------

@@ -22,10 +22,10 @@ from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
 from rl_algo_impls_amd.ppo import PPO  # noqa: E402
 from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 
-NAMES = ["X + fwd1 + publish H1", "A wait (wave 1: advantage norm)", "gather H1", "fwd2 + partials + publish P",
-         "B wait", "load partials", "head + loss (wave 0)", "bwd2 dZ2 + publish", "small grads + dW2 rows",
-         "C wait", "gather dZ2", "dW2 cols", "dH1 + dZ1", "dW1 + db1 + norm share", "D wait (wave 1: stats)",
-         "clip + Adam"]
+NAMES = ["X + fwd1 + publish H1", "A wait (wave 1: Gaussian constants)", "gather H1", "fwd2 tile",
+         "partials + publish P", "B wait", "load partials", "loss compute (wave 0)", "loss LDS out + barrier",
+         "bwd2 dZ2 + publish", "small grads", "dW2 rows", "C wait", "gather dZ2", "dW2 cols", "dH1 + dZ1", "dW1",
+         "db1 (wave 3)", "norm share + drain", "prefetch issue", "D wait (wave 1: stats)", "clip + Adam"]
 lib = _lib.lib()
 fn = getattr(lib, "rai_wide_epoch_debug_stamps")
 fn.restype = C.c_int
@@ -42,16 +42,16 @@ algo = PPO(policy, dev, None, batch_size=64, n_epochs=1, learning_rate=2e-5, gam
 r = gen.rollout(gamma=0.98, gae_lambda=0.92)
 algo.update(r)  # warm
 torch.cuda.synchronize()
-out0 = (C.c_ulonglong * 32)()
+out0 = (C.c_ulonglong * 48)()
 assert fn(out0) == 0
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
 algo.update(r)
 ev1.record()
 ev1.synchronize()
-out = (C.c_ulonglong * 32)()
+out = (C.c_ulonglong * 48)()
 assert fn(out) == 0
-st = (np.array(out, dtype=np.float64) - np.array(out0, dtype=np.float64)).reshape(2, 16)
+st = (np.array(out, dtype=np.float64) - np.array(out0, dtype=np.float64)).reshape(2, 24)
 nmb = (r.total_steps + 63) // 64
 assert algo._we_ws is not None, "whole-epoch kernel not used"
 print(f"epoch {ev0.elapsed_time(ev1):.2f} ms for {nmb} minibatches -> {ev0.elapsed_time(ev1) * 1e3 / nmb:.2f} us/mb")
