@@ -90,7 +90,7 @@ struct WeSmem {
   float Act[WE_B][WE_HP];     // H1 of the minibatch (all columns), later dZ2
   float W2r[WE_SL][WE_HP];    // W2[16 j + i][:]
   float W2c[WE_SL][WE_HP];    // W2[:][16 j + i] (transposed)
-  float Xl[WE_B * WE_INMAX + 4];  // minibatch observations, row stride IN (a linear copy; zero tail)
+  alignas(16) float Xl[WE_B * WE_INMAX + 4];  // minibatch observations, row stride IN (a linear copy; zero tail)
   float W1j[WE_SL][WE_XLD];   // W1[16 j + i][:]
   float H1j[WE_B][WE_SP];
   float H2j[WE_B][WE_SP];
@@ -99,7 +99,8 @@ struct WeSmem {
   float dOut[WE_B][WE_OUTM];
   float dls[WE_B][WE_OUTM];
   float Pw[4][WE_B][WE_OUTM];  // per-wave sums of 4 slices' output partials
-  float small[WE_NSMALL];     // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
+  alignas(16) float small[WE_NSMALL];  // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
+  float gsm[WE_NSMALL];       // small-parameter gradients (MFMA column sums), by small index
   double st[4][WE_B];         // per-row loss statistics, reduced off the critical path (D wait)
   float ginv[WE_OUTM], glsc[WE_OUTM], entc;  // Gaussian 1 / variance, log scale, per-row entropy
   float adamc[2];             // this step's Adam bias-correction constants (formed during the D wait)
@@ -274,6 +275,21 @@ __device__ __forceinline__ void adam_fast(float& p, float& m, float& v, float g,
 
 // arrive on counter `ci` after every wave's stores drained (caller: s_waitcnt vmcnt(0) in every
 // storing wave, then this); lane 0 polls until ctr[ci] >= want.
+// Gather a published 64 x H exchange slot (workspace byte offset `base`) into Act (LDS rows of WE_HP
+// floats) by LDS-DMA: one global_load_lds_dwordx4 per row (H / 4 lanes x 16 B, landing contiguously
+// at the row's start), sc1 like every load of handed-off bytes; wave w takes rows w, w + 4, ...  The
+// data lands without VGPRs or ds_write instructions; the caller's barrier follows the vmcnt(0) here.
+__device__ __forceinline__ void we_gather_lds(const unsigned char* ws, int64_t base, int H, float (*Act)[WE_HP], int w,
+                                              int lane) {
+  if (lane < (H >> 2)) {
+    const float* src = reinterpret_cast<const float*>(ws + base) + 4 * lane;
+#pragma unroll
+    for (int r = w; r < WE_B; r += 4)
+      __builtin_amdgcn_global_load_lds(src + (int64_t)r * H, &Act[r][0], 16, 0, WE_SC1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Wave 1 runs `side` (work off the critical path: LDS in, LDS / plain global out) while lane 0 polls.
 template <typename F>
 __device__ __forceinline__ bool we_arrive_wait(unsigned long long* ctr, int ci, unsigned long long want,
@@ -391,19 +407,34 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 
   // the next minibatch's inputs are loaded into registers one step ahead: its observations (all
   // threads) and, for wave 0 (lane = row), the per-row loss inputs
-  constexpr int XU = (WE_B * WE_INMAX + WE_NT - 1) / WE_NT;
-  float xr[XU];
+  // The minibatch's rows are contiguous in the permuted copy: a linear copy of rws * IN floats, as
+  // 16-B loads when every minibatch starts 16-B aligned and the array's end is (x4), else 4-B loads.
+  // Loads past the data are not issued (wave-uniform skip); their registers hold zeros.
+  constexpr int XU4 = WE_B * WE_INMAX / 4 / WE_NT;  // 4 x 16 B per thread
+  const bool x4 = (B * IN) % 4 == 0 && (n_rows * IN) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0;
+  f4 xr[XU4];
   float pa[WE_OUTM], p_lpold = 0.f, p_adv = 0.f, p_ret = 0.f, p_vold = 0.f;
   int64_t p_ai = 0;
   auto prefetch = [&](int m) {
     const int64_t r0 = (int64_t)m * B;
     const int rws = (int)min((int64_t)B, n_rows - r0);
+    const int n = rws * IN;
+    if (x4) {
+      const f4* src = reinterpret_cast<const f4*>(a.obs + r0 * IN);
 #pragma unroll
-    for (int u = 0; u < XU; ++u) {  // the minibatch's rows are contiguous: a linear copy
-      const int e = tid + WE_NT * u;
-      const bool ok = e < rws * IN;
-      const float x = a.obs[r0 * IN + (ok ? e : 0)];
-      xr[u] = ok ? x : 0.f;
+      for (int u = 0; u < XU4; ++u) {
+        const int e4 = tid + WE_NT * u;
+        xr[u] = f4{0.f, 0.f, 0.f, 0.f};
+        if (4 * (WE_NT * u + 64 * w) < n && 4 * e4 < n) xr[u] = src[e4];  // n % 4 == 0 here
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4 * XU4; ++u) {
+        const int e = tid + WE_NT * u;
+        float x = 0.f;
+        if (WE_NT * u + 64 * w < n && e < n) x = a.obs[r0 * IN + e];
+        xr[u >> 2][u & 3] = x;
+      }
     }
     if (w == 0) {
       const bool ok = lane < rws;
@@ -435,8 +466,13 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     const int rows = (int)min((int64_t)B, n_rows - row0);
     const unsigned long long want = (unsigned long long)G * (mb + 1);
     // ---- observations of the minibatch -> LDS (zero rows / columns beyond the data) ----------
+    if (x4) {
 #pragma unroll
-    for (int u = 0; u < XU; ++u) S.Xl[tid + WE_NT * u] = xr[u];
+      for (int u = 0; u < XU4; ++u) reinterpret_cast<f4*>(S.Xl)[tid + WE_NT * u] = xr[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4 * XU4; ++u) S.Xl[tid + WE_NT * u] = xr[u >> 2][u & 3];
+    }
     float c_act[WE_OUTM];
 #pragma unroll
     for (int o = 0; o < WE_OUTM; ++o) c_act[o] = pa[o];
@@ -514,24 +550,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     WSTAMP(0);
     if (!we_arrive_wait(ctr, WE_CA + net, want, a.state, S.bail, w, side_a)) break;
     WSTAMP(1);
-    {  // gather H1 (B x H) -> Act
-      const int n4 = WE_B * H / 4, per_row = H / 4;
-      const int64_t base = WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
-      f4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = min(tid + WE_NT * u, n4 - 1);
-        v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)(base + 16 * (int64_t)i), 0, WE_SC1));
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = tid + WE_NT * u;
-        if (i < n4) {
-          const int r = i / per_row, c = (i - r * per_row) * 4;
-          *reinterpret_cast<f4*>(&S.Act[r][c]) = v[u];
-        }
-      }
-    }
+    we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // H1 -> Act
     lds_barrier();
     WSTAMP(2);
     // ============ fwd2: H2[:, j] = act(H1 W2[j]^T + b2[j]); wave w: row tile w =============
@@ -741,17 +760,17 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     // ============ bwd2 (local): dZ2[:, j], publish; dW2 rows j; small gradients ===============
     {
       const int r = tid >> 2, q = tid & 3;
+      const f4 d0 = *reinterpret_cast<const f4*>(&S.dOut[r][0]), d1 = *reinterpret_cast<const f4*>(&S.dOut[r][4]);
+      const float dr[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+      f4 dh = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int o = 0; o < WE_OUTM; ++o)
+        if (o < O) dh += dr[o] * *reinterpret_cast<const f4*>(&S.small[2 * WE_SL + o * WE_SL + 4 * q]);
+      const f4 h2 = *reinterpret_cast<const f4*>(&S.H2j[r][4 * q]);
       f4 z;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = 4 * q + u;
-        float dh = 0.f;
-#pragma unroll
-        for (int o = 0; o < WE_OUTM; ++o)
-          if (o < O) dh += S.dOut[r][o] * S.small[2 * WE_SL + o * WE_SL + c];
-        z[u] = dh * we_actd(act, S.H2j[r][c]);
-        S.Z2j[r][c] = z[u];
-      }
+      for (int u = 0; u < 4; ++u) z[u] = dh[u] * we_actd(act, h2[u]);
+      *reinterpret_cast<f4*>(&S.Z2j[r][4 * q]) = z;
       const int64_t off = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT + ((int64_t)r * H + WE_SL * j + 4 * q) * 4;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, z), wrs, (int)off, 0, WE_SC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -761,21 +780,34 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
                                          __HIP_MEMORY_SCOPE_AGENT);
     WSTAMP(9);
     // while dZ2 lands: small-parameter gradients and dW2 rows j (H1 still in Act)
-    float g_s = 0.f;
-    if (tid < WE_NSMALL && fs >= 0) {
-      int e = tid;
-      if (e >= WE_SL) {  // b1 j is formed after dZ1 (below)
-        e -= WE_SL;
-        if (e < WE_SL) {  // db2
-          g_s = we_rowsum([&](int r) { return S.Z2j[r][e]; });
-        } else if ((e -= WE_SL) < WE_OUTM * WE_SL) {  // dW3[o][16 j + c]
-          const int o = e / WE_SL, c = e - o * WE_SL;
-          g_s = we_rowsum([&](int r) { return S.dOut[r][o] * S.H2j[r][c]; });
-        } else if ((e -= WE_OUTM * WE_SL) < WE_OUTM) {  // db3
-          g_s = we_rowsum([&](int r) { return S.dOut[r][e]; });
-        } else {  // dlog_std
-          e -= WE_OUTM;
-          g_s = we_rowsum([&](int r) { return S.dls[r][e]; });
+    // small-parameter gradients as three MFMA tiles over the 64 rows (D[i][jj] = sum_k A[k][i] B[k][jj]),
+    // one per wave: wave 0 dW3 = dOut^T H2 (i = o), wave 1 the column sums of [dOut | dls] (db3,
+    // dlog_std), wave 2 those of dZ2 (db2); b1 j is formed after dZ1 (below).  Every workgroup forms
+    // db3 / dlog_std with the same code on the same rows, so their copies stay identical.
+    if (w < 3) {
+      const float* a_src;
+      int lda;
+      if (w == 0) { a_src = li < WE_OUTM ? &S.dOut[0][li] : nullptr; lda = WE_OUTM; }
+      else if (w == 1) { a_src = li < WE_OUTM ? &S.dOut[0][li] : &S.dls[0][li - WE_OUTM]; lda = WE_OUTM; }
+      else { a_src = &S.Z2j[0][li]; lda = WE_SP; }
+      f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+      for (int kk = 0; kk < WE_B / 4; ++kk) {
+        const int k = we_krow(kk, g);
+        const float av = a_src ? a_src[k * lda] : 0.f;
+        const float bv = w == 0 ? S.H2j[k][li] : 1.f;
+        if (kk & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc1, 0, 0, 0);
+        else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
+      }
+      const f4 dsm = acc0 + acc1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * g + r;  // D row; column jj = li
+        if (w == 0) {
+          if (i < WE_OUTM) S.gsm[2 * WE_SL + i * WE_SL + li] = dsm[r];
+        } else if (li == 0) {
+          if (w == 1) S.gsm[2 * WE_SL + WE_OUTM * WE_SL + i] = dsm[r];  // db3 (i < 8), dlog_std (i >= 8)
+          else S.gsm[WE_SL + i] = dsm[r];                               // db2
         }
       }
     }
@@ -802,24 +834,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     __syncthreads();  // also: every wave is done reading H1 from Act
     if (S.bail) break;
     WSTAMP(12);
-    {  // gather dZ2 (B x H) -> Act
-      const int n4 = WE_B * H / 4, per_row = H / 4;
-      const int64_t base = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT;
-      f4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = min(tid + WE_NT * u, n4 - 1);
-        v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)(base + 16 * (int64_t)i), 0, WE_SC1));
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = tid + WE_NT * u;
-        if (i < n4) {
-          const int r = i / per_row, c = (i - r * per_row) * 4;
-          *reinterpret_cast<f4*>(&S.Act[r][c]) = v[u];
-        }
-      }
-    }
+    we_gather_lds(a.ws, WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // dZ2 -> Act
     lds_barrier();
     WSTAMP(13);
     // ============ bwd1: dW2 columns j, dH1[:, j] -> dZ1, dW1 rows j, db1 j ====================
@@ -901,6 +916,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       // b3 and log_std are counted once, by workgroup 0
       const bool count_small = tid < WE_NSMALL && fs >= 0 &&
                                (tid < 2 * WE_SL + WE_OUTM * WE_SL || j == 0);
+      const float g_s = tid < WE_SL ? 0.f : S.gsm[min(tid, WE_NSMALL - 1)];
       if (count_small && tid >= WE_SL) ss += (double)g_s * (double)g_s;  // db1: wave 3 below
       ss += (double)db1_sq * (double)db1_sq;
       ss = wave_sum_dpp(ss);
@@ -971,7 +987,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
       if (tid < WE_NSMALL && fs >= 0) {
         float pv = S.small[tid];
-        adam_fast(pv, m_s, v_s, (tid < WE_SL ? S.db1[tid] : g_s) * coef, c1, c2, beta2, inv_c3, c4, eps);
+        adam_fast(pv, m_s, v_s, (tid < WE_SL ? S.db1[tid] : S.gsm[tid]) * coef, c1, c2, beta2, inv_c3, c4, eps);
         S.small[tid] = pv;
       }
     }

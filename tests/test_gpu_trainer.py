@@ -500,6 +500,7 @@ def _graphed_vs_eager(kind, T, N, bs, extra):
     ("cartpole", 256, "tanh", dict(ent_coef=0.01)),                        # Categorical head, 256 wide
     ("halfcheetah", 64, "relu", dict(gradient_accumulation=True)),         # accumulate mode
     ("halfcheetah", 192, "relu", dict(N=25, clip_range_vf=0.1)),           # 400 rows: ragged tail of 16
+    ("halfcheetah", 128, "relu", dict(bs=50)),  # B IN = 850: 4-B observation staging; ragged tail of 34
 ])
 @pytest.mark.parametrize("epoch", ["1", "0"], ids=["whole_epoch_kernel", "per_minibatch_kernels"])
 def test_wide_mlp_kernels_match_pytorch_path(kind, hidden, act, extra, epoch, monkeypatch):
@@ -514,7 +515,7 @@ def test_wide_mlp_kernels_match_pytorch_path(kind, hidden, act, extra, epoch, mo
     monkeypatch.setenv("RAI_WIDE_EPOCH", epoch)
 
     extra = dict(extra)
-    T, N, bs = 16, extra.pop("N", 24), 64  # 384 rows: 6 minibatches
+    T, N, bs = 16, extra.pop("N", 24), extra.pop("bs", 64)  # 384 rows: 6 minibatches of 64
     res = []
     for wide in (True, False):
         torch.manual_seed(7)
