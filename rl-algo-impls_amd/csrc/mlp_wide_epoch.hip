@@ -55,9 +55,13 @@ constexpr int64_t WE_CTR_STRIDE = 128;                                  // one c
 constexpr int64_t WE_CTR_BYTES = 8 * WE_CTR_STRIDE;                     // A0 A1 B0 B1 C0 C1 D
 constexpr int64_t WE_ACT_SLOT = (int64_t)WE_B * WE_HMAX * 4;            // one [64][H] f32 slot
 constexpr int64_t WE_H1_OFF = WE_CTR_BYTES;                             // [net][par] H1 slots
-constexpr int64_t WE_Z2_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dZ2 slots
+// dH1 partial tiles: [producer slice][unit tile][row tile][64 lanes][4] f32, one 1-KB MFMA tile each
+constexpr int64_t WE_DH_TILE = 1024;
+constexpr int64_t WE_DH_PROD = (int64_t)WE_GMAX * 4 * WE_DH_TILE;        // one producer's tiles
+constexpr int64_t WE_DH_SLOT = WE_GMAX * WE_DH_PROD;
+constexpr int64_t WE_DH_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dH1 partial slots
 constexpr int64_t WE_P_SLOT = (int64_t)WE_GMAX * WE_B * WE_OUTM * 4;    // [slice][64][8] f32
-constexpr int64_t WE_P_OFF = WE_Z2_OFF + 4 * WE_ACT_SLOT;               // [net][par] partial slots
+constexpr int64_t WE_P_OFF = WE_DH_OFF + 4 * WE_DH_SLOT;                // [net][par] output-layer partial slots
 constexpr int64_t WE_N_OFF = WE_P_OFF + 4 * WE_P_SLOT;                  // [par][net][slice] f64
 constexpr int64_t WE_ADV_OFF = WE_N_OFF + 2 * 2 * WE_GMAX * 8;        // (n_rows) normalized advantages
 inline int64_t we_ws_bytes(int64_t n_rows) { return WE_ADV_OFF + ((n_rows * 4 + 255) & ~(int64_t)255); }
@@ -89,7 +93,6 @@ struct WeArgs {
 struct WeSmem {
   float Act[WE_B][WE_HP];     // H1 of the minibatch (all columns), later dZ2
   float W2r[WE_SL][WE_HP];    // W2[16 j + i][:]
-  float W2c[WE_SL][WE_HP];    // W2[:][16 j + i] (transposed)
   alignas(16) float Xl[WE_B * WE_INMAX + 4];  // minibatch observations, row stride IN (a linear copy; zero tail)
   float W1j[WE_SL][WE_XLD];   // W1[16 j + i][:]
   float H1j[WE_B][WE_SP];
@@ -338,7 +341,6 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   for (int e = tid; e < WE_SL * H; e += WE_NT) {
     const int i = e / H, k = e - i * H;
     S.W2r[i][k] = W[2][(int64_t)(WE_SL * j + i) * H + k];
-    S.W2c[i][k] = W[2][(int64_t)k * H + WE_SL * j + i];
   }
   // small parameters: index e -> (tensor, element) in the flat buffer (-1: padding)
   auto small_flat = [&](int e) -> int64_t {
@@ -364,9 +366,8 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     v_s = fs >= 0 ? a.exp_avg_sq[fs] : 0.f;
   }
   // W2 row slice: wave w holds column tiles 4 w + t (t < 4) of row tile j: lane element (t, r) =
-  // W2[16 j + 4 g + r][16 (4 w + t) + li]; column slice: row tiles 4 w + t of column tile j: lane
-  // element (t, r) = W2[16 (4 w + t) + 4 g + r][16 j + li].  Tiles beyond H are inactive.
-  float m_r[4][4], v_r[4][4], m_c[4][4], v_c[4][4];
+  // W2[16 j + 4 g + r][16 (4 w + t) + li].  Tiles beyond H are inactive.
+  float m_r[4][4], v_r[4][4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int ct = 4 * w + t;
@@ -374,11 +375,8 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     for (int r = 0; r < 4; ++r) {
       const bool on = ct < G;
       const int64_t fr = foff(W[2]) + (int64_t)(WE_SL * j + 4 * g + r) * H + WE_SL * ct + li;
-      const int64_t fc = foff(W[2]) + (int64_t)(WE_SL * ct + 4 * g + r) * H + WE_SL * j + li;
       m_r[t][r] = on ? a.exp_avg[fr] : 0.f;
       v_r[t][r] = on ? a.exp_avg_sq[fr] : 0.f;
-      m_c[t][r] = on ? a.exp_avg[fc] : 0.f;
-      v_c[t][r] = on ? a.exp_avg_sq[fc] : 0.f;
     }
   }
   // W1 rows j: wave w holds column tile w: lane element r = W1[16 j + 4 g + r][16 w + li]
@@ -771,15 +769,40 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma unroll
       for (int u = 0; u < 4; ++u) z[u] = dh[u] * we_actd(act, h2[u]);
       *reinterpret_cast<f4*>(&S.Z2j[r][4 * q]) = z;
-      const int64_t off = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT + ((int64_t)r * H + WE_SL * j + 4 * q) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, z), wrs, (int)off, 0, WE_SC1);
+    }
+    lds_barrier();
+    {  // dH1 partials of slice j: P_j[rows 16 w .., units 16 ut ..] = dZ2[:, slice j] W2[slice j, :]
+      // (K = 16, four MFMAs), for every unit tile ut; tile (ut, w) goes lane-major (1 KB, one 16-B
+      // write-through store per lane) to its consumer, workgroup ut, which sums the G producers'
+      // tiles in slice order.  W2 thus lives only in its row owner (one copy, one Adam update).
+      float za[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) za[s4] = S.Z2j[16 * w + li][4 * s4 + g];
+      const int64_t base = WE_DH_OFF + (int64_t)(net * 2 + par) * WE_DH_SLOT + (int64_t)j * WE_DH_PROD +
+                           (int64_t)w * WE_DH_TILE + lane * 16;
+      for (int u0 = 0; u0 < G; u0 += 4) {
+        f4 d[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) d[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[s4], S.W2r[4 * s4 + g][WE_SL * min(u0 + t, G - 1) + li], d[t],
+                                                        0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (u0 + t < G)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d[t]), wrs,
+                                                   (int)(base + (int64_t)(u0 + t) * 4 * WE_DH_TILE), 0, WE_SC1);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     WSTAMP(9);
-    // while dZ2 lands: small-parameter gradients and dW2 rows j (H1 still in Act)
+    // while the partials land: small-parameter gradients and dW2 rows j (H1 still in Act)
     // small-parameter gradients as three MFMA tiles over the 64 rows (D[i][jj] = sum_k A[k][i] B[k][jj]),
     // one per wave: wave 0 dW3 = dOut^T H2 (i = o), wave 1 the column sums of [dOut | dls] (db3,
     // dlog_std), wave 2 those of dZ2 (db2); b1 j is formed after dZ1 (below).  Every workgroup forms
@@ -818,7 +841,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     for (int t = 0; t < 4; ++t)
       if (4 * w + t >= G) g_r[t] = f4{0.f, 0.f, 0.f, 0.f};
     WSTAMP(11);
-    // wait for every workgroup's dZ2 slice
+    // wait for every workgroup's dH1 partials
     if (tid == 0) {
       const unsigned long long t0 = rai_clock();
       while (__hip_atomic_load(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
@@ -831,26 +854,32 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    __syncthreads();  // also: every wave is done reading H1 from Act
+    __syncthreads();
     if (S.bail) break;
     WSTAMP(12);
-    we_gather_lds(a.ws, WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // dZ2 -> Act
-    lds_barrier();
-    WSTAMP(13);
-    // ============ bwd1: dW2 columns j, dH1[:, j] -> dZ1, dW1 rows j, db1 j ====================
-    f4 g_c[4];
-    we_dw2_tiles4<WE_SL, 0>(&S.Act[0][WE_SL * 4 * w], WE_HP, &S.H1j[0][0], WE_SP, lane, g_c);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (4 * w + t >= G) g_c[t] = f4{0.f, 0.f, 0.f, 0.f};
-    WSTAMP(14);
+    // ============ bwd1: dH1[:, j] = sum of the G producers' partial tiles -> dZ1, dW1 rows j, db1 j
     {
-      const f4 z = we_tile_dot(&S.Act[16 * w][0], &S.W2c[0][0], H, lane);
+      // wave w: row tile w; lane (li, g) receives dH1[16 w + 4 g + r][16 j + li], r < 4 (MFMA layout)
+      const int64_t base = WE_DH_OFF + (int64_t)(net * 2 + par) * WE_DH_SLOT + (int64_t)j * 4 * WE_DH_TILE +
+                           (int64_t)w * WE_DH_TILE + lane * 16;
+      f4 z = {0.f, 0.f, 0.f, 0.f};
+      for (int p0 = 0; p0 < G; p0 += 8) {
+        f4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wrs, (int)(base + (int64_t)min(p0 + u, G - 1) * WE_DH_PROD), 0, WE_SC1));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (p0 + u < G) z += v[u];  // producer (slice) order
+      }
+      WSTAMP(13);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * w + 4 * g + r;
         S.Z1j[row][li] = z[r] * we_actd(act, S.H1j[row][li]);
       }
+      WSTAMP(14);
     }
     lds_barrier();
     WSTAMP(15);
@@ -958,20 +987,6 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
             float& p = S.W2r[4 * g + r][WE_SL * ct + li];
             float pv = p;
             adam_fast(pv, m_r[t][r], v_r[t][r], g_r[t][r] * coef, c1, c2, beta2, inv_c3, c4, eps);
-            p = pv;
-          }
-        }
-      }
-      // W2 column slice (the same elements' other copy)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int rt = 4 * w + t;
-        if (rt < G) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float& p = S.W2c[li][WE_SL * rt + 4 * g + r];
-            float pv = p;
-            adam_fast(pv, m_c[t][r], v_c[t][r], g_c[t][r] * coef, c1, c2, beta2, inv_c3, c4, eps);
             p = pv;
           }
         }
