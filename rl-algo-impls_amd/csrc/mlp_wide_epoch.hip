@@ -252,6 +252,33 @@ __device__ __forceinline__ void we_dw2_tiles4(const float* A, int lda, const flo
   for (int t = 0; t < 4; ++t) out[t] = acc[t];
 }
 
+// One 16 x 16 MFMA tile over the 64 minibatch rows, D[i][jj] = sum_k A[k][i] B[k][jj], for the
+// small-parameter gradients: lane (li, g) feeds A = a0[k LDA] * amul and B = b0[k WE_SP] * bm + bo at
+// rows k = we_krow(kk, g); every operand is read first, then two MFMA chains.
+template <int LDA>
+__device__ __forceinline__ f4 we_small_tile(const float* a0, float amul, const float* b0, float bm, float bo, int g) {
+  const int k0 = we_krow(0, g);
+  a0 += k0 * LDA;
+  b0 += k0 * WE_SP;
+  float av[WE_B / 4], bv[WE_B / 4];
+#pragma unroll
+  for (int kk = 0; kk < WE_B / 4; ++kk) {
+    const int dk = 8 * (kk >> 1) + (kk & 1);
+    av[kk] = a0[dk * LDA] * amul;
+    bv[kk] = b0[dk * WE_SP] * bm + bo;
+  }
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+  for (int kk = 0; kk < WE_B / 4; ++kk) {
+    if (kk & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc1, 0, 0, 0);
+    else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc0, 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 32, 0);  // all operand reads first
+  __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);  // their scaling
+  __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);  // then the MFMAs
+  return acc0 + acc1;
+}
+
 // sum over the 64 minibatch rows of f(r), as four interleaved partial sums (rows r = q mod 4) added
 // in a fixed order: four independent dependency chains instead of one, identical on every workgroup
 template <typename F>
@@ -780,49 +807,52 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       for (int s4 = 0; s4 < 4; ++s4) za[s4] = S.Z2j[16 * w + li][4 * s4 + g];
       const int64_t base = WE_DH_OFF + (int64_t)(net * 2 + par) * WE_DH_SLOT + (int64_t)j * WE_DH_PROD +
                            (int64_t)w * WE_DH_TILE + lane * 16;
-      for (int u0 = 0; u0 < G; u0 += 4) {
-        f4 d[4];
+      // groups of four unit tiles; the next group's 16 W2 operands are read while this group's MFMAs issue
+      const float* w2 = &S.W2r[g][li];
+      float wb[16];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) d[t] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < 16; ++e) wb[e] = w2[(4 * (e >> 2)) * WE_HP + WE_SL * min(e & 3, G - 1)];
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
+      for (int u0 = 0; u0 < WE_GMAX; u0 += 4) {
+        if (u0 < G) {
+          float wn[16];  // (the last group re-reads clamped tiles: harmless)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) wn[e] = w2[(4 * (e >> 2)) * WE_HP + WE_SL * min(u0 + 4 + (e & 3), G - 1)];
+          f4 d[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) d[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[s4], wb[4 * s4 + t], d[t], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // the next group's DS reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);  // this group's MFMAs
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-            d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[s4], S.W2r[4 * s4 + g][WE_SL * min(u0 + t, G - 1) + li], d[t],
-                                                        0, 0, 0);
+            if (u0 + t < G)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d[t]), wrs,
+                                                     (int)(base + (int64_t)(u0 + t) * 4 * WE_DH_TILE), 0, WE_SC1);
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (u0 + t < G)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d[t]), wrs,
-                                                   (int)(base + (int64_t)(u0 + t) * 4 * WE_DH_TILE), 0, WE_SC1);
+          for (int e = 0; e < 16; ++e) wb[e] = wn[e];
+        }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
     WSTAMP(9);
-    // while the partials land: small-parameter gradients and dW2 rows j (H1 still in Act)
+    // while the partial tiles drain (64 KB of write-through stores per workgroup, the step's largest
+    // publish): small-parameter gradients and dW2 rows j (H1 still in Act); no global memory access
+    // here, so the drain and the arrival follow this work instead of preceding it
     // small-parameter gradients as three MFMA tiles over the 64 rows (D[i][jj] = sum_k A[k][i] B[k][jj]),
     // one per wave: wave 0 dW3 = dOut^T H2 (i = o), wave 1 the column sums of [dOut | dls] (db3,
     // dlog_std), wave 2 those of dZ2 (db2); b1 j is formed after dZ1 (below).  Every workgroup forms
     // db3 / dlog_std with the same code on the same rows, so their copies stay identical.
     if (w < 3) {
-      const float* a_src;
-      int lda;
-      if (w == 0) { a_src = li < WE_OUTM ? &S.dOut[0][li] : nullptr; lda = WE_OUTM; }
-      else if (w == 1) { a_src = li < WE_OUTM ? &S.dOut[0][li] : &S.dls[0][li - WE_OUTM]; lda = WE_OUTM; }
-      else { a_src = &S.Z2j[0][li]; lda = WE_SP; }
-      f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-#pragma unroll
-      for (int kk = 0; kk < WE_B / 4; ++kk) {
-        const int k = we_krow(kk, g);
-        const float av = a_src ? a_src[k * lda] : 0.f;
-        const float bv = w == 0 ? S.H2j[k][li] : 1.f;
-        if (kk & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc1, 0, 0, 0);
-        else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
-      }
-      const f4 dsm = acc0 + acc1;
+      // A = a0[k lda] * amul, B = H2[k][li] * bm + bo; row offsets are compile-time so the reads use
+      // immediate offsets from one base (no per-row address registers)
+      const float amul = (w == 0 && li >= WE_OUTM) ? 0.f : 1.f;
+      const float bm = w == 0 ? 1.f : 0.f, bo = 1.f - bm;
+      const f4 dsm = w == 2 ? we_small_tile<WE_SP>(&S.Z2j[0][li], amul, &S.H2j[0][li], bm, bo, g)
+                            : we_small_tile<WE_OUTM>(li < WE_OUTM || w == 0 ? &S.dOut[0][li & 7] : &S.dls[0][li - WE_OUTM],
+                                                     amul, &S.H2j[0][li], bm, bo, g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 4 * g + r;  // D row; column jj = li
@@ -841,6 +871,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     for (int t = 0; t < 4; ++t)
       if (4 * w + t >= G) g_r[t] = f4{0.f, 0.f, 0.f, 0.f};
     WSTAMP(11);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial-tile stores
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
     // wait for every workgroup's dH1 partials
     if (tid == 0) {
       const unsigned long long t0 = rai_clock();
@@ -863,16 +897,15 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       const int64_t base = WE_DH_OFF + (int64_t)(net * 2 + par) * WE_DH_SLOT + (int64_t)j * 4 * WE_DH_TILE +
                            (int64_t)w * WE_DH_TILE + lane * 16;
       f4 z = {0.f, 0.f, 0.f, 0.f};
-      for (int p0 = 0; p0 < G; p0 += 8) {
-        f4 v[8];
+      f4 v[WE_GMAX];  // all G loads in flight at once
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            wrs, (int)(base + (int64_t)min(p0 + u, G - 1) * WE_DH_PROD), 0, WE_SC1));
+      for (int u = 0; u < WE_GMAX; ++u)
+        if (u < G)
+          v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)(base + (int64_t)u * WE_DH_PROD),
+                                                                              0, WE_SC1));
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (p0 + u < G) z += v[u];  // producer (slice) order
-      }
+      for (int u = 0; u < WE_GMAX; ++u)
+        if (u < G) z += v[u];  // producer (slice) order
       WSTAMP(13);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1087,7 +1120,7 @@ __global__ __launch_bounds__(256) void we_adv_norm_kernel(const float* adv, int6
 }
 
 template <int HEAD>
-__global__ __launch_bounds__(WE_NT) void mlp_wide_epoch_kernel(const WeArgs a) {
+__global__ __launch_bounds__(WE_NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void mlp_wide_epoch_kernel(const WeArgs a) {
   static_assert(sizeof(WeSmem) <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[sizeof(WeSmem)];
   const int b = blockIdx.x, grp = b & 7, j = b >> 3;
