@@ -54,7 +54,12 @@ typedef unsigned int u2v __attribute__((ext_vector_type(2)));
 constexpr int64_t WE_CTR_STRIDE = 128;                                  // one counter per 128-B line
 constexpr int64_t WE_CTR_BYTES = 8 * WE_CTR_STRIDE;                     // A0 A1 B0 B1 C0 C1 D
 constexpr int64_t WE_ACT_SLOT = (int64_t)WE_B * WE_HMAX * 4;            // one [64][H] f32 slot
-constexpr int64_t WE_H1_OFF = WE_CTR_BYTES;                             // [net][par] H1 slots
+// the D exchange as granules (8-B {tag = step + 1, 32-bit value} words, agent-scope atomic stores and
+// loads: the data is the flag -- no drain, no counter), zeroed with the counters before every launch.
+// (The B exchange measured 3x slower as granules -- 24 polled words per lane -- and keeps the counter.)
+constexpr int64_t WE_GD_OFF = WE_CTR_BYTES;                             // D: [par][net][slice][hi, lo]
+constexpr int64_t WE_STATE_BYTES = WE_GD_OFF + 2 * 2 * WE_GMAX * 2 * 8;  // the memset block
+constexpr int64_t WE_H1_OFF = WE_STATE_BYTES;                           // [net][par] H1 slots
 // dH1 partial tiles: [producer slice][unit tile][row tile][64 lanes][4] f32, one 1-KB MFMA tile each
 constexpr int64_t WE_DH_TILE = 1024;
 constexpr int64_t WE_DH_PROD = (int64_t)WE_GMAX * 4 * WE_DH_TILE;        // one producer's tiles
@@ -62,10 +67,19 @@ constexpr int64_t WE_DH_SLOT = WE_GMAX * WE_DH_PROD;
 constexpr int64_t WE_DH_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dH1 partial slots
 constexpr int64_t WE_P_SLOT = (int64_t)WE_GMAX * WE_B * WE_OUTM * 4;    // [slice][64][8] f32
 constexpr int64_t WE_P_OFF = WE_DH_OFF + 4 * WE_DH_SLOT;                // [net][par] output-layer partial slots
-constexpr int64_t WE_N_OFF = WE_P_OFF + 4 * WE_P_SLOT;                  // [par][net][slice] f64
-constexpr int64_t WE_ADV_OFF = WE_N_OFF + 2 * 2 * WE_GMAX * 8;        // (n_rows) normalized advantages
+constexpr int64_t WE_ADV_OFF = WE_P_OFF + 4 * WE_P_SLOT;                // (n_rows) normalized advantages
 inline int64_t we_ws_bytes(int64_t n_rows) { return WE_ADV_OFF + ((n_rows * 4 + 255) & ~(int64_t)255); }
-enum { WE_CA = 0, WE_CB = 2, WE_CC = 4, WE_CD = 6 };
+enum { WE_CA = 0, WE_CB = 2, WE_CC = 4 };  // counters (A: H1, B: head partials, C: dH1 tiles); D: granules
+static_assert(WE_STATE_BYTES % 16 == 0, "memset block");
+
+typedef __attribute__((address_space(1))) unsigned long long we_gu64;
+__device__ __forceinline__ we_gu64* we_gptr(unsigned char* p) { return (we_gu64*)p; }  // global, never flat
+__device__ __forceinline__ void we_put(we_gu64* g, unsigned tag, unsigned value) {
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long we_get(we_gu64* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 struct WeArgs {
   rai_mlp_wide_desc d;
@@ -99,7 +113,7 @@ struct WeSmem {
   float H2j[WE_B][WE_SP];
   float Z2j[WE_B][WE_SP];
   float Z1j[WE_B][WE_SP];
-  float dOut[WE_B][WE_OUTM];
+  alignas(16) float dOut[WE_B][WE_OUTM];
   float dls[WE_B][WE_OUTM];
   float Pw[4][WE_B][WE_OUTM];  // per-wave sums of 4 slices' output partials
   alignas(16) float small[WE_NSMALL];  // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
@@ -107,6 +121,7 @@ struct WeSmem {
   double st[4][WE_B];         // per-row loss statistics, reduced off the critical path (D wait)
   float ginv[WE_OUTM], glsc[WE_OUTM], entc;  // Gaussian 1 / variance, log scale, per-row entropy
   float adamc[2];             // this step's Adam bias-correction constants (formed during the D wait)
+  float coef;                 // this step's clip coefficient
   float db1[WE_SL];           // db1 j (wave 3)
   double red[4][8];
   float adv_mean, adv_den;
@@ -636,11 +651,21 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     if (w == 0) {
       const int r = lane;
       const bool valid = r < rows;
+      // head outputs: the four waves' slice sums in order, + b3 (16-B LDS reads; entries o >= O are
+      // zero throughout -- partials, W3 columns and b3 padding -- so no per-dimension branches)
       float out[WE_OUTM];
+      {
+        const f4* pw = reinterpret_cast<const f4*>(&S.Pw[0][r][0]);
+        constexpr int WS = WE_B * WE_OUTM / 4;  // f4 stride between the waves' copies
+        const f4 lo = ((pw[0] + pw[WS]) + pw[2 * WS]) + pw[3 * WS];
+        const f4 hi = ((pw[1] + pw[WS + 1]) + pw[2 * WS + 1]) + pw[3 * WS + 1];
+        const f4* b3 = reinterpret_cast<const f4*>(&S.small[2 * WE_SL + WE_OUTM * WE_SL]);
+        const f4 ol = lo + b3[0], oh = hi + b3[1];
 #pragma unroll
-      for (int o = 0; o < WE_OUTM; ++o) {
-        const float acc = ((S.Pw[0][r][o] + S.Pw[1][r][o]) + S.Pw[2][r][o]) + S.Pw[3][r][o];
-        out[o] = o < O ? acc + S.small[2 * WE_SL + WE_OUTM * WE_SL + o] : 0.f;
+        for (int o = 0; o < 4; ++o) {
+          out[o] = ol[o];
+          out[4 + o] = oh[o];
+        }
       }
       float dout[WE_OUTM], dl[WE_OUTM];
 #pragma unroll
@@ -659,11 +684,11 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o) ginv[o] = S.ginv[o];
 #pragma unroll
-          for (int o = 0; o < WE_OUTM; ++o)
-            if (o < O) {
-              const float xo = c_act[o] - out[o];
-              lp += -(xo * xo) * (0.5f * ginv[o]) - S.glsc[o] - 0.91893853320467274f;
-            }
+          for (int o = 0; o < WE_OUTM; ++o) {  // dimensions o >= O masked (no uniform branches)
+            const float xo = c_act[o] - out[o];
+            const float term = -(xo * xo) * (0.5f * ginv[o]) - S.glsc[o] - 0.91893853320467274f;
+            lp += o < O ? term : 0.f;
+          }
           ent = S.entc;
         } else {
           const int64_t ai = c_ai;
@@ -704,12 +729,12 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         const float d_ent = valid ? -hp.ent_coef / n_ent : 0.f;
         if (HEAD == 1) {
 #pragma unroll
-          for (int o = 0; o < WE_OUTM; ++o)
-            if (o < O) {
-              const float xo = c_act[o] - out[o];
-              dout[o] = d_logp * (xo * ginv[o]);
-              dl[o] = d_logp * ((xo * xo) * ginv[o] - 1.f) + d_ent;
-            }
+          for (int o = 0; o < WE_OUTM; ++o) {
+            const float xo = c_act[o] - out[o];
+            const bool on = o < O;
+            dout[o] = on ? d_logp * (xo * ginv[o]) : 0.f;
+            dl[o] = on ? d_logp * ((xo * xo) * ginv[o] - 1.f) + d_ent : 0.f;
+          }
         } else {
           const int64_t ai = c_ai;
           float mx = out[0];
@@ -772,11 +797,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         }
       }
       WSTAMP(7);
-#pragma unroll
-      for (int o = 0; o < WE_OUTM; ++o) {
-        S.dOut[r][o] = dout[o];
-        S.dls[r][o] = dl[o];
-      }
+      *reinterpret_cast<f4*>(&S.dOut[r][0]) = f4{dout[0], dout[1], dout[2], dout[3]};
+      *reinterpret_cast<f4*>(&S.dOut[r][4]) = f4{dout[4], dout[5], dout[6], dout[7]};
+      *reinterpret_cast<f4*>(&S.dls[r][0]) = f4{dl[0], dl[1], dl[2], dl[3]};
+      *reinterpret_cast<f4*>(&S.dls[r][4]) = f4{dl[4], dl[5], dl[6], dl[7]};
 #pragma unroll
       for (int i = 0; i < 4; ++i) S.st[i][r] = st[i];
     }
@@ -984,31 +1008,57 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       ss = wave_sum_dpp(ss);
       if (lane == 0) S.red[0][w] = ss;
       __syncthreads();
-      if (tid == 0) {
+      we_gu64* gd = we_gptr(a.ws + WE_GD_OFF);
+      if (tid == 0) {  // the share as two granules (hi, lo words of the double)
         const double tot = ((S.red[0][0] + S.red[0][1]) + S.red[0][2]) + S.red[0][3];
-        const int64_t off = WE_N_OFF + ((int64_t)(par * 2 + net) * WE_GMAX + j) * 8;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, tot), wrs, (int)off, 0, WE_SC1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long u = __double_as_longlong(tot);
+        we_gu64* gs = gd + ((int64_t)(par * 2 + net) * WE_GMAX + j) * 2;
+        we_put(gs, (unsigned)mb + 1, (unsigned)(u >> 32));
+        we_put(gs + 1, (unsigned)mb + 1, (unsigned)u);
       }
     }
     WSTAMP(18);
-    // the next minibatch's inputs, issued after this step's last store drain: they land during the
-    // D wait and Adam, before the next drain (vmcnt counts loads and stores together)
+    // the next minibatch's inputs: they land during the D sweep and Adam
     if (mb + 1 < nmb) prefetch(mb + 1);
     WSTAMP(19);
-    if (!we_arrive_wait(ctr, WE_CD, 2 * want, a.state, S.bail, w, side_d)) break;
-    WSTAMP(20);
-    {
-      // the 2 G shares, net-major then slice order: lane l < 2 G loads share l; fixed-order wave sum
+    // D: wave 0 sweeps the 2 G shares (both networks: clip_grad_norm_ is over all parameters) and
+    // forms the clip coefficient; wave 1 meanwhile runs the stats / Adam-constant side job
+    if (w == 0) {
       const int l = lane < 2 * G ? lane : 0;
       const int nn = l / G, jj = l - nn * G;
-      const int64_t off = WE_N_OFF + ((int64_t)(par * 2 + nn) * WE_GMAX + jj) * 8;
-      const double sh = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wrs, (int)off, 0, WE_SC1));
+      we_gu64* gs = we_gptr(a.ws + WE_GD_OFF) + ((int64_t)(par * 2 + nn) * WE_GMAX + jj) * 2;
+      const unsigned tag = (unsigned)mb + 1;
+      unsigned long long hi, lo;
+      const unsigned long long t0 = rai_clock();
+      for (;;) {
+        hi = we_get(gs);
+        lo = we_get(gs + 1);
+        if (__all((unsigned)(hi >> 32) == tag && (unsigned)(lo >> 32) == tag)) break;
+        if (rai_expired(t0, RAI_SPIN_LOCAL)) {
+          if (lane == 0) {
+            __hip_atomic_store(&a.state->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.bail = 1;
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const double sh = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+      // the 2 G shares, net-major then slice order, fixed-order wave sum
       const double tot = wave_sum_dpp(lane < 2 * G ? sh : 0.0);
       const float total_norm = (float)sqrt(tot);
       float coef = 1.f;
       if (ohp.max_grad_norm > 0.f) coef = fminf(ohp.max_grad_norm / (total_norm + 1e-6f), 1.f);
-      if (net == 0 && j == 0 && tid == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;
+      if (lane == 0) S.coef = coef;
+      if (net == 0 && j == 0 && lane == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;
+    } else if (w == 1) {
+      side_d();
+    }
+    __syncthreads();
+    if (S.bail) break;
+    WSTAMP(20);
+    {
+      const float coef = S.coef;
       const float inv_c3 = S.adamc[0], c4 = S.adamc[1];
       // W2 row slice
 #pragma unroll
@@ -1189,7 +1239,8 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   a.max_norms = max_norms;
   a.ws = static_cast<unsigned char*>(workspace);
   hipStream_t s = rai_stream(stream);
-  const hipError_t e = hipMemsetAsync(workspace, 0, WE_CTR_BYTES, s);  // monotonic counters start at 0
+  // monotonic counters and granule tags start at 0 (tags are step + 1 >= 1)
+  const hipError_t e = hipMemsetAsync(workspace, 0, WE_STATE_BYTES, s);
   if (e != hipSuccess) return (int)e;
   const int64_t nmb = (n_rows + batch_size - 1) / batch_size;
   hipLaunchKernelGGL(we_adv_norm_kernel, dim3((unsigned)((nmb + 3) / 4)), dim3(256), 0, s, advantages, n_rows,
