@@ -484,9 +484,10 @@ int rai_mlp_wide_backward(const rai_mlp_wide_desc* desc, const float* obs, const
  * rai_mlp_ppo_epoch (stats[0] excludes the value term: the host adds vf_coef * stats[5]).
  * Options outside K = 1, Adam, no gradient accumulation / kl_cutoff / multi-reward weights
  * are not covered (the caller keeps the per-minibatch path).  workspace:
- * rai_mlp_wide_epoch_workspace_bytes(hidden, n_rows) (its counters are reset by the call; it also
- * holds the per-minibatch normalized advantages, formed by a first small launch on the stream). */
-int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden, int64_t n_rows);
+ * rai_mlp_wide_epoch_workspace_bytes(hidden, in_dim, n_rows) (its counters are reset by the call; it
+ * also holds the epoch's per-row records -- minibatch-normalized advantage, loss inputs, padded
+ * observation -- built by a first small launch on the stream). */
+int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden, int32_t in_dim, int64_t n_rows);
 int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq, int64_t P,
                        const float* obs, const void* actions, const float* old_logp, const float* old_values,
                        const float* advantages, const float* returns, int64_t n_rows, int32_t batch_size,

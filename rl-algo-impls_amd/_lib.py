@@ -155,7 +155,7 @@ _SIGNATURES = {
                                             _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_mlp_wide_backward": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "rai_mlp_wide_dist_params": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
-    "rai_mlp_wide_epoch_workspace_bytes": (_i64, [_i32, _i64]),
+    "rai_mlp_wide_epoch_workspace_bytes": (_i64, [_i32, _i32, _i64]),
     "rai_mlp_wide_epoch": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp,
                                      _vp, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
     "rai_gae_skips": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),

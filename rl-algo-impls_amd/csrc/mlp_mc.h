@@ -118,45 +118,9 @@ __device__ __forceinline__ f4 as_f4(u4v v) { return __builtin_bit_cast(f4, v); }
 __device__ __forceinline__ u4v as_u4(f4 v) { return __builtin_bit_cast(u4v, v); }
 
 // Wave-wide sums on the VALU (DPP row butterflies + lane swaps) instead of ds_bpermute shuffles:
-// a fixed combination order in which every lane ends with the same bits.
-__device__ __forceinline__ float wave_sum_v(float v) {
-  v = row_sum16(v);
-  const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(a16[0]) + __uint_as_float(a16[1]);
-  const auto a32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(a32[0]) + __uint_as_float(a32[1]);
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
-  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ double swap_d16(double v, bool s32) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
-  unsigned lo0, lo1, hi0, hi1;
-  if (s32) {
-    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    lo0 = l[0]; lo1 = l[1]; hi0 = h[0]; hi1 = h[1];
-  } else {
-    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    lo0 = l[0]; lo1 = l[1]; hi0 = h[0]; hi1 = h[1];
-  }
-  return __builtin_bit_cast(double, ((unsigned long long)hi0 << 32) | lo0) +
-         __builtin_bit_cast(double, ((unsigned long long)hi1 << 32) | lo1);
-}
-__device__ __forceinline__ double wave_sum_v(double v) {
-  v += dpp_d<0xB1>(v);
-  v += dpp_d<0x4E>(v);
-  v += dpp_d<0x141>(v);
-  v += dpp_d<0x140>(v);
-  v = swap_d16(v, false);
-  return swap_d16(v, true);
-}
+// a fixed combination order in which every lane ends with the same bits (common.h wave_sum_dpp).
+__device__ __forceinline__ float wave_sum_v(float v) { return wave_sum_dpp(v); }
+__device__ __forceinline__ double wave_sum_v(double v) { return wave_sum_dpp(v); }
 
 // torch Adam step (m, v, denom = sqrt(v)/sqrt(bc2) + eps, p -= lr/bc1 * m/denom) with the
 // hardware sqrt / reciprocal (1 ulp each) instead of the IEEE-exact sequences: ~1e-7 relative

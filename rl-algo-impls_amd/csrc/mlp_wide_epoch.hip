@@ -9,22 +9,23 @@
 // and only blocks b % 8 == 0 (actor) / == 1 (critic) work, so each network's workgroups share one
 // XCD's L2 -- placement is a speed choice only, the hand-offs below are placement-independent).
 // Workgroup j OWNS hidden units [16 j, 16 j + 16) of both hidden layers and keeps in LDS, updated
-// by its own Adam every step: W1 rows j, b1 j, W2 rows j (for the forward), W2 columns j (for the
-// backward dH1 = dZ2 W2), b2 j, W3 columns j, and copies of b3 / log_std.  Its Adam moments live
-// in registers.  A W2 element is thus held by its row owner and its column owner; both compute its
-// gradient with the same MFMA tile code on the same operands in the same order (we_dw2_tile), so
-// the two copies stay bitwise equal.
+// by its own Adam every step: W1 rows j, b1 j, W2 rows j, b2 j, W3 columns j, and copies of b3 /
+// log_std.  Its Adam moments live in registers.  W2 is held once, by its row owner.
 //
-// One optimizer step = four hand-offs through L2 (16-B write-through (sc1) stores, every storing
-// wave drained, one agent-scope arrival per workgroup on a monotonic counter, sc1 loads after the
-// poll -- MI355X_MICROARCH.md "Valid forms", row 1):
-//   A  H1[:, j] published; every workgroup of the network gathers H1 (B x H)
-//   B  output-layer partials H2[:, j] W3[:, j]^T published; every workgroup sums them in slice
+// Before the epoch, we_pack_kernel builds one record per row (minibatch-normalized advantage, loss
+// inputs, zero-padded observation), so each step's inputs are one contiguous prefetched block.
+//
+// One optimizer step = four hand-offs:
+//   A  H1[:, j] published (16-B write-through (sc1) stores, every storing wave drained, one
+//      agent-scope arrival per workgroup on a monotonic counter -- MI355X_MICROARCH.md "Valid forms",
+//      row 1); every workgroup gathers H1 (B x H) by LDS-DMA sc1 loads
+//   B  output-layer partials H2[:, j] W3[:, j]^T published (as A); every workgroup sums them in slice
 //      order and runs the head + loss for all rows (identical everywhere), then dZ2[:, j]
-//   C  dZ2[:, j] published (dW2 rows j computed while it lands); every workgroup gathers dZ2 and
-//      forms dW2 columns j, dH1[:, j], dZ1, dW1 rows j
-//   D  (both networks) each workgroup's share of the squared gradient norm; every workgroup sums
-//      the 2 G shares in a fixed order (clip_grad_norm_ over all parameters, bit-identical on every
+//   C  dH1 partial tiles dZ2[:, j] W2[j rows, :] published (as A; the drain deferred past the dW2-row
+//      work) to their unit tiles' owners, which sum the G producers in slice order -> dZ1, dW1 rows j
+//   D  (both networks) each workgroup's share of the squared gradient norm as two tagged 8-B
+//      granules (agent-scope atomic store / load, no drain or counter); every workgroup sums the 2 G
+//      shares in a fixed order (clip_grad_norm_ over all parameters, bit-identical on every
 //      workgroup) and applies clip + Adam to what it owns.
 // Every spin is bounded and sets state->err.  Numerics: fp32 like the reference, exact-f32 MFMA
 // (v_mfma_f32_16x16x4f32), Adam with the hardware sqrt / rcp (as the CartPole epoch kernel); parity
@@ -67,8 +68,17 @@ constexpr int64_t WE_DH_SLOT = WE_GMAX * WE_DH_PROD;
 constexpr int64_t WE_DH_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dH1 partial slots
 constexpr int64_t WE_P_SLOT = (int64_t)WE_GMAX * WE_B * WE_OUTM * 4;    // [slice][64][8] f32
 constexpr int64_t WE_P_OFF = WE_DH_OFF + 4 * WE_DH_SLOT;                // [net][par] output-layer partial slots
-constexpr int64_t WE_ADV_OFF = WE_P_OFF + 4 * WE_P_SLOT;                // (n_rows) normalized advantages
-inline int64_t we_ws_bytes(int64_t n_rows) { return WE_ADV_OFF + ((n_rows * 4 + 255) & ~(int64_t)255); }
+// per-row records of the epoch, built by we_pack_kernel before the epoch: [0] normalized advantage,
+// [1] old log-prob, [2] return, [3] old value, [4, 12) action (Gaussian: O floats; Categorical: the
+// index's int32 bits), [12, 12 + IN4) observation (zero-padded): one contiguous 16-B-aligned block per
+// minibatch, staged by WE_RU 16-B loads per thread
+constexpr int WE_LIN = 12;
+constexpr int64_t WE_REC_OFF = WE_P_OFF + 4 * WE_P_SLOT;
+inline int we_rec_floats(int in_dim) { return WE_LIN + ((in_dim + 3) & ~3); }
+inline int64_t we_ws_bytes(int in_dim, int64_t n_rows) {
+  return WE_REC_OFF + ((n_rows * we_rec_floats(in_dim) * 4 + 255) & ~(int64_t)255);
+}
+constexpr int WE_RU = (WE_B * (WE_LIN + WE_INMAX) / 4 + 255) / 256;  // 16-B record loads per thread
 enum { WE_CA = 0, WE_CB = 2, WE_CC = 4 };  // counters (A: H1, B: head partials, C: dH1 tiles); D: granules
 static_assert(WE_STATE_BYTES % 16 == 0, "memset block");
 
@@ -86,12 +96,7 @@ struct WeArgs {
   float* params;       // flat parameter buffer (desc.w point into it)
   float* exp_avg;      // Adam state, same layout as params
   float* exp_avg_sq;
-  const float* obs;    // (n_rows, in) of the epoch's permuted copy
-  const void* actions; // Gaussian (n_rows, out) f32; Categorical (n_rows,) i64
-  const float* old_logp;
-  const float* old_values;
-  const float* adv;
-  const float* ret;
+  const float* rec;    // (n_rows, we_rec_floats(in)) per-row records (we_pack_kernel)
   int64_t n_rows;
   int32_t batch;
   const rai_ppo_hparams* hp;
@@ -107,7 +112,8 @@ struct WeArgs {
 struct WeSmem {
   float Act[WE_B][WE_HP];     // H1 of the minibatch (all columns), later dZ2
   float W2r[WE_SL][WE_HP];    // W2[16 j + i][:]
-  alignas(16) float Xl[WE_B * WE_INMAX + 4];  // minibatch observations, row stride IN (a linear copy; zero tail)
+  // minibatch observations, row stride IN4 (zero-padded), then the loss inputs [64][12] (record words 0-11)
+  alignas(16) float Xl[WE_B * WE_INMAX + WE_B * WE_LIN];
   float W1j[WE_SL][WE_XLD];   // W1[16 j + i][:]
   float H1j[WE_B][WE_SP];
   float H2j[WE_B][WE_SP];
@@ -369,7 +375,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   const rai_ppo_hparams& hp = *a.hp;
   const rai_optim_hparams& ohp = *a.ohp;
   unsigned long long* ctr = reinterpret_cast<unsigned long long*>(a.ws);
-  const __amdgpu_buffer_rsrc_t wrs = we_rsrc(a.ws, WE_ADV_OFF);  // the exchange region
+  const __amdgpu_buffer_rsrc_t wrs = we_rsrc(a.ws, WE_REC_OFF);  // the exchange region
   const float* const* W = d.w[net];
   const int64_t pbase_off = 0;
   (void)pbase_off;
@@ -442,57 +448,31 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   const float c1 = (float)(1.0 - beta1_d), c2 = (float)(1.0 - beta2_d);
   double pw1 = ipow(beta1_d, step0), pw2 = ipow(beta2_d, step0);
   if (tid == 0) S.bail = 0;
-  if (tid < 4) S.Xl[WE_B * WE_INMAX + tid] = 0.f;
   __syncthreads();
 
-  // the next minibatch's inputs are loaded into registers one step ahead: its observations (all
-  // threads) and, for wave 0 (lane = row), the per-row loss inputs
-  // The minibatch's rows are contiguous in the permuted copy: a linear copy of rws * IN floats, as
-  // 16-B loads when every minibatch starts 16-B aligned and the array's end is (x4), else 4-B loads.
-  // Loads past the data are not issued (wave-uniform skip); their registers hold zeros.
-  constexpr int XU4 = WE_B * WE_INMAX / 4 / WE_NT;  // 4 x 16 B per thread
-  const bool x4 = (B * IN) % 4 == 0 && (n_rows * IN) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0;
-  f4 xr[XU4];
-  float pa[WE_OUTM], p_lpold = 0.f, p_adv = 0.f, p_ret = 0.f, p_vold = 0.f;
-  int64_t p_ai = 0;
+  // the next minibatch's records are loaded into registers one step ahead: one contiguous block of
+  // rws x R floats (R = 12 + IN4), WE_RU 16-B loads per thread (those past the block not issued:
+  // wave-uniform skip); the staging destination of each (Lin row or Xl row, both 16-B aligned) is
+  // fixed per thread and computed once
+  const int R = WE_LIN + IN4, R4 = R >> 2;
+  f4 xr[WE_RU];
+  int dst[WE_RU];  // LDS float index of the 16 B this thread stages (-1: none); Lin words 0-11, Xl beyond
+#pragma unroll
+  for (int u = 0; u < WE_RU; ++u) {
+    const int e4 = tid + WE_NT * u;
+    const int row = e4 / R4, c4 = e4 - row * R4;
+    dst[u] = row >= WE_B ? -1 : (c4 < WE_LIN / 4 ? WE_B * WE_INMAX + row * WE_LIN + 4 * c4 : row * IN4 + 4 * (c4 - WE_LIN / 4));
+  }
   auto prefetch = [&](int m) {
     const int64_t r0 = (int64_t)m * B;
     const int rws = (int)min((int64_t)B, n_rows - r0);
-    const int n = rws * IN;
-    if (x4) {
-      const f4* src = reinterpret_cast<const f4*>(a.obs + r0 * IN);
+    const int n4 = rws * R4;
+    const f4* src = reinterpret_cast<const f4*>(a.rec + r0 * R);
 #pragma unroll
-      for (int u = 0; u < XU4; ++u) {
-        const int e4 = tid + WE_NT * u;
-        xr[u] = f4{0.f, 0.f, 0.f, 0.f};
-        if (4 * (WE_NT * u + 64 * w) < n && 4 * e4 < n) xr[u] = src[e4];  // n % 4 == 0 here
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4 * XU4; ++u) {
-        const int e = tid + WE_NT * u;
-        float x = 0.f;
-        if (WE_NT * u + 64 * w < n && e < n) x = a.obs[r0 * IN + e];
-        xr[u >> 2][u & 3] = x;
-      }
-    }
-    if (w == 0) {
-      const bool ok = lane < rws;
-      const int64_t gr = r0 + (ok ? lane : 0);
-      if (net == 0) {
-        if (HEAD == 1) {
-          const float* av = static_cast<const float*>(a.actions) + gr * O;
-#pragma unroll
-          for (int o = 0; o < WE_OUTM; ++o) pa[o] = av[o < O ? o : 0];
-        } else {
-          p_ai = static_cast<const int64_t*>(a.actions)[gr];
-        }
-        p_lpold = a.old_logp[gr];
-        p_adv = a.adv[gr];
-      } else {
-        p_ret = a.ret[gr];
-        p_vold = a.old_values[gr];
-      }
+    for (int u = 0; u < WE_RU; ++u) {
+      const int e4 = tid + WE_NT * u;
+      xr[u] = f4{0.f, 0.f, 0.f, 0.f};
+      if (WE_NT * u + 64 * w < n4 && e4 < n4) xr[u] = src[e4];
     }
   };
   if (nmb > 0) prefetch(0);
@@ -505,20 +485,11 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     const int64_t row0 = (int64_t)mb * B;
     const int rows = (int)min((int64_t)B, n_rows - row0);
     const unsigned long long want = (unsigned long long)G * (mb + 1);
-    // ---- observations of the minibatch -> LDS (zero rows / columns beyond the data) ----------
-    if (x4) {
+    // ---- the minibatch's records -> LDS: loss inputs to Lin, observations to Xl (rows beyond the
+    // data are zero) ----------------------------------------------------------------------------
 #pragma unroll
-      for (int u = 0; u < XU4; ++u) reinterpret_cast<f4*>(S.Xl)[tid + WE_NT * u] = xr[u];
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4 * XU4; ++u) S.Xl[tid + WE_NT * u] = xr[u >> 2][u & 3];
-    }
-    float c_act[WE_OUTM];
-#pragma unroll
-    for (int o = 0; o < WE_OUTM; ++o) c_act[o] = pa[o];
-    const int64_t c_ai = p_ai;
-    const float c_lpold = p_lpold, c_ret = p_ret, c_vold = p_vold;
-    const float c_adv = p_adv;
+    for (int u = 0; u < WE_RU; ++u)
+      if (dst[u] >= 0) *reinterpret_cast<f4*>(&S.Xl[dst[u]]) = xr[u];
     lds_barrier();
     // wave 1 during the A wait: the Gaussian head's per-step constants of Normal(mu, exp(log_std)) --
     // variance, log scale (lane o) and the per-row entropy summed over dims in order
@@ -573,7 +544,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       for (int kk = 0; kk < IN4 / 4; ++kk) {
         const int k = 4 * kk + g;
         // k in [IN, IN4) reads the next row (or the zero tail) against W1j's zero padding
-        z = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Xl[(16 * w + li) * IN + k], S.W1j[li][k], z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Xl[(16 * w + li) * IN4 + k], S.W1j[li][k], z, 0, 0, 0);
       }
       const float bj = S.small[li];
 #pragma unroll
@@ -651,6 +622,11 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     if (w == 0) {
       const int r = lane;
       const bool valid = r < rows;
+      const f4* lin = reinterpret_cast<const f4*>(&S.Xl[WE_B * WE_INMAX + r * WE_LIN]);
+      const f4 l0 = lin[0], l1 = lin[1], l2 = lin[2];
+      const float c_adv = l0.x, c_lpold = l0.y, c_ret = l0.z, c_vold = l0.w;
+      const float c_act[WE_OUTM] = {l1.x, l1.y, l1.z, l1.w, l2.x, l2.y, l2.z, l2.w};
+      const int64_t c_ai = __float_as_int(l1.x);
       // head outputs: the four waves' slice sums in order, + b3 (16-B LDS reads; entries o >= O are
       // zero throughout -- partials, W3 columns and b3 padding -- so no per-dimension branches)
       float out[WE_OUTM];
@@ -944,7 +920,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     if (WE_SL * w < IN) {
       // two accumulator chains (even / odd kk), operands read one step ahead
       const float* za = &S.Z1j[we_krow(0, g)][li];
-      const float* xa = &S.Xl[we_krow(0, g) * IN + min(WE_SL * w + li, IN - 1)];
+      const float* xa = &S.Xl[we_krow(0, g) * IN4 + min(WE_SL * w + li, IN - 1)];
       f4 g_1b = {0.f, 0.f, 0.f, 0.f};
       float zv = za[0], xv = xa[0];
 #pragma unroll
@@ -953,7 +929,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         float zn = zv, xn = xv;
         if (kk + 1 < WE_B / 4) {
           zn = za[dk * WE_SP];
-          xn = xa[dk * IN];
+          xn = xa[dk * IN4];
         }
         if (kk & 1) g_1b = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, xv, g_1b, 0, 0, 0);
         else g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, xv, g_1, 0, 0, 0);
@@ -1142,12 +1118,15 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   }
 }
 
-// Per-minibatch advantage normalization of the epoch's permuted rows (ppo.py:313-316: mean and the
-// unbiased std over the minibatch, fp64 two-pass sums), one wave per minibatch, before the epoch:
-// it depends on no parameter, so the epoch kernel reads the normalized values instead of forming
-// them on its critical path.  Without normalization the values are copied.
-__global__ __launch_bounds__(256) void we_adv_norm_kernel(const float* adv, int64_t n_rows, int B,
-                                                          const rai_ppo_hparams* hpp, float* out) {
+// The epoch's per-row records (layout at WE_REC_OFF) from its permuted rollout copy, one wave per
+// minibatch (lane = row), before the epoch: the advantage normalized over the minibatch
+// (ppo.py:313-316: mean and the unbiased std, fp64 two-pass sums; copied when neither normalization
+// is on) -- it depends on no parameter, so the epoch kernel reads it instead of forming it on its
+// critical path -- then the loss inputs and the zero-padded observation.
+__global__ __launch_bounds__(256) void we_pack_kernel(const float* obs, const void* actions, const float* old_logp,
+                                                      const float* old_values, const float* adv, const float* ret,
+                                                      int64_t n_rows, int B, int IN, int O, int head,
+                                                      const rai_ppo_hparams* hpp, float* rec) {
 #pragma clang fp contract(off)
   const int64_t mb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -1156,7 +1135,8 @@ __global__ __launch_bounds__(256) void we_adv_norm_kernel(const float* adv, int6
   const rai_ppo_hparams& hp = *hpp;
   const int rows = (int)min((int64_t)B, n_rows - r0);
   const bool valid = lane < rows;
-  const float x = valid ? adv[r0 + lane] : 0.f;
+  const int64_t gr = r0 + (valid ? lane : 0);
+  const float x = valid ? adv[gr] : 0.f;
   float A = x;
   if (hp.normalize_advantage || hp.standardize_advantage) {
     const double s1 = wave_sum_dpp(valid ? (double)x : 0.0);
@@ -1166,7 +1146,20 @@ __global__ __launch_bounds__(256) void we_adv_norm_kernel(const float* adv, int6
     const float den = (float)sqrt(s2 / (double)(rows - 1)) + 1e-8f;
     A = hp.normalize_advantage ? (x - mean) / den : x / den;
   }
-  if (valid) out[r0 + lane] = A;
+  if (!valid) return;
+  const int IN4 = (IN + 3) & ~3, R = WE_LIN + IN4;
+  float* out = rec + gr * R;
+  out[0] = A;
+  out[1] = old_logp[gr];
+  out[2] = ret[gr];
+  out[3] = old_values[gr];
+  for (int o = 0; o < 8; ++o) {
+    float v = 0.f;
+    if (head == 1) v = o < O ? static_cast<const float*>(actions)[gr * O + o] : 0.f;
+    else if (o == 0) v = __int_as_float((int)static_cast<const int64_t*>(actions)[gr]);
+    out[4 + o] = v;
+  }
+  for (int k = 0; k < IN4; ++k) out[WE_LIN + k] = k < IN ? obs[gr * IN + k] : 0.f;
 }
 
 template <int HEAD>
@@ -1186,9 +1179,9 @@ extern "C" int rai_wide_epoch_debug_stamps(unsigned long long* host_out) {
 }
 #endif
 
-extern "C" int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden, int64_t n_rows) {
+extern "C" int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden, int32_t in_dim, int64_t n_rows) {
   (void)hidden;
-  return n_rows < 0 ? -1 : we_ws_bytes(n_rows);
+  return (n_rows < 0 || in_dim < 1 || in_dim > WE_INMAX) ? -1 : we_ws_bytes(in_dim, n_rows);
 }
 
 extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq,
@@ -1202,7 +1195,8 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
       !returns || !hp || !ohp || !state || !workspace)
     return RAI_E_NULLPTR;
   if (n_rows < 2 || batch_size < 2 || batch_size > WE_B) return RAI_E_SHAPE;
-  if (workspace_bytes < we_ws_bytes(n_rows)) return RAI_E_WORKSPACE;
+  if (desc->in_dim < 1 || desc->in_dim > WE_INMAX) return RAI_E_UNSUPPORTED;
+  if (workspace_bytes < we_ws_bytes(desc->in_dim, n_rows)) return RAI_E_WORKSPACE;
   if (n_rows % batch_size == 1) return RAI_E_SHAPE;  // a 1-row minibatch has no unbiased std
   const int H = desc->hidden;
   if (H < WE_SL || H > WE_HMAX || H % WE_SL != 0) return RAI_E_UNSUPPORTED;
@@ -1222,12 +1216,7 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   a.params = params;
   a.exp_avg = exp_avg;
   a.exp_avg_sq = exp_avg_sq;
-  a.obs = obs;
-  a.actions = actions;
-  a.old_logp = old_logp;
-  a.old_values = old_values;
-  a.adv = reinterpret_cast<const float*>(static_cast<unsigned char*>(workspace) + WE_ADV_OFF);
-  a.ret = returns;
+  a.rec = reinterpret_cast<const float*>(static_cast<unsigned char*>(workspace) + WE_REC_OFF);
   a.n_rows = n_rows;
   a.batch = batch_size;
   a.hp = hp;
@@ -1243,8 +1232,9 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   const hipError_t e = hipMemsetAsync(workspace, 0, WE_STATE_BYTES, s);
   if (e != hipSuccess) return (int)e;
   const int64_t nmb = (n_rows + batch_size - 1) / batch_size;
-  hipLaunchKernelGGL(we_adv_norm_kernel, dim3((unsigned)((nmb + 3) / 4)), dim3(256), 0, s, advantages, n_rows,
-                     (int)batch_size, hp, const_cast<float*>(a.adv));
+  hipLaunchKernelGGL(we_pack_kernel, dim3((unsigned)((nmb + 3) / 4)), dim3(256), 0, s, obs, actions, old_logp, old_values,
+                     advantages, returns, n_rows, (int)batch_size, desc->in_dim, desc->out_pi, desc->head, hp,
+                     const_cast<float*>(a.rec));
   RAI_LAUNCH_CHECK();
   const dim3 grid(8 * (H / WE_SL));
   if (desc->head == 1) hipLaunchKernelGGL(mlp_wide_epoch_kernel<1>, grid, dim3(WE_NT), 0, s, a);

@@ -584,7 +584,7 @@ class PPO:
         opt = self.optimizer
         L = _lib.lib()
         st = _lib.stream_handle(self.device)
-        ws_bytes = int(L.rai_mlp_wide_epoch_workspace_bytes(wide.spec["hidden"], r.total_steps))
+        ws_bytes = int(L.rai_mlp_wide_epoch_workspace_bytes(wide.spec["hidden"], wide.desc.in_dim, r.total_steps))
         if getattr(self, "_we_ws", None) is None or self._we_ws.numel() < ws_bytes:
             self._we_ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
         cur = torch.cuda.current_stream(self.device)
