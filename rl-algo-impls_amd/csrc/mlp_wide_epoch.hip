@@ -61,13 +61,13 @@ constexpr int64_t WE_ACT_SLOT = (int64_t)WE_B * WE_HMAX * 4;            // one [
 constexpr int64_t WE_GD_OFF = WE_CTR_BYTES;                             // D: [par][net][slice][hi, lo]
 constexpr int64_t WE_STATE_BYTES = WE_GD_OFF + 2 * 2 * WE_GMAX * 2 * 8;  // the memset block
 constexpr int64_t WE_H1_OFF = WE_STATE_BYTES;                           // [net][par] H1 slots
-// dH1 partial tiles: [producer slice][unit tile][row tile][64 lanes][4] f32, one 1-KB MFMA tile each
-constexpr int64_t WE_DH_TILE = 1024;
-constexpr int64_t WE_DH_PROD = (int64_t)WE_GMAX * 4 * WE_DH_TILE;        // one producer's tiles
-constexpr int64_t WE_DH_SLOT = WE_GMAX * WE_DH_PROD;
-constexpr int64_t WE_DH_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dH1 partial slots
+constexpr int64_t WE_Z2_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dZ2 slots
+// W2 as its row owners publish it after every Adam step, for the column owners' dH1: [net][producer
+// p][unit tile ct] transposed 16 x 16 tiles of 1 KB, tile (p, ct)[u][kk] = W2[16 p + kk][16 ct + u]
+constexpr int64_t WE_W2T_NET = (int64_t)WE_GMAX * WE_GMAX * 1024;
+constexpr int64_t WE_W2T_OFF = WE_Z2_OFF + 4 * WE_ACT_SLOT;
 constexpr int64_t WE_P_SLOT = (int64_t)WE_GMAX * WE_B * WE_OUTM * 4;    // [slice][64][8] f32
-constexpr int64_t WE_P_OFF = WE_DH_OFF + 4 * WE_DH_SLOT;                // [net][par] output-layer partial slots
+constexpr int64_t WE_P_OFF = WE_W2T_OFF + 2 * WE_W2T_NET;              // [net][par] output-layer partial slots
 // per-row records of the epoch, built by we_pack_kernel before the epoch: [0] normalized advantage,
 // [1] old log-prob, [2] return, [3] old value, [4, 12) action (Gaussian: O floats; Categorical: the
 // index's int32 bits), [12, 12 + IN4) observation (zero-padded): one contiguous 16-B-aligned block per
@@ -112,6 +112,7 @@ struct WeArgs {
 struct WeSmem {
   float Act[WE_B][WE_HP];     // H1 of the minibatch (all columns), later dZ2
   float W2r[WE_SL][WE_HP];    // W2[16 j + i][:]
+  alignas(16) float W2cT[WE_GMAX][WE_SL][WE_SL];  // W2[:, 16 j ..] as [k / 16][u][k % 16] (this step's)
   // minibatch observations, row stride IN4 (zero-padded), then the loss inputs [64][12] (record words 0-11)
   alignas(16) float Xl[WE_B * WE_INMAX + WE_B * WE_LIN];
   float W1j[WE_SL][WE_XLD];   // W1[16 j + i][:]
@@ -326,6 +327,71 @@ __device__ __forceinline__ void adam_fast(float& p, float& m, float& v, float g,
 
 // arrive on counter `ci` after every wave's stores drained (caller: s_waitcnt vmcnt(0) in every
 // storing wave, then this); lane 0 polls until ctr[ci] >= want.
+// dH1 tile of wave w: D[i][u] = sum_k dZ2[16 w + i][k] W2[k][16 j + u] over k in [0, H): lane group g
+// takes k in [g KQ, (g + 1) KQ), four at a time: A from the Act row (16-B reads), B from W2cT[k / 16][u]
+// (16-B reads); four accumulator chains, unrolled and read one step ahead for the common widths
+template <int KQ>
+__device__ __forceinline__ f4 we_dh1_tile_k(const float* ra, const float* wt, int k0) {
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+  auto bptr = [&](int kk) { return wt + ((k0 + kk) >> 4) * (WE_SL * WE_SL) + ((k0 + kk) & 15); };
+  f4 av = *reinterpret_cast<const f4*>(ra), bv = *reinterpret_cast<const f4*>(bptr(0));
+#pragma unroll
+  for (int kk = 0; kk < KQ; kk += 4) {
+    f4 an = av, bn = bv;
+    if (kk + 4 < KQ) {
+      an = *reinterpret_cast<const f4*>(ra + kk + 4);
+      bn = *reinterpret_cast<const f4*>(bptr(kk + 4));
+    }
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc3, 0, 0, 0);
+    if (kk + 4 < KQ) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    av = an;
+    bv = bn;
+  }
+  return (acc0 + acc1) + (acc2 + acc3);
+}
+__device__ __forceinline__ f4 we_dh1_tile(const float* act_row, const float* w2t_u, int H, int g) {
+  const int KQ = H >> 2, k0 = g * KQ;
+  const float* ra = act_row + k0;
+  if (H == 256) return we_dh1_tile_k<64>(ra, w2t_u, k0);
+  if (H == 128) return we_dh1_tile_k<32>(ra, w2t_u, k0);
+  if (H == 64) return we_dh1_tile_k<16>(ra, w2t_u, k0);
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+  for (int kk = 0; kk < KQ; kk += 4) {
+    const int k = k0 + kk;
+    const f4 av = *reinterpret_cast<const f4*>(ra + kk);
+    const f4 bv = *reinterpret_cast<const f4*>(w2t_u + (k >> 4) * (WE_SL * WE_SL) + (k & 15));
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc3, 0, 0, 0);
+  }
+  return (acc0 + acc1) + (acc2 + acc3);
+}
+
+// Publish W2 rows j for the column owners as transposed 16 x 16 tiles (16-B sc1 stores; no drain
+// here: the next H1 publish's drain covers them, before the A arrival their readers wait on).  Wave
+// w writes tiles ct = w + 4 m; lane (u = lane >> 2, kk4 = lane & 3) one 16-B row piece of each.
+__device__ __forceinline__ void we_publish_w2(const float (*W2r)[WE_HP], __amdgpu_buffer_rsrc_t wrs, int64_t base,
+                                              int G, int w, int lane) {
+  const int u = lane >> 2, kk4 = lane & 3;
+#pragma unroll
+  for (int m = 0; m < WE_GMAX / 4; ++m) {
+    const int ct = w + 4 * m;
+    if (ct < G) {
+      const f4 v = {W2r[4 * kk4][WE_SL * ct + u], W2r[4 * kk4 + 1][WE_SL * ct + u], W2r[4 * kk4 + 2][WE_SL * ct + u],
+                    W2r[4 * kk4 + 3][WE_SL * ct + u]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), wrs,
+                                             (int)(base + (int64_t)ct * 1024 + (u * WE_SL + 4 * kk4) * 4), 0, WE_SC1);
+    }
+  }
+}
+
 // Gather a published 64 x H exchange slot (workspace byte offset `base`) into Act (LDS rows of WE_HP
 // floats) by LDS-DMA: one global_load_lds_dwordx4 per row (H / 4 lanes x 16 B, landing contiguously
 // at the row's start), sc1 like every load of handed-off bytes; wave w takes rows w, w + 4, ...  The
@@ -449,6 +515,8 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   double pw1 = ipow(beta1_d, step0), pw2 = ipow(beta2_d, step0);
   if (tid == 0) S.bail = 0;
   __syncthreads();
+  const int64_t w2t_mine = WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * WE_GMAX * 1024;  // my published tiles
+  we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane);  // the initial W2, for step 0's column owners
 
   // the next minibatch's records are loaded into registers one step ahead: one contiguous block of
   // rws x R floats (R = 12 + IN4), WE_RU 16-B loads per thread (those past the block not issued:
@@ -561,7 +629,19 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     WSTAMP(0);
     if (!we_arrive_wait(ctr, WE_CA + net, want, a.state, S.bail, w, side_a)) break;
     WSTAMP(1);
-    we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // H1 -> Act
+    // W2's column slice j as the row owners published it after the last Adam step (16 tiles of 1 KB,
+    // one LDS-DMA load each; drained by the gather's vmcnt below), then H1 -> Act
+    {
+      const unsigned char* src = a.ws + WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * 1024 + lane * 16;
+#pragma unroll
+      for (int m = 0; m < WE_GMAX / 4; ++m) {
+        const int p = w + 4 * m;
+        if (p < G)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(src + (int64_t)p * WE_GMAX * 1024),
+                                           &S.W2cT[p][0][0], 16, 0, WE_SC1);
+      }
+    }
+    we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);
     lds_barrier();
     WSTAMP(2);
     // ============ fwd2: H2[:, j] = act(H1 W2[j]^T + b2[j]); wave w: row tile w =============
@@ -796,51 +876,15 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma unroll
       for (int u = 0; u < 4; ++u) z[u] = dh[u] * we_actd(act, h2[u]);
       *reinterpret_cast<f4*>(&S.Z2j[r][4 * q]) = z;
+      const int64_t off = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT + ((int64_t)r * H + WE_SL * j + 4 * q) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, z), wrs, (int)off, 0, WE_SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    lds_barrier();
-    {  // dH1 partials of slice j: P_j[rows 16 w .., units 16 ut ..] = dZ2[:, slice j] W2[slice j, :]
-      // (K = 16, four MFMAs), for every unit tile ut; tile (ut, w) goes lane-major (1 KB, one 16-B
-      // write-through store per lane) to its consumer, workgroup ut, which sums the G producers'
-      // tiles in slice order.  W2 thus lives only in its row owner (one copy, one Adam update).
-      float za[4];
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) za[s4] = S.Z2j[16 * w + li][4 * s4 + g];
-      const int64_t base = WE_DH_OFF + (int64_t)(net * 2 + par) * WE_DH_SLOT + (int64_t)j * WE_DH_PROD +
-                           (int64_t)w * WE_DH_TILE + lane * 16;
-      // groups of four unit tiles; the next group's 16 W2 operands are read while this group's MFMAs issue
-      const float* w2 = &S.W2r[g][li];
-      float wb[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) wb[e] = w2[(4 * (e >> 2)) * WE_HP + WE_SL * min(e & 3, G - 1)];
-#pragma unroll
-      for (int u0 = 0; u0 < WE_GMAX; u0 += 4) {
-        if (u0 < G) {
-          float wn[16];  // (the last group re-reads clamped tiles: harmless)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) wn[e] = w2[(4 * (e >> 2)) * WE_HP + WE_SL * min(u0 + 4 + (e & 3), G - 1)];
-          f4 d[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) d[t] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[s4], wb[4 * s4 + t], d[t], 0, 0, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // the next group's DS reads
-          __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);  // this group's MFMAs
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            if (u0 + t < G)
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d[t]), wrs,
-                                                     (int)(base + (int64_t)(u0 + t) * 4 * WE_DH_TILE), 0, WE_SC1);
-#pragma unroll
-          for (int e = 0; e < 16; ++e) wb[e] = wn[e];
-        }
-      }
-    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
     WSTAMP(9);
-    // while the partial tiles drain (64 KB of write-through stores per workgroup, the step's largest
-    // publish): small-parameter gradients and dW2 rows j (H1 still in Act); no global memory access
-    // here, so the drain and the arrival follow this work instead of preceding it
+    // while dZ2 lands: small-parameter gradients and dW2 rows j (H1 still in Act)
     // small-parameter gradients as three MFMA tiles over the 64 rows (D[i][jj] = sum_k A[k][i] B[k][jj]),
     // one per wave: wave 0 dW3 = dOut^T H2 (i = o), wave 1 the column sums of [dOut | dls] (db3,
     // dlog_std), wave 2 those of dZ2 (db2); b1 j is formed after dZ1 (below).  Every workgroup forms
@@ -871,11 +915,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     for (int t = 0; t < 4; ++t)
       if (4 * w + t >= G) g_r[t] = f4{0.f, 0.f, 0.f, 0.f};
     WSTAMP(11);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial-tile stores
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    // wait for every workgroup's dH1 partials
+    // wait for every workgroup's dZ2 slice
     if (tid == 0) {
       const unsigned long long t0 = rai_clock();
       while (__hip_atomic_load(&ctr[(WE_CC + net) * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
@@ -891,22 +931,13 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     __syncthreads();
     if (S.bail) break;
     WSTAMP(12);
-    // ============ bwd1: dH1[:, j] = sum of the G producers' partial tiles -> dZ1, dW1 rows j, db1 j
+    we_gather_lds(a.ws, WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // dZ2 -> Act
+    lds_barrier();
+    WSTAMP(13);
+    // ============ bwd1: dH1[:, j] = dZ2 W2[:, slice j] -> dZ1, dW1 rows j, db1 j ==================
     {
-      // wave w: row tile w; lane (li, g) receives dH1[16 w + 4 g + r][16 j + li], r < 4 (MFMA layout)
-      const int64_t base = WE_DH_OFF + (int64_t)(net * 2 + par) * WE_DH_SLOT + (int64_t)j * 4 * WE_DH_TILE +
-                           (int64_t)w * WE_DH_TILE + lane * 16;
-      f4 z = {0.f, 0.f, 0.f, 0.f};
-      f4 v[WE_GMAX];  // all G loads in flight at once
-#pragma unroll
-      for (int u = 0; u < WE_GMAX; ++u)
-        if (u < G)
-          v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)(base + (int64_t)u * WE_DH_PROD),
-                                                                              0, WE_SC1));
-#pragma unroll
-      for (int u = 0; u < WE_GMAX; ++u)
-        if (u < G) z += v[u];  // producer (slice) order
-      WSTAMP(13);
+      // wave w: row tile w; lane (li, g) holds dH1[16 w + 4 g + r][16 j + li], r < 4 (MFMA layout)
+      const f4 z = we_dh1_tile(&S.Act[16 * w + li][0], &S.W2cT[0][li][0], H, g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * w + 4 * g + r;
@@ -1066,6 +1097,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
+    if (mb + 1 < nmb) we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane);  // for the next step's column owners
     WSTAMP(21);
   }
 #ifdef RAI_STAMPS
