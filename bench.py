@@ -414,9 +414,17 @@ def main():
         # per-kernel MFMA-busy PMC in profiles/r2k_pong_mfma_pmc_kernels.json (C3)
         fl = UPDATE_FLOPS[args.config] * T * N
         tf = fl / (elapsed / args.steps) / 1e12
+        # traffic: L2-miss (fabric) bytes per update, 2 x FETCH_SIZE + WRITE_SIZE summed over the update's
+        # kernels (tools/c3_pmc.sh + tools/c3_traffic.py; the newest profiles/r*_<config>_traffic.json)
+        upd_traffic = None
+        for tp in sorted((ROOT / "profiles").glob(f"r*_{args.config}_traffic.json"), reverse=True):
+            td = json.loads(tp.read_text())
+            if td.get("workload", "").startswith(workload):
+                upd_traffic = td.get("bytes_per_update")
+                break
         roofline = {"kernel": "whole update (MIOpen / hipBLASLt contractions + HIP epilogues)", "bound": "mfma",
                     "achieved": round(tf, 3), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 4),
-                    "traffic": None, "flops_per_update": fl}
+                    "traffic": upd_traffic, "traffic_unit": "bytes per update", "flops_per_update": fl}
         roof_lat = None
     else:
         roofline = roof_gae

@@ -27,6 +27,7 @@ minibatch always runs eagerly through the same gather with its own buffers.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -52,6 +53,10 @@ class MinibatchStepGraph:
         self.static = static_buffers(fields, self.B, device, xforms)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.eager_runs = 0
+        # RAI_GRAPH_EAGER=1 (diagnostic): the same step body, launched eagerly and never captured --
+        # for profilers that cannot follow graph launches (rocprofv3 counter collection segfaults on
+        # graph-replayed dispatches: profiles/r3c_pong_fetch_pmc_crash_mapped.txt)
+        self.eager_only = os.environ.get("RAI_GRAPH_EAGER") == "1"
 
     def gather(self, desc: torch.Tensor, bufs: List[torch.Tensor]) -> None:
         gather_next(self.device, desc, bufs, self.row_bytes, self.xforms)
@@ -66,7 +71,7 @@ class MinibatchStepGraph:
         if self.graph is not None:
             self.graph.replay()
             return
-        if self.eager_runs < self.WARMUP:
+        if self.eager_only or self.eager_runs < self.WARMUP:
             self._body(desc, step)
             self.eager_runs += 1
             return

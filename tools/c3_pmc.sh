@@ -1,6 +1,8 @@
 #!/bin/bash
-# C3 (NatureCNN, 1024 envs x 128 steps) HBM-traffic counters for one whole update, eager
-# (RAI_GRAPHS=0): two rocprofv3 passes (FETCH_SIZE and WRITE_SIZE cannot share a pass: 3 + 2 TCC
+# C3 (NatureCNN, 1024 envs x 128 steps) HBM-traffic counters for one whole update.  rocprofv3's
+# counter collection segfaults on graph-replayed dispatches (profiles/r3c_pong_fetch_pmc_crash_mapped.txt),
+# so the product's graphed step body runs eagerly (GRAPHS=1 GRAPH_EAGER=1: same kernels, no capture).
+# Two rocprofv3 passes (FETCH_SIZE and WRITE_SIZE cannot share a pass: 3 + 2 TCC
 # counters), each aggregated per kernel ON the box (tools/pmc_kernels.py) so the per-dispatch CSV
 # never travels.  Each pass has its own time limit; the script stops at the first failure.
 set -u
@@ -12,7 +14,7 @@ mkdir -p "$OUT/diag"
 export RAI_DIAG_DIR="$OUT/diag"   # bench.py dumps /proc/self/maps (start, setup, update0) + faulthandler
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== $C" | tee -a "$OUT/steps.log"
-  RAI_GRAPHS=${GRAPHS:-0} RAI_ROLLOUT_GRAPH=${GRAPHS:-0} timeout -s KILL 400 rocprofv3 --pmc $C ${KREGEX:+--kernel-include-regex "$KREGEX"} --output-format csv -d "$OUT/$C" -o run -- \
+  RAI_GRAPHS=${GRAPHS:-0} RAI_ROLLOUT_GRAPH=${GRAPHS:-0} RAI_GRAPH_EAGER=${GRAPH_EAGER:-0} timeout -s KILL 400 rocprofv3 --pmc $C ${KREGEX:+--kernel-include-regex "$KREGEX"} --output-format csv -d "$OUT/$C" -o run -- \
     python3 bench.py --config pong --no-cpu-baseline --roofline-reps 1 --steps 1 --warmup 0 > "$OUT/$C.log" 2>&1
   rc=$?
   echo "== $C rc=$rc" | tee -a "$OUT/steps.log"
