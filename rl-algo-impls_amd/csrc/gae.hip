@@ -263,7 +263,7 @@ __global__ __launch_bounds__(GAE_WAVES * 64) void gae_kernel(const GaeArgs a) {
 constexpr int GAE_STREAM_NT = 256;
 constexpr int64_t GAE_STREAM_MIN_C = 1LL << 18;
 
-template <typename Acc, int D, bool K1, int NT>
+template <typename Acc, int D, bool K1, int NT, bool NTM = false>
 __global__ __launch_bounds__(NT) void gae_stream_kernel(const GaeArgs a) {
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int64_t C = a.C, N = a.N, T = a.T;
@@ -309,8 +309,15 @@ __global__ __launch_bounds__(NT) void gae_stream_kernel(const GaeArgs a) {
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       const int64_t t = top - i < 0 ? 0 : top - i;
-      ch.r[i] = *reinterpret_cast<const f4v*>(rewards + t * C + c0);
-      ch.v[i] = *reinterpret_cast<const f4v*>(values + t * C + c0);
+      // NTM: the streams (read once, written once, each far larger than L2) carry the nontemporal
+      // hint; the values are the same either way
+      if (NTM) {
+        ch.r[i] = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(rewards + t * C + c0));
+        ch.v[i] = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(values + t * C + c0));
+      } else {
+        ch.r[i] = *reinterpret_cast<const f4v*>(rewards + t * C + c0);
+        ch.v[i] = *reinterpret_cast<const f4v*>(values + t * C + c0);
+      }
       load_e(es + t * N, ch.e[i]);
     }
   };
@@ -333,8 +340,13 @@ __global__ __launch_bounds__(NT) void gae_stream_kernel(const GaeArgs a) {
         adv4[q] = (float)carry[q];
         ret4[q] = adv4[q] + cur.v[i][q];
       }
-      *reinterpret_cast<f4v*>(a.adv + t * C + c0) = adv4;
-      if (a.ret) *reinterpret_cast<f4v*>(a.ret + t * C + c0) = ret4;
+      if (NTM) {
+        __builtin_nontemporal_store(adv4, reinterpret_cast<f4v*>(a.adv + t * C + c0));
+        if (a.ret) __builtin_nontemporal_store(ret4, reinterpret_cast<f4v*>(a.ret + t * C + c0));
+      } else {
+        *reinterpret_cast<f4v*>(a.adv + t * C + c0) = adv4;
+        if (a.ret) *reinterpret_cast<f4v*>(a.ret + t * C + c0) = ret4;
+      }
       vprev = cur.v[i];
 #pragma unroll
       for (int q = 0; q < 4; ++q) eprev[q] = cur.e[i][q];
@@ -404,7 +416,14 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
     if (k1) hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, true, NTT>), grid, block, 0, st, a);     \
     else hipLaunchKernelGGL((gae_stream_kernel<ACC, DD, false, NTT>), grid, block, 0, st, a);       \
   } while (0)
-    if (nt == 1024) {  // 128 VGPRs per lane at 4 waves per SIMD: 4 rows in flight
+    // K = 1, 1024 threads: nontemporal loads / stores (the streams are read or written once, each far
+    // larger than L2): 128 x 2^20 at 5.63 TB/s against 4.81 with the default policy
+    // (profiles/r3h_gae_bench.txt); RAI_GAE_NT=0 turns it off (diagnostics, tools/gae_bench.py)
+    const char* ntm = getenv("RAI_GAE_NT");
+    if (nt == 1024 && !(ntm && atoi(ntm) == 0)) {
+      if (mode == RAI_GAE_EXACT) hipLaunchKernelGGL((gae_stream_kernel<double, 4, true, 1024, true>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((gae_stream_kernel<float, 4, true, 1024, true>), grid, block, 0, st, a);
+    } else if (nt == 1024) {  // 128 VGPRs per lane at 4 waves per SIMD: 4 rows in flight
       if (mode == RAI_GAE_EXACT) hipLaunchKernelGGL((gae_stream_kernel<double, 4, true, 1024>), grid, block, 0, st, a);
       else hipLaunchKernelGGL((gae_stream_kernel<float, 4, true, 1024>), grid, block, 0, st, a);
     } else if (nt == 512) {  // 256 VGPRs per lane at 2 waves per SIMD: 8 rows in flight

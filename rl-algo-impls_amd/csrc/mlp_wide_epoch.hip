@@ -330,10 +330,16 @@ __device__ __forceinline__ void adam_fast(float& p, float& m, float& v, float g,
 // dH1 tile of wave w: D[i][u] = sum_k dZ2[16 w + i][k] W2[k][16 j + u] over k in [0, H): lane group g
 // takes k in [g KQ, (g + 1) KQ), four at a time: A from the Act row (16-B reads), B from W2cT[k / 16][u]
 // (16-B reads); four accumulator chains, unrolled and read one step ahead for the common widths
+// W2cT rows are stored swizzled (we_w2t_src): unit u's 16-B piece kk4 sits at slot kk4 ^ ((u >> 2) & 3),
+// so the 16 units' reads of one piece spread over all 16 bank groups (a plain [u][16] row stride of
+// 64 B put four units on every bank group)
+__device__ __forceinline__ int we_w2t_slot(int u, int kk4) { return kk4 ^ ((u >> 2) & 3); }
 template <int KQ>
-__device__ __forceinline__ f4 we_dh1_tile_k(const float* ra, const float* wt, int k0) {
+__device__ __forceinline__ f4 we_dh1_tile_k(const float* ra, const float* wt, int k0, int u) {
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
-  auto bptr = [&](int kk) { return wt + ((k0 + kk) >> 4) * (WE_SL * WE_SL) + ((k0 + kk) & 15); };
+  auto bptr = [&](int kk) {
+    return wt + ((k0 + kk) >> 4) * (WE_SL * WE_SL) + 4 * we_w2t_slot(u, ((k0 + kk) & 15) >> 2);
+  };
   f4 av = *reinterpret_cast<const f4*>(ra), bv = *reinterpret_cast<const f4*>(bptr(0));
 #pragma unroll
   for (int kk = 0; kk < KQ; kk += 4) {
@@ -355,17 +361,17 @@ __device__ __forceinline__ f4 we_dh1_tile_k(const float* ra, const float* wt, in
   }
   return (acc0 + acc1) + (acc2 + acc3);
 }
-__device__ __forceinline__ f4 we_dh1_tile(const float* act_row, const float* w2t_u, int H, int g) {
+__device__ __forceinline__ f4 we_dh1_tile(const float* act_row, const float* w2t_u, int H, int g, int u) {
   const int KQ = H >> 2, k0 = g * KQ;
   const float* ra = act_row + k0;
-  if (H == 256) return we_dh1_tile_k<64>(ra, w2t_u, k0);
-  if (H == 128) return we_dh1_tile_k<32>(ra, w2t_u, k0);
-  if (H == 64) return we_dh1_tile_k<16>(ra, w2t_u, k0);
+  if (H == 256) return we_dh1_tile_k<64>(ra, w2t_u, k0, u);
+  if (H == 128) return we_dh1_tile_k<32>(ra, w2t_u, k0, u);
+  if (H == 64) return we_dh1_tile_k<16>(ra, w2t_u, k0, u);
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
   for (int kk = 0; kk < KQ; kk += 4) {
     const int k = k0 + kk;
     const f4 av = *reinterpret_cast<const f4*>(ra + kk);
-    const f4 bv = *reinterpret_cast<const f4*>(w2t_u + (k >> 4) * (WE_SL * WE_SL) + (k & 15));
+    const f4 bv = *reinterpret_cast<const f4*>(w2t_u + (k >> 4) * (WE_SL * WE_SL) + 4 * we_w2t_slot(u, (k & 15) >> 2));
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
     acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc1, 0, 0, 0);
     acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc2, 0, 0, 0);
@@ -389,6 +395,38 @@ __device__ __forceinline__ void we_publish_w2(const float (*W2r)[WE_HP], __amdgp
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), wrs,
                                              (int)(base + (int64_t)ct * 1024 + (u * WE_SL + 4 * kk4) * 4), 0, WE_SC1);
     }
+  }
+}
+
+// fwd1 tile: sum over k = 4 kk + g < IN4 of X[row][k] W1j[unit][k]; operands read first, then the
+// MFMAs in two chains (unrolled for each K-step count up to 16)
+template <int NK>
+__device__ __forceinline__ f4 we_fwd1_k(const float* xa, const float* wa) {
+  float xv[NK], wv[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    xv[kk] = xa[4 * kk];
+    wv[kk] = wa[4 * kk];
+  }
+  f4 z0 = {0.f, 0.f, 0.f, 0.f}, z1 = z0;
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    if (kk & 1) z1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[kk], wv[kk], z1, 0, 0, 0);
+    else z0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[kk], wv[kk], z0, 0, 0, 0);
+  }
+  return z0 + z1;
+}
+__device__ __forceinline__ f4 we_fwd1(const float* xa, const float* wa, int nk) {
+  switch (nk) {
+#define WE_FWD1_CASE(n) \
+  case n:               \
+    return we_fwd1_k<n>(xa, wa);
+    WE_FWD1_CASE(1) WE_FWD1_CASE(2) WE_FWD1_CASE(3) WE_FWD1_CASE(4) WE_FWD1_CASE(5) WE_FWD1_CASE(6)
+    WE_FWD1_CASE(7) WE_FWD1_CASE(8) WE_FWD1_CASE(9) WE_FWD1_CASE(10) WE_FWD1_CASE(11) WE_FWD1_CASE(12)
+    WE_FWD1_CASE(13) WE_FWD1_CASE(14) WE_FWD1_CASE(15)
+#undef WE_FWD1_CASE
+    default:
+      return we_fwd1_k<16>(xa, wa);  // IN4 <= 64
   }
 }
 
@@ -608,12 +646,8 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     };
     // ============ fwd1: H1[:, j] = act(X W1[j]^T + b1[j]); wave w: row tile w =============
     {
-      f4 z = {0.f, 0.f, 0.f, 0.f};
-      for (int kk = 0; kk < IN4 / 4; ++kk) {
-        const int k = 4 * kk + g;
-        // k in [IN, IN4) reads the next row (or the zero tail) against W1j's zero padding
-        z = __builtin_amdgcn_mfma_f32_16x16x4f32(S.Xl[(16 * w + li) * IN4 + k], S.W1j[li][k], z, 0, 0, 0);
-      }
+      // k in [IN, IN4) reads the observation's zero padding against W1j's
+      const f4 z = we_fwd1(&S.Xl[(16 * w + li) * IN4 + g], &S.W1j[li][g], IN4 / 4);
       const float bj = S.small[li];
 #pragma unroll
       for (int r = 0; r < 4; ++r) S.H1j[16 * w + 4 * g + r][li] = we_act(act, z[r] + bj);
@@ -632,7 +666,11 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     // W2's column slice j as the row owners published it after the last Adam step (16 tiles of 1 KB,
     // one LDS-DMA load each; drained by the gather's vmcnt below), then H1 -> Act
     {
-      const unsigned char* src = a.ws + WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * 1024 + lane * 16;
+      // lane l lands at LDS slot (u = l >> 2, s = l & 3): it fetches piece we_w2t_slot(u, s) of row u
+      // (the swizzle is an involution), pre-swizzling the source as LDS-DMA requires
+      const int u = lane >> 2;
+      const unsigned char* src =
+          a.ws + WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * 1024 + (u * WE_SL + 4 * we_w2t_slot(u, lane & 3)) * 4;
 #pragma unroll
       for (int m = 0; m < WE_GMAX / 4; ++m) {
         const int p = w + 4 * m;
@@ -656,14 +694,21 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     {  // output-layer partials over the slice: P[row][o] = sum_c H2[row][c] W3[o][16 j + c]
       if (tid < WE_B * 2) {
         const int r = tid >> 1, o0 = 4 * (tid & 1);
+        // 16-B LDS reads, no per-output branches: W3 rows o >= O are zero, so those sums are 0
         f4 p = {0.f, 0.f, 0.f, 0.f};
+        const f4* h4 = reinterpret_cast<const f4*>(&S.H2j[r][0]);
+        const f4 h[4] = {h4[0], h4[1], h4[2], h4[3]};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int o = o0 + q;
+          const f4* w4 = reinterpret_cast<const f4*>(&S.small[2 * WE_SL + (o0 + q) * WE_SL]);
           float s = 0.f;
-          if (o < O) {
 #pragma unroll
-            for (int c = 0; c < WE_SL; ++c) s += S.H2j[r][c] * S.small[2 * WE_SL + o * WE_SL + c];
+          for (int c4 = 0; c4 < 4; ++c4) {
+            const f4 wv = w4[c4];
+            s += h[c4].x * wv.x;
+            s += h[c4].y * wv.y;
+            s += h[c4].z * wv.z;
+            s += h[c4].w * wv.w;
           }
           p[q] = s;
         }
@@ -937,7 +982,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     // ============ bwd1: dH1[:, j] = dZ2 W2[:, slice j] -> dZ1, dW1 rows j, db1 j ==================
     {
       // wave w: row tile w; lane (li, g) holds dH1[16 w + 4 g + r][16 j + li], r < 4 (MFMA layout)
-      const f4 z = we_dh1_tile(&S.Act[16 * w + li][0], &S.W2cT[0][li][0], H, g);
+      const f4 z = we_dh1_tile(&S.Act[16 * w + li][0], &S.W2cT[0][li][0], H, g, li);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * w + 4 * g + r;

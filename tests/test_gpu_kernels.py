@@ -60,8 +60,9 @@ def test_gae_full_size_exact_vs_c_oracle(T, N, K, dens):
     np.testing.assert_array_equal(ret.cpu().numpy(), ret_ref)
 
 
-@pytest.mark.parametrize("D,NT", [("8", "256"), ("4", "256"), ("8", "512"), ("4", "1024"), ("8", "default")])
-def test_gae_stream_kernel_rows_in_flight_variants(D, NT, monkeypatch):
+@pytest.mark.parametrize("D,NT,NTM", [("8", "256", "0"), ("4", "256", "0"), ("8", "512", "0"), ("4", "1024", "0"),
+                                      ("4", "1024", "1"), ("8", "default", "1")])
+def test_gae_stream_kernel_rows_in_flight_variants(D, NT, NTM, monkeypatch):
     """Both chunk depths of the streaming GAE kernel (RAI_GAE_STREAM_D) and the tiled kernel forced on
     the same large input (RAI_GAE_STREAM=0) give the C oracle's bits."""
     rng = np.random.default_rng(41)
@@ -75,6 +76,7 @@ def test_gae_stream_kernel_rows_in_flight_variants(D, NT, monkeypatch):
     for stream in ("1", "0"):
         monkeypatch.setenv("RAI_GAE_STREAM_D", D)
         monkeypatch.setenv("RAI_GAE_STREAM_NT", NT)
+        monkeypatch.setenv("RAI_GAE_NT", NTM)  # nontemporal loads / stores
         monkeypatch.setenv("RAI_GAE_STREAM", stream)
         adv, ret = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), 0.98, 0.8, want_returns=True)
         np.testing.assert_array_equal(adv.cpu().numpy(), adv_ref)

@@ -22,10 +22,11 @@ VARIANTS = [("default", {})]
 if os.environ.get("GAE_BENCH_VARIANTS", "1") != "0":
     VARIANTS += [("tiled", {"RAI_GAE_STREAM": "0"}), ("stream_d8", {"RAI_GAE_STREAM_D": "8", "RAI_GAE_STREAM_NT": "256"}),
                  ("stream_d4", {"RAI_GAE_STREAM_D": "4", "RAI_GAE_STREAM_NT": "256"}), ("stream_512", {"RAI_GAE_STREAM_NT": "512"}),
-                 ("stream_1k", {"RAI_GAE_STREAM_NT": "1024"})]
+                 ("stream_1k_plain", {"RAI_GAE_STREAM_NT": "1024", "RAI_GAE_NT": "0"}),
+                 ("stream_1k_nt", {"RAI_GAE_STREAM_NT": "1024"})]
 CASES = [(128, 4096, 1), (512, 2048, 1), (128, 1024, 1), (512, 512, 3), (128, 1 << 20, 1), (512, 1 << 18, 3)]
 for (T, N, K, vname, venv) in [c + v for c in CASES for v in (VARIANTS if c[1] >= (1 << 18) else VARIANTS[:1])]:
-    for k in ("RAI_GAE_STREAM", "RAI_GAE_STREAM_D", "RAI_GAE_STREAM_NT"):
+    for k in ("RAI_GAE_STREAM", "RAI_GAE_STREAM_D", "RAI_GAE_STREAM_NT", "RAI_GAE_NT"):
         os.environ.pop(k, None)
     os.environ.update(venv)
     shp = (T, N) if K == 1 else (T, N, K)
