@@ -179,6 +179,7 @@ template <int KQ>
 __device__ __forceinline__ f4 we_tile_dot_k(const float* ra, const float* cb) {
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
   f4 av = *reinterpret_cast<const f4*>(ra), bv = *reinterpret_cast<const f4*>(cb);
+  __builtin_amdgcn_sched_barrier(0);  // the prologue reads stay outside the loop's schedule groups
 #pragma unroll
   for (int kk = 0; kk < KQ; kk += 4) {
     f4 an = av, bn = bv;
@@ -337,10 +338,14 @@ __device__ __forceinline__ int we_w2t_slot(int u, int kk4) { return kk4 ^ ((u >>
 template <int KQ>
 __device__ __forceinline__ f4 we_dh1_tile_k(const float* ra, const float* wt, int k0, int u) {
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
-  auto bptr = [&](int kk) {
-    return wt + ((k0 + kk) >> 4) * (WE_SL * WE_SL) + 4 * we_w2t_slot(u, ((k0 + kk) & 15) >> 2);
-  };
+  // k0 is a multiple of 16 here (KQ >= 16): the four swizzled piece bases once, then every read is
+  // one of them plus a compile-time offset (no per-step address arithmetic between the reads)
+  const float* bp[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) bp[c] = wt + (k0 >> 4) * (WE_SL * WE_SL) + 4 * we_w2t_slot(u, c);
+  auto bptr = [&](int kk) { return bp[(kk >> 2) & 3] + (kk >> 4) * (WE_SL * WE_SL); };
   f4 av = *reinterpret_cast<const f4*>(ra), bv = *reinterpret_cast<const f4*>(bptr(0));
+  __builtin_amdgcn_sched_barrier(0);  // the prologue reads stay outside the loop's schedule groups
 #pragma unroll
   for (int kk = 0; kk < KQ; kk += 4) {
     f4 an = av, bn = bv;
@@ -408,6 +413,7 @@ __device__ __forceinline__ f4 we_fwd1_k(const float* xa, const float* wa) {
     xv[kk] = xa[4 * kk];
     wv[kk] = wa[4 * kk];
   }
+  __builtin_amdgcn_sched_barrier(0);
   f4 z0 = {0.f, 0.f, 0.f, 0.f}, z1 = z0;
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
@@ -954,11 +960,13 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     WSTAMP(10);
-    f4 g_r[4];
-    we_dw2_tiles4<0, WE_SL>(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * 4 * w], WE_HP, lane, g_r);
+    f4 g_rv[4];
+    we_dw2_tiles4<0, WE_SL>(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * 4 * w], WE_HP, lane, g_rv);
+    float g_r[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      if (4 * w + t >= G) g_r[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g_r[t][r] = 4 * w + t >= G ? 0.f : g_rv[t][r];
     WSTAMP(11);
     // wait for every workgroup's dZ2 slice
     if (tid == 0) {
@@ -994,27 +1002,23 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     WSTAMP(15);
     f4 g_1 = {0.f, 0.f, 0.f, 0.f};  // dW1[16 j + 4 g + r][16 w + li]
     if (WE_SL * w < IN) {
-      // two accumulator chains (even / odd kk), operands read one step ahead
+      // all 32 operands read first (the observation rows' stride IN4 is a runtime value, so their
+      // addresses are formed here, outside the MFMA sequence), then two accumulator chains
       const float* za = &S.Z1j[we_krow(0, g)][li];
       const float* xa = &S.Xl[we_krow(0, g) * IN4 + min(WE_SL * w + li, IN - 1)];
-      f4 g_1b = {0.f, 0.f, 0.f, 0.f};
-      float zv = za[0], xv = xa[0];
+      float zv[WE_B / 4], xv[WE_B / 4];
 #pragma unroll
       for (int kk = 0; kk < WE_B / 4; ++kk) {
-        const int dk = 8 * ((kk + 1) >> 1) + ((kk + 1) & 1);
-        float zn = zv, xn = xv;
-        if (kk + 1 < WE_B / 4) {
-          zn = za[dk * WE_SP];
-          xn = xa[dk * IN4];
-        }
-        if (kk & 1) g_1b = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, xv, g_1b, 0, 0, 0);
-        else g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv, xv, g_1, 0, 0, 0);
-        if (kk + 1 < WE_B / 4) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        }
-        zv = zn;
-        xv = xn;
+        const int dk = 8 * (kk >> 1) + (kk & 1);  // we_krow(kk, g) - we_krow(0, g)
+        zv[kk] = za[dk * WE_SP];
+        xv[kk] = xa[dk * IN4];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f4 g_1b = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < WE_B / 4; ++kk) {
+        if (kk & 1) g_1b = __builtin_amdgcn_mfma_f32_16x16x4f32(zv[kk], xv[kk], g_1b, 0, 0, 0);
+        else g_1 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv[kk], xv[kk], g_1, 0, 0, 0);
       }
       g_1 += g_1b;
     }
@@ -1046,7 +1050,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ss += (double)g_r[t][r] * (double)g_r[t][r];
+        for (int r = 0; r < 4; ++r) {
+          const double gv = (double)g_r[t][r];
+          ss += gv * gv;
+        }
       if (WE_SL * w + li < IN) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) ss += (double)g_1[r] * (double)g_1[r];
