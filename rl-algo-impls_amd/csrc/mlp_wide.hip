@@ -177,7 +177,7 @@ __global__ __launch_bounds__(WT) void wide_fwd1_kernel(const WideArgs a) {
   if (t < SL) b1s[t] = d.w[n][1][s * SL + t];
   const WideWs w = ws_of(a.ws, n, B, H);
   const int j = t % SL, r0 = t / SL;
-  for (int c0 = 0; c0 < B; c0 += RC) {
+  for (int c0 = blockIdx.z * RC; c0 < B; c0 += RC * gridDim.z) {  // row chunks over grid.z
     const int nr = min(RC, B - c0);
     __syncthreads();
     stage1<16>(&xs[0][0], RAI_WIDE_MAX_IN + 1, a.obs + (int64_t)c0 * IN, IN, nr, IN);
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(WT) void wide_fwd2_kernel(const WideArgs a) {
   const WideWs w = ws_of(a.ws, n, B, H);
   stage4(&w2s[0][0], HP, d.w[n][2] + (int64_t)s * SL * H, H, SL, H);
   for (int i = t; i < O * SL; i += WT) w3s[i / SL][i % SL] = d.w[n][4][(int64_t)(i / SL) * H + s * SL + i % SL];
-  for (int c0 = 0; c0 < B; c0 += RC) {
+  for (int c0 = blockIdx.z * RC; c0 < B; c0 += RC * gridDim.z) {  // row chunks over grid.z
     const int nr = min(RC, B - c0);
     __syncthreads();
     stage4(&hs[0][0], HP, w.H1 + (int64_t)c0 * H, H, nr, H);
@@ -561,7 +561,8 @@ extern "C" int rai_mlp_wide_forward(const rai_mlp_wide_desc* desc, const float* 
   a.logp = logp_out;
   a.ent = entropy_out;
   a.v = v_out;
-  const dim3 grid(desc->hidden / SL, 2);
+  // the forward's row chunks (RC rows each) run on separate workgroups: the rollout's B = N envs
+  const dim3 grid(desc->hidden / SL, 2, (unsigned)((B + RC - 1) / RC));
   hipStream_t st = rai_stream(stream);
   hipLaunchKernelGGL(wide_fwd1_kernel, grid, dim3(WT), 0, st, a);
   RAI_LAUNCH_CHECK();
@@ -579,7 +580,8 @@ extern "C" int rai_mlp_wide_dist_params(const rai_mlp_wide_desc* desc, const flo
   if (!params_out || !v_out) return RAI_E_NULLPTR;
   WideArgs a = make_args(desc, obs, B, workspace);
   a.v = v_out;
-  const dim3 grid(desc->hidden / SL, 2);
+  // the forward's row chunks (RC rows each) run on separate workgroups: the rollout's B = N envs
+  const dim3 grid(desc->hidden / SL, 2, (unsigned)((B + RC - 1) / RC));
   hipStream_t st = rai_stream(stream);
   hipLaunchKernelGGL(wide_fwd1_kernel, grid, dim3(WT), 0, st, a);
   RAI_LAUNCH_CHECK();
@@ -625,7 +627,8 @@ extern "C" int rai_mlp_wide_forward_loss(const rai_mlp_wide_desc* desc, const fl
   la.n_entropy = desc->head == 1 ? B * desc->out_pi : B;
   la.K = 1;
   la.max_stats = max_stats;
-  const dim3 grid(desc->hidden / SL, 2);
+  // the forward's row chunks (RC rows each) run on separate workgroups: the rollout's B = N envs
+  const dim3 grid(desc->hidden / SL, 2, (unsigned)((B + RC - 1) / RC));
   hipStream_t st = rai_stream(stream);
   hipLaunchKernelGGL(wide_fwd1_kernel, grid, dim3(WT), 0, st, a);
   RAI_LAUNCH_CHECK();

@@ -550,8 +550,8 @@ def test_wide_mlp_kernels_match_pytorch_path(kind, hidden, act, extra, epoch, mo
         np.testing.assert_allclose(n_w, n_t, rtol=1e-4)
 
 
-@pytest.mark.parametrize("kind", ["halfcheetah", "cartpole"])
-def test_wide_rollout_forward_matches_module(kind, monkeypatch):
+@pytest.mark.parametrize("kind,N", [("halfcheetah", 64), ("cartpole", 64), ("halfcheetah", 200)])
+def test_wide_rollout_forward_matches_module(kind, N, monkeypatch):
     """The rollout's policy forward through rai_mlp_wide_dist_params (3 launches, graph-replayed)
     against the PyTorch module forward (RAI_ROLLOUT_WIDE=0): same seeded sampler, so the sampled
     actions, log-probs and values of 16 env steps agree to fp32 tolerance (the Gaussian action is
@@ -563,7 +563,7 @@ def test_wide_rollout_forward_matches_module(kind, monkeypatch):
     for wide in ("1", "0"):
         monkeypatch.setenv("RAI_ROLLOUT_WIDE", wide)
         torch.manual_seed(3)
-        env = SyntheticVecEnv(64, kind, seed=5)
+        env = SyntheticVecEnv(N, kind, seed=5)  # N = 200: four 64-row chunks (grid.z), the last ragged
         pkw = dict(pi_hidden_sizes=[256, 256], v_hidden_sizes=[256, 256], activation_fn="relu")
         if kind == "halfcheetah":
             pkw.update(log_std_init=-1.0, init_layers_orthogonal=False)
