@@ -276,10 +276,11 @@ __device__ __forceinline__ void we_dw2_tiles4(const float* A, int lda, const flo
 }
 
 // One 16 x 16 MFMA tile over the 64 minibatch rows, D[i][jj] = sum_k A[k][i] B[k][jj], for the
-// small-parameter gradients: lane (li, g) feeds A = a0[k LDA] * amul and B = b0[k WE_SP] * bm + bo at
-// rows k = we_krow(kk, g); every operand is read first, then two MFMA chains.
-template <int LDA>
-__device__ __forceinline__ f4 we_small_tile(const float* a0, float amul, const float* b0, float bm, float bo, int g) {
+// small-parameter gradients: lane (li, g) feeds A = a0[k LDA] and B = b0[k WE_SP] (ONES: B = 1) at
+// rows k = we_krow(kk, g); every operand is read first, then two MFMA chains.  Rows i of D that come
+// from padding lanes are never stored, so no operand needs masking.
+template <int LDA, bool ONES>
+__device__ __forceinline__ f4 we_small_tile(const float* a0, const float* b0, int g) {
   const int k0 = we_krow(0, g);
   a0 += k0 * LDA;
   b0 += k0 * WE_SP;
@@ -287,18 +288,16 @@ __device__ __forceinline__ f4 we_small_tile(const float* a0, float amul, const f
 #pragma unroll
   for (int kk = 0; kk < WE_B / 4; ++kk) {
     const int dk = 8 * (kk >> 1) + (kk & 1);
-    av[kk] = a0[dk * LDA] * amul;
-    bv[kk] = b0[dk * WE_SP] * bm + bo;
+    av[kk] = a0[dk * LDA];
+    bv[kk] = ONES ? 1.f : b0[dk * WE_SP];
   }
+  __builtin_amdgcn_sched_barrier(0);
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
 #pragma unroll
   for (int kk = 0; kk < WE_B / 4; ++kk) {
     if (kk & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc1, 0, 0, 0);
     else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc0, 0, 0, 0);
   }
-  __builtin_amdgcn_sched_group_barrier(0x100, 32, 0);  // all operand reads first
-  __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);  // their scaling
-  __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);  // then the MFMAs
   return acc0 + acc1;
 }
 
@@ -941,13 +940,12 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     // dlog_std), wave 2 those of dZ2 (db2); b1 j is formed after dZ1 (below).  Every workgroup forms
     // db3 / dlog_std with the same code on the same rows, so their copies stay identical.
     if (w < 3) {
-      // A = a0[k lda] * amul, B = H2[k][li] * bm + bo; row offsets are compile-time so the reads use
-      // immediate offsets from one base (no per-row address registers)
-      const float amul = (w == 0 && li >= WE_OUTM) ? 0.f : 1.f;
-      const float bm = w == 0 ? 1.f : 0.f, bo = 1.f - bm;
-      const f4 dsm = w == 2 ? we_small_tile<WE_SP>(&S.Z2j[0][li], amul, &S.H2j[0][li], bm, bo, g)
-                            : we_small_tile<WE_OUTM>(li < WE_OUTM || w == 0 ? &S.dOut[0][li & 7] : &S.dls[0][li - WE_OUTM],
-                                                     amul, &S.H2j[0][li], bm, bo, g);
+      // row offsets are compile-time, so the reads use immediate offsets from one base
+      f4 dsm;
+      if (w == 0) dsm = we_small_tile<WE_OUTM, false>(&S.dOut[0][li & 7], &S.H2j[0][li], g);
+      else if (w == 1)
+        dsm = we_small_tile<WE_OUTM, true>(li < WE_OUTM ? &S.dOut[0][li] : &S.dls[0][li - WE_OUTM], nullptr, g);
+      else dsm = we_small_tile<WE_SP, true>(&S.Z2j[0][li], nullptr, g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 4 * g + r;  // D row; column jj = li
