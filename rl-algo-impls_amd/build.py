@@ -45,7 +45,9 @@ def lib_path(variant: str = "") -> Path:
     return Path(override) if override else LIBDIR / LIBNAME
 
 
-VARIANT_FLAGS = {"": [], "stamps": ["-DRAI_STAMPS"]}
+# "alt": an A/B build of the same sources with extra -D flags from RAI_ALT_FLAGS (tools/ab_bench.sh;
+# diagnostic, never loaded by the product)
+VARIANT_FLAGS = {"": [], "stamps": ["-DRAI_STAMPS"], "alt": os.environ.get("RAI_ALT_FLAGS", "").split()}
 
 
 def _compile(src: Path, variant: str = "") -> Path:

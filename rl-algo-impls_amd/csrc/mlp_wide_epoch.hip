@@ -21,8 +21,9 @@
 //      row 1); every workgroup gathers H1 (B x H) by LDS-DMA sc1 loads
 //   B  output-layer partials H2[:, j] W3[:, j]^T published (as A); every workgroup sums them in slice
 //      order and runs the head + loss for all rows (identical everywhere), then dZ2[:, j]
-//   C  dH1 partial tiles dZ2[:, j] W2[j rows, :] published (as A; the drain deferred past the dW2-row
-//      work) to their unit tiles' owners, which sum the G producers in slice order -> dZ1, dW1 rows j
+//   C  dZ2[:, j] published (as A); every workgroup gathers dZ2 and forms dH1[:, j] = dZ2 W2[:, j]
+//      from W2's column slice, which the row owners publish each step after their H1 gather (drained
+//      before their B arrival) and the column owners load by LDS-DMA after the B wait
 //   D  (both networks) each workgroup's share of the squared gradient norm as two tagged 8-B
 //      granules (agent-scope atomic store / load, no drain or counter); every workgroup sums the 2 G
 //      shares in a fixed order (clip_grad_norm_ over all parameters, bit-identical on every
@@ -62,7 +63,8 @@ constexpr int64_t WE_GD_OFF = WE_CTR_BYTES;                             // D: [p
 constexpr int64_t WE_STATE_BYTES = WE_GD_OFF + 2 * 2 * WE_GMAX * 2 * 8;  // the memset block
 constexpr int64_t WE_H1_OFF = WE_STATE_BYTES;                           // [net][par] H1 slots
 constexpr int64_t WE_Z2_OFF = WE_H1_OFF + 4 * WE_ACT_SLOT;              // [net][par] dZ2 slots
-// W2 as its row owners publish it after every Adam step, for the column owners' dH1: [net][producer
+// W2 as its row owners publish it each step (after the H1 gather: the last Adam step's rows), for
+// the column owners' dH1 (loaded after the B wait): [net][producer
 // p][unit tile ct] transposed 16 x 16 tiles of 1 KB, tile (p, ct)[u][kk] = W2[16 p + kk][16 ct + u]
 constexpr int64_t WE_W2T_NET = (int64_t)WE_GMAX * WE_GMAX * 1024;
 constexpr int64_t WE_W2T_OFF = WE_Z2_OFF + 4 * WE_ACT_SLOT;
@@ -668,23 +670,12 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     WSTAMP(0);
     if (!we_arrive_wait(ctr, WE_CA + net, want, a.state, S.bail, w, side_a)) break;
     WSTAMP(1);
-    // W2's column slice j as the row owners published it after the last Adam step (16 tiles of 1 KB,
-    // one LDS-DMA load each; drained by the gather's vmcnt below), then H1 -> Act
-    {
-      // lane l lands at LDS slot (u = l >> 2, s = l & 3): it fetches piece we_w2t_slot(u, s) of row u
-      // (the swizzle is an involution), pre-swizzling the source as LDS-DMA requires
-      const int u = lane >> 2;
-      const unsigned char* src =
-          a.ws + WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * 1024 + (u * WE_SL + 4 * we_w2t_slot(u, lane & 3)) * 4;
-#pragma unroll
-      for (int m = 0; m < WE_GMAX / 4; ++m) {
-        const int p = w + 4 * m;
-        if (p < G)
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(src + (int64_t)p * WE_GMAX * 1024),
-                                           &S.W2cT[p][0][0], 16, 0, WE_SC1);
-      }
-    }
-    we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);
+    we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // H1 -> Act
+    // W2 rows j (as updated by the last Adam step) for this step's column owners: issued after the
+    // gather's drain, so they drain in the background during fwd2 -- by the B publish's drain, before
+    // this workgroup's B arrival, after which the column owners load them (step 0: the tiles published
+    // before the loop)
+    if (mb > 0) we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane);
     lds_barrier();
     WSTAMP(2);
     // ============ fwd2: H2[:, j] = act(H1 W2[j]^T + b2[j]); wave w: row tile w =============
@@ -737,6 +728,24 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         qb[u] = O > 4 ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (int)off + 16, 0, WE_SC1))
                       : f4{0.f, 0.f, 0.f, 0.f};
       }
+#ifdef RAI_WE_W2T_EARLY  // A/B: the W2 column tiles issued before the partials land
+      // after the partials landed (in-order vmcnt: issued earlier, they would delay them): W2's column
+      // slice j (16 tiles of 1 KB, one LDS-DMA load each; needed at dH1, drained by the
+      // dZ2 gather's vmcnt).  Lane l lands at LDS slot (u = l >> 2, s = l & 3) and fetches piece
+      // we_w2t_slot(u, s) of row u (the swizzle is an involution: pre-swizzled source, as LDS-DMA needs)
+      {
+        const int u = lane >> 2;
+        const unsigned char* src =
+            a.ws + WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * 1024 + (u * WE_SL + 4 * we_w2t_slot(u, lane & 3)) * 4;
+#pragma unroll
+        for (int m = 0; m < WE_GMAX / 4; ++m) {
+          const int p = w + 4 * m;
+          if (p < G)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(src + (int64_t)p * WE_GMAX * 1024),
+                                             &S.W2cT[p][0][0], 16, 0, WE_SC1);
+        }
+      }
+#endif
       f4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -746,6 +755,24 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         }
       *reinterpret_cast<f4*>(&S.Pw[w][lane][0]) = sa;
       *reinterpret_cast<f4*>(&S.Pw[w][lane][4]) = sb;
+#ifndef RAI_WE_W2T_EARLY
+      // after the partials landed (in-order vmcnt: issued earlier, they would delay them): W2's column
+      // slice j (16 tiles of 1 KB, one LDS-DMA load each; needed at dH1, drained by the
+      // dZ2 gather's vmcnt).  Lane l lands at LDS slot (u = l >> 2, s = l & 3) and fetches piece
+      // we_w2t_slot(u, s) of row u (the swizzle is an involution: pre-swizzled source, as LDS-DMA needs)
+      {
+        const int u = lane >> 2;
+        const unsigned char* src =
+            a.ws + WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * 1024 + (u * WE_SL + 4 * we_w2t_slot(u, lane & 3)) * 4;
+#pragma unroll
+        for (int m = 0; m < WE_GMAX / 4; ++m) {
+          const int p = w + 4 * m;
+          if (p < G)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(src + (int64_t)p * WE_GMAX * 1024),
+                                             &S.W2cT[p][0][0], 16, 0, WE_SC1);
+        }
+      }
+#endif
     }
     lds_barrier();
     WSTAMP(6);
@@ -1147,7 +1174,6 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     lds_barrier();
-    if (mb + 1 < nmb) we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane);  // for the next step's column owners
     WSTAMP(21);
   }
 #ifdef RAI_STAMPS
