@@ -425,17 +425,27 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       f4 dh1[CT];
 #pragma unroll
       for (int tt = 0; tt < CT; ++tt) dh1[tt] = f4{0.f, 0.f, 0.f, 0.f};
+      // every operand read before the first MFMA (one LDS latency instead of one per k step)
+      f2 avs[8];
+      float bxs[8][CT], bys[8][CT];
 #pragma unroll
-      for (int kk = 0; kk < 16; kk += 2) {
-        const int kq = kmap(g, kk);
-        const f2 av = *reinterpret_cast<const f2*>(&S.Z2[16 * T_ + li][kq]);
+      for (int k2 = 0; k2 < 8; ++k2) {
+        const int kq = kmap(g, 2 * k2);
+        avs[k2] = *reinterpret_cast<const f2*>(&S.Z2[16 * T_ + li][kq]);
 #pragma unroll
         for (int tt = 0; tt < CT; ++tt) {
           const int t = CT * hf_ + tt;
-          const float bx = S.Wt[WL_W2 + kq * LD + 16 * t + li];
-          const float by = S.Wt[WL_W2 + (kq + 1) * LD + 16 * t + li];
-          dh1[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bx, dh1[tt], 0, 0, 0);
-          dh1[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, by, dh1[tt], 0, 0, 0);
+          bxs[k2][tt] = S.Wt[WL_W2 + kq * LD + 16 * t + li];
+          bys[k2][tt] = S.Wt[WL_W2 + (kq + 1) * LD + 16 * t + li];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) {
+#pragma unroll
+        for (int tt = 0; tt < CT; ++tt) {
+          dh1[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(avs[k2].x, bxs[k2][tt], dh1[tt], 0, 0, 0);
+          dh1[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(avs[k2].y, bys[k2][tt], dh1[tt], 0, 0, 0);
         }
       }
       float pb1[CT], pw1[CT][4];
@@ -474,16 +484,27 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[OUTP + 2 + k] = red4(pw1[tt][k]);
         if (g == tt) {
-          const int t = CT * hf_ + tt;
+          const int j = 16 * (CT * hf_ + tt) + li;
+          if constexpr (NTILE == 1) {  // one tile: its partials are the CU's sums (P_B copies nothing)
 #pragma unroll
-          for (int p = 0; p < NPART; ++p) S.Ps[T_][p][16 * t + li] = v[p];
+            for (int o = 0; o < OUTP; ++o) S.Gb[WL_W3 + o * LD + j] = v[o];
+            S.Gb[WL_B2 + j] = v[OUTP];
+            S.Gb[WL_B1 + j] = v[OUTP + 1];
+            *reinterpret_cast<f4*>(&S.Gb[WL_W1 + 4 * j]) = f4{v[OUTP + 2], v[OUTP + 3], v[OUTP + 4], v[OUTP + 5]};
+          } else {
+#pragma unroll
+            for (int p = 0; p < NPART; ++p) S.Ps[T_][p][j] = v[p];
+          }
         }
       }
       if (hf_ == 0) {  // per-tile loss sums, once per tile
 #pragma unroll
         for (int o = 0; o < OUTP; ++o) {
           const float t3 = wave_sum_v(li < 4 ? dq[o] : 0.f);
-          if (lane == 0) S.db3p[T_][o] = t3;
+          if (lane == 0) {
+            if constexpr (NTILE == 1) S.Gb[WL_B3 + o] = t3;
+            else S.db3p[T_][o] = t3;
+          }
         }
       }
     }
@@ -495,19 +516,27 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       f4 gacc[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) gacc[t] = f4{0.f, 0.f, 0.f, 0.f};
+      float avs[RC / 4], bvs[RC / 4][4];
 #pragma unroll
       for (int kk = 0; kk < RC / 4; ++kk) {
         const int s = g * (RC / 4) + kk;  // lane group g: rows [g RC/4, +RC/4)
-        const float av = S.Z2[s][w * 16 + li];
+        avs[kk] = S.Z2[s][w * 16 + li];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bvs[kk][t] = S.H1[s][t * 16 + li];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < RC / 4; ++kk) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-          gacc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, S.H1[s][t * 16 + li], gacc[t], 0, 0, 0);
+          gacc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(avs[kk], bvs[kk][t], gacc[t], 0, 0, 0);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) S.Gb[WL_W2 + (w * 16 + g * 4 + r) * LD + t * 16 + li] = gacc[t][r];
-      // the other tensors: sum of the tiles' partials in tile order
+      // the other tensors: sum of the tiles' partials in tile order (one tile: already in S.Gb)
+      if constexpr (NTILE > 1) {
       auto tsum = [&](int p, int j) {
         float v = S.Ps[0][p][j];
 #pragma unroll
@@ -543,6 +572,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         }
         S.Gb[dst] = sum;
       }
+      }
     }
     lds_barrier();
     STAMP(5);
@@ -550,13 +580,13 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
     {
       RELANE();
       const int sbase = ((net * 2 + par) * G + c) * WL_N * (int)sizeof(float);
+      f4 pv[MC_CPT];
+#pragma unroll
+      for (int i = 0; i < MC_CPT; ++i) pv[i] = *reinterpret_cast<const f4*>(&S.Gb[4 * min(tid + M8_NT * i, WL_CH - 1)]);
 #pragma unroll
       for (int i = 0; i < MC_CPT; ++i) {
         const int ch = tid + M8_NT * i;
-        if (ch < WL_CH) {
-          const f4 v = *reinterpret_cast<const f4*>(&S.Gb[4 * ch]);
-          __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), srs, sbase + 16 * ch, 0, 16);
-        }
+        if (ch < WL_CH) __builtin_amdgcn_raw_buffer_store_b128(as_u4(pv[i]), srs, sbase + 16 * ch, 0, 16);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
     }
