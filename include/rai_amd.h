@@ -168,6 +168,39 @@ int rai_bias_relu_fwd_nchw(const float* x, const float* b, int64_t B, int32_t HW
                            void* stream);
 int rai_bias_relu_bwd_nchw(const float* dy, const float* y, int64_t B, int32_t HW, int32_t C, float* dx, float* db,
                            int32_t accumulate, void* workspace, int64_t workspace_bytes, void* stream);
+/* NatureCNN Conv2d -> ReLU forward in ONE launch (nature_cnn.py:31-41; replaces MIOpen's bias-free
+ * convolution + rai_bias_relu_fwd): a hand-written f32 MFMA implicit GEMM with the bias + ReLU in its
+ * store.  x NHWC fp32 (B, H, W, Ci); w channels_last (Co, KH, KW, Ci); b (Co); padding 0, dilation 1.
+ * y: NHWC (B, OH, OW, Co), or with out_nchw != 0 the nn.Flatten order (B, Co * OH * OW).
+ * Ci % 4 == 0, Co % 16 == 0 (the NatureCNN layers: Co 32 / 64), KH * KW * Ci % 32 == 0 and <= 8192,
+ * every pointer 16-B aligned.  f32 products, summation order of the kernel (fp32 tolerance vs
+ * PyTorch); deterministic. */
+int rai_conv2d_bias_relu_fwd(const float* x, const float* w, const float* b, int64_t B, int32_t H, int32_t W,
+                             int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, int32_t out_nchw,
+                             float* y, void* stream);
+/* The same with a fixed workgroup blocking (variant 0 = chosen by shape, as above; 1-11 = the blockings and prefetch depths
+ * in csrc/conv.hip, for same-box A/B timing in tools/conv_bench.py). */
+int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const float* b, int64_t B, int32_t H, int32_t W,
+                               int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, int32_t out_nchw,
+                               float* y, int32_t variant, void* stream);
+/* Weight gradient of the same convolution (the dW of Conv2d's autograd backward, nature_cnn.py:31-41):
+ * dw[co][kh][kw][ci] (channels_last, as optim.FlatParams stores it) = sum over the B * OH * OW output
+ * pixels p of dz[p][co] * x[receptive field of p][kh][kw][ci]; accumulate != 0 adds it to dw (the
+ * flat .grad view).  dz NHWC (B, OH, OW, Co) (the bias + ReLU backward's output).  Co 32 or 64,
+ * Ci % 4 == 0, KH * KW * Ci % 64 == 0, pointers 16-B aligned.  Hand-written f32 MFMA: per-workgroup
+ * partial tiles in workspace (rai_conv2d_wgrad_workspace_bytes, no zeroing needed), summed in a fixed
+ * order by a second launch (deterministic).  Replaces MIOpen's weight-gradient solver, its split-K
+ * zero-fill and the gradient's accumulate. */
+int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH,
+                                         int32_t KW, int32_t stride);
+int rai_conv2d_wgrad(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
+                     int32_t KH, int32_t KW, int32_t stride, float* dw, int32_t accumulate, void* workspace,
+                     int64_t workspace_bytes, void* stream);
+/* The same with a fixed launch shape for same-box A/B (tools/conv_bench.py): target_wgs workgroups
+ * (0 = 512, at most 1024), pf pixel steps in flight per wave (0 = 4; 4 or 8). */
+int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
+                       int32_t KH, int32_t KW, int32_t stride, float* dw, int32_t accumulate, void* workspace,
+                       int64_t workspace_bytes, int32_t target_wgs, int32_t pf, void* stream);
 
 /* --------------------------------------------------------------------------
  * Device-resident hyperparameters and training state.

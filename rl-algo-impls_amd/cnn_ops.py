@@ -10,6 +10,13 @@ MIOpen / hipBLASLt (MFMA), bias-free, and the epilogue is one HIP pass each way
     forward    y = relu(conv(x, W) + b)             conv bias-free, then one pass
     backward   dz = dy * (y > 0), db (+)= sum dz     one launch, deterministic order
 
+Convolutions on hand-written MFMA kernels (round 3, csrc/conv.hip).  The forward of every NatureCNN
+conv -> ReLU pair is ONE launch, rai_conv2d_bias_relu_fwd (f32 MFMA implicit GEMM, bias + ReLU in its
+store, conv3 writing nn.Flatten's NCHW order directly), and the weight gradient is
+rai_conv2d_wgrad (f32 MFMA, fixed-order split reduction) added straight into the flat .grad view.
+The input gradient (conv2, conv3) stays on MIOpen.  Shapes those kernels do not take fall back to
+MIOpen (still on the GPU); RAI_CONV_MFMA=0 selects MIOpen everywhere (same-box A/B).
+
 Direct gradient accumulation.  Inside the trainer's update (`direct_grads(module)`), every
 parameter's .grad is a view into the flat gradient buffer (optim.FlatParams), zeroed by the
 optimizer step.  The bias gradient is then added by the backward kernel straight into that view,
@@ -21,6 +28,7 @@ etc. see ordinary gradients).
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 import weakref
 from typing import Dict
@@ -123,6 +131,71 @@ class _Workspaces:
 
 _WS = _Workspaces()
 
+_CONV_MFMA = os.environ.get("RAI_CONV_MFMA", "1") != "0"
+
+
+class _WgradWorkspaces:
+    """rai_conv2d_wgrad's partial tiles per (layer, size): allocated outside graph capture (the
+    graphed step's eager warm-up runs request it first), no zeroing needed."""
+
+    def __init__(self):
+        self._ws: "weakref.WeakKeyDictionary[torch.nn.Module, Dict[tuple, torch.Tensor]]" = \
+            weakref.WeakKeyDictionary()
+
+    def get(self, module: torch.nn.Module, nbytes: int, device) -> torch.Tensor:
+        per = self._ws.setdefault(module, {})
+        k = (nbytes, str(device))
+        ws = per.get(k)
+        if ws is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("cnn_ops: convolution weight-gradient workspace first requested inside a graph "
+                                   "capture")
+            ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+            per[k] = ws
+        return ws
+
+
+_WG_WS = _WgradWorkspaces()
+
+
+def _mfma_conv_ok(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride, padding) -> bool:
+    """The shapes and layouts csrc/conv.hip takes: NHWC fp32 input, channels_last weight, no padding,
+    Ci % 4 == 0, Co 32 / 64, KH * KW * Ci % 64 == 0, 16-B aligned pointers."""
+    if not _CONV_MFMA or tuple(_pair(padding)) != (0, 0):
+        return False
+    Co, Ci, KH, KW = (int(v) for v in w.shape)
+    return (x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and w.is_contiguous(memory_format=torch.channels_last) and Ci % 4 == 0 and Co in (32, 64)
+            and (KH * KW * Ci) % 64 == 0 and KH * KW * Ci <= 8192 and b.is_contiguous()
+            and all(t.data_ptr() % 16 == 0 for t in (x, w, b)))
+
+
+def _conv_fwd_mfma(x, w, b, stride, flatten) -> torch.Tensor:
+    B, Ci, H, W = (int(v) for v in x.shape)
+    Co, _, KH, KW = (int(v) for v in w.shape)
+    s = _pair(stride)[0]
+    OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+    if flatten:
+        y = torch.empty((B, Co * OH * OW), dtype=torch.float32, device=x.device)
+    else:
+        y = torch.empty((B, Co, OH, OW), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    _lib.check(_lib.lib().rai_conv2d_bias_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), B, H, W, Ci, Co, KH,
+                                                   KW, s, 1 if flatten else 0, y.data_ptr(),
+                                                   _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd")
+    return y
+
+
+def _conv_wgrad_mfma(module, x, dz, w, stride, out: torch.Tensor, accumulate: bool) -> None:
+    B, Ci, H, W = (int(v) for v in x.shape)
+    Co, _, KH, KW = (int(v) for v in w.shape)
+    s = _pair(stride)[0]
+    L = _lib.lib()
+    nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, s))
+    ws = _WG_WS.get(module, nb, x.device)
+    _lib.check(L.rai_conv2d_wgrad(x.data_ptr(), dz.data_ptr(), B, H, W, Ci, Co, KH, KW, s, out.data_ptr(),
+                                  1 if accumulate else 0, ws.data_ptr(), nb, _lib.stream_handle(x.device)),
+               "rai_conv2d_wgrad")
+
 
 def _bias_relu_fwd(z: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     C = int(z.shape[1])
@@ -170,18 +243,26 @@ class ConvBiasReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, stride, padding, key, flatten=False):
-        z = F.conv2d(x, w, None, stride, padding)
-        z = z.contiguous(memory_format=torch.channels_last)
-        y = _bias_relu_fwd_nchw(z, b) if flatten else _bias_relu_fwd(z, b)
+        mfma = _mfma_conv_ok(x, w, b, stride, padding) and len(set(_pair(stride))) == 1
+        if mfma:
+            y = _conv_fwd_mfma(x, w, b, stride, flatten)
+            B, _, H, W = x.shape
+            s = _pair(stride)[0]
+            zshape = (int(B), int(w.shape[0]), (int(H) - int(w.shape[2])) // s + 1, (int(W) - int(w.shape[3])) // s + 1)
+        else:
+            z = F.conv2d(x, w, None, stride, padding)
+            z = z.contiguous(memory_format=torch.channels_last)
+            y = _bias_relu_fwd_nchw(z, b) if flatten else _bias_relu_fwd(z, b)
+            zshape = tuple(int(v) for v in z.shape)
         ctx.save_for_backward(x, w, b, y)
-        ctx.conf = (stride, padding, key, _direct(b, raw=True), _direct(w), flatten, tuple(int(v) for v in z.shape))
+        ctx.conf = (stride, padding, key, _direct(b, raw=True), _direct(w), flatten, zshape, mfma)
         ctx.pending = _state.pending if ctx.conf[4] else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, b, y = ctx.saved_tensors
-        stride, padding, key, direct_b, direct_w, flatten, zshape = ctx.conf
+        stride, padding, key, direct_b, direct_w, flatten, zshape, mfma = ctx.conf
         ws = _WS.get(key, zshape[1], y.device)
         if flatten:
             dz, db = _bias_relu_bwd_nchw(dy.contiguous(), y, b, ws, direct_b, zshape)
@@ -189,6 +270,23 @@ class ConvBiasReLU(torch.autograd.Function):
             dy = dy.contiguous(memory_format=torch.channels_last)
             dz, db = _bias_relu_bwd(dy, y, b, ws, direct_b)
         need_dx = ctx.needs_input_grad[0]
+        if mfma and dz.is_contiguous(memory_format=torch.channels_last) and dz.data_ptr() % 16 == 0:
+            dx = None
+            if need_dx:
+                dx = torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), _pair(padding), [1, 1], False,
+                                                         [0, 0], 1, [True, False, False])[0]
+            g = w.grad
+            if (direct_w and g.is_contiguous(memory_format=torch.channels_last) and g.data_ptr() % 16 == 0):
+                _conv_wgrad_mfma(key, x, dz, w, stride, g, accumulate=True)  # straight into the flat .grad
+                notify_grad_written(w)
+                dw = None
+            else:
+                dw = torch.empty_like(w, memory_format=torch.channels_last)
+                _conv_wgrad_mfma(key, x, dz, w, stride, dw, accumulate=False)
+                if direct_w:
+                    ctx.pending.add(w, dw)
+                    dw = None
+            return dx, dw, db, None, None, None, None
         dx, dw, _ = torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), _pair(padding), [1, 1],
                                                         False, [0, 0], 1, [need_dx, True, False])
         if direct_w:  # accumulated with the other layers' at direct_grads() exit

@@ -1,0 +1,455 @@
+// NatureCNN convolutions (config C3) as hand-written f32 MFMA implicit GEMMs on gfx950.
+//
+// Reference: rl_algo_impls/shared/encoder/nature_cnn.py:31-41 (Conv2d 8x8/4, 4x4/2, 3x3/1, each
+// followed by ReLU) and cnn.py:24-27; the bias + ReLU of the reference's Conv2d -> ReLU pair is the
+// store epilogue here, so one launch replaces MIOpen's convolution plus rai_bias_relu_fwd.
+//
+// Layouts (what the C3 trainer already holds in HBM): activations NHWC fp32 (the minibatch gather
+// writes obs / 255 as NHWC), weights channels_last [Co][KH][KW][Ci] (optim.FlatParams stores the
+// conv weights that way), bias [Co].  Output NHWC [B][OH][OW][Co], or, for the layer nn.Flatten
+// follows, the NCHW-flattened (B, Co*OH*OW) that Linear consumes.
+//
+// GEMM view: y^T[co][p] = sum_k W[co][k] * im2col(x)[p][k], k = (kh, kw, ci) -- the order of both
+// the NHWC input and the channels_last weight, so 4 consecutive k (Ci % 4 == 0) are one 16-B load
+// of either operand.  v_mfma_f32_16x16x4f32 takes lane (i, g) = (lane % 16, lane / 16) as row i of A
+// and column i of B at reduction index g.  A "quad" is 16 consecutive k = 4 chunks of 4: lane group g
+// loads chunk 4*quad + g of its weight row (A) and of its pixel's im2col row (B) as float4, and the
+// quad's four MFMAs take component j of both -- every k pairs the same weight and input element, so
+// the products are exact f32 and only the summation order differs from MIOpen's (fp32 tolerance).
+// The chunk -> im2col offset table (independent of the pixel) sits in LDS.
+//
+// The output of one MFMA is co rows 4g..4g+3 at pixel column i: a lane adds the bias, applies the
+// ReLU (t < 0 ? 0 : t, NaN kept, as rai_bias_relu_fwd) and stores one float4 of the NHWC row.
+//
+// Blocking: a wave computes TCO x TPX 16x16 output blocks (co x pixels); per quad it loads TCO + TPX
+// float4 and issues 4 * TCO * TPX MFMAs.  Operands are read straight from global memory (L1/L2:
+// the weights are shared by every workgroup, overlapping receptive fields re-read the same lines),
+// two quads in flight per wave.
+#include "common.h"
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int CV_THREADS = 256;
+constexpr int CV_MAXCHUNK = 2048;  // K <= 8192
+
+struct ConvFwdArgs {
+  const float* x;
+  const float* w;
+  const float* b;
+  float* y;
+  int64_t M;  // B * OH * OW output pixels
+  int H, W, Ci, Co, KW, S, OH, OW, K;
+};
+
+template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF>
+__global__ __launch_bounds__(CV_THREADS) void conv_fwd_kernel(const ConvFwdArgs a) {
+  static_assert(WCO * WPX == CV_THREADS / 64, "four waves");
+  __shared__ int xoff[CV_MAXCHUNK];
+  const int nch = a.K >> 2;
+  for (int q = threadIdx.x; q < nch; q += CV_THREADS) {
+    const int k = 4 * q, kpos = k / a.Ci, ci0 = k - kpos * a.Ci, kh = kpos / a.KW, kw = kpos - kh * a.KW;
+    xoff[q] = (kh * a.W + kw) * a.Ci + ci0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int wco = wv % WCO, wpx = wv / WCO;
+  const int64_t px0 = (int64_t)blockIdx.x * (16 * TPX * WPX) + 16 * TPX * wpx;
+  const int co0 = blockIdx.y * (16 * TCO * WCO) + 16 * TCO * wco;
+  const int OHW = a.OH * a.OW;
+
+  const float* xb[TPX];
+#pragma unroll
+  for (int tp = 0; tp < TPX; ++tp) {
+    int64_t p = px0 + 16 * tp + li;
+    p = p < a.M ? p : a.M - 1;
+    const int64_t n = p / OHW;
+    const int r = (int)(p - n * OHW), oh = r / a.OW, ow = r - oh * a.OW;
+    xb[tp] = a.x + ((n * a.H + (int64_t)oh * a.S) * a.W + (int64_t)ow * a.S) * a.Ci;
+  }
+  const float* wb[TCO];
+#pragma unroll
+  for (int tc = 0; tc < TCO; ++tc) wb[tc] = a.w + (int64_t)(co0 + 16 * tc + li) * a.K;
+
+  f4 acc[TCO][TPX];
+#pragma unroll
+  for (int tc = 0; tc < TCO; ++tc)
+#pragma unroll
+    for (int tp = 0; tp < TPX; ++tp) acc[tc][tp] = f4{0.f, 0.f, 0.f, 0.f};
+
+  auto load = [&](int qd, f4(&A)[TCO], f4(&Bv)[TPX]) {
+    const int q = 4 * qd + g;
+    const int xo = xoff[q];
+#pragma unroll
+    for (int tc = 0; tc < TCO; ++tc) A[tc] = *reinterpret_cast<const f4*>(wb[tc] + 4 * q);
+#pragma unroll
+    for (int tp = 0; tp < TPX; ++tp) Bv[tp] = *reinterpret_cast<const f4*>(xb[tp] + xo);
+  };
+  auto mma = [&](const f4(&A)[TCO], const f4(&Bv)[TPX]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tc = 0; tc < TCO; ++tc)
+#pragma unroll
+        for (int tp = 0; tp < TPX; ++tp)
+          acc[tc][tp] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[tc][j], Bv[tp][j], acc[tc][tp], 0, 0, 0);
+  };
+
+  const int nq = nch >> 2;  // quads (host guarantees K % 32 == 0)
+  f4 Ar[PF][TCO], Br[PF][TPX];
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nq) load(u, Ar[u], Br[u]);
+  for (int qd = 0; qd < nq; qd += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (qd + u < nq) mma(Ar[u], Br[u]);
+      if (qd + u + PF < nq) load(qd + u + PF, Ar[u], Br[u]);
+    }
+  }
+
+#pragma unroll
+  for (int tc = 0; tc < TCO; ++tc) {
+    const int co = co0 + 16 * tc + 4 * g;
+    const f4 bv = *reinterpret_cast<const f4*>(a.b + co);
+#pragma unroll
+    for (int tp = 0; tp < TPX; ++tp) {
+      const int64_t p = px0 + 16 * tp + li;
+      if (p >= a.M) continue;
+      f4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t = acc[tc][tp][r] + bv[r];
+        v[r] = t < 0.f ? 0.f : t;
+      }
+      if (!NCHW) {
+        *reinterpret_cast<f4*>(a.y + p * a.Co + co) = v;
+      } else {
+        const int64_t n = p / OHW;
+        float* yb = a.y + n * (int64_t)a.Co * OHW + (p - n * OHW) + (int64_t)co * OHW;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) yb[(int64_t)r * OHW] = v[r];
+      }
+    }
+  }
+}
+
+template <int TCO, int TPX, int WCO, int WPX, int PF = 2>
+int launch_fwd(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
+  constexpr int PXT = 16 * TPX * WPX, COT = 16 * TCO * WCO;
+  if (a.Co % COT) return RAI_E_SHAPE;
+  const int64_t gx = (a.M + PXT - 1) / PXT;
+  if (gx > 0x7fffffffLL) return RAI_E_SHAPE;
+  const dim3 grid((unsigned)gx, (unsigned)(a.Co / COT));
+  if (nchw)
+    hipLaunchKernelGGL((conv_fwd_kernel<TCO, TPX, WCO, WPX, true, PF>), grid, dim3(CV_THREADS), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<TCO, TPX, WCO, WPX, false, PF>), grid, dim3(CV_THREADS), 0, st, a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient: dW[co][k] = sum_p dz[p][co] * im2col(x)[p][k] (the reduction runs over the
+// B * OH * OW output pixels).  MFMA rows = co, columns = k, reduction index = pixel.  The 4-wide
+// trick runs along the OUTPUT dimensions here: lane (i, g) loads VC consecutive co of dz at pixel
+// p_g (VC = 4: 16 B) and 4 consecutive k of x's im2col row (16 B).  MFMA (j, j') takes component j of
+// the first and j' of the second, so it accumulates the 16 x 16 block of co = VC*i + j, k = k0 + 4i + j':
+// one pixel step (4 pixels) is 4 * VC MFMAs fed by two loads per lane.  A wave owns all Co = 16 * VC
+// output channels x one 64-wide k tile (grid.y); the workgroup's four waves split its pixels (each
+// 256-pixel chunk: 64 per wave) and add their tiles through LDS in wave order; grid.x splits the
+// pixels over workgroups.  Every workgroup writes one partial tile; conv_wrw_reduce sums the S splits
+// in a fixed order (deterministic, no atomics) and writes or adds dW (accumulate: straight into the
+// flat .grad).
+constexpr int WR_MAXPX = 8192;  // pixels per split (their base offsets sit in LDS)
+
+struct ConvWrwArgs {
+  const float* x;
+  const float* dz;
+  float* part;  // [S][Co][K]
+  int64_t M;    // pixels
+  int64_t per;  // pixels per split
+  int H, W, Ci, Co, KW, S_, OH, OW, K;
+};
+
+template <int VC, int PF>
+__global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs a) {
+  constexpr int NB = VC * 4;  // 16x16 accumulator blocks per wave
+  // LDS: the split's pixel -> input offset table, later reused for the cross-wave sum of the tiles
+  constexpr int TAB_BYTES = WR_MAXPX * 4, RED_BYTES = 3 * NB * 64 * 16;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[TAB_BYTES > RED_BYTES ? TAB_BYTES : RED_BYTES];
+  int* const xbase_l = reinterpret_cast<int*>(lds);
+  f4* const red = reinterpret_cast<f4*>(lds);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int k0 = blockIdx.y * 64 + 4 * li;  // this lane's 4 k (one chunk: Ci % 4 == 0)
+  int xo;
+  {
+    const int kpos = k0 / a.Ci, ci0 = k0 - kpos * a.Ci, kh = kpos / a.KW, kw = kpos - kh * a.KW;
+    xo = (kh * a.W + kw) * a.Ci + ci0;
+  }
+  const int64_t pbeg = (int64_t)blockIdx.x * a.per;
+  const int n_p = (int)max((int64_t)0, min(a.per, a.M - pbeg));
+  const int OHW = a.OH * a.OW;
+  const int64_t n0 = pbeg / OHW;  // offsets are relative to the split's first sample
+  for (int t = threadIdx.x; t < n_p; t += CV_THREADS) {
+    const int64_t p = pbeg + t;
+    const int64_t n = p / OHW;
+    const int r = (int)(p - n * OHW), oh = r / a.OW, ow = r - oh * a.OW;
+    xbase_l[t] = (int)((((n - n0) * a.H + (int64_t)oh * a.S_) * a.W + (int64_t)ow * a.S_) * a.Ci);
+  }
+  __syncthreads();
+  typedef float fv __attribute__((ext_vector_type(VC)));
+  f4 acc[VC][4];
+#pragma unroll
+  for (int j = 0; j < VC; ++j)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[j][jj] = f4{0.f, 0.f, 0.f, 0.f};
+  {
+    // wave w: the split's pixels [lo, hi), in steps of 4 (lane group g: pixel lo + 4 st + g)
+    const int q4 = (((n_p + 3) >> 2) + 3) >> 2;  // steps per wave
+    const int lo = min(4 * q4 * wv, n_p), hi = min(lo + 4 * q4, n_p);
+    const float* xc = a.x + n0 * (int64_t)a.H * a.W * a.Ci + xo;
+    const float* dzc = a.dz + pbeg * a.Co + VC * li;
+    const int nst = (hi - lo + 3) >> 2;
+    auto ld = [&](int st, fv& dv, f4& xv) {
+      const int pl = lo + 4 * st + g;
+      if (pl < hi) {
+        dv = *reinterpret_cast<const fv*>(dzc + (int64_t)pl * a.Co);
+        xv = *reinterpret_cast<const f4*>(xc + xbase_l[pl]);
+      } else {
+        dv = fv{};
+        xv = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    auto mma = [&](const fv& dv, const f4& xv) {
+#pragma unroll
+      for (int j = 0; j < VC; ++j)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          acc[j][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[j], xv[jj], acc[j][jj], 0, 0, 0);
+    };
+    fv dv[PF];
+    f4 xv[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) ld(u, dv[u], xv[u]);
+    for (int st = 0; st < nst; st += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if (st + u < nst) mma(dv[u], xv[u]);
+        if (st + u + PF < nst) ld(st + u + PF, dv[u], xv[u]);
+      }
+    }
+  }
+  __syncthreads();  // the table's last readers are done: its LDS becomes the reduction buffer
+  // the four waves' tiles, added in wave order
+  if (wv > 0) {
+#pragma unroll
+    for (int j = 0; j < VC; ++j)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) red[((wv - 1) * NB + j * 4 + jj) * 64 + lane] = acc[j][jj];
+  }
+  __syncthreads();
+  if (wv > 0) return;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < VC; ++j)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[j][jj] += red[(q * NB + j * 4 + jj) * 64 + lane];
+  // partial tile: lane (i, g) holds co = VC*(4g + r) + j, k = k0 .. k0 + 3 (one float4 per (j, r))
+  float* pp = a.part + (int64_t)blockIdx.x * a.Co * a.K;
+#pragma unroll
+  for (int j = 0; j < VC; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = VC * (4 * g + r) + j;
+      *reinterpret_cast<f4*>(pp + (int64_t)co * a.K + k0) = f4{acc[j][0][r], acc[j][1][r], acc[j][2][r], acc[j][3][r]};
+    }
+}
+
+// dW (+)= sum over s of part[s] (fixed order: 16 lane groups each add S / 16 consecutive splits, then
+// the 16 group sums are added in group order through LDS)
+__global__ __launch_bounds__(CV_THREADS) void conv_wrw_reduce_kernel(const f4* __restrict__ part, int S, int64_t n4,
+                                                                    f4* __restrict__ dw, int accumulate) {
+  __shared__ f4 red[16][16];
+  const int o = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + o;
+  const int per = S >> 4;
+  f4 s = f4{0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    f4 v[8];
+    for (int b = 0; b < per; b += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = b + u < per ? part[(int64_t)(sg * per + b + u) * n4 + i] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+  }
+  red[sg][o] = s;
+  __syncthreads();
+  if (sg == 0 && i < n4) {
+    f4 t = red[0][o];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += red[q][o];
+    dw[i] = accumulate ? dw[i] + t : t;
+  }
+}
+
+struct WrwPlan {
+  int VC, S, KT;
+  int64_t per;
+};
+
+// target_wgs workgroups in all (default 512: two per CU), S a multiple of 16, each split at most
+// WR_MAXPX pixels and at least 64
+static WrwPlan wrw_plan(int64_t M, int Co, int K, int target_wgs) {
+  WrwPlan p;
+  p.VC = Co / 16;
+  p.KT = K / 64;  // k tiles (grid.y)
+  if (target_wgs <= 0) target_wgs = 512;  // measured best of 256 / 512 / 768 / 1024 at B = 256 (r3r)
+  int64_t S = target_wgs / p.KT;
+  S = S < 16 ? 16 : (S / 16) * 16;
+  while (S > 16 && (M + S - 1) / S < 64) S -= 16;
+  while ((M + S - 1) / S > WR_MAXPX) S += 16;
+  p.S = (int)S;
+  p.per = (M + S - 1) / S;
+  return p;
+}
+
+}  // namespace
+
+extern "C" int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
+                                                    int32_t KH, int32_t KW, int32_t stride) {
+  if (B < 1 || H < KH || W < KW || stride < 1 || Co < 16 || KH < 1 || KW < 1 || Ci < 4) return 0;
+  const int64_t M = B * ((H - KH) / stride + 1) * ((W - KW) / stride + 1);
+  const int K = KH * KW * Ci;
+  // the largest split count any target_wgs <= 1024 gives (the _v variants share the workspace size)
+  int64_t mx = 0;
+  for (int t = 256; t <= 1024; t += 256) {
+    const WrwPlan p = wrw_plan(M, Co, K, t);
+    mx = p.S > mx ? p.S : mx;
+  }
+  return mx * Co * K * (int64_t)sizeof(float);
+}
+
+extern "C" int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci,
+                                  int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dw, int32_t accumulate,
+                                  void* workspace, int64_t workspace_bytes, int32_t target_wgs, int32_t pf,
+                                  void* stream) {
+  if (B < 0 || H < 1 || W < 1 || Ci < 4 || Ci % 4 || (Co != 32 && Co != 64) || KH < 1 || KW < 1 || stride < 1 ||
+      KH > H || KW > W)
+    return RAI_E_SHAPE;
+  const int64_t K = (int64_t)KH * KW * Ci;
+  if (K % 64 || K > (1 << 20)) return RAI_E_SHAPE;
+  hipStream_t st = rai_stream(stream);
+  if (B == 0) {
+    if (!accumulate) {
+      if (!dw) return RAI_E_NULLPTR;
+      const hipError_t e = hipMemsetAsync(dw, 0, (size_t)Co * K * 4, st);
+      if (e != hipSuccess) return (int)e;
+    }
+    return RAI_OK;
+  }
+  if (!x || !dz || !dw || !workspace) return RAI_E_NULLPTR;
+  if (((uintptr_t)x | (uintptr_t)dz | (uintptr_t)dw | (uintptr_t)workspace) & 15) return RAI_E_SHAPE;
+  if ((int64_t)H * W * Ci > (1LL << 30)) return RAI_E_SHAPE;  // per-chunk offsets are int32
+  if (workspace_bytes < rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, stride)) return RAI_E_WORKSPACE;
+  ConvWrwArgs a;
+  a.x = x;
+  a.dz = dz;
+  a.part = static_cast<float*>(workspace);
+  a.H = H;
+  a.W = W;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.KW = KW;
+  a.S_ = stride;
+  a.OH = (H - KH) / stride + 1;
+  a.OW = (W - KW) / stride + 1;
+  a.K = (int)K;
+  a.M = B * a.OH * a.OW;
+  if (target_wgs < 0 || target_wgs > 1024) return RAI_E_SHAPE;
+  const WrwPlan p = wrw_plan(a.M, Co, a.K, target_wgs);
+  a.per = p.per;
+  // a split's offsets from its first sample fit int32
+  if ((int64_t)(WR_MAXPX / (a.OH * a.OW) + 2) * H * W * Ci > 0x7fffffffLL) return RAI_E_SHAPE;
+  const dim3 grid((unsigned)p.S, (unsigned)p.KT);
+  if (pf <= 0) pf = 4;
+  if (p.VC == 2) {
+    if (pf == 4) hipLaunchKernelGGL((conv_wrw_kernel<2, 4>), grid, dim3(CV_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((conv_wrw_kernel<2, 8>), grid, dim3(CV_THREADS), 0, st, a);
+  } else {
+    if (pf == 4) hipLaunchKernelGGL((conv_wrw_kernel<4, 4>), grid, dim3(CV_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((conv_wrw_kernel<4, 8>), grid, dim3(CV_THREADS), 0, st, a);
+  }
+  RAI_LAUNCH_CHECK();
+  const int64_t n4 = (int64_t)Co * K / 4;
+  hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(CV_THREADS), 0, st,
+                     reinterpret_cast<const f4*>(workspace), p.S, n4, reinterpret_cast<f4*>(dw), accumulate);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+// variant: 0 = by shape (the shipped choice); 1.. = a fixed blocking (tools/conv_bench.py A/B)
+extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const float* b, int64_t B, int32_t H,
+                                         int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride,
+                                         int32_t out_nchw, float* y, int32_t variant, void* stream) {
+  if (B < 0 || H < 1 || W < 1 || Ci < 4 || Ci % 4 || Co < 16 || Co % 16 || KH < 1 || KW < 1 || stride < 1 ||
+      KH > H || KW > W)
+    return RAI_E_SHAPE;
+  const int64_t K = (int64_t)KH * KW * Ci;
+  if (K % 32 || K / 4 > CV_MAXCHUNK) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!x || !w || !b || !y) return RAI_E_NULLPTR;
+  if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y) & 15) return RAI_E_SHAPE;
+  ConvFwdArgs a;
+  a.x = x;
+  a.w = w;
+  a.b = b;
+  a.y = y;
+  a.H = H;
+  a.W = W;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.KW = KW;
+  a.S = stride;
+  a.OH = (H - KH) / stride + 1;
+  a.OW = (W - KW) / stride + 1;
+  a.K = (int)K;
+  a.M = B * a.OH * a.OW;
+  if ((int64_t)H * W * Ci * B > (1LL << 40)) return RAI_E_SHAPE;
+  hipStream_t st = rai_stream(stream);
+  const bool nchw = out_nchw != 0;
+  if (variant == 0) variant = (Co % 64 == 0) ? 10 : (Co % 32 == 0) ? 11 : 7;
+  switch (variant) {
+    case 1: return launch_fwd<2, 2, 1, 4>(a, nchw, st);  // 32 co x 128 px
+    case 2: return launch_fwd<1, 2, 2, 2>(a, nchw, st);  // 32 co x 64 px
+    case 3: return launch_fwd<2, 1, 2, 2>(a, nchw, st);  // 64 co x 32 px
+    case 4: return launch_fwd<4, 1, 1, 4>(a, nchw, st);  // 64 co x 64 px
+    case 5: return launch_fwd<2, 2, 2, 2>(a, nchw, st);  // 64 co x 64 px
+    case 6: return launch_fwd<1, 1, 2, 2>(a, nchw, st);  // 32 co x 32 px
+    case 7: return launch_fwd<1, 1, 1, 4>(a, nchw, st);  // 16 co x 64 px
+    case 8: return launch_fwd<2, 2, 1, 4, 4>(a, nchw, st);  // variant 1, four quads in flight
+    case 9: return launch_fwd<2, 2, 2, 2, 4>(a, nchw, st);  // variant 5, four quads in flight
+    case 10: return launch_fwd<2, 2, 2, 2, 3>(a, nchw, st);  // variant 5, three quads in flight
+    case 11: return launch_fwd<2, 2, 1, 4, 3>(a, nchw, st);  // variant 1, three quads in flight
+    default: return RAI_E_SHAPE;
+  }
+}
+
+extern "C" int rai_conv2d_bias_relu_fwd(const float* x, const float* w, const float* b, int64_t B, int32_t H,
+                                       int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride,
+                                       int32_t out_nchw, float* y, void* stream) {
+  return rai_conv2d_bias_relu_fwd_v(x, w, b, B, H, W, Ci, Co, KH, KW, stride, out_nchw, y, 0, stream);
+}
+
+extern "C" int rai_conv2d_wgrad(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci,
+                                int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dw, int32_t accumulate,
+                                void* workspace, int64_t workspace_bytes, void* stream) {
+  return rai_conv2d_wgrad_v(x, dz, B, H, W, Ci, Co, KH, KW, stride, dw, accumulate, workspace, workspace_bytes, 0, 0,
+                            stream);
+}

@@ -110,3 +110,15 @@ def test_bias_relu_workspaces_are_freed_with_their_layer():
     del a
     gc.collect()
     assert len(ws._ws) == 1
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes binding (_lib._SIGNATURES) passes exactly as many arguments as the C declaration
+    in include/rai_amd.h takes (a short list silently shifts every later argument)."""
+    hdr = (ROOT / "include" / "rai_amd.h").read_text()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    decls = {m.group(1): m.group(2) for m in re.finditer(r"\b(rai_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", hdr, flags=re.S)}
+    for name, (_, args) in _lib._SIGNATURES.items():
+        params = decls[name].strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert len(args) == n, (name, len(args), n)

@@ -1,0 +1,180 @@
+"""NatureCNN convolutions as hand-written f32 MFMA implicit GEMMs (csrc/conv.hip) against a float64
+PyTorch convolution of the same inputs (reference layer: rl_algo_impls/shared/encoder/nature_cnn.py:31-41,
+Conv2d -> ReLU).  f32 products with the kernel's own summation order: the tolerance below is a few
+f32 ulps of the sum of |products| (K up to 576 terms)."""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from rl_algo_impls_amd import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+# (Ci, H, Co, k, stride, flatten): the three NatureCNN layers, plus ragged / odd shapes
+CASES = [
+    (4, 84, 32, 8, 4, False),
+    (32, 20, 64, 4, 2, False),
+    (64, 9, 64, 3, 1, True),
+    (64, 9, 64, 3, 1, False),
+    (8, 13, 16, 2, 1, False),
+    (32, 11, 48, 3, 2, True),
+]
+
+
+def _inputs(B, Ci, H, Co, k, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(B, Ci, H, H, generator=g)
+    w = torch.randn(Co, Ci, k, k, generator=g) * (2.0 / (Ci * k * k)) ** 0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    return x, w, b
+
+
+def _run(x, w, b, stride, flatten, variant=0):
+    B, Ci, H, W = x.shape
+    Co, _, KH, KW = w.shape
+    OH, OW = (H - KH) // stride + 1, (W - KW) // stride + 1
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
+    bd = b.to(DEV)
+    y = torch.full((B, Co * OH * OW), float("nan"), device=DEV)
+    rc = _lib.lib().rai_conv2d_bias_relu_fwd_v(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), B, H, W, Ci, Co, KH, KW,
+                                               stride, 1 if flatten else 0, y.data_ptr(), variant,
+                                               _lib.stream_handle(DEV))
+    _lib.check(rc, "rai_conv2d_bias_relu_fwd")
+    torch.cuda.synchronize()
+    return y.cpu()
+
+
+def _reference(x, w, b, stride, flatten):
+    xd, wd = x.double(), w.double()
+    y = torch.relu(F.conv2d(xd, wd, b.double(), stride))
+    bound = F.conv2d(xd.abs(), wd.abs(), b.double().abs(), stride)  # sum of |terms| per output
+    if flatten:
+        return torch.flatten(y, 1), torch.flatten(bound, 1)
+    return y.permute(0, 2, 3, 1).reshape(x.shape[0], -1), bound.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(str(v) for v in c[:5]) + ("-flat" if c[5] else ""))
+@pytest.mark.parametrize("B", [1, 7, 64])
+def test_conv_bias_relu_fwd_matches_fp64(case, B):
+    Ci, H, Co, k, s, flat = case
+    x, w, b = _inputs(B, Ci, H, Co, k, seed=B)
+    y = _run(x, w, b, s, flat)
+    ref, bound = _reference(x, w, b, s, flat)
+    assert torch.isfinite(y).all()
+    err = (y.double() - ref).abs()
+    # the worst-case bound of ANY f32 summation order of K = Ci*k*k products plus the bias:
+    # gamma_(K+2) * sum|terms| (an indexing error is O(1) relative, far outside it)
+    tol = (Ci * k * k + 2) * 2.0 ** -24 * bound + 1e-30
+    assert (err <= tol).all(), float((err / tol).max())
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
+def test_conv_every_blocking_variant(variant):
+    Ci, H, Co, k, s, flat = 32, 20, 64, 4, 2, False
+    x, w, b = _inputs(9, Ci, H, Co, k, seed=3)
+    ref, bound = _reference(x, w, b, s, flat)
+    y = _run(x, w, b, s, flat, variant)
+    assert ((y.double() - ref).abs() <= (32 * 16 + 2) * 2.0 ** -24 * bound + 1e-30).all()
+
+
+def test_conv_relu_keeps_nan_and_zeroes_negatives():
+    x, w, b = _inputs(2, 4, 84, 32, 8)
+    x[0, 0, 0, 0] = float("nan")  # poisons the first output pixel of sample 0 only
+    b[:] = -1e6  # every finite output negative -> 0
+    y = _run(x, w, b, 4, False)
+    assert torch.isnan(y[0, :32]).all()
+    assert (y[0, 32:] == 0).all() and (y[1] == 0).all()
+
+
+def test_conv_rejects_unsupported_shapes():
+    L = _lib.lib()
+    st = _lib.stream_handle(DEV)
+    # Ci % 4, Co % 16, K % 32
+    assert L.rai_conv2d_bias_relu_fwd(None, None, None, 1, 8, 8, 3, 16, 2, 2, 1, 0, None, st) == -2
+    assert L.rai_conv2d_bias_relu_fwd(None, None, None, 1, 8, 8, 4, 24, 2, 2, 1, 0, None, st) == -2
+    assert L.rai_conv2d_bias_relu_fwd(None, None, None, 1, 8, 8, 4, 16, 3, 3, 1, 0, None, st) == -2
+    assert L.rai_conv2d_bias_relu_fwd(None, None, None, 0, 8, 8, 8, 16, 2, 2, 1, 0, None, st) == 0
+    assert L.rai_conv2d_bias_relu_fwd(None, None, None, 1, 8, 8, 8, 16, 2, 2, 1, 0, None, st) == -1
+
+
+def _wgrad(x, dz, KH, KW, stride, dw0=None):
+    """rai_conv2d_wgrad: x (B, Ci, H, W), dz (B, Co, OH, OW) NCHW tensors on the CPU; returns dw in
+    (Co, Ci, KH, KW) NCHW order.  dw0: accumulate onto it."""
+    B, Ci, H, W = x.shape
+    Co = dz.shape[1]
+    L = _lib.lib()
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    dzd = dz.to(DEV).contiguous(memory_format=torch.channels_last)
+    dw = (dw0 if dw0 is not None else torch.full((Co, Ci, KH, KW), float("nan"))).to(DEV)
+    dw = dw.contiguous(memory_format=torch.channels_last)
+    nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, stride))
+    ws = torch.full((max(nb, 16) // 4,), float("nan"), device=DEV)  # needs no zeroing
+    rc = L.rai_conv2d_wgrad(xd.data_ptr(), dzd.data_ptr(), B, H, W, Ci, Co, KH, KW, stride, dw.data_ptr(),
+                            0 if dw0 is None else 1, ws.data_ptr(), nb, _lib.stream_handle(DEV))
+    _lib.check(rc, "rai_conv2d_wgrad")
+    torch.cuda.synchronize()
+    return dw.cpu()
+
+
+WGRAD_CASES = [  # (Ci, H, Co, k, stride): the three NatureCNN layers + a ragged small one
+    (4, 84, 32, 8, 4),
+    (32, 20, 64, 4, 2),
+    (64, 9, 64, 3, 1),
+    (16, 7, 32, 2, 1),
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_CASES, ids=lambda c: "x".join(str(v) for v in c))
+@pytest.mark.parametrize("B", [1, 5, 256])
+def test_conv_wgrad_matches_fp64(case, B):
+    Ci, H, Co, k, s = case
+    if B == 256 and Ci == 4:
+        B = 64  # conv1 at 64 samples keeps the fp64 CPU reference fast; 256 runs below at 16
+    x, w, _ = _inputs(B, Ci, H, Co, k, seed=B + 11)
+    OH = (H - k) // s + 1
+    g = torch.Generator().manual_seed(B)
+    dz = torch.randn(B, Co, OH, OH, generator=g) * (torch.rand(B, Co, OH, OH, generator=g) > 0.4)
+    dw = _wgrad(x, dz, k, k, s)
+    xd, dzd = x.double(), dz.double()
+    ref = torch.ops.aten.convolution_backward(dzd, xd, w.double(), None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                              [False, True, False])[1]
+    bound = torch.ops.aten.convolution_backward(dzd.abs(), xd.abs(), w.double(), None, [s, s], [0, 0], [1, 1], False,
+                                                [0, 0], 1, [False, True, False])[1]
+    M = B * OH * OH
+    tol = (M + 2) * 2.0 ** -24 * bound + 1e-30
+    assert torch.isfinite(dw).all()
+    assert ((dw.double() - ref).abs() <= tol).all(), float(((dw.double() - ref).abs() / tol).max())
+
+
+def test_conv_wgrad_accumulates_and_is_deterministic():
+    Ci, H, Co, k, s = 32, 20, 64, 4, 2
+    x, w, _ = _inputs(48, Ci, H, Co, k, seed=5)
+    dz = torch.randn(48, Co, 9, 9, generator=torch.Generator().manual_seed(2))
+    base = torch.randn(Co, Ci, k, k, generator=torch.Generator().manual_seed(3))
+    a = _wgrad(x, dz, k, k, s)
+    b = _wgrad(x, dz, k, k, s)
+    assert torch.equal(a, b)
+    acc = _wgrad(x, dz, k, k, s, dw0=base)
+    assert torch.equal(acc, base + a)  # one f32 add per element, after the fixed-order sum
+
+
+def test_conv_wgrad_full_c3_minibatch_against_miopen():
+    """conv1 at the C3 minibatch (B = 256, 102,400 pixels): against MIOpen's f32 weight gradient on the
+    same device (both f32 sums of 102,400 terms; the bound is the f32 worst case of their difference)."""
+    Ci, H, Co, k, s = 4, 84, 32, 8, 4
+    x, w, _ = _inputs(256, Ci, H, Co, k, seed=9)
+    dz = torch.randn(256, Co, 20, 20, generator=torch.Generator().manual_seed(4)) * 0.01
+    dw = _wgrad(x, dz, k, k, s)
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    dzd = dz.to(DEV).contiguous(memory_format=torch.channels_last)
+    ref = torch.ops.aten.convolution_backward(dzd, xd, w.to(DEV).contiguous(memory_format=torch.channels_last), None,
+                                              [s, s], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    bound = torch.ops.aten.convolution_backward(dzd.abs(), xd, w.to(DEV), None, [s, s], [0, 0], [1, 1], False,
+                                                [0, 0], 1, [False, True, False])[1]
+    err = (dw.to(DEV) - ref).abs()
+    assert (err <= 2 * (256 * 400 + 2) * 2.0 ** -24 * bound + 1e-30).all()
+    assert (err <= 1e-4 * bound.max()).all()  # and far tighter in practice

@@ -1,0 +1,131 @@
+"""Same-box timing of the NatureCNN (C3) convolution forward: hand-written f32 MFMA implicit GEMM with
+the bias + ReLU in its store (rai_conv2d_bias_relu_fwd, csrc/conv.hip, every blocking variant) against
+the product's previous path (MIOpen F.conv2d in find mode + rai_bias_relu_fwd), per layer at the update
+minibatch B = 256 and the rollout batch B = 1024.  Also checks each variant against an fp64 CPU
+convolution of the same inputs.
+
+    python tools/conv_bench.py [--reps 50]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import _pkgload  # noqa: E402
+
+_pkgload.load()
+
+from rl_algo_impls_amd import _lib  # noqa: E402
+from rl_algo_impls_amd import cnn_ops  # noqa: E402
+
+LAYERS = [  # name, Ci, H, Co, k, stride, flatten
+    ("conv1", 4, 84, 32, 8, 4, False),
+    ("conv2", 32, 20, 64, 4, 2, False),
+    ("conv3", 64, 9, 64, 3, 1, True),
+]
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--batches", default="256,1024")
+    ap.add_argument("--variants", default="0,1,5,8,9,10,11")
+    args = ap.parse_args()
+    torch.backends.cudnn.benchmark = True
+    dev = torch.device("cuda:0")
+    L = _lib.lib()
+    st = _lib.stream_handle(dev)
+    out = []
+    for B in [int(v) for v in args.batches.split(",")]:
+        for name, Ci, H, Co, k, s, flat in LAYERS:
+            g = torch.Generator().manual_seed(1)
+            x = torch.rand(B, Ci, H, H, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+            w = (torch.randn(Co, Ci, k, k, generator=g) * (2.0 / (Ci * k * k)) ** 0.5).to(dev)
+            w = w.contiguous(memory_format=torch.channels_last)
+            b = (torch.randn(Co, generator=g) * 0.1).to(dev)
+            OH = (H - k) // s + 1
+
+            def ref_path():
+                z = F.conv2d(x, w, None, s).contiguous(memory_format=torch.channels_last)
+                return cnn_ops._bias_relu_fwd_nchw(z, b) if flat else cnn_ops._bias_relu_fwd(z, b)
+
+            t_ref = timeit(ref_path, args.reps)
+            # fp64 CPU check on the first 8 samples
+            xd, wd, bd = x[:8].double().cpu(), w.double().cpu(), b.double().cpu()
+            yd = torch.relu(F.conv2d(xd, wd, bd, s))
+            yd = torch.flatten(yd, 1) if flat else yd.permute(0, 2, 3, 1).reshape(8, -1)
+            row = {"B": B, "layer": name, "ref_us": round(t_ref, 2), "flops": 2 * B * OH * OH * Co * Ci * k * k}
+            y = torch.empty((B, Co * OH * OH), dtype=torch.float32, device=dev)
+            for v in [int(t) for t in args.variants.split(",")]:
+                def mine():
+                    return L.rai_conv2d_bias_relu_fwd_v(x.data_ptr(), w.data_ptr(), b.data_ptr(), B, H, H, Ci, Co,
+                                                        k, k, s, 1 if flat else 0, y.data_ptr(), v, st)
+                rc = mine()
+                if rc != 0:
+                    row[f"v{v}"] = f"rc={rc}"
+                    continue
+                torch.cuda.synchronize()
+                err = (y[:8].double().cpu() - yd).abs().max().item() / max(yd.abs().max().item(), 1e-30)
+                t = timeit(mine, args.reps)
+                row[f"v{v}"] = {"us": round(t, 2), "tflops": round(row["flops"] / t / 1e6, 1), "relerr": err}
+            # weight gradient: MIOpen (find mode) + the accumulate into .grad vs rai_conv2d_wgrad
+            dz = (torch.randn(B, Co, OH, OH, generator=g) * 0.01).to(dev).contiguous(memory_format=torch.channels_last)
+            grad = torch.zeros_like(w)
+
+            def ref_wgrad():
+                dw = torch.ops.aten.convolution_backward(dz, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                                         [False, True, False])[1]
+                grad.add_(dw)
+
+            row["wgrad_ref_us"] = round(timeit(ref_wgrad, args.reps), 2)
+            nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, H, Ci, Co, k, k, s))
+            ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+            grad2 = torch.zeros_like(w)
+
+            def mine_wgrad(tw=0, pf=0):
+                return L.rai_conv2d_wgrad_v(x.data_ptr(), dz.data_ptr(), B, H, H, Ci, Co, k, k, s, grad2.data_ptr(), 1,
+                                            ws.data_ptr(), nb, tw, pf, st)
+
+            rc = mine_wgrad()
+            if rc == 0:
+                torch.cuda.synchronize()
+                grad.zero_()
+                grad2.zero_()
+                ref_wgrad()
+                mine_wgrad()
+                torch.cuda.synchronize()
+                row["wgrad_relerr"] = ((grad2 - grad).abs().max() / grad.abs().max()).item()
+                row["wgrad_us"] = round(timeit(mine_wgrad, args.reps), 2)
+                row["wgrad_tflops"] = round(row["flops"] / row["wgrad_us"] / 1e6, 1)
+                for tw, pf in ((256, 4), (256, 8), (512, 4), (768, 8), (1024, 8)):
+                    row[f"wgrad_{tw}_{pf}_us"] = round(timeit(lambda: mine_wgrad(tw, pf), args.reps), 2)
+                row["wgrad_ws_mb"] = round(nb / 2**20, 2)
+            else:
+                row["wgrad_us"] = f"rc={rc}"
+            print(json.dumps(row), flush=True)
+            out.append(row)
+    return out
+
+
+if __name__ == "__main__":
+    main()
