@@ -196,6 +196,21 @@ int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_
 int rai_conv2d_wgrad(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
                      int32_t KH, int32_t KW, int32_t stride, float* dw, int32_t accumulate, void* workspace,
                      int64_t workspace_bytes, void* stream);
+/* rai_conv2d_wgrad in two parts, so the backward's convolutions share ONE reduction launch: the
+ * partials launch per layer (workspace as above, kept until the reduce has run), then
+ * rai_conv2d_wgrad_reduce over up to RAI_WGRAD_MAX_JOBS layers (host array of jobs; each job's
+ * shape arguments as passed to its partials call). */
+#define RAI_WGRAD_MAX_JOBS 4
+typedef struct rai_conv2d_wgrad_job {
+  const void* workspace;
+  float* dw;
+  int64_t B;
+  int32_t H, W, Ci, Co, KH, KW, stride, reserved;
+} rai_conv2d_wgrad_job;
+int rai_conv2d_wgrad_partials(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci,
+                              int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
+                              int64_t workspace_bytes, void* stream);
+int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_t accumulate, void* stream);
 /* The same with a fixed launch shape for same-box A/B (tools/conv_bench.py): target_wgs workgroups
  * (0 = 512, at most 1024), pf pixel steps in flight per wave (0 = 4; 4 or 8). */
 int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,

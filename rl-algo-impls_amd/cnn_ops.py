@@ -28,6 +28,7 @@ etc. see ordinary gradients).
 from __future__ import annotations
 
 import contextlib
+import ctypes as C
 import os
 import threading
 import weakref
@@ -67,12 +68,38 @@ def direct_grads(enabled: bool = True):
         pending.close(flush=ok)
 
 
+class _WgradJob(C.Structure):
+    """rai_conv2d_wgrad_job (include/rai_amd.h)."""
+    _fields_ = [("workspace", C.c_void_p), ("dw", C.c_void_p), ("B", C.c_int64), ("H", C.c_int32), ("W", C.c_int32),
+                ("Ci", C.c_int32), ("Co", C.c_int32), ("KH", C.c_int32), ("KW", C.c_int32), ("stride", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+_MAX_JOBS = 4  # RAI_WGRAD_MAX_JOBS
+
+
+def _reduce_wgrad_jobs(jobs: list, device) -> None:
+    """One rai_conv2d_wgrad_reduce launch per RAI_WGRAD_MAX_JOBS layers: each layer's partial tiles
+    summed in a fixed order and added into its flat .grad view."""
+    L = _lib.lib()
+    for i in range(0, len(jobs), _MAX_JOBS):
+        chunk = jobs[i:i + _MAX_JOBS]
+        arr = (_WgradJob * len(chunk))(*[j for j, _ws, _w in chunk])
+        _lib.check(L.rai_conv2d_wgrad_reduce(C.cast(arr, C.c_void_p), len(chunk), 1, _lib.stream_handle(device)),
+                   "rai_conv2d_wgrad_reduce")
+    for _j, _ws, w in jobs:
+        notify_grad_written(w)
+
+
 class _PendingGrads:
-    """(weight, gradient) pairs awaiting their accumulate; a backward that runs after the context
-    has closed (forward inside it, backward outside) accumulates its own at once."""
+    """Gradient accumulates deferred to the context's exit: (weight, gradient) pairs (one multi-tensor
+    add) and MFMA weight-gradient partials (one reduction launch for the backward's convolutions).  A
+    backward that runs after the context has closed (forward inside it, backward outside) accumulates
+    its own at once."""
 
     def __init__(self):
         self.items: list = []
+        self.jobs: list = []  # (rai_conv2d_wgrad_job, workspace tensor kept alive, weight)
         self.closed = False
 
     def add(self, w: torch.Tensor, dw: torch.Tensor) -> None:
@@ -82,8 +109,24 @@ class _PendingGrads:
         else:
             self.items.append((w, dw))
 
+    def add_wgrad(self, job: "_WgradJob", ws: torch.Tensor, w: torch.Tensor) -> None:
+        if self.closed:
+            _reduce_wgrad_jobs([(job, ws, w)], ws.device)
+            return
+        if any(ws is other for _j, other, _w in self.jobs):  # the layer's workspace is about to be reused
+            self.flush_jobs()
+        self.jobs.append((job, ws, w))
+
+    def flush_jobs(self) -> None:
+        jobs, self.jobs = self.jobs, []
+        if jobs:
+            _reduce_wgrad_jobs(jobs, jobs[0][1].device)
+
     def close(self, flush: bool) -> None:
         self.closed = True
+        if flush:
+            self.flush_jobs()
+        self.jobs = []
         items, self.items = self.items, []
         if flush and items:
             torch._foreach_add_([w.grad for w, _ in items], [dw for _, dw in items])
@@ -132,6 +175,7 @@ class _Workspaces:
 _WS = _Workspaces()
 
 _CONV_MFMA = os.environ.get("RAI_CONV_MFMA", "1") != "0"
+_MFMA_FWD_MAX_PIXELS_64 = 40000
 
 
 class _WgradWorkspaces:
@@ -164,6 +208,14 @@ def _mfma_conv_ok(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride, pad
     if not _CONV_MFMA or tuple(_pair(padding)) != (0, 0):
         return False
     Co, Ci, KH, KW = (int(v) for v in w.shape)
+    if Co == 64 and x.dim() == 4:
+        # measured (profiles/r3r_conv_bench.txt): the 64-channel layers are faster here at the update's
+        # minibatch (B = 256: conv2 20,736 / conv3 12,544 output pixels) and slower than MIOpen's
+        # implicit GEMMs at the rollout's B = 1,024 (82,944 / 50,176 pixels)
+        s = _pair(stride)[0]
+        M = int(x.shape[0]) * ((int(x.shape[2]) - KH) // s + 1) * ((int(x.shape[3]) - KW) // s + 1)
+        if M > _MFMA_FWD_MAX_PIXELS_64:
+            return False
     return (x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
             and w.is_contiguous(memory_format=torch.channels_last) and Ci % 4 == 0 and Co in (32, 64)
             and (KH * KW * Ci) % 64 == 0 and KH * KW * Ci <= 8192 and b.is_contiguous()
@@ -183,6 +235,19 @@ def _conv_fwd_mfma(x, w, b, stride, flatten) -> torch.Tensor:
                                                    KW, s, 1 if flatten else 0, y.data_ptr(),
                                                    _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd")
     return y
+
+
+def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor):
+    """rai_conv2d_wgrad_partials for this layer; returns (job, workspace) for the deferred reduction."""
+    B, Ci, H, W = (int(v) for v in x.shape)
+    Co, _, KH, KW = (int(v) for v in w.shape)
+    s = _pair(stride)[0]
+    L = _lib.lib()
+    nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, s))
+    ws = _WG_WS.get(module, nb, x.device)
+    _lib.check(L.rai_conv2d_wgrad_partials(x.data_ptr(), dz.data_ptr(), B, H, W, Ci, Co, KH, KW, s, ws.data_ptr(), nb,
+                                           _lib.stream_handle(x.device)), "rai_conv2d_wgrad_partials")
+    return _WgradJob(ws.data_ptr(), grad.data_ptr(), B, H, W, Ci, Co, KH, KW, s, 0), ws
 
 
 def _conv_wgrad_mfma(module, x, dz, w, stride, out: torch.Tensor, accumulate: bool) -> None:
@@ -277,8 +342,10 @@ class ConvBiasReLU(torch.autograd.Function):
                                                          [0, 0], 1, [True, False, False])[0]
             g = w.grad
             if (direct_w and g.is_contiguous(memory_format=torch.channels_last) and g.data_ptr() % 16 == 0):
-                _conv_wgrad_mfma(key, x, dz, w, stride, g, accumulate=True)  # straight into the flat .grad
-                notify_grad_written(w)
+                # partial tiles now; their reduction into the flat .grad joins the other layers' in one
+                # launch at direct_grads() exit
+                job, ws = _conv_wgrad_partials(key, x, dz, w, stride, g)
+                ctx.pending.add_wgrad(job, ws, w)
                 dw = None
             else:
                 dw = torch.empty_like(w, memory_format=torch.channels_last)

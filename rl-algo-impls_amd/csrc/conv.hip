@@ -271,12 +271,34 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
 }
 
 // dW (+)= sum over s of part[s] (fixed order: 16 lane groups each add S / 16 consecutive splits, then
-// the 16 group sums are added in group order through LDS)
-__global__ __launch_bounds__(CV_THREADS) void conv_wrw_reduce_kernel(const f4* __restrict__ part, int S, int64_t n4,
-                                                                    f4* __restrict__ dw, int accumulate) {
+// the 16 group sums are added in group order through LDS).  One launch serves up to RAI_WGRAD_MAX_JOBS
+// layers (the backward's convolutions, reduced together once the backward has ended): block b works
+// on the job whose block range holds it.
+struct WrwReduceJob {
+  const f4* part;
+  f4* dw;
+  int64_t n4;
+  int S;
+  int blk0;  // first block of this job
+};
+struct WrwReduceArgs {
+  WrwReduceJob j[RAI_WGRAD_MAX_JOBS];
+  int n;
+  int accumulate;
+};
+
+__global__ __launch_bounds__(CV_THREADS) void conv_wrw_reduce_kernel(const WrwReduceArgs a) {
   __shared__ f4 red[16][16];
+  int jb = 0;
+#pragma unroll
+  for (int q = 1; q < RAI_WGRAD_MAX_JOBS; ++q)
+    if (q < a.n && (int)blockIdx.x >= a.j[q].blk0) jb = q;
+  const f4* __restrict__ part = a.j[jb].part;
+  f4* __restrict__ dw = a.j[jb].dw;
+  const int64_t n4 = a.j[jb].n4;
+  const int S = a.j[jb].S;
   const int o = threadIdx.x & 15, sg = threadIdx.x >> 4;
-  const int64_t i = (int64_t)blockIdx.x * 16 + o;
+  const int64_t i = (int64_t)(blockIdx.x - a.j[jb].blk0) * 16 + o;
   const int per = S >> 4;
   f4 s = f4{0.f, 0.f, 0.f, 0.f};
   if (i < n4) {
@@ -295,7 +317,7 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_reduce_kernel(const f4* _
     f4 t = red[0][o];
 #pragma unroll
     for (int q = 1; q < 16; ++q) t += red[q][o];
-    dw[i] = accumulate ? dw[i] + t : t;
+    dw[i] = a.accumulate ? dw[i] + t : t;
   }
 }
 
@@ -336,26 +358,22 @@ extern "C" int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_
   return mx * Co * K * (int64_t)sizeof(float);
 }
 
-extern "C" int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci,
-                                  int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dw, int32_t accumulate,
-                                  void* workspace, int64_t workspace_bytes, int32_t target_wgs, int32_t pf,
-                                  void* stream) {
+static bool wgrad_shape_ok(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW,
+                           int32_t stride) {
   if (B < 0 || H < 1 || W < 1 || Ci < 4 || Ci % 4 || (Co != 32 && Co != 64) || KH < 1 || KW < 1 || stride < 1 ||
       KH > H || KW > W)
-    return RAI_E_SHAPE;
+    return false;
   const int64_t K = (int64_t)KH * KW * Ci;
-  if (K % 64 || K > (1 << 20)) return RAI_E_SHAPE;
-  hipStream_t st = rai_stream(stream);
-  if (B == 0) {
-    if (!accumulate) {
-      if (!dw) return RAI_E_NULLPTR;
-      const hipError_t e = hipMemsetAsync(dw, 0, (size_t)Co * K * 4, st);
-      if (e != hipSuccess) return (int)e;
-    }
-    return RAI_OK;
-  }
-  if (!x || !dz || !dw || !workspace) return RAI_E_NULLPTR;
-  if (((uintptr_t)x | (uintptr_t)dz | (uintptr_t)dw | (uintptr_t)workspace) & 15) return RAI_E_SHAPE;
+  return K % 64 == 0 && K <= (1 << 20);
+}
+
+// the first launch of rai_conv2d_wgrad: every workgroup's partial tile into workspace (B >= 1)
+static int wgrad_partials(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
+                          int32_t KH, int32_t KW, int32_t stride, void* workspace, int64_t workspace_bytes,
+                          int32_t target_wgs, int32_t pf, hipStream_t st) {
+  const int64_t K = (int64_t)KH * KW * Ci;
+  if (!x || !dz || !workspace) return RAI_E_NULLPTR;
+  if (((uintptr_t)x | (uintptr_t)dz | (uintptr_t)workspace) & 15) return RAI_E_SHAPE;
   if ((int64_t)H * W * Ci > (1LL << 30)) return RAI_E_SHAPE;  // per-chunk offsets are int32
   if (workspace_bytes < rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, stride)) return RAI_E_WORKSPACE;
   ConvWrwArgs a;
@@ -387,11 +405,91 @@ extern "C" int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, in
     else hipLaunchKernelGGL((conv_wrw_kernel<4, 8>), grid, dim3(CV_THREADS), 0, st, a);
   }
   RAI_LAUNCH_CHECK();
-  const int64_t n4 = (int64_t)Co * K / 4;
-  hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(CV_THREADS), 0, st,
-                     reinterpret_cast<const f4*>(workspace), p.S, n4, reinterpret_cast<f4*>(dw), accumulate);
+  return RAI_OK;
+}
+
+static int wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_t accumulate, hipStream_t st) {
+  WrwReduceArgs ra;
+  ra.n = 0;
+  ra.accumulate = accumulate ? 1 : 0;
+  int blocks = 0;
+  for (int q = 0; q < n_jobs; ++q) {
+    const rai_conv2d_wgrad_job& jb = jobs[q];
+    if (!wgrad_shape_ok(jb.B, jb.H, jb.W, jb.Ci, jb.Co, jb.KH, jb.KW, jb.stride)) return RAI_E_SHAPE;
+    const int64_t K = (int64_t)jb.KH * jb.KW * jb.Ci;
+    if (jb.B == 0) {
+      if (!accumulate) {
+        if (!jb.dw) return RAI_E_NULLPTR;
+        const hipError_t e = hipMemsetAsync(jb.dw, 0, (size_t)jb.Co * K * 4, st);
+        if (e != hipSuccess) return (int)e;
+      }
+      continue;
+    }
+    if (!jb.dw || !jb.workspace) return RAI_E_NULLPTR;
+    if (((uintptr_t)jb.dw | (uintptr_t)jb.workspace) & 15) return RAI_E_SHAPE;
+    const int64_t M = jb.B * ((jb.H - jb.KH) / jb.stride + 1) * ((jb.W - jb.KW) / jb.stride + 1);
+    const WrwPlan p = wrw_plan(M, jb.Co, (int)K, 0);
+    WrwReduceJob& r = ra.j[ra.n++];
+    r.part = static_cast<const f4*>(jb.workspace);
+    r.dw = reinterpret_cast<f4*>(jb.dw);
+    r.n4 = (int64_t)jb.Co * K / 4;
+    r.S = p.S;
+    r.blk0 = blocks;
+    blocks += (int)((r.n4 + 15) / 16);
+  }
+  if (ra.n == 0) return RAI_OK;
+  hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)blocks), dim3(CV_THREADS), 0, st, ra);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
+}
+
+extern "C" int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci,
+                                  int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dw, int32_t accumulate,
+                                  void* workspace, int64_t workspace_bytes, int32_t target_wgs, int32_t pf,
+                                  void* stream) {
+  if (!wgrad_shape_ok(B, H, W, Ci, Co, KH, KW, stride)) return RAI_E_SHAPE;
+  hipStream_t st = rai_stream(stream);
+  if (B > 0) {
+    if (!dw) return RAI_E_NULLPTR;
+    const int rc = wgrad_partials(x, dz, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, target_wgs,
+                                  pf, st);
+    if (rc != RAI_OK) return rc;
+    if (target_wgs != 0) {  // the reduce below follows the default plan: re-derive S for this one
+      // (A/B only) the reduction reads the split count the partials were launched with
+      const int64_t K = (int64_t)KH * KW * Ci;
+      const int64_t M = B * ((H - KH) / stride + 1) * ((W - KW) / stride + 1);
+      const WrwPlan p = wrw_plan(M, Co, (int)K, target_wgs);
+      WrwReduceArgs ra;
+      ra.n = 1;
+      ra.accumulate = accumulate ? 1 : 0;
+      ra.j[0].part = static_cast<const f4*>(workspace);
+      ra.j[0].dw = reinterpret_cast<f4*>(dw);
+      ra.j[0].n4 = (int64_t)Co * K / 4;
+      ra.j[0].S = p.S;
+      ra.j[0].blk0 = 0;
+      hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)((ra.j[0].n4 + 15) / 16)), dim3(CV_THREADS), 0, st,
+                         ra);
+      RAI_LAUNCH_CHECK();
+      return RAI_OK;
+    }
+  }
+  rai_conv2d_wgrad_job jb = {workspace, dw, B, H, W, Ci, Co, KH, KW, stride, 0};
+  return wgrad_reduce(&jb, 1, accumulate, st);
+}
+
+extern "C" int rai_conv2d_wgrad_partials(const float* x, const float* dz, int64_t B, int32_t H, int32_t W,
+                                         int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride,
+                                         void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!wgrad_shape_ok(B, H, W, Ci, Co, KH, KW, stride)) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  return wgrad_partials(x, dz, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, 0, 0, rai_stream(stream));
+}
+
+extern "C" int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_t accumulate,
+                                       void* stream) {
+  if (n_jobs < 0 || n_jobs > RAI_WGRAD_MAX_JOBS) return RAI_E_SHAPE;
+  if (n_jobs > 0 && !jobs) return RAI_E_NULLPTR;
+  return wgrad_reduce(jobs, n_jobs, accumulate, rai_stream(stream));
 }
 
 // variant: 0 = by shape (the shipped choice); 1.. = a fixed blocking (tools/conv_bench.py A/B)

@@ -178,3 +178,35 @@ def test_conv_wgrad_full_c3_minibatch_against_miopen():
     err = (dw.to(DEV) - ref).abs()
     assert (err <= 2 * (256 * 400 + 2) * 2.0 ** -24 * bound + 1e-30).all()
     assert (err <= 1e-4 * bound.max()).all()  # and far tighter in practice
+
+
+def test_conv_wgrad_partials_and_one_reduce_for_three_layers():
+    """The backward's form: each layer's partials, then ONE rai_conv2d_wgrad_reduce over the three
+    NatureCNN layers, accumulating into existing gradients -- bit-identical to rai_conv2d_wgrad per
+    layer (same plan, same fixed-order sums)."""
+    from rl_algo_impls_amd.cnn_ops import _WgradJob
+    L = _lib.lib()
+    st = _lib.stream_handle(DEV)
+    jobs, keep, outs, refs = [], [], [], []
+    for li, (Ci, H, Co, k, s) in enumerate(WGRAD_CASES[:3]):
+        x, w, _ = _inputs(32, Ci, H, Co, k, seed=20 + li)
+        OH = (H - k) // s + 1
+        dz = torch.randn(32, Co, OH, OH, generator=torch.Generator().manual_seed(li))
+        base = torch.randn(Co, Ci, k, k, generator=torch.Generator().manual_seed(40 + li))
+        refs.append(_wgrad(x, dz, k, k, s, dw0=base))
+        xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+        dzd = dz.to(DEV).contiguous(memory_format=torch.channels_last)
+        g = base.to(DEV).contiguous(memory_format=torch.channels_last)
+        nb = int(L.rai_conv2d_wgrad_workspace_bytes(32, H, H, Ci, Co, k, k, s))
+        ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+        _lib.check(L.rai_conv2d_wgrad_partials(xd.data_ptr(), dzd.data_ptr(), 32, H, H, Ci, Co, k, k, s,
+                                               ws.data_ptr(), nb, st), "partials")
+        jobs.append(_WgradJob(ws.data_ptr(), g.data_ptr(), 32, H, H, Ci, Co, k, k, s, 0))
+        keep += [xd, dzd, ws]
+        outs.append(g)
+    arr = (_WgradJob * 3)(*jobs)
+    _lib.check(L.rai_conv2d_wgrad_reduce(C.cast(arr, C.c_void_p), 3, 1, st), "reduce")
+    torch.cuda.synchronize()
+    for g, ref in zip(outs, refs):
+        assert torch.equal(g.cpu(), ref)
+    assert L.rai_conv2d_wgrad_reduce(C.cast(arr, C.c_void_p), 5, 1, st) == -2
