@@ -178,7 +178,7 @@ int rai_bias_relu_bwd_nchw(const float* dy, const float* y, int64_t B, int32_t H
 int rai_conv2d_bias_relu_fwd(const float* x, const float* w, const float* b, int64_t B, int32_t H, int32_t W,
                              int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, int32_t out_nchw,
                              float* y, void* stream);
-/* The same with a fixed workgroup blocking (variant 0 = chosen by shape, as above; 1-11 = the blockings and prefetch depths
+/* The same with a fixed workgroup blocking (variant 0 = chosen by shape, as above; 1-15 = the blockings, prefetch depths and LDS-resident-weight forms
  * in csrc/conv.hip, for same-box A/B timing in tools/conv_bench.py). */
 int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const float* b, int64_t B, int32_t H, int32_t W,
                                int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, int32_t out_nchw,
@@ -211,6 +211,12 @@ int rai_conv2d_wgrad_partials(const float* x, const float* dz, int64_t B, int32_
                               int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
                               int64_t workspace_bytes, void* stream);
 int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_t accumulate, void* stream);
+/* Input gradient of the same convolution (Conv2d's autograd dx; NatureCNN conv2 / conv3): dx (B, H, W, Ci)
+ * NHWC = the transposed convolution of dz (B, OH, OW, Co) NHWC with w (Co, KH, KW, Ci) channels_last,
+ * every element written (no accumulate, no zero-fill).  Ci 32 or 64, Co % 16 == 0, KH and KW multiples
+ * of stride, padding 0, pointers 16-B aligned.  Hand-written f32 MFMA, deterministic. */
+int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
+                     int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream);
 /* The same with a fixed launch shape for same-box A/B (tools/conv_bench.py): target_wgs workgroups
  * (0 = 512, at most 1024), pf pixel steps in flight per wave (0 = 4; 4 or 8). */
 int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,

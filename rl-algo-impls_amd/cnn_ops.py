@@ -14,7 +14,7 @@ Convolutions on hand-written MFMA kernels (round 3, csrc/conv.hip).  The forward
 conv -> ReLU pair is ONE launch, rai_conv2d_bias_relu_fwd (f32 MFMA implicit GEMM, bias + ReLU in its
 store, conv3 writing nn.Flatten's NCHW order directly), and the weight gradient is
 rai_conv2d_wgrad (f32 MFMA, fixed-order split reduction) added straight into the flat .grad view.
-The input gradient (conv2, conv3) stays on MIOpen.  Shapes those kernels do not take fall back to
+The input gradient (conv2, conv3) is rai_conv2d_dgrad (f32 MFMA over same-parity pixel classes).  Shapes those kernels do not take fall back to
 MIOpen (still on the GPU); RAI_CONV_MFMA=0 selects MIOpen everywhere (same-box A/B).
 
 Direct gradient accumulation.  Inside the trainer's update (`direct_grads(module)`), every
@@ -175,7 +175,7 @@ class _Workspaces:
 _WS = _Workspaces()
 
 _CONV_MFMA = os.environ.get("RAI_CONV_MFMA", "1") != "0"
-_MFMA_FWD_MAX_PIXELS_64 = 40000
+_CONV_MFMA_DGRAD = os.environ.get("RAI_CONV_MFMA_DGRAD", "0") == "1"  # measured no faster than MIOpen (r3u)
 
 
 class _WgradWorkspaces:
@@ -208,14 +208,6 @@ def _mfma_conv_ok(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride, pad
     if not _CONV_MFMA or tuple(_pair(padding)) != (0, 0):
         return False
     Co, Ci, KH, KW = (int(v) for v in w.shape)
-    if Co == 64 and x.dim() == 4:
-        # measured (profiles/r3r_conv_bench.txt): the 64-channel layers are faster here at the update's
-        # minibatch (B = 256: conv2 20,736 / conv3 12,544 output pixels) and slower than MIOpen's
-        # implicit GEMMs at the rollout's B = 1,024 (82,944 / 50,176 pixels)
-        s = _pair(stride)[0]
-        M = int(x.shape[0]) * ((int(x.shape[2]) - KH) // s + 1) * ((int(x.shape[3]) - KW) // s + 1)
-        if M > _MFMA_FWD_MAX_PIXELS_64:
-            return False
     return (x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
             and w.is_contiguous(memory_format=torch.channels_last) and Ci % 4 == 0 and Co in (32, 64)
             and (KH * KW * Ci) % 64 == 0 and KH * KW * Ci <= 8192 and b.is_contiguous()
@@ -235,6 +227,21 @@ def _conv_fwd_mfma(x, w, b, stride, flatten) -> torch.Tensor:
                                                    KW, s, 1 if flatten else 0, y.data_ptr(),
                                                    _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd")
     return y
+
+
+def _conv_dgrad(x, dz, w, stride) -> torch.Tensor:
+    """dx of the convolution: rai_conv2d_dgrad (MFMA) where it applies (Ci 32 / 64, kernel a multiple of
+    the stride), else MIOpen."""
+    B, Ci, H, W = (int(v) for v in x.shape)
+    Co, _, KH, KW = (int(v) for v in w.shape)
+    s = _pair(stride)[0]
+    if _CONV_MFMA_DGRAD and Ci in (32, 64) and KH % s == 0 and KW % s == 0:
+        dx = torch.empty((B, Ci, H, W), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+        _lib.check(_lib.lib().rai_conv2d_dgrad(dz.data_ptr(), w.data_ptr(), B, H, W, Ci, Co, KH, KW, s, dx.data_ptr(),
+                                               _lib.stream_handle(x.device)), "rai_conv2d_dgrad")
+        return dx
+    return torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), [0, 0], [1, 1], False, [0, 0], 1,
+                                               [True, False, False])[0]
 
 
 def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor):
@@ -338,8 +345,7 @@ class ConvBiasReLU(torch.autograd.Function):
         if mfma and dz.is_contiguous(memory_format=torch.channels_last) and dz.data_ptr() % 16 == 0:
             dx = None
             if need_dx:
-                dx = torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), _pair(padding), [1, 1], False,
-                                                         [0, 0], 1, [True, False, False])[0]
+                dx = _conv_dgrad(x, dz, w, stride)
             g = w.grad
             if (direct_w and g.is_contiguous(memory_format=torch.channels_last) and g.data_ptr() % 16 == 0):
                 # partial tiles now; their reduction into the flat .grad joins the other layers' in one

@@ -136,6 +136,136 @@ __global__ __launch_bounds__(CV_THREADS) void conv_fwd_kernel(const ConvFwdArgs 
   }
 }
 
+// The same forward with the workgroup's weight rows resident in LDS: a persistent workgroup (8 waves,
+// one per CU) copies its COT rows x K once (row stride K + 4 floats: the 16 lanes of a ds_read_b128
+// group land on distinct banks), then loops over pixel tiles; only the im2col operand is read from
+// L1/L2 per quad.
+template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF>
+__global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) {
+  static_assert(WCO * WPX == 8, "eight waves");
+  constexpr int COT = 16 * TCO * WCO, PXT = 16 * TPX * WPX;
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [COT][K + 4]
+  __shared__ int xoff[CV_MAXCHUNK];
+  const int K = a.K, KP = K + 4;
+  const int nch = K >> 2;
+  const int co_wg = blockIdx.y * COT;
+  for (int q = threadIdx.x; q < nch; q += 512) {
+    const int k = 4 * q, kpos = k / a.Ci, ci0 = k - kpos * a.Ci, kh = kpos / a.KW, kw = kpos - kh * a.KW;
+    xoff[q] = (kh * a.W + kw) * a.Ci + ci0;
+  }
+  for (int e = threadIdx.x; e < COT * nch; e += 512) {
+    const int r = e / nch, q = e - r * nch;
+    *reinterpret_cast<f4*>(wl + r * KP + 4 * q) = *reinterpret_cast<const f4*>(a.w + (int64_t)(co_wg + r) * K + 4 * q);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int wco = wv % WCO, wpx = wv / WCO;
+  const int OHW = a.OH * a.OW;
+  const float* wrow[TCO];
+#pragma unroll
+  for (int tc = 0; tc < TCO; ++tc) wrow[tc] = wl + (16 * (TCO * wco + tc) + li) * KP;
+  const int64_t ntiles = (a.M + PXT - 1) / PXT;
+  const int nq = nch >> 2;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t px0 = tile * PXT + 16 * TPX * wpx;
+    const float* xb[TPX];
+#pragma unroll
+    for (int tp = 0; tp < TPX; ++tp) {
+      int64_t p = px0 + 16 * tp + li;
+      p = p < a.M ? p : a.M - 1;
+      const int64_t n = p / OHW;
+      const int r = (int)(p - n * OHW), oh = r / a.OW, ow = r - oh * a.OW;
+      xb[tp] = a.x + ((n * a.H + (int64_t)oh * a.S) * a.W + (int64_t)ow * a.S) * a.Ci;
+    }
+    f4 acc[TCO][TPX];
+#pragma unroll
+    for (int tc = 0; tc < TCO; ++tc)
+#pragma unroll
+      for (int tp = 0; tp < TPX; ++tp) acc[tc][tp] = f4{0.f, 0.f, 0.f, 0.f};
+    f4 Br[PF][TPX];
+    auto ldb = [&](int qd, f4(&Bv)[TPX]) {
+      const int xo = xoff[4 * qd + g];
+#pragma unroll
+      for (int tp = 0; tp < TPX; ++tp) Bv[tp] = *reinterpret_cast<const f4*>(xb[tp] + xo);
+    };
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (u < nq) ldb(u, Br[u]);
+    for (int qd = 0; qd < nq; qd += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if (qd + u < nq) {
+          f4 A[TCO];
+#pragma unroll
+          for (int tc = 0; tc < TCO; ++tc) A[tc] = *reinterpret_cast<const f4*>(wrow[tc] + 4 * (4 * (qd + u) + g));
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int tc = 0; tc < TCO; ++tc)
+#pragma unroll
+              for (int tp = 0; tp < TPX; ++tp)
+                acc[tc][tp] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[tc][j], Br[u][tp][j], acc[tc][tp], 0, 0, 0);
+        }
+        if (qd + u + PF < nq) ldb(qd + u + PF, Br[u]);
+      }
+    }
+#pragma unroll
+    for (int tc = 0; tc < TCO; ++tc) {
+      const int co = co_wg + 16 * (TCO * wco + tc) + 4 * g;
+      const f4 bv = *reinterpret_cast<const f4*>(a.b + co);
+#pragma unroll
+      for (int tp = 0; tp < TPX; ++tp) {
+        const int64_t p = px0 + 16 * tp + li;
+        if (p >= a.M) continue;
+        f4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = acc[tc][tp][r] + bv[r];
+          v[r] = t < 0.f ? 0.f : t;
+        }
+        if (!NCHW) {
+          *reinterpret_cast<f4*>(a.y + p * a.Co + co) = v;
+        } else {
+          const int64_t n = p / OHW;
+          float* yb = a.y + n * (int64_t)a.Co * OHW + (p - n * OHW) + (int64_t)co * OHW;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) yb[(int64_t)r * OHW] = v[r];
+        }
+      }
+    }
+  }
+}
+
+template <int TCO, int TPX, int WCO, int WPX, int PF>
+int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
+  constexpr int PXT = 16 * TPX * WPX, COT = 16 * TCO * WCO;
+  if (a.Co % COT) return RAI_E_SHAPE;
+  const size_t lds = (size_t)COT * (a.K + 4) * sizeof(float);
+  if (lds + CV_MAXCHUNK * 4 > 160 * 1024) return RAI_E_SHAPE;
+  const int64_t ntiles = (a.M + PXT - 1) / PXT;
+  const int64_t cot = a.Co / COT;
+  int64_t gx = 256 / cot;  // one persistent workgroup per CU
+  if (gx > ntiles) gx = ntiles;
+  if (gx < 1) gx = 1;
+  const dim3 grid((unsigned)gx, (unsigned)cot);
+  if (nchw) {
+    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF>;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
+  } else {
+    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, false, PF>;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
+  }
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
 template <int TCO, int TPX, int WCO, int WPX, int PF = 2>
 int launch_fwd(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   constexpr int PXT = 16 * TPX * WPX, COT = 16 * TCO * WCO;
@@ -342,6 +472,112 @@ static WrwPlan wrw_plan(int64_t M, int Co, int K, int target_wgs) {
   return p;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Input gradient (the dx of Conv2d's autograd backward; conv2 / conv3 of NatureCNN, whose inputs
+// need gradients): dx[n][ih][iw][ci] = sum over taps (kh, kw) with oh = (ih - kh) / S, ow = (iw - kw) / S
+// integral and in range, and over co, of dz[n][oh][ow][co] * W[co][kh][kw][ci].  Input pixels are
+// grouped into S x S classes (ih % S, iw % S): every pixel of a class sees the same taps
+// kh = ih % S + S * th (th < KH / S), so a column block of 16 same-class pixels shares the A operand.
+// MFMA rows = ci, columns = input pixels, reduction = (tap, co).  Both 4-wide tricks: lane (i, g)
+// loads VC consecutive ci of W at co = c0 + 4g + m (m = 0..3: four loads) and 4 consecutive co of dz
+// at its pixel's output position (one float4 per column block); MFMA (m, j) takes W component j of
+// load m and dz component m, accumulating rows ci = VC * i + j.  A wave owns all Ci = 16 * VC rows x
+// TQ column blocks; invalid taps (outside the output) load zeros.  Every dx element is written once
+// (no split, no zero-fill, deterministic).
+struct ConvDgradArgs {
+  const float* dz;  // (B, OH, OW, Co)
+  const float* w;   // (Co, KH, KW, Ci)
+  float* dx;        // (B, H, W, Ci)
+  int64_t B;
+  int H, W, Ci, Co, KH, KW, S, OH, OW;
+};
+
+template <int VC, int TQ>
+__global__ __launch_bounds__(CV_THREADS) void conv_dgrad_kernel(const ConvDgradArgs a) {
+  typedef float fv __attribute__((ext_vector_type(VC)));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int cls = blockIdx.y, ph = cls / a.S, pw = cls - ph * a.S;
+  const int Hc = (a.H - ph + a.S - 1) / a.S, Wc = (a.W - pw + a.S - 1) / a.S;  // this class's grid
+  const int64_t ncls = a.B * Hc * Wc;
+  const int TH = a.KH / a.S, TW = a.KW / a.S;
+  int64_t pix[TQ];   // this lane's class pixel per column block (clamped), -1 past the end
+  int ihc[TQ], iwc[TQ];
+  int64_t dzb[TQ];   // dz pixel index of tap (0, 0)
+#pragma unroll
+  for (int tq = 0; tq < TQ; ++tq) {
+    const int64_t c = (int64_t)blockIdx.x * (64 * TQ) + (int64_t)(wv * TQ + tq) * 16 + li;
+    const int64_t cc = c < ncls ? c : ncls - 1;
+    pix[tq] = c < ncls ? c : -1;
+    const int64_t n = cc / (Hc * Wc);
+    const int r = (int)(cc - n * Hc * Wc);
+    ihc[tq] = r / Wc;
+    iwc[tq] = r - ihc[tq] * Wc;
+    dzb[tq] = (n * a.OH + ihc[tq]) * a.OW + iwc[tq];
+  }
+  f4 acc[VC][TQ];
+#pragma unroll
+  for (int j = 0; j < VC; ++j)
+#pragma unroll
+    for (int tq = 0; tq < TQ; ++tq) acc[j][tq] = f4{0.f, 0.f, 0.f, 0.f};
+  const int ncc = a.Co >> 4;
+  const int nsteps = TH * TW * ncc;  // (tap, 16-co chunk) steps
+  auto ld = [&](int stp, fv (&A)[4], f4 (&Bv)[TQ]) {
+    const int t = stp / ncc, c0 = (stp - t * ncc) * 16;
+    const int th = t / TW, tw = t - th * TW;
+    const int kh = ph + a.S * th, kw = pw + a.S * tw;
+    const float* wp = a.w + ((int64_t)((c0 + 4 * g) * a.KH + kh) * a.KW + kw) * a.Ci + VC * li;
+    const int64_t wco = (int64_t)a.KH * a.KW * a.Ci;  // one co further
+#pragma unroll
+    for (int m = 0; m < 4; ++m) A[m] = *reinterpret_cast<const fv*>(wp + m * wco);
+#pragma unroll
+    for (int tq = 0; tq < TQ; ++tq) {
+      const int oh = ihc[tq] - th, ow = iwc[tq] - tw;
+      if (pix[tq] >= 0 && oh >= 0 && oh < a.OH && ow >= 0 && ow < a.OW)
+        Bv[tq] = *reinterpret_cast<const f4*>(a.dz + (dzb[tq] - (int64_t)th * a.OW - tw) * a.Co + c0 + 4 * g);
+      else
+        Bv[tq] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto mma = [&](const fv (&A)[4], const f4 (&Bv)[TQ]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < VC; ++j)
+#pragma unroll
+        for (int tq = 0; tq < TQ; ++tq)
+          acc[j][tq] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[m][j], Bv[tq][m], acc[j][tq], 0, 0, 0);
+  };
+  constexpr int PF = 2;
+  fv A[PF][4];
+  f4 Bv[PF][TQ];
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nsteps) ld(u, A[u], Bv[u]);
+  for (int st = 0; st < nsteps; st += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (st + u < nsteps) mma(A[u], Bv[u]);
+      if (st + u + PF < nsteps) ld(st + u + PF, A[u], Bv[u]);
+    }
+  }
+  // lane (i, g), block tq: rows ci = VC * (4g + r) + j for pixel column i -> VC consecutive ci per r
+#pragma unroll
+  for (int tq = 0; tq < TQ; ++tq) {
+    if (pix[tq] < 0) continue;
+    const int64_t n = pix[tq] / (Hc * Wc);
+    const int ih = ph + a.S * ihc[tq], iw = pw + a.S * iwc[tq];
+    float* dp = a.dx + ((n * a.H + ih) * a.W + iw) * a.Ci;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      fv v;
+#pragma unroll
+      for (int j = 0; j < VC; ++j) v[j] = acc[j][tq][r];
+      *reinterpret_cast<fv*>(dp + VC * (4 * g + r)) = v;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
@@ -522,7 +758,18 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
   if ((int64_t)H * W * Ci * B > (1LL << 40)) return RAI_E_SHAPE;
   hipStream_t st = rai_stream(stream);
   const bool nchw = out_nchw != 0;
-  if (variant == 0) variant = (Co % 64 == 0) ? 10 : (Co % 32 == 0) ? 11 : 7;
+  if (variant == 0) {
+    // measured (profiles/r3v_conv_bench.txt): the LDS-resident-weight forms win wherever the weight rows
+    // fit (<= ~150 KB); 32 co x 256 px tiles once they give >= 256 workgroup tiles, else 64 co x 64 px
+    const size_t lds32 = (size_t)32 * (K + 4) * 4, lds64 = (size_t)64 * (K + 4) * 4;
+    const int64_t t14 = (a.M + 255) / 256 * (Co / 32);
+    if (Co % 32 == 0 && lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && (t14 >= 256 || Co % 64 != 0))
+      variant = 14;
+    else if (Co % 64 == 0 && lds64 + CV_MAXCHUNK * 4 <= 160 * 1024)
+      variant = 13;
+    else
+      variant = (Co % 64 == 0) ? 10 : (Co % 32 == 0) ? 11 : 7;
+  }
   switch (variant) {
     case 1: return launch_fwd<2, 2, 1, 4>(a, nchw, st);  // 32 co x 128 px
     case 2: return launch_fwd<1, 2, 2, 2>(a, nchw, st);  // 32 co x 64 px
@@ -535,6 +782,10 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
     case 9: return launch_fwd<2, 2, 2, 2, 4>(a, nchw, st);  // variant 5, four quads in flight
     case 10: return launch_fwd<2, 2, 2, 2, 3>(a, nchw, st);  // variant 5, three quads in flight
     case 11: return launch_fwd<2, 2, 1, 4, 3>(a, nchw, st);  // variant 1, three quads in flight
+    case 12: return launch_fwd_lds<2, 2, 2, 4, 3>(a, nchw, st);  // LDS weights, 64 co x 128 px, 8 waves
+    case 13: return launch_fwd_lds<2, 1, 2, 4, 4>(a, nchw, st);  // LDS weights, 64 co x 64 px, 8 waves
+    case 14: return launch_fwd_lds<2, 2, 1, 8, 3>(a, nchw, st);  // LDS weights, 32 co x 256 px, 8 waves
+    case 15: return launch_fwd_lds<1, 2, 2, 4, 4>(a, nchw, st);  // LDS weights, 32 co x 128 px, 8 waves
     default: return RAI_E_SHAPE;
   }
 }
@@ -550,4 +801,41 @@ extern "C" int rai_conv2d_wgrad(const float* x, const float* dz, int64_t B, int3
                                 void* workspace, int64_t workspace_bytes, void* stream) {
   return rai_conv2d_wgrad_v(x, dz, B, H, W, Ci, Co, KH, KW, stride, dw, accumulate, workspace, workspace_bytes, 0, 0,
                             stream);
+}
+
+extern "C" int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci,
+                                int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream) {
+  if (B < 0 || H < 1 || W < 1 || (Ci != 32 && Ci != 64) || Co < 16 || Co % 16 || KH < 1 || KW < 1 || stride < 1 ||
+      KH > H || KW > W || KH % stride || KW % stride)
+    return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!dz || !w || !dx) return RAI_E_NULLPTR;
+  if (((uintptr_t)dz | (uintptr_t)w | (uintptr_t)dx) & 15) return RAI_E_SHAPE;
+  ConvDgradArgs a;
+  a.dz = dz;
+  a.w = w;
+  a.dx = dx;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.KH = KH;
+  a.KW = KW;
+  a.S = stride;
+  a.OH = (H - KH) / stride + 1;
+  a.OW = (W - KW) / stride + 1;
+  const int64_t maxcls = B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
+  hipStream_t st = rai_stream(stream);
+  if (Ci == 32) {  // 32 rows: four column blocks per wave
+    const int64_t gx = (maxcls + 255) / 256;
+    hipLaunchKernelGGL((conv_dgrad_kernel<2, 4>), dim3((unsigned)gx, (unsigned)(stride * stride)), dim3(CV_THREADS),
+                       0, st, a);
+  } else {  // 64 rows: one column block per wave
+    const int64_t gx = (maxcls + 63) / 64;
+    hipLaunchKernelGGL((conv_dgrad_kernel<4, 1>), dim3((unsigned)gx, (unsigned)(stride * stride)), dim3(CV_THREADS),
+                       0, st, a);
+  }
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
 }

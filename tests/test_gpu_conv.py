@@ -72,7 +72,7 @@ def test_conv_bias_relu_fwd_matches_fp64(case, B):
     assert (err <= tol).all(), float((err / tol).max())
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", list(range(1, 16)))
 def test_conv_every_blocking_variant(variant):
     Ci, H, Co, k, s, flat = 32, 20, 64, 4, 2, False
     x, w, b = _inputs(9, Ci, H, Co, k, seed=3)
@@ -210,3 +210,34 @@ def test_conv_wgrad_partials_and_one_reduce_for_three_layers():
     for g, ref in zip(outs, refs):
         assert torch.equal(g.cpu(), ref)
     assert L.rai_conv2d_wgrad_reduce(C.cast(arr, C.c_void_p), 5, 1, st) == -2
+
+
+DGRAD_CASES = [  # (Ci, H, Co, k, stride): NatureCNN conv2 / conv3, odd sizes, a border-only tap case
+    (32, 20, 64, 4, 2),
+    (64, 9, 64, 3, 1),
+    (32, 11, 16, 2, 2),
+    (64, 7, 32, 4, 2),
+]
+
+
+@pytest.mark.parametrize("case", DGRAD_CASES, ids=lambda c: "x".join(str(v) for v in c))
+@pytest.mark.parametrize("B", [1, 3, 64])
+def test_conv_dgrad_matches_fp64(case, B):
+    Ci, H, Co, k, s = case
+    x, w, _ = _inputs(B, Ci, H, Co, k, seed=B + 31)
+    OH = (H - k) // s + 1
+    dz = torch.randn(B, Co, OH, OH, generator=torch.Generator().manual_seed(B + 7))
+    dzd = dz.to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
+    dx = torch.full((B, Ci, H, H), float("nan"), device=DEV).contiguous(memory_format=torch.channels_last)
+    _lib.check(_lib.lib().rai_conv2d_dgrad(dzd.data_ptr(), wd.data_ptr(), B, H, H, Ci, Co, k, k, s, dx.data_ptr(),
+                                           _lib.stream_handle(DEV)), "rai_conv2d_dgrad")
+    torch.cuda.synchronize()
+    ref = torch.ops.aten.convolution_backward(dz.double(), x.double(), w.double(), None, [s, s], [0, 0], [1, 1], False,
+                                              [0, 0], 1, [True, False, False])[0]
+    bound = torch.ops.aten.convolution_backward(dz.double().abs(), x.double(), w.double().abs(), None, [s, s], [0, 0],
+                                                [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    got = dx.cpu().double()
+    assert torch.isfinite(got).all()
+    tol = (Co * k * k + 2) * 2.0 ** -24 * bound + 1e-30
+    assert ((got - ref).abs() <= tol).all(), float(((got - ref).abs() / tol).max())
