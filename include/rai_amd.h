@@ -217,6 +217,10 @@ int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, in
  * of stride, padding 0, pointers 16-B aligned.  Hand-written f32 MFMA, deterministic. */
 int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
                      int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream);
+/* The same with a fixed form (variant 0 = default; 1, 2 = weights resident in LDS, persistent workgroups;
+ * tools/conv_bench.py A/B). */
+int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
+                       int32_t KH, int32_t KW, int32_t stride, float* dx, int32_t variant, void* stream);
 /* The same with a fixed launch shape for same-box A/B (tools/conv_bench.py): target_wgs workgroups
  * (0 = 512, at most 1024), pf pixel steps in flight per wave (0 = 4; 4 or 8). */
 int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,

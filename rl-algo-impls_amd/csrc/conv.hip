@@ -578,6 +578,131 @@ __global__ __launch_bounds__(CV_THREADS) void conv_dgrad_kernel(const ConvDgradA
   }
 }
 
+// The input gradient with the whole weight tensor resident in LDS (<= ~150 KB: NatureCNN conv2 128 KB,
+// conv3 147 KB), persistent 8-wave workgroups looping over (class, pixel tile) work items: only dz is
+// read from L1/L2 per step.  Waves split the rows (WCI groups of 16 * VC ci) and the pixel blocks.
+template <int VC, int TQ, int WCI>
+__global__ __launch_bounds__(512) void conv_dgrad_lds_kernel(const ConvDgradArgs a) {
+  typedef float fv __attribute__((ext_vector_type(VC)));
+  constexpr int WQ = 8 / WCI;             // waves along pixels
+  constexpr int PXT = 16 * TQ * WQ;       // pixels per work item
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // (Co, KH, KW, Ci)
+  const int64_t wn = (int64_t)a.Co * a.KH * a.KW * a.Ci;
+  for (int64_t e = threadIdx.x; e < wn / 4; e += 512)
+    reinterpret_cast<f4*>(wl)[e] = reinterpret_cast<const f4*>(a.w)[e];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int wci = wv % WCI, wq = wv / WCI;
+  const int ci0 = 16 * VC * wci;
+  const int TH = a.KH / a.S, TW = a.KW / a.S;
+  const int ncc = a.Co >> 4;
+  const int nsteps = TH * TW * ncc;
+  const int wco = a.KH * a.KW * a.Ci;
+  // work items: class-major, tiles of PXT pixels of the class
+  const int Hc0 = (a.H + a.S - 1) / a.S, Wc0 = (a.W + a.S - 1) / a.S;
+  const int64_t tiles_per_cls = (a.B * Hc0 * Wc0 + PXT - 1) / PXT;
+  const int64_t nitems = tiles_per_cls * a.S * a.S;
+  for (int64_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const int cls = (int)(item / tiles_per_cls);
+    const int64_t tile = item - (int64_t)cls * tiles_per_cls;
+    const int ph = cls / a.S, pw = cls - ph * a.S;
+    const int Hc = (a.H - ph + a.S - 1) / a.S, Wc = (a.W - pw + a.S - 1) / a.S;
+    const int64_t ncls = a.B * Hc * Wc;
+    if (tile * PXT >= ncls) continue;  // uniform over the workgroup
+    int64_t pix[TQ];
+    int ihc[TQ], iwc[TQ];
+    int64_t dzb[TQ];
+#pragma unroll
+    for (int tq = 0; tq < TQ; ++tq) {
+      const int64_t c = tile * PXT + (int64_t)(wq * TQ + tq) * 16 + li;
+      const int64_t cc = c < ncls ? c : ncls - 1;
+      pix[tq] = c < ncls ? c : -1;
+      const int64_t n = cc / (Hc * Wc);
+      const int r = (int)(cc - n * Hc * Wc);
+      ihc[tq] = r / Wc;
+      iwc[tq] = r - ihc[tq] * Wc;
+      dzb[tq] = (n * a.OH + ihc[tq]) * a.OW + iwc[tq];
+    }
+    f4 acc[VC][TQ];
+#pragma unroll
+    for (int j = 0; j < VC; ++j)
+#pragma unroll
+      for (int tq = 0; tq < TQ; ++tq) acc[j][tq] = f4{0.f, 0.f, 0.f, 0.f};
+    auto ldb = [&](int stp, f4 (&Bv)[TQ]) {
+      const int t = stp / ncc, c0 = (stp - t * ncc) * 16;
+      const int th = t / TW, tw = t - th * TW;
+#pragma unroll
+      for (int tq = 0; tq < TQ; ++tq) {
+        const int oh = ihc[tq] - th, ow = iwc[tq] - tw;
+        if (pix[tq] >= 0 && oh >= 0 && oh < a.OH && ow >= 0 && ow < a.OW)
+          Bv[tq] = *reinterpret_cast<const f4*>(a.dz + (dzb[tq] - (int64_t)th * a.OW - tw) * a.Co + c0 + 4 * g);
+        else
+          Bv[tq] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    constexpr int PF = 3;
+    f4 Bv[PF][TQ];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (u < nsteps) ldb(u, Bv[u]);
+    for (int st = 0; st < nsteps; st += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if (st + u < nsteps) {
+          const int stp = st + u;
+          const int t = stp / ncc, c0 = (stp - t * ncc) * 16;
+          const int th = t / TW, tw = t - th * TW;
+          const int kh = ph + a.S * th, kw = pw + a.S * tw;
+          const float* wp = wl + ((c0 + 4 * g) * a.KH + kh) * a.KW * a.Ci + kw * a.Ci + ci0 + VC * li;
+          fv A[4];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) A[m] = *reinterpret_cast<const fv*>(wp + m * wco);
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int j = 0; j < VC; ++j)
+#pragma unroll
+              for (int tq = 0; tq < TQ; ++tq)
+                acc[j][tq] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[m][j], Bv[u][tq][m], acc[j][tq], 0, 0, 0);
+        }
+        if (st + u + PF < nsteps) ldb(st + u + PF, Bv[u]);
+      }
+    }
+#pragma unroll
+    for (int tq = 0; tq < TQ; ++tq) {
+      if (pix[tq] < 0) continue;
+      const int64_t n = pix[tq] / (Hc * Wc);
+      const int ih = ph + a.S * ihc[tq], iw = pw + a.S * iwc[tq];
+      float* dp = a.dx + ((n * a.H + ih) * a.W + iw) * a.Ci + ci0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        fv v;
+#pragma unroll
+        for (int j = 0; j < VC; ++j) v[j] = acc[j][tq][r];
+        *reinterpret_cast<fv*>(dp + VC * (4 * g + r)) = v;
+      }
+    }
+  }
+}
+
+template <int VC, int TQ, int WCI>
+int launch_dgrad_lds(const ConvDgradArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)a.Co * a.KH * a.KW * a.Ci * sizeof(float);
+  if (lds > 160 * 1024 || 16 * VC * WCI != a.Ci) return RAI_E_SHAPE;
+  constexpr int PXT = 16 * TQ * (8 / WCI);
+  const int64_t Hc0 = (a.H + a.S - 1) / a.S, Wc0 = (a.W + a.S - 1) / a.S;
+  const int64_t nitems = (a.B * Hc0 * Wc0 + PXT - 1) / PXT * a.S * a.S;
+  const int64_t gx = nitems < 256 ? nitems : 256;
+  auto k = conv_dgrad_lds_kernel<VC, TQ, WCI>;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k, dim3((unsigned)gx), dim3(512), lds, st, a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
 }  // namespace
 
 extern "C" int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
@@ -803,8 +928,9 @@ extern "C" int rai_conv2d_wgrad(const float* x, const float* dz, int64_t B, int3
                             stream);
 }
 
-extern "C" int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci,
-                                int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream) {
+extern "C" int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci,
+                                  int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx, int32_t variant,
+                                  void* stream) {
   if (B < 0 || H < 1 || W < 1 || (Ci != 32 && Ci != 64) || Co < 16 || Co % 16 || KH < 1 || KW < 1 || stride < 1 ||
       KH > H || KW > W || KH % stride || KW % stride)
     return RAI_E_SHAPE;
@@ -827,6 +953,10 @@ extern "C" int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int3
   a.OW = (W - KW) / stride + 1;
   const int64_t maxcls = B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
   hipStream_t st = rai_stream(stream);
+  if (variant == 1 && Ci == 32) return launch_dgrad_lds<2, 2, 1>(a, st);  // LDS weights, 32 ci x 32 px per wave
+  if (variant == 2 && Ci == 32) return launch_dgrad_lds<2, 1, 1>(a, st);  // LDS weights, 32 ci x 16 px per wave
+  if (variant == 1 && Ci == 64) return launch_dgrad_lds<2, 1, 2>(a, st);  // LDS weights, ci halves over waves
+  if (variant == 2 && Ci == 64) return launch_dgrad_lds<4, 1, 1>(a, st);  // LDS weights, 64 ci x 16 px per wave
   if (Ci == 32) {  // 32 rows: four column blocks per wave
     const int64_t gx = (maxcls + 255) / 256;
     hipLaunchKernelGGL((conv_dgrad_kernel<2, 4>), dim3((unsigned)gx, (unsigned)(stride * stride)), dim3(CV_THREADS),
@@ -838,4 +968,9 @@ extern "C" int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int3
   }
   RAI_LAUNCH_CHECK();
   return RAI_OK;
+}
+
+extern "C" int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci,
+                                int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream) {
+  return rai_conv2d_dgrad_v(dz, w, B, H, W, Ci, Co, KH, KW, stride, dx, 0, stream);
 }

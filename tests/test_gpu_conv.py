@@ -222,7 +222,8 @@ DGRAD_CASES = [  # (Ci, H, Co, k, stride): NatureCNN conv2 / conv3, odd sizes, a
 
 @pytest.mark.parametrize("case", DGRAD_CASES, ids=lambda c: "x".join(str(v) for v in c))
 @pytest.mark.parametrize("B", [1, 3, 64])
-def test_conv_dgrad_matches_fp64(case, B):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_conv_dgrad_matches_fp64(case, B, variant):
     Ci, H, Co, k, s = case
     x, w, _ = _inputs(B, Ci, H, Co, k, seed=B + 31)
     OH = (H - k) // s + 1
@@ -230,8 +231,8 @@ def test_conv_dgrad_matches_fp64(case, B):
     dzd = dz.to(DEV).contiguous(memory_format=torch.channels_last)
     wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
     dx = torch.full((B, Ci, H, H), float("nan"), device=DEV).contiguous(memory_format=torch.channels_last)
-    _lib.check(_lib.lib().rai_conv2d_dgrad(dzd.data_ptr(), wd.data_ptr(), B, H, H, Ci, Co, k, k, s, dx.data_ptr(),
-                                           _lib.stream_handle(DEV)), "rai_conv2d_dgrad")
+    _lib.check(_lib.lib().rai_conv2d_dgrad_v(dzd.data_ptr(), wd.data_ptr(), B, H, H, Ci, Co, k, k, s, dx.data_ptr(),
+                                             variant, _lib.stream_handle(DEV)), "rai_conv2d_dgrad")
     torch.cuda.synchronize()
     ref = torch.ops.aten.convolution_backward(dz.double(), x.double(), w.double(), None, [s, s], [0, 0], [1, 1], False,
                                               [0, 0], 1, [True, False, False])[0]

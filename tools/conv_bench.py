@@ -141,6 +141,15 @@ def main():
                     r = ref_dgrad()
                     row["dgrad_relerr"] = ((dx - r).abs().max() / r.abs().max()).item()
                     row["dgrad_us"] = round(timeit(mine_dgrad, args.reps), 2)
+                    for dv in (1, 2):
+                        def mine_dgrad_v():
+                            return L.rai_conv2d_dgrad_v(dz.data_ptr(), wt.data_ptr(), B, H, H, Ci, Co, k, k, s,
+                                                        dx.data_ptr(), dv, st)
+                        rc = mine_dgrad_v()
+                        torch.cuda.synchronize()
+                        r = ref_dgrad()
+                        row[f"dgrad_v{dv}_relerr"] = ((dx - r).abs().max() / r.abs().max()).item() if rc == 0 else rc
+                        row[f"dgrad_v{dv}_us"] = round(timeit(mine_dgrad_v, args.reps), 2) if rc == 0 else rc
                 else:
                     row["dgrad_us"] = f"rc={rc}"
             print(json.dumps(row), flush=True)
