@@ -418,15 +418,23 @@ def main():
         tf = fl / (elapsed / args.steps) / 1e12
         # traffic: L2-miss (fabric) bytes per update, 2 x FETCH_SIZE + WRITE_SIZE summed over the update's
         # kernels (tools/c3_pmc.sh + tools/c3_traffic.py; the newest profiles/r*_<config>_traffic.json)
-        upd_traffic = None
+        upd_traffic, traffic_src = None, None
         for tp in sorted((ROOT / "profiles").glob(f"r*_{args.config}_traffic.json"), reverse=True):
             td = json.loads(tp.read_text())
             if td.get("workload", "").startswith(workload):
                 upd_traffic = td.get("bytes_per_update")
+                traffic_src = tp.name + (" (" + td["contractions"] + ")" if td.get("contractions") else "")
                 break
-        roofline = {"kernel": "whole update (MIOpen / hipBLASLt contractions + HIP epilogues)", "bound": "mfma",
+        kname = "whole update (MIOpen / hipBLASLt contractions + HIP epilogues)"
+        if args.config == "pong":
+            from rl_algo_impls_amd import cnn_ops as _cnn
+            if _cnn._CONV_MFMA:
+                kname = ("whole update (hand-written MFMA convolution forward + weight gradient, MIOpen input "
+                         "gradient, hipBLASLt fc GEMMs, HIP epilogues)")
+        roofline = {"kernel": kname, "bound": "mfma",
                     "achieved": round(tf, 3), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 4),
-                    "traffic": upd_traffic, "traffic_unit": "bytes per update", "flops_per_update": fl}
+                    "traffic": upd_traffic, "traffic_source": traffic_src, "traffic_unit": "bytes per update",
+                    "flops_per_update": fl}
         roof_lat = None
     else:
         roofline = roof_gae
