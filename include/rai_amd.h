@@ -204,6 +204,7 @@ int rai_conv2d_wgrad(const float* x, const float* dz, int64_t B, int32_t H, int3
 typedef struct rai_conv2d_wgrad_job {
   const void* workspace;
   float* dw;
+  float* db; /* NULL, or (after rai_conv2d_wgrad_relu_partials) the bias gradient, Co floats, 16-B aligned */
   int64_t B;
   int32_t H, W, Ci, Co, KH, KW, stride, reserved;
 } rai_conv2d_wgrad_job;
@@ -211,6 +212,14 @@ int rai_conv2d_wgrad_partials(const float* x, const float* dz, int64_t B, int32_
                               int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
                               int64_t workspace_bytes, void* stream);
 int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_t accumulate, void* stream);
+/* The partials with the layer's bias + ReLU backward folded in, for a convolution whose dz has no other
+ * consumer (NatureCNN conv1, whose input needs no gradient): dz = y > 0 ? dy : 0 (threshold_backward on
+ * the saved output y) is formed on the fly from dy and y (both NHWC (B, OH, OW, Co)), and the bias
+ * gradient's per-split partials are written after the weight tiles; the job's db receives their sum
+ * in the reduce.  Replaces rai_bias_relu_bwd + rai_conv2d_wgrad_partials for that layer. */
+int rai_conv2d_wgrad_relu_partials(const float* dy, const float* y, const float* x, int64_t B, int32_t H, int32_t W,
+                                   int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
+                                   int64_t workspace_bytes, void* stream);
 /* Input gradient of the same convolution (Conv2d's autograd dx; NatureCNN conv2 / conv3): dx (B, H, W, Ci)
  * NHWC = the transposed convolution of dz (B, OH, OW, Co) NHWC with w (Co, KH, KW, Ci) channels_last,
  * every element written (no accumulate, no zero-fill).  Ci 32 or 64, Co % 16 == 0, KH and KW multiples

@@ -179,6 +179,7 @@ _SIGNATURES = {
     "rai_conv2d_wgrad_v": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _i32, _vp, _i64, _i32, _i32, _vp]),
     "rai_conv2d_wgrad_partials": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _i64, _vp]),
     "rai_conv2d_wgrad_reduce": (C.c_int, [_vp, _i32, _i32, _vp]),
+    "rai_conv2d_wgrad_relu_partials": (C.c_int, [_vp, _vp, _vp, _i64] + [_i32] * 7 + [_vp, _i64, _vp]),
     "rai_conv2d_dgrad": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _vp]),
     "rai_conv2d_dgrad_v": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _i32, _vp]),
     "rai_bias_relu_bwd_nchw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),

@@ -70,7 +70,7 @@ def direct_grads(enabled: bool = True):
 
 class _WgradJob(C.Structure):
     """rai_conv2d_wgrad_job (include/rai_amd.h)."""
-    _fields_ = [("workspace", C.c_void_p), ("dw", C.c_void_p), ("B", C.c_int64), ("H", C.c_int32), ("W", C.c_int32),
+    _fields_ = [("workspace", C.c_void_p), ("dw", C.c_void_p), ("db", C.c_void_p), ("B", C.c_int64), ("H", C.c_int32), ("W", C.c_int32),
                 ("Ci", C.c_int32), ("Co", C.c_int32), ("KH", C.c_int32), ("KW", C.c_int32), ("stride", C.c_int32),
                 ("reserved", C.c_int32)]
 
@@ -175,6 +175,7 @@ class _Workspaces:
 _WS = _Workspaces()
 
 _CONV_MFMA = os.environ.get("RAI_CONV_MFMA", "1") != "0"
+_CONV_FUSE_RELU_BWD = os.environ.get("RAI_CONV_FUSE_RELU_BWD", "0") == "1"
 _CONV_MFMA_DGRAD = os.environ.get("RAI_CONV_MFMA_DGRAD", "0") == "1"  # measured no faster than MIOpen (r3u)
 
 
@@ -244,17 +245,25 @@ def _conv_dgrad(x, dz, w, stride) -> torch.Tensor:
                                                [True, False, False])[0]
 
 
-def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor):
-    """rai_conv2d_wgrad_partials for this layer; returns (job, workspace) for the deferred reduction."""
+def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, y=None, db=None):
+    """rai_conv2d_wgrad_partials for this layer (with y: rai_conv2d_wgrad_relu_partials, dz being the ReLU
+    output's gradient dy, and the bias gradient reduced into db); returns (job, workspace) for the
+    deferred reduction."""
     B, Ci, H, W = (int(v) for v in x.shape)
     Co, _, KH, KW = (int(v) for v in w.shape)
     s = _pair(stride)[0]
     L = _lib.lib()
     nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, s))
     ws = _WG_WS.get(module, nb, x.device)
-    _lib.check(L.rai_conv2d_wgrad_partials(x.data_ptr(), dz.data_ptr(), B, H, W, Ci, Co, KH, KW, s, ws.data_ptr(), nb,
-                                           _lib.stream_handle(x.device)), "rai_conv2d_wgrad_partials")
-    return _WgradJob(ws.data_ptr(), grad.data_ptr(), B, H, W, Ci, Co, KH, KW, s, 0), ws
+    st = _lib.stream_handle(x.device)
+    if y is None:
+        _lib.check(L.rai_conv2d_wgrad_partials(x.data_ptr(), dz.data_ptr(), B, H, W, Ci, Co, KH, KW, s, ws.data_ptr(),
+                                               nb, st), "rai_conv2d_wgrad_partials")
+    else:
+        _lib.check(L.rai_conv2d_wgrad_relu_partials(dz.data_ptr(), y.data_ptr(), x.data_ptr(), B, H, W, Ci, Co, KH, KW,
+                                                    s, ws.data_ptr(), nb, st), "rai_conv2d_wgrad_relu_partials")
+    return _WgradJob(ws.data_ptr(), grad.data_ptr(), None if db is None else db.data_ptr(), B, H, W, Ci, Co, KH, KW,
+                     s, 0), ws
 
 
 def _conv_wgrad_mfma(module, x, dz, w, stride, out: torch.Tensor, accumulate: bool) -> None:
@@ -335,6 +344,15 @@ class ConvBiasReLU(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, b, y = ctx.saved_tensors
         stride, padding, key, direct_b, direct_w, flatten, zshape, mfma = ctx.conf
+        if (mfma and _CONV_FUSE_RELU_BWD and not ctx.needs_input_grad[0] and not flatten and direct_b and direct_w
+                and w.grad.is_contiguous(memory_format=torch.channels_last) and w.grad.data_ptr() % 16 == 0
+                and b.grad.data_ptr() % 16 == 0 and y.is_contiguous(memory_format=torch.channels_last)):
+            # the layer's dz has no consumer but the weight gradient (conv1: its input needs no gradient):
+            # the bias + ReLU backward and the bias gradient are folded into the weight-gradient partials
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, y=y, db=b.grad)
+            ctx.pending.add_wgrad(job, wsp, w)
+            return None, None, None, None, None, None, None
         ws = _WS.get(key, zshape[1], y.device)
         if flatten:
             dz, db = _bias_relu_bwd_nchw(dy.contiguous(), y, b, ws, direct_b, zshape)

@@ -297,16 +297,18 @@ constexpr int WR_MAXPX = 8192;  // pixels per split (their base offsets sit in L
 
 struct ConvWrwArgs {
   const float* x;
-  const float* dz;
-  float* part;  // [S][Co][K]
+  const float* dz;  // RB: dy, the gradient of the ReLU's output
+  const float* y;   // RB: the forward output (dz = y > 0 ? dy : 0, as threshold_backward)
+  float* part;      // [S][Co][K], then (RB) the bias-gradient partials [S][Co]
   int64_t M;    // pixels
   int64_t per;  // pixels per split
   int H, W, Ci, Co, KW, S_, OH, OW, K;
 };
 
-template <int VC, int PF>
+template <int VC, int PF, bool RB>
 __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs a) {
   constexpr int NB = VC * 4;  // 16x16 accumulator blocks per wave
+  __shared__ float dbl[RB ? 4 * 16 * VC : 1];  // RB: the waves' bias-gradient sums
   // LDS: the split's pixel -> input offset table, later reused for the cross-wave sum of the tiles
   constexpr int TAB_BYTES = WR_MAXPX * 4, RED_BYTES = 3 * NB * 64 * 16;
   __shared__ __attribute__((aligned(16))) unsigned char lds[TAB_BYTES > RED_BYTES ? TAB_BYTES : RED_BYTES];
@@ -343,11 +345,17 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
     const int lo = min(4 * q4 * wv, n_p), hi = min(lo + 4 * q4, n_p);
     const float* xc = a.x + n0 * (int64_t)a.H * a.W * a.Ci + xo;
     const float* dzc = a.dz + pbeg * a.Co + VC * li;
+    const float* yc = RB ? a.y + pbeg * a.Co + VC * li : nullptr;
     const int nst = (hi - lo + 3) >> 2;
     auto ld = [&](int st, fv& dv, f4& xv) {
       const int pl = lo + 4 * st + g;
       if (pl < hi) {
         dv = *reinterpret_cast<const fv*>(dzc + (int64_t)pl * a.Co);
+        if (RB) {
+          const fv yv = *reinterpret_cast<const fv*>(yc + (int64_t)pl * a.Co);
+#pragma unroll
+          for (int j = 0; j < VC; ++j) dv[j] = yv[j] > 0.f ? dv[j] : 0.f;
+        }
         xv = *reinterpret_cast<const f4*>(xc + xbase_l[pl]);
       } else {
         dv = fv{};
@@ -363,13 +371,26 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
     };
     fv dv[PF];
     f4 xv[PF];
+    fv dsum = fv{};  // RB: this lane's bias-gradient sum (its pixels, in step order)
 #pragma unroll
     for (int u = 0; u < PF; ++u) ld(u, dv[u], xv[u]);
     for (int st = 0; st < nst; st += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
-        if (st + u < nst) mma(dv[u], xv[u]);
+        if (st + u < nst) {
+          mma(dv[u], xv[u]);
+          if (RB) dsum += dv[u];
+        }
         if (st + u + PF < nst) ld(st + u + PF, dv[u], xv[u]);
+      }
+    }
+    if (RB) {  // the four lane groups (rows of the step), then the waves in order through LDS
+#pragma unroll
+      for (int j = 0; j < VC; ++j) {
+        float v = dsum[j];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (g == 0) dbl[(wv * 16 + li) * VC + j] = v;
       }
     }
   }
@@ -383,6 +404,16 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
   }
   __syncthreads();
   if (wv > 0) return;
+  if (RB && blockIdx.y == 0 && g == 0) {  // this split's bias-gradient partial (one k tile writes it)
+    float* dp = a.part + (int64_t)gridDim.x * a.Co * a.K + (int64_t)blockIdx.x * a.Co;
+#pragma unroll
+    for (int j = 0; j < VC; ++j) {
+      float v = dbl[li * VC + j];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) v += dbl[(q * 16 + li) * VC + j];
+      dp[VC * li + j] = v;
+    }
+  }
 #pragma unroll
   for (int q = 0; q < 3; ++q)
 #pragma unroll
@@ -412,7 +443,7 @@ struct WrwReduceJob {
   int blk0;  // first block of this job
 };
 struct WrwReduceArgs {
-  WrwReduceJob j[RAI_WGRAD_MAX_JOBS];
+  WrwReduceJob j[2 * RAI_WGRAD_MAX_JOBS];  // a layer with a bias gradient is two jobs
   int n;
   int accumulate;
 };
@@ -421,7 +452,7 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_reduce_kernel(const WrwRe
   __shared__ f4 red[16][16];
   int jb = 0;
 #pragma unroll
-  for (int q = 1; q < RAI_WGRAD_MAX_JOBS; ++q)
+  for (int q = 1; q < 2 * RAI_WGRAD_MAX_JOBS; ++q)
     if (q < a.n && (int)blockIdx.x >= a.j[q].blk0) jb = q;
   const f4* __restrict__ part = a.j[jb].part;
   f4* __restrict__ dw = a.j[jb].dw;
@@ -716,7 +747,7 @@ extern "C" int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_
     const WrwPlan p = wrw_plan(M, Co, K, t);
     mx = p.S > mx ? p.S : mx;
   }
-  return mx * Co * K * (int64_t)sizeof(float);
+  return mx * Co * (K + 1) * (int64_t)sizeof(float);  // + the bias-gradient partials (relu_partials)
 }
 
 static bool wgrad_shape_ok(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW,
@@ -729,9 +760,9 @@ static bool wgrad_shape_ok(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t 
 }
 
 // the first launch of rai_conv2d_wgrad: every workgroup's partial tile into workspace (B >= 1)
-static int wgrad_partials(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
-                          int32_t KH, int32_t KW, int32_t stride, void* workspace, int64_t workspace_bytes,
-                          int32_t target_wgs, int32_t pf, hipStream_t st) {
+static int wgrad_partials(const float* x, const float* dz, const float* y, int64_t B, int32_t H, int32_t W,
+                          int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
+                          int64_t workspace_bytes, int32_t target_wgs, int32_t pf, hipStream_t st) {
   const int64_t K = (int64_t)KH * KW * Ci;
   if (!x || !dz || !workspace) return RAI_E_NULLPTR;
   if (((uintptr_t)x | (uintptr_t)dz | (uintptr_t)workspace) & 15) return RAI_E_SHAPE;
@@ -740,6 +771,7 @@ static int wgrad_partials(const float* x, const float* dz, int64_t B, int32_t H,
   ConvWrwArgs a;
   a.x = x;
   a.dz = dz;
+  a.y = y;
   a.part = static_cast<float*>(workspace);
   a.H = H;
   a.W = W;
@@ -758,12 +790,16 @@ static int wgrad_partials(const float* x, const float* dz, int64_t B, int32_t H,
   if ((int64_t)(WR_MAXPX / (a.OH * a.OW) + 2) * H * W * Ci > 0x7fffffffLL) return RAI_E_SHAPE;
   const dim3 grid((unsigned)p.S, (unsigned)p.KT);
   if (pf <= 0) pf = 4;
-  if (p.VC == 2) {
-    if (pf == 4) hipLaunchKernelGGL((conv_wrw_kernel<2, 4>), grid, dim3(CV_THREADS), 0, st, a);
-    else hipLaunchKernelGGL((conv_wrw_kernel<2, 8>), grid, dim3(CV_THREADS), 0, st, a);
+  if (y) {  // the ReLU backward and the bias gradient fused in (rai_conv2d_wgrad_relu_partials)
+    if (((uintptr_t)y) & 15) return RAI_E_SHAPE;
+    if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true>), grid, dim3(CV_THREADS), 0, st, a);
+  } else if (p.VC == 2) {
+    if (pf == 4) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, false>), grid, dim3(CV_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((conv_wrw_kernel<2, 8, false>), grid, dim3(CV_THREADS), 0, st, a);
   } else {
-    if (pf == 4) hipLaunchKernelGGL((conv_wrw_kernel<4, 4>), grid, dim3(CV_THREADS), 0, st, a);
-    else hipLaunchKernelGGL((conv_wrw_kernel<4, 8>), grid, dim3(CV_THREADS), 0, st, a);
+    if (pf == 4) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, false>), grid, dim3(CV_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((conv_wrw_kernel<4, 8, false>), grid, dim3(CV_THREADS), 0, st, a);
   }
   RAI_LAUNCH_CHECK();
   return RAI_OK;
@@ -797,6 +833,16 @@ static int wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_
     r.S = p.S;
     r.blk0 = blocks;
     blocks += (int)((r.n4 + 15) / 16);
+    if (jb.db) {  // the bias-gradient partials of rai_conv2d_wgrad_relu_partials, after the weight tiles
+      if (((uintptr_t)jb.db) & 15) return RAI_E_SHAPE;
+      WrwReduceJob& rb = ra.j[ra.n++];
+      rb.part = reinterpret_cast<const f4*>(static_cast<const float*>(jb.workspace) + (int64_t)p.S * jb.Co * K);
+      rb.dw = reinterpret_cast<f4*>(jb.db);
+      rb.n4 = jb.Co / 4;
+      rb.S = p.S;
+      rb.blk0 = blocks;
+      blocks += (int)((rb.n4 + 15) / 16);
+    }
   }
   if (ra.n == 0) return RAI_OK;
   hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)blocks), dim3(CV_THREADS), 0, st, ra);
@@ -812,8 +858,8 @@ extern "C" int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, in
   hipStream_t st = rai_stream(stream);
   if (B > 0) {
     if (!dw) return RAI_E_NULLPTR;
-    const int rc = wgrad_partials(x, dz, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, target_wgs,
-                                  pf, st);
+    const int rc = wgrad_partials(x, dz, nullptr, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes,
+                                  target_wgs, pf, st);
     if (rc != RAI_OK) return rc;
     if (target_wgs != 0) {  // the reduce below follows the default plan: re-derive S for this one
       // (A/B only) the reduction reads the split count the partials were launched with
@@ -834,7 +880,7 @@ extern "C" int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, in
       return RAI_OK;
     }
   }
-  rai_conv2d_wgrad_job jb = {workspace, dw, B, H, W, Ci, Co, KH, KW, stride, 0};
+  rai_conv2d_wgrad_job jb = {workspace, dw, nullptr, B, H, W, Ci, Co, KH, KW, stride, 0};
   return wgrad_reduce(&jb, 1, accumulate, st);
 }
 
@@ -843,7 +889,19 @@ extern "C" int rai_conv2d_wgrad_partials(const float* x, const float* dz, int64_
                                          void* workspace, int64_t workspace_bytes, void* stream) {
   if (!wgrad_shape_ok(B, H, W, Ci, Co, KH, KW, stride)) return RAI_E_SHAPE;
   if (B == 0) return RAI_OK;
-  return wgrad_partials(x, dz, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, 0, 0, rai_stream(stream));
+  return wgrad_partials(x, dz, nullptr, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, 0, 0,
+                        rai_stream(stream));
+}
+
+extern "C" int rai_conv2d_wgrad_relu_partials(const float* dy, const float* y, const float* x, int64_t B, int32_t H,
+                                              int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW,
+                                              int32_t stride, void* workspace, int64_t workspace_bytes,
+                                              void* stream) {
+  if (!wgrad_shape_ok(B, H, W, Ci, Co, KH, KW, stride)) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!y) return RAI_E_NULLPTR;
+  return wgrad_partials(x, dy, y, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, 0, 0,
+                        rai_stream(stream));
 }
 
 extern "C" int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_t accumulate,

@@ -201,7 +201,7 @@ def test_conv_wgrad_partials_and_one_reduce_for_three_layers():
         ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
         _lib.check(L.rai_conv2d_wgrad_partials(xd.data_ptr(), dzd.data_ptr(), 32, H, H, Ci, Co, k, k, s,
                                                ws.data_ptr(), nb, st), "partials")
-        jobs.append(_WgradJob(ws.data_ptr(), g.data_ptr(), 32, H, H, Ci, Co, k, k, s, 0))
+        jobs.append(_WgradJob(ws.data_ptr(), g.data_ptr(), None, 32, H, H, Ci, Co, k, k, s, 0))
         keep += [xd, dzd, ws]
         outs.append(g)
     arr = (_WgradJob * 3)(*jobs)
@@ -242,3 +242,37 @@ def test_conv_dgrad_matches_fp64(case, B, variant):
     assert torch.isfinite(got).all()
     tol = (Co * k * k + 2) * 2.0 ** -24 * bound + 1e-30
     assert ((got - ref).abs() <= tol).all(), float(((got - ref).abs() / tol).max())
+
+
+@pytest.mark.parametrize("case", [(4, 84, 32, 8, 4), (32, 20, 64, 4, 2)], ids=["conv1", "conv2"])
+def test_conv_wgrad_relu_partials_fold_the_relu_backward_and_bias_gradient(case):
+    """rai_conv2d_wgrad_relu_partials + the reduce: dW and db of dz = (y > 0 ? dy : 0) from dy and the
+    saved output y, accumulated into existing gradients -- against fp64 (bound as above) and, for dW,
+    bit-identical to rai_conv2d_wgrad on the materialized dz."""
+    from rl_algo_impls_amd.cnn_ops import _WgradJob
+    Ci, H, Co, k, s = case
+    B = 24
+    x, w, _ = _inputs(B, Ci, H, Co, k, seed=77)
+    OH = (H - k) // s + 1
+    gen = torch.Generator().manual_seed(5)
+    dy = torch.randn(B, Co, OH, OH, generator=gen)
+    y = torch.relu(torch.randn(B, Co, OH, OH, generator=gen))  # zeros where the ReLU clipped
+    dz = torch.where(y > 0, dy, torch.zeros_like(dy))
+    w0 = torch.randn(Co, Ci, k, k, generator=gen)
+    b0 = torch.randn(Co, generator=gen)
+    L = _lib.lib()
+    st = _lib.stream_handle(DEV)
+    cl = lambda t: t.to(DEV).contiguous(memory_format=torch.channels_last)
+    xd, dyd, yd, gw = cl(x), cl(dy), cl(y), cl(w0)
+    gb = b0.to(DEV).clone()
+    nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, H, Ci, Co, k, k, s))
+    ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    _lib.check(L.rai_conv2d_wgrad_relu_partials(dyd.data_ptr(), yd.data_ptr(), xd.data_ptr(), B, H, H, Ci, Co, k, k,
+                                                s, ws.data_ptr(), nb, st), "relu_partials")
+    job = (_WgradJob * 1)(_WgradJob(ws.data_ptr(), gw.data_ptr(), gb.data_ptr(), B, H, H, Ci, Co, k, k, s, 0))
+    _lib.check(L.rai_conv2d_wgrad_reduce(C.cast(job, C.c_void_p), 1, 1, st), "reduce")
+    torch.cuda.synchronize()
+    assert torch.equal(gw.cpu(), _wgrad(x, dz, k, k, s, dw0=w0))
+    db_ref = b0.double() + dz.double().sum(dim=(0, 2, 3))
+    bound = b0.double().abs() + dz.double().abs().sum(dim=(0, 2, 3))
+    assert ((gb.cpu().double() - db_ref).abs() <= (B * OH * OH + 2) * 2.0 ** -24 * bound).all()
