@@ -243,6 +243,18 @@ def main():
     if os.environ.get("RAI_CUDNN_BENCHMARK") is not None:
         cudnn_benchmark = os.environ["RAI_CUDNN_BENCHMARK"] == "1"
     torch.backends.cudnn.benchmark = bool(cudnn_benchmark) and not args.deterministic
+    # GEMM library A/B for the torch GEMMs left in the CNN configs (the fc layer): RAI_BLAS_ROCBLAS=1 routes
+    # them to rocBLAS, RAI_TUNABLEOP=1 lets PyTorch's TunableOp time hipBLASLt / rocBLAS solutions per shape
+    if os.environ.get("RAI_BLAS_ROCBLAS") == "1":
+        torch.backends.cuda.preferred_blas_library("cublas")  # = rocBLAS on ROCm
+    # TunableOp is on by default for C3 (its fc GEMMs: 147.2k -> 152.7-153.5k env-steps/s same box,
+    # profiles/r3zb_c3_blas_ab.txt; rocBLAS alone 151k); off in deterministic mode (it picks by timing)
+    tunableop = os.environ.get("RAI_TUNABLEOP", "1" if args.config == "pong" else "0") == "1" and not args.deterministic
+    if tunableop:
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_max_tuning_duration(20)
+        torch.cuda.tunable.set_filename(os.path.join(os.environ.get("TMPDIR", "/tmp"), "rai_tunableop_results%d.csv"))
 
     cfg = CONFIGS[args.config]
     N, T = (args.num_envs or cfg["num_envs"]), cfg["n_steps"]
@@ -466,6 +478,7 @@ def main():
                        "n_epochs": algo_kw["n_epochs"], "batch_policy": args.batch_policy, "seq_len": T,
                        "deterministic": bool(args.deterministic),
                        "miopen_find_mode": bool(torch.backends.cudnn.benchmark),
+                       "gemm_tunableop": bool(tunableop),
                        "parallelism": f"dp{world}"},
             "roofline": roofline,
             "roofline_latency": roof_lat,
