@@ -25,6 +25,9 @@
 // float4 and issues 4 * TCO * TPX MFMAs.  Operands are read straight from global memory (L1/L2:
 // the weights are shared by every workgroup, overlapping receptive fields re-read the same lines),
 // two quads in flight per wave.
+#include <mutex>
+#include <unordered_set>
+
 #include "common.h"
 
 namespace {
@@ -134,6 +137,22 @@ __global__ __launch_bounds__(CV_THREADS) void conv_fwd_kernel(const ConvFwdArgs 
       }
     }
   }
+}
+
+// Raise a kernel's dynamic-LDS limit to the 160 KB of a CU (minus its static LDS) once per kernel (a host call; not repeated per
+// launch, so a graph-captured or eager step pays it only on its first launch).
+static int allow_lds(const void* kernel) {
+  static std::mutex mu;
+  static std::unordered_set<const void*> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count(kernel)) return RAI_OK;
+  hipFuncAttributes fa;
+  hipError_t e = hipFuncGetAttributes(&fa, kernel);
+  if (e != hipSuccess) return (int)e;
+  e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)fa.sharedSizeBytes);
+  if (e != hipSuccess) return (int)e;
+  done.insert(kernel);
+  return RAI_OK;
 }
 
 // The same forward with the workgroup's weight rows resident in LDS: a persistent workgroup (8 waves,
@@ -251,15 +270,13 @@ int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   const dim3 grid((unsigned)gx, (unsigned)cot);
   if (nchw) {
     auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF>;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
+    const int e = allow_lds(reinterpret_cast<const void*>(k));
+    if (e != RAI_OK) return e;
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
   } else {
     auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, false, PF>;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
+    const int e = allow_lds(reinterpret_cast<const void*>(k));
+    if (e != RAI_OK) return e;
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
   }
   RAI_LAUNCH_CHECK();
@@ -726,9 +743,8 @@ int launch_dgrad_lds(const ConvDgradArgs& a, hipStream_t st) {
   const int64_t nitems = (a.B * Hc0 * Wc0 + PXT - 1) / PXT * a.S * a.S;
   const int64_t gx = nitems < 256 ? nitems : 256;
   auto k = conv_dgrad_lds_kernel<VC, TQ, WCI>;
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return (int)e;
+  const int e = allow_lds(reinterpret_cast<const void*>(k));
+  if (e != RAI_OK) return e;
   hipLaunchKernelGGL(k, dim3((unsigned)gx), dim3(512), lds, st, a);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
