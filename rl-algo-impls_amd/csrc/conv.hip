@@ -26,6 +26,7 @@
 // the weights are shared by every workgroup, overlapping receptive fields re-read the same lines),
 // two quads in flight per wave.
 #include <mutex>
+#include <unordered_map>
 #include <unordered_set>
 
 #include "common.h"
@@ -137,6 +138,21 @@ __global__ __launch_bounds__(CV_THREADS) void conv_fwd_kernel(const ConvFwdArgs 
       }
     }
   }
+}
+
+// Compute units of the current device (256 on MI355X), queried once per device.
+static int num_cus() {
+  static std::mutex mu;
+  static std::unordered_map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+  cache[dev] = n;
+  return n;
 }
 
 // Raise a kernel's dynamic-LDS limit to the 160 KB of a CU (minus its static LDS) once per kernel (a host call; not repeated per
@@ -264,7 +280,7 @@ int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   if (lds + CV_MAXCHUNK * 4 > 160 * 1024) return RAI_E_SHAPE;
   const int64_t ntiles = (a.M + PXT - 1) / PXT;
   const int64_t cot = a.Co / COT;
-  int64_t gx = 256 / cot;  // one persistent workgroup per CU
+  int64_t gx = num_cus() / cot;  // one persistent workgroup per CU
   if (gx > ntiles) gx = ntiles;
   if (gx < 1) gx = 1;
   const dim3 grid((unsigned)gx, (unsigned)cot);
@@ -741,7 +757,7 @@ int launch_dgrad_lds(const ConvDgradArgs& a, hipStream_t st) {
   constexpr int PXT = 16 * TQ * (8 / WCI);
   const int64_t Hc0 = (a.H + a.S - 1) / a.S, Wc0 = (a.W + a.S - 1) / a.S;
   const int64_t nitems = (a.B * Hc0 * Wc0 + PXT - 1) / PXT * a.S * a.S;
-  const int64_t gx = nitems < 256 ? nitems : 256;
+  const int64_t gx = nitems < num_cus() ? nitems : num_cus();
   auto k = conv_dgrad_lds_kernel<VC, TQ, WCI>;
   const int e = allow_lds(reinterpret_cast<const void*>(k));
   if (e != RAI_OK) return e;
