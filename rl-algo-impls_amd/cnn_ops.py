@@ -175,6 +175,7 @@ class _Workspaces:
 _WS = _Workspaces()
 
 _CONV_MFMA = os.environ.get("RAI_CONV_MFMA", "1") != "0"
+_FC_ADDMM_RELU = os.environ.get("RAI_FC_ADDMM_RELU", "0") == "1"
 _CONV_FUSE_RELU_BWD = os.environ.get("RAI_CONV_FUSE_RELU_BWD", "1") != "0"  # +0.45 % C3 (r3z)
 _CONV_MFMA_DGRAD = os.environ.get("RAI_CONV_MFMA_DGRAD", "0") == "1"  # measured no faster than MIOpen (r3u)
 
@@ -391,8 +392,12 @@ class LinearBiasReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, key):
-        z = torch.mm(x, w.t())
-        y = _bias_relu_fwd(z, b)
+        if _FC_ADDMM_RELU:
+            # the GEMM library's bias + ReLU epilogue (hipBLASLt; F.linear's addmm(b, x, W^T) then relu)
+            y = torch._addmm_activation(b, x, w.t(), use_gelu=False)
+        else:
+            z = torch.mm(x, w.t())
+            y = _bias_relu_fwd(z, b)
         ctx.save_for_backward(x, w, b, y)
         ctx.conf = (key, _direct(b, raw=True), _direct(w))
         return y
