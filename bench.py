@@ -6,7 +6,8 @@ steps on the seeded synthetic CartPole-shaped VecEnv (host), GAE on device, and
 n_epochs x minibatches of fused loss / backward / clip+Adam — exactly the region
 the reference times as train/steps_per_second (rl_algo_impls/ppo/ppo.py:221,422-427).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config cartpole|pong|halfcheetah|microrts]
+    python bench.py [--gpus N --steps K --warmup W]   (N > 1: the N ranks are started here unless a
+                                                       launcher such as torch.distributed.run already did) [--config cartpole|pong|halfcheetah|microrts]
                     [--batch-policy yaml|scaled] [--env-partition split|per-rank] [--dp-batch global|per-rank]
 
 Multi-GPU: one process per GPU (torch.distributed.run).  Default = SURVEY.md 8(d)/8(e): the config's
@@ -199,8 +200,50 @@ def _diagnostics(tag: str) -> None:
     print(f"[bench] diag: {tag} pid {os.getpid()}", file=sys.stderr, flush=True)
 
 
+def self_launch(args) -> int | None:
+    """`bench.py --gpus N` (N > 1) run without a launcher: start the N ranks here, one child process
+    per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (what torch.distributed.run exports), wait
+    for all of them and return the job's exit status.  Rank 0's JSON line is the job's output.  Runs
+    before anything touches the GPU, and starts the ranks as children (no exec).  Returns None when this
+    process already is a rank (a launcher set WORLD_SIZE) or N == 1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        if args.gpus > 1 and int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']}")
+        return None
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=os.environ.get("MASTER_PORT", str(port)))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    status = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            rc = p.poll()
+            if rc is None:
+                continue
+            pending.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in pending:  # a failed rank leaves the others waiting in a collective: stop them
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return status
+
+
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     _diagnostics("start")
     import numpy as np
     import torch
@@ -235,7 +278,15 @@ def main():
     _lib.lib()
     from rl_algo_impls_amd.running_utils import set_device_optimizations
 
+    # TunableOp for the torch library GEMMs (C3's fc layer) is the trainer's own setting: on whenever
+    # deterministic mode is off (running_utils.set_gemm_tuning, called by set_device_optimizations;
+    # RAI_TUNABLEOP=0 turns it off).  The bench points its results file at this run's TMPDIR, so every
+    # bench run tunes in its warm-up update instead of inheriting an earlier run's picks
+    os.environ.setdefault("RAI_TUNABLEOP_FILE", os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                                             f"rai_bench_{os.getpid()}_tunableop%d.csv"))
+
     set_device_optimizations(dev, use_deterministic_algorithms=bool(args.deterministic))
+    tunableop = torch.cuda.tunable.is_enabled()
     # MIOpen find mode for the CNN convolutions (C3 / C5): every candidate solver timed at the first call
     # of each problem, the fastest kept.  Measured C3: 1.10 s per update against 1.26 s with the default
     # immediate-mode choice (profiles/r2o_pong_find_mode_bench_line.json vs r2l)
@@ -247,14 +298,6 @@ def main():
     # them to rocBLAS, RAI_TUNABLEOP=1 lets PyTorch's TunableOp time hipBLASLt / rocBLAS solutions per shape
     if os.environ.get("RAI_BLAS_ROCBLAS") == "1":
         torch.backends.cuda.preferred_blas_library("cublas")  # = rocBLAS on ROCm
-    # TunableOp is on by default for C3 (its fc GEMMs: 147.2k -> 152.7-153.5k env-steps/s same box,
-    # profiles/r3zb_c3_blas_ab.txt; rocBLAS alone 151k); off in deterministic mode (it picks by timing)
-    tunableop = os.environ.get("RAI_TUNABLEOP", "1" if args.config == "pong" else "0") == "1" and not args.deterministic
-    if tunableop:
-        torch.cuda.tunable.enable(True)
-        torch.cuda.tunable.tuning_enable(True)
-        torch.cuda.tunable.set_max_tuning_duration(20)
-        torch.cuda.tunable.set_filename(os.path.join(os.environ.get("TMPDIR", "/tmp"), "rai_tunableop_results%d.csv"))
 
     cfg = CONFIGS[args.config]
     N, T = (args.num_envs or cfg["num_envs"]), cfg["n_steps"]
@@ -279,7 +322,10 @@ def main():
         with torch.no_grad():
             for p in policy.parameters():
                 torch.distributed.broadcast(p.data, 0)
-    gen = SyncStepRolloutGenerator(policy, env, n_steps=T, seed=1234 + rank)
+    # the reference runner's rollout kwargs: the policy's subaction_mask goes to the generator too
+    # (rl_algo_impls/runner/train.py:159-162), where it gates Batch.num_actions
+    rollout_kw = {"subaction_mask": cfg["policy"]["subaction_mask"]} if "subaction_mask" in cfg["policy"] else {}
+    gen = SyncStepRolloutGenerator(policy, env, n_steps=T, seed=1234 + rank, **rollout_kw)
     algo = PPO(policy, dev, None, **algo_kw)
     if world > 1 or args.dp_rehearsal:  # minibatch rule: one for every config, named in the JSON line
         algo.enable_data_parallel(dp_batch=args.dp_batch)

@@ -124,6 +124,20 @@ int rai_gridnet_backward(const float* logits, const uint8_t* mask, const int64_t
 int rai_gridnet_sample(const float* logits, const uint8_t* mask, int64_t B, int32_t C, int32_t G,
                        const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val, uint64_t seed,
                        uint64_t offset, int64_t* actions_out, float* logp_out, void* stream);
+/* Batch.num_actions of a GridNet rollout: rl_algo_impls/rollout/rollout.py:158-180
+ * (per_position_num_actions, via num_actions :130-155 from VecRollout.__init__,
+ * rl_algo_impls/rollout/vec_rollout.py:69-76).  For each of the B = T*N rows:
+ *   per_group = 0 (no subaction_mask): out[b] = #cells whose A mask bytes hold any 1
+ *                                      (np.sum(np.any(mask, -1), -1));
+ *   per_group = 1: out[b] = sum over cells and groups g of any(mask[cell, group g]), group g
+ *                  counted only where actions[b, cell, sub_ref[g]] == sub_val[g] (the
+ *                  ValueDependentMask gate; sub_ref[g] = -1: always counted).
+ * mask (B, C, A) u8/bool; actions (B, C, G) int64 (read only when per_group and a gate exists;
+ * may be NULL otherwise).  out (B,) int32 when out_bytes == 4 (the reference's dtype with a
+ * subaction mask), int64 when 8 (without).  Exact integer counts. */
+int rai_gridnet_num_actions(const uint8_t* mask, const int64_t* actions, int64_t B, int32_t C, int32_t G,
+                            const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val,
+                            int32_t per_group, int32_t out_bytes, void* out, void* stream);
 
 /* --------------------------------------------------------------------------
  * Squeeze-excitation residual epilogue of the squeeze-U-Net backbone (config C5):

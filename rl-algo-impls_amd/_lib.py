@@ -149,6 +149,7 @@ _SIGNATURES = {
     "rai_bias_gelu_bwd": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     "rai_gridnet_sample": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                      _vp]),
+    "rai_gridnet_num_actions": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp]),
     "rai_mlp_wide_workspace_bytes": (_i64, [_i64, _i32]),
     "rai_mlp_wide_forward": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "rai_mlp_wide_forward_loss": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

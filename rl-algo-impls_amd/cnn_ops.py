@@ -113,9 +113,15 @@ class _PendingGrads:
         if self.closed:
             _reduce_wgrad_jobs([(job, ws, w)], ws.device)
             return
-        if any(ws is other for _j, other, _w in self.jobs):  # the layer's workspace is about to be reused
-            self.flush_jobs()
+        assert not any(ws is other for _j, other, _w in self.jobs), "reserve(ws) before writing its partials"
         self.jobs.append((job, ws, w))
+
+    def reserve(self, ws: torch.Tensor) -> None:
+        """Called BEFORE a weight-gradient partials launch writes `ws`: a job still pending on that
+        workspace (the same layer run twice in one backward) is reduced first, while its partials are
+        intact (stream order puts that reduction ahead of the overwrite)."""
+        if not self.closed and any(ws is other for _j, other, _w in self.jobs):
+            self.flush_jobs()
 
     def flush_jobs(self) -> None:
         jobs, self.jobs = self.jobs, []
@@ -210,7 +216,10 @@ def _mfma_conv_ok(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride, pad
     if not _CONV_MFMA or tuple(_pair(padding)) != (0, 0):
         return False
     Co, Ci, KH, KW = (int(v) for v in w.shape)
-    return (x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+    # operand shapes must agree (the kernels take Ci, H, W from x): mismatches go to F.conv2d, which raises
+    if x.dim() != 4 or int(x.shape[1]) != Ci or int(x.shape[2]) < KH or int(x.shape[3]) < KW:
+        return False
+    return (x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
             and w.is_contiguous(memory_format=torch.channels_last) and Ci % 4 == 0 and Co in (32, 64)
             and (KH * KW * Ci) % 64 == 0 and KH * KW * Ci <= 8192 and b.is_contiguous()
             and all(t.data_ptr() % 16 == 0 for t in (x, w, b)))
@@ -246,16 +255,17 @@ def _conv_dgrad(x, dz, w, stride) -> torch.Tensor:
                                                [True, False, False])[0]
 
 
-def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, y=None, db=None):
+def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, pending: "_PendingGrads", y=None, db=None):
     """rai_conv2d_wgrad_partials for this layer (with y: rai_conv2d_wgrad_relu_partials, dz being the ReLU
     output's gradient dy, and the bias gradient reduced into db); returns (job, workspace) for the
-    deferred reduction."""
+    deferred reduction.  A reduction still pending on the layer's workspace runs first (pending.reserve)."""
     B, Ci, H, W = (int(v) for v in x.shape)
     Co, _, KH, KW = (int(v) for v in w.shape)
     s = _pair(stride)[0]
     L = _lib.lib()
     nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, s))
     ws = _WG_WS.get(module, nb, x.device)
+    pending.reserve(ws)
     st = _lib.stream_handle(x.device)
     if y is None:
         _lib.check(L.rai_conv2d_wgrad_partials(x.data_ptr(), dz.data_ptr(), B, H, W, Ci, Co, KH, KW, s, ws.data_ptr(),
@@ -351,7 +361,7 @@ class ConvBiasReLU(torch.autograd.Function):
             # the layer's dz has no consumer but the weight gradient (conv1: its input needs no gradient):
             # the bias + ReLU backward and the bias gradient are folded into the weight-gradient partials
             dy = dy.contiguous(memory_format=torch.channels_last)
-            job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, y=y, db=b.grad)
+            job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, ctx.pending, y=y, db=b.grad)
             ctx.pending.add_wgrad(job, wsp, w)
             return None, None, None, None, None, None, None
         ws = _WS.get(key, zshape[1], y.device)
@@ -369,7 +379,7 @@ class ConvBiasReLU(torch.autograd.Function):
             if (direct_w and g.is_contiguous(memory_format=torch.channels_last) and g.data_ptr() % 16 == 0):
                 # partial tiles now; their reduction into the flat .grad joins the other layers' in one
                 # launch at direct_grads() exit
-                job, ws = _conv_wgrad_partials(key, x, dz, w, stride, g)
+                job, ws = _conv_wgrad_partials(key, x, dz, w, stride, g, ctx.pending)
                 ctx.pending.add_wgrad(job, ws, w)
                 dw = None
             else:

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(GN_THREADS) void gridnet_sample_kernel(const GridAr
 }
 
 int setup(GridArgs& a, const float* logits, const uint8_t* mask, const int64_t* actions, int64_t B, int32_t C,
-          int32_t G, const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val) {
+          int32_t G, const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val, bool need_logits = true) {
   if (B < 0 || C < 1 || G < 1) return RAI_E_SHAPE;
   if (G > RAI_GRID_MAX_G) return RAI_E_UNSUPPORTED;
   if (!nvec) return RAI_E_NULLPTR;
@@ -318,7 +318,7 @@ int setup(GridArgs& a, const float* logits, const uint8_t* mask, const int64_t* 
   if (A > RAI_GRID_MAX_A) return RAI_E_UNSUPPORTED;
   a.off[G] = A;
   a.A = A;
-  if (B > 0 && (!logits || !mask)) return RAI_E_NULLPTR;
+  if (B > 0 && ((need_logits && !logits) || !mask)) return RAI_E_NULLPTR;
   return RAI_OK;
 }
 
@@ -376,6 +376,86 @@ extern "C" int rai_gridnet_sample(const float* logits, const uint8_t* mask, int6
   a.offset = offset;
   hipLaunchKernelGGL(gridnet_sample_kernel, dim3((unsigned)B), dim3(GN_THREADS), smem_bytes(a.A),
                      rai_stream(stream), a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+// ---- Batch.num_actions (rl_algo_impls/rollout/rollout.py:158-180) ------------------------------
+// HBM-bound byte work: one 256-thread workgroup per row b streams the row's C*A mask bytes through
+// LDS in tiles of NA_CELLS cells (dword loads when the row is 4-B aligned), then one thread per cell
+// scans its A bytes group by group.  C5: 256 cells x 78 B = 19,968 B per row, 262,144 rows.
+namespace {
+constexpr int NA_THREADS = 256;
+constexpr int NA_CELLS = 256;
+
+__global__ void __launch_bounds__(NA_THREADS) gridnet_num_actions_kernel(GridArgs a, int per_group, int out_bytes,
+                                                                         void* out) {
+  extern __shared__ uint8_t na_tile[];
+  __shared__ int na_part[NA_THREADS / RAI_WAVE];
+  const int64_t b = blockIdx.x;
+  const int A = a.A, C = a.C, G = a.G;
+  const uint8_t* row = a.mask + b * (int64_t)C * A;
+  const bool dw = ((reinterpret_cast<uintptr_t>(row) | (uintptr_t)((int64_t)C * A)) & 3) == 0;
+  int count = 0;
+  for (int c0 = 0; c0 < C; c0 += NA_CELLS) {
+    const int nc = min(NA_CELLS, C - c0);
+    const int nbytes = nc * A;
+    const uint8_t* src = row + (int64_t)c0 * A;
+    __syncthreads();
+    if (dw && (nbytes & 3) == 0) {
+      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+      uint32_t* d4 = reinterpret_cast<uint32_t*>(na_tile);
+      for (int i = threadIdx.x; i < nbytes / 4; i += NA_THREADS) d4[i] = __builtin_nontemporal_load(s4 + i);
+    } else {
+      for (int i = threadIdx.x; i < nbytes; i += NA_THREADS) na_tile[i] = src[i];
+    }
+    __syncthreads();
+    for (int cl = threadIdx.x; cl < nc; cl += NA_THREADS) {
+      const uint8_t* m = na_tile + cl * A;
+      if (!per_group) {
+        int any = 0;
+        for (int j = 0; j < A; ++j) any |= m[j];
+        count += any != 0;
+      } else {
+        const int64_t* act = a.actions ? a.actions + (b * C + c0 + cl) * G : nullptr;
+        for (int g = 0; g < G; ++g) {
+          int any = 0;
+          for (int j = a.off[g]; j < a.off[g + 1]; ++j) any |= m[j];
+          const int r = a.sub_ref[g];
+          const bool gate = r < 0 || act[r] == (int64_t)a.sub_val[g];
+          count += (any != 0) && gate;
+        }
+      }
+    }
+  }
+  // fixed-order block sum (integers: any order is exact)
+  for (int o = RAI_WAVE / 2; o > 0; o >>= 1) count += __shfl_xor(count, o);
+  if ((threadIdx.x & (RAI_WAVE - 1)) == 0) na_part[threadIdx.x / RAI_WAVE] = count;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int w = 0; w < NA_THREADS / RAI_WAVE; ++w) tot += na_part[w];
+    if (out_bytes == 8) static_cast<int64_t*>(out)[b] = tot;
+    else static_cast<int32_t*>(out)[b] = tot;
+  }
+}
+}  // namespace
+
+extern "C" int rai_gridnet_num_actions(const uint8_t* mask, const int64_t* actions, int64_t B, int32_t C, int32_t G,
+                                       const int32_t* nvec, const int32_t* sub_ref, const int32_t* sub_val,
+                                       int32_t per_group, int32_t out_bytes, void* out, void* stream) {
+  GridArgs a;
+  int rc = setup(a, nullptr, mask, actions, B, C, G, nvec, per_group ? sub_ref : nullptr, sub_val, false);
+  if (rc != RAI_OK) return rc;
+  if (out_bytes != 4 && out_bytes != 8) return RAI_E_SHAPE;
+  if (B > 0x7fffffff) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!out) return RAI_E_NULLPTR;
+  bool gated = false;
+  for (int g = 0; g < G; ++g) gated |= a.sub_ref[g] >= 0;
+  if (per_group && gated && !actions) return RAI_E_NULLPTR;
+  hipLaunchKernelGGL(gridnet_num_actions_kernel, dim3((unsigned)B), dim3(NA_THREADS), (size_t)NA_CELLS * a.A,
+                     rai_stream(stream), a, (int)per_group, (int)out_bytes, out);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

@@ -68,6 +68,32 @@ def _u8(m: torch.Tensor) -> torch.Tensor:
     return m.view(torch.uint8) if m.dtype == torch.bool else m.to(torch.uint8)
 
 
+def gridnet_num_actions(actions: torch.Tensor, action_masks: torch.Tensor, action_vec,
+                        subaction_mask: Optional[Dict[int, ValueDependentMask]]) -> torch.Tensor:
+    """Batch.num_actions of a GridNet rollout, rl_algo_impls/rollout/rollout.py:158-180
+    (per_position_num_actions): actions (..., C, G) int64, action_masks (..., C, A) bool -> (...,)
+    counts, one launch (rai_gridnet_num_actions).  Without a subaction mask: cells with any valid
+    action, int64 (np.sum of a bool array; actions may be None); with one: valid groups per cell, each gated by its
+    ValueDependentMask, int32 (the reference's np.zeros(..., dtype=np.int32) accumulator)."""
+    _lib.require_device(actions, action_masks)
+    per_group = bool(subaction_mask)
+    spec = _Spec(action_vec if per_group else [int(action_masks.shape[-1])], subaction_mask)
+    lead = tuple(action_masks.shape[:-2])
+    Cc, A = int(action_masks.shape[-2]), int(action_masks.shape[-1])
+    if A != spec.A or (per_group and (tuple(actions.shape[:-1]) != lead + (Cc,) or int(actions.shape[-1]) != spec.G)):
+        raise AssertionError(f"num_actions: actions {None if actions is None else tuple(actions.shape)} / masks "
+                             f"{tuple(action_masks.shape)} do not match nvec {np.asarray(action_vec).tolist()}")
+    out = torch.empty(lead, dtype=torch.int32 if per_group else torch.int64, device=action_masks.device)
+    m = _u8(action_masks)
+    act = actions.contiguous() if per_group else None  # the plain count never reads the actions
+    nv, sr, sv = spec.ptrs()
+    rc = _lib.lib().rai_gridnet_num_actions(m.data_ptr(), _lib.ptr(act), int(out.numel()), Cc, spec.G, nv, sr, sv,
+                                            int(per_group), out.element_size(), out.data_ptr(),
+                                            _lib.stream_handle(m.device))
+    _lib.check(rc, "rai_gridnet_num_actions")
+    return out
+
+
 class GridnetLogpEntropy(torch.autograd.Function):
     """(logits (B, C, A), masks (B, C, A), actions (B, C, G) | None) -> (logp (B,), entropy (B,))."""
 

@@ -100,7 +100,7 @@ class PPO:
 
     # -- data parallel (one process per GPU) ------------------------------------------------
     def enable_data_parallel(self, group=None, native_dp: bool = True, xdp: Optional[bool] = None,
-                             dp_batch: str = "per-rank") -> None:
+                             dp_batch: str = "global") -> None:
         """Data parallelism: every rank owns its own env group and HBM rollout; a global
         minibatch is the union of the ranks' minibatch slices, gradients are summed over ranks
         with one all-reduce per optimizer step (RCCL over xGMI via torch.distributed, or the

@@ -128,6 +128,23 @@ def gather_rows(srcs: List[torch.Tensor], dsts: List[torch.Tensor], idx: torch.T
     _lib.check(rc, "rai_gather_rows")
 
 
+def _num_actions(actions: torch.Tensor, action_masks: torch.Tensor, subaction_mask, action_plane_space):
+    """rl_algo_impls/rollout/rollout.py:130-180 for per-position (GridNet) masks: (T, N) counts
+    (gridnet.gridnet_num_actions).  subaction_mask is the YAML's {reference index: {index: value}}
+    (ValueDependentMask.from_reference_index_to_index_to_value, vec_rollout.py:72-74)."""
+    from .gridnet import ValueDependentMask, gridnet_num_actions
+
+    if isinstance(action_masks, dict):
+        raise NotImplementedError("pick_position (Lux) action masks are outside the hot path")
+    if action_masks.dim() < 4:
+        raise NotImplementedError("num_actions of flat (non-GridNet) action masks is outside the hot path")
+    sub = ValueDependentMask.from_reference_index_to_index_to_value(subaction_mask) if subaction_mask else None
+    if not sub:  # any over each cell's whole mask, the plane split unused (rollout.py:164-165)
+        return gridnet_num_actions(None, action_masks, None, None)
+    assert action_plane_space  # rollout.py:166
+    return gridnet_num_actions(actions, action_masks, np.asarray(action_plane_space.nvec), sub)
+
+
 class DeviceRollout(Rollout):
     """VecRollout equivalent over HBM-resident (T, N, ...) tensors."""
 
@@ -137,7 +154,8 @@ class DeviceRollout(Rollout):
                  action_masks: Optional[torch.Tensor], gamma, gae_lambda,
                  scale_advantage_by_values_accuracy: bool = False, gae_mode: int = EXACT,
                  perm_source: Optional[Callable[[int], torch.Tensor]] = None,
-                 generator: Optional[torch.Generator] = None) -> None:
+                 generator: Optional[torch.Generator] = None,
+                 subaction_mask: Optional[Dict[int, Dict[int, int]]] = None, action_plane_space=None) -> None:
         super().__init__()
         self.device = device
         self.obs, self.actions, self.rewards = obs, actions, rewards
@@ -145,8 +163,8 @@ class DeviceRollout(Rollout):
         self.action_masks = action_masks
         self.next_episode_starts, self.next_values = next_episode_starts, next_values
         self.num_actions = None
-        if action_masks is not None:  # rollout.py:130-180 (no subaction masks on the hot path)
-            self.num_actions = action_masks.any(-1).sum(-1) if action_masks.dim() > 3 else None
+        if action_masks is not None:  # vec_rollout.py:69-76 -> rollout.py:130-180, one launch
+            self.num_actions = _num_actions(actions, action_masks, subaction_mask, action_plane_space)
         self.advantages, self.returns = compute_advantages_device(
             rewards, values, episode_starts, next_episode_starts, next_values, gamma, gae_lambda,
             mode=gae_mode, want_returns=True)
@@ -194,15 +212,28 @@ class DeviceRollout(Rollout):
             self._flat = fields
         return self._flat
 
+    def _epoch_fields(self) -> List[torch.Tensor]:
+        """The fields an epoch's permuted copy carries: _flat_fields() (what the update's kernels read)
+        plus Batch.num_actions when the rollout has action masks."""
+        fields = self._flat_fields()
+        if self.num_actions is not None:
+            fields = fields + [self.num_actions.reshape(-1)]
+        return fields
+
     def _batch_from(self, fields: List[torch.Tensor], sl: slice) -> Batch:
+        """A Batch over rows sl of fields laid out as _epoch_fields() (num_actions optional)."""
         obs, actions, values, adv, ret = (f[sl] for f in fields[:5])
         i = 5
         logprobs = None
         if self.logprobs is not None:
             logprobs = fields[i][sl]
             i += 1
-        masks = fields[i][sl] if self.action_masks is not None else None
-        return Batch(obs, logprobs, actions, masks, None, values, adv, ret)
+        masks = None
+        if self.action_masks is not None:
+            masks = fields[i][sl]
+            i += 1
+        num_actions = fields[i][sl] if len(fields) > i else None
+        return Batch(obs, logprobs, actions, masks, num_actions, values, adv, ret)
 
     def permutation(self) -> torch.Tensor:
         if self._perm_source is not None:
@@ -213,14 +244,14 @@ class DeviceRollout(Rollout):
         """Allocate the permuted copy `slot` (on the current stream) ahead of an epoch_batch that
         will run on another stream."""
         if slot not in self._perm_bufs:
-            self._perm_bufs[slot] = [torch.empty_like(f) for f in self._flat_fields()]
+            self._perm_bufs[slot] = [torch.empty_like(f) for f in self._epoch_fields()]
 
     def epoch_batch(self, shuffle: bool = True, slot: int = 0) -> Batch:
         """The whole rollout as one flat Batch, permuted for this epoch (one gather
         kernel); minibatch i is rows [i*batch_size, (i+1)*batch_size).  slot selects the
         permuted copy written (two slots: the next epoch's batch is prepared while the current
         one is read)."""
-        flat = self._flat_fields()
+        flat = self._epoch_fields()
         if shuffle:
             self.alloc_epoch_buffers(slot)
             gather_rows(flat, self._perm_bufs[slot], self.permutation())
@@ -234,7 +265,7 @@ class DeviceRollout(Rollout):
         for i in range(0, self.total_steps, batch_size):
             sl = slice(i, i + batch_size)
             g = lambda t: None if t is None else t[sl]
-            yield Batch(full.obs[sl], g(full.logprobs), full.actions[sl], g(full.action_masks), None,
+            yield Batch(full.obs[sl], g(full.logprobs), full.actions[sl], g(full.action_masks), g(full.num_actions),
                         full.values[sl], full.advantages[sl], full.returns[sl])
 
     def add_to_batch(self, map_fn: BatchMapFn, batch_size: int) -> None:
@@ -263,8 +294,12 @@ class SyncStepRolloutGenerator(RolloutGenerator):
                                  ("prepare_steps", prepare_steps, 0),
                                  ("rolling_num_envs_reset_every_prepare_step",
                                   rolling_num_envs_reset_every_prepare_step, 0)] if v != d]
-        if bad or subaction_mask or full_batch_off_accelerator:
-            raise NotImplementedError(f"rollout options outside the hot-path scope: {bad or 'subaction_mask/full_batch_off_accelerator'}")
+        if bad or full_batch_off_accelerator:
+            raise NotImplementedError(f"rollout options outside the hot-path scope: {bad or 'full_batch_off_accelerator'}")
+        # rl_algo_impls/runner/train.py:159-162 copies the policy's subaction_mask into these kwargs; it
+        # gates Batch.num_actions (sync_step_rollout.py:39,177 -> vec_rollout.py:69-76)
+        self.subaction_mask = subaction_mask
+        self.action_plane_space = getattr(vec_env, "action_plane_space", None)
         self.gridnet = bool(getattr(policy, "gridnet", False))
         self.get_action_mask = getattr(vec_env, "get_action_mask", None)
         if self.get_action_mask is not None and not self.gridnet:
@@ -508,4 +543,4 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             self.device, self.next_episode_starts.clone(), next_values, self.obs, self.actions, self.rewards,
             self.episode_starts, self.values, self.logprobs if self.include_logp else None, self.action_masks, gamma,
             gae_lambda, self.scale_advantage_by_values_accuracy, self.gae_mode, self.perm_source,
-            self.generator)
+            self.generator, subaction_mask=self.subaction_mask, action_plane_space=self.action_plane_space)

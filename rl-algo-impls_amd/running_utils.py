@@ -37,7 +37,8 @@ import torch
 
 def set_device_optimizations(device: torch.device, set_float32_matmul_precision: Optional[str] = None,
                              use_deterministic_algorithms: bool = True) -> None:
-    """running_utils.py:161-172."""
+    """running_utils.py:161-172, plus GEMM tuning when determinism is off (set_gemm_tuning)."""
+    set_gemm_tuning(device, not use_deterministic_algorithms)
     torch.use_deterministic_algorithms(use_deterministic_algorithms)
     torch.backends.cudnn.deterministic = bool(use_deterministic_algorithms)
     if use_deterministic_algorithms and "MIOPEN_USER_DB_PATH" not in os.environ:
@@ -46,6 +47,29 @@ def set_device_optimizations(device: torch.device, set_float32_matmul_precision:
     if torch.device(device).type == "cuda" and set_float32_matmul_precision:
         logging.info(f"Setting torch.set_float32_matmul_precision to {set_float32_matmul_precision}")
         torch.set_float32_matmul_precision(set_float32_matmul_precision)
+
+
+def set_gemm_tuning(device: torch.device, enabled: bool) -> bool:
+    """PyTorch TunableOp for the library GEMMs the update leaves to PyTorch (C3: the NatureCNN fc layer's
+    forward, dx and beta = 1 weight-gradient GEMMs; hipBLASLt's heuristic picks ran them at ~40
+    TFLOP/s).  Each GEMM shape's hipBLASLt and rocBLAS solutions are timed once, at its first call, and
+    the fastest is kept (C3: 147.2k -> 152.7-153.5k env-steps/s, profiles/r3zb_c3_blas_ab.txt).
+
+    On only when deterministic mode is off: the pick is by timing, so it can differ between runs.
+    RAI_TUNABLEOP=0 turns it off.  The picks are kept in a results file per device,
+    RAI_TUNABLEOP_FILE or ~/.cache/rl_algo_impls_amd/tunableop_results<device>.csv, which later runs
+    of the same user READ instead of re-tuning: delete it to re-tune (e.g. after a driver or library
+    update).  Returns whether tuning is on."""
+    on = bool(enabled) and torch.device(device).type == "cuda" and os.environ.get("RAI_TUNABLEOP", "1") != "0"
+    if on:
+        path = os.environ.get("RAI_TUNABLEOP_FILE") or os.path.join(
+            os.path.expanduser("~"), ".cache", "rl_algo_impls_amd", "tunableop_results%d.csv")
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        torch.cuda.tunable.set_filename(path)
+        torch.cuda.tunable.set_max_tuning_duration(20)
+    torch.cuda.tunable.enable(on)
+    torch.cuda.tunable.tuning_enable(on)
+    return on
 
 
 def set_seeds(seed: Optional[int]) -> None:

@@ -13,6 +13,9 @@ sys.path.insert(0, str(ROOT))
 # tests switch MIOpen to its deterministic solvers (~100x slower at the C3 shapes), so they keep a
 # database of their own instead of leaving those choices to later runs on the same machine
 os.environ.setdefault("MIOPEN_USER_DB_PATH", tempfile.mkdtemp(prefix="rai-miopen-tests-"))
+# likewise TunableOp's GEMM picks (running_utils.set_gemm_tuning, on when deterministic mode is off)
+os.environ.setdefault("RAI_TUNABLEOP_FILE", os.path.join(tempfile.mkdtemp(prefix="rai-tunableop-tests-"),
+                                                         "tunableop_results%d.csv"))
 sys.path.insert(0, str(ROOT / "oracle"))
 
 import _pkgload  # noqa: E402

@@ -257,7 +257,7 @@ def mc_dp_worker(rank, world, port, q, after):
     dev = torch.device("cuda", 0)
     policy, r = mc_policy_and_rollout(make_mc_rank_data(rank), dev)
     algo = PPO(policy, dev, None, batch_size=32, normalize_advantages_after_scaling=after, **MC_KW)
-    algo.enable_data_parallel()
+    algo.enable_data_parallel(dp_batch="per-rank")
     stats, norms, _ = algo.update(r)
     q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
     import torch.distributed as dist
@@ -336,7 +336,7 @@ def cnn_dp_worker(rank, world, port, q, mode):
     algo = PPO(policy, dev, None, batch_size=128, n_epochs=2, learning_rate=2.5e-4, clip_range=0.1, vf_coef=0.5,
                ent_coef=0.01)
     if mode != "single":
-        algo.enable_data_parallel()
+        algo.enable_data_parallel(dp_batch="per-rank")
         assert algo._dp_comm is not None
     stats, norms, _ = algo.update(r)
     torch.cuda.synchronize()

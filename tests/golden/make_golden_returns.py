@@ -16,7 +16,8 @@ the last 100 training episode returns) curve, the final rolling mean, and a 10-e
 deterministic evaluation (rl_algo_impls/shared/callbacks/eval_callback.py:79-240) of the final
 policy on a fresh CartPoleVecEnv(8, seed + 1000).  Only outputs are stored.
 
-    python tests/golden/make_golden_returns.py            # all configs and seeds (~10 min, 4 procs)
+    python tests/golden/make_golden_returns.py                 # all configs and seeds
+    python tests/golden/make_golden_returns.py c2_4096x128     # one config; other configs' runs kept
 """
 from __future__ import annotations
 
@@ -35,12 +36,17 @@ CONFIGS = {
     "yaml_8x32": dict(n_envs=8, n_steps=32, n_timesteps=100_000),
     # BASELINE configs[0]: the reference CPU path at num_envs=8, n_steps=128
     "c1_8x128": dict(n_envs=8, n_steps=128, n_timesteps=100_000),
+    # BASELINE configs[1] / the north star's headline config: 4096 envs x 128 steps, the YAML's
+    # batch_size 256 x 20 epochs (40,960 optimizer steps per update), 4 updates with the YAML's
+    # linear lr / clip decay over them.  ~3 min of CPU per update per process.
+    "c2_4096x128": dict(n_envs=4096, n_steps=128, n_timesteps=4 * 4096 * 128),
 }
+# seeds per config (the C2 runs are ~40x the CPU time of the 8-env ones)
+CONFIG_SEEDS = {"yaml_8x32": (1, 2, 3, 4, 5), "c1_8x128": (1, 2, 3, 4, 5), "c2_4096x128": (1, 2, 3)}
 ALGO_KW = dict(batch_size=256, n_epochs=20, gae_lambda=0.8, gamma=0.98, ent_coef=0.0,
                learning_rate=0.001, clip_range=0.2)
 PHASES = [{"learning_rate": 0.001, "clip_range": 0.2}, {"learning_rate": 0.0, "clip_range": 0.0}]
 DURATIONS = [0.0, 1.0, 0.0]
-SEEDS = (1, 2, 3, 4, 5)
 EVAL_EPISODES = 10
 
 
@@ -113,6 +119,7 @@ def run_one(args):
             eps = list(env.episodes)
             curve.append([int(self.timesteps_elapsed),
                           float(np.mean([e.score for e in eps])) if eps else 0.0, len(eps)])
+            print(cfg_name, seed, curve[-1], flush=True)
             return True
 
     algo.learn(c["n_timesteps"], gen, callbacks=[ht, Record()])
@@ -123,15 +130,20 @@ def run_one(args):
 
 
 def main():
-    jobs = [(c, s) for c in CONFIGS for s in SEEDS]
-    with mp.get_context("spawn").Pool(4) as pool:
+    names = sys.argv[1:] or list(CONFIGS)
+    jobs = [(c, s) for c in names for s in CONFIG_SEEDS[c]]
+    with mp.get_context("spawn").Pool(min(4, len(jobs))) as pool:
         res = pool.map(run_one, jobs)
-    out = dict(configs=CONFIGS, algo_kw=ALGO_KW, phases=PHASES, durations=DURATIONS,
-               eval_episodes=EVAL_EPISODES, runs={})
+    path = HERE / "returns_cartpole.json"
+    out = json.loads(path.read_text()) if path.exists() else dict(runs={})
+    out.update(configs={k: CONFIGS[k] for k in set(out["runs"]) | set(names)}, algo_kw=ALGO_KW, phases=PHASES,
+               durations=DURATIONS, eval_episodes=EVAL_EPISODES)
+    for c in names:
+        out["runs"][c] = {}
     for cfg, seed, r in res:
         out["runs"].setdefault(cfg, {})[str(seed)] = r
         print(cfg, seed, "final rolling", round(r["final_rolling_mean"], 1), "eval", r["eval_mean"])
-    (HERE / "returns_cartpole.json").write_text(json.dumps(out))
+    path.write_text(json.dumps(out))
 
 
 if __name__ == "__main__":

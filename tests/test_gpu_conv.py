@@ -276,3 +276,38 @@ def test_conv_wgrad_relu_partials_fold_the_relu_backward_and_bias_gradient(case)
     db_ref = b0.double() + dz.double().sum(dim=(0, 2, 3))
     bound = b0.double().abs() + dz.double().abs().sum(dim=(0, 2, 3))
     assert ((gb.cpu().double() - db_ref).abs() <= (B * OH * OH + 2) * 2.0 ** -24 * bound).all()
+
+
+def test_same_conv_twice_in_one_backward_accumulates_both_uses():
+    """One conv module applied to two same-shape inputs inside one direct_grads() backward:
+    both uses write their weight-gradient partials into the layer's one workspace, so the first use's
+    pending reduction must run before the second overwrites it.  One input needs its gradient (partials
+    from dz), the other does not (the ReLU backward folded into the partials).  dW, db and dx against
+    fp64 autograd of the same graph."""
+    from rl_algo_impls_amd import cnn_ops
+
+    torch.manual_seed(3)
+    conv = torch.nn.Conv2d(32, 32, 4, stride=2)
+    w64, b64 = conv.weight.detach().double(), conv.bias.detach().double()
+    x1 = torch.randn(8, 32, 14, 14)
+    x2 = torch.randn(8, 32, 14, 14)
+    gy = torch.randn(8, 32, 6, 6)
+    r1 = x1.double().requires_grad_(True)
+    w_r, b_r = w64.clone().requires_grad_(True), b64.clone().requires_grad_(True)
+    out = torch.relu(F.conv2d(r1, w_r, b_r, 2)) + torch.relu(F.conv2d(x2.double(), w_r, b_r, 2))
+    (out * gy.double()).sum().backward()
+
+    w = conv.weight.detach().to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    b = conv.bias.detach().to(DEV).clone().requires_grad_(True)
+    w.grad = torch.zeros_like(w, memory_format=torch.channels_last)
+    b.grad = torch.zeros_like(b)
+    d1 = x1.to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    d2 = x2.to(DEV).contiguous(memory_format=torch.channels_last)
+    with cnn_ops.direct_grads():
+        y = cnn_ops.ConvBiasReLU.apply(d1, w, b, 2, 0, conv) + cnn_ops.ConvBiasReLU.apply(d2, w, b, 2, 0, conv)
+        (y * gy.to(DEV).contiguous(memory_format=torch.channels_last)).sum().backward()
+    torch.cuda.synchronize()
+    for got, ref in [(w.grad, w_r.grad), (b.grad, b_r.grad), (d1.grad, r1.grad)]:
+        got = got.detach().cpu().double()
+        assert torch.isfinite(got).all()
+        assert ((got - ref).abs() <= 1e-4 * ref.abs().max() + 1e-6).all(), float((got - ref).abs().max())

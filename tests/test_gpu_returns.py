@@ -26,7 +26,7 @@ REF = json.loads((GOLDEN / "returns_cartpole.json").read_text())
 
 
 def _ref(cfg):
-    runs = REF["runs"][cfg]
+    runs = {k: REF["runs"][cfg][k] for k in sorted(REF["runs"][cfg], key=int)}
     finals = np.array([r["final_rolling_mean"] for r in runs.values()])
     aucs = np.array([np.mean([c[1] for c in r["curve"]]) for r in runs.values()])
     evals = np.array([r["eval_mean"] for r in runs.values()])
@@ -34,9 +34,10 @@ def _ref(cfg):
 
 
 def test_reference_return_fixture_is_consistent():
-    """The reference curves: one point per update (ceil(1e5 / (envs x steps)) of them), the final
-    rolling mean is the last point over a full 100-episode window, and the reference solves CartPole
-    (rolling mean >= 475) in most seeds, as its YAML is tuned to."""
+    """The reference curves: one point per update (ceil(n_timesteps / (envs x steps)) of them), the
+    final rolling mean is the last point over a full 100-episode window.  At 8 envs the reference
+    solves CartPole (rolling mean >= 475) in most seeds, as its YAML is tuned to; at C2 (4096 x 128,
+    4 updates of 40,960 optimizer steps each) it learns monotonically from ~22 to ~100-140."""
     for cfg, c in REF["configs"].items():
         per_update = c["n_envs"] * c["n_steps"]
         n_updates = -(-c["n_timesteps"] // per_update)
@@ -45,8 +46,13 @@ def test_reference_return_fixture_is_consistent():
             assert len(r["curve"]) == n_updates
             assert r["curve"][-1][0] == n_updates * per_update
             assert r["curve"][-1][1] == r["final_rolling_mean"] and r["curve"][-1][2] == 100
-        assert (finals >= 475).sum() >= 3, finals
-        assert 200 < aucs.mean() < 450
+        if cfg.startswith("c2_"):
+            for r in REF["runs"][cfg].values():
+                assert np.all(np.diff([p[1] for p in r["curve"]]) > 0), r["curve"]
+            assert len(REF["runs"][cfg]) == 3 and 80 < finals.mean() < 200
+        else:
+            assert (finals >= 475).sum() >= 3, finals
+            assert 200 < aucs.mean() < 450
 
 
 def _device_run(cfg, seed):
@@ -105,9 +111,13 @@ def _device_result(cfg, seed):
     return _RUNS[(cfg, seed)]
 
 
+def _seeds(cfg):
+    return sorted(int(s) for s in REF["runs"][cfg])
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
-@pytest.mark.parametrize("cfg", ["yaml_8x32", "c1_8x128"])
+@pytest.mark.parametrize("cfg,seed", [(c, s) for c in ("yaml_8x32", "c1_8x128", "c2_4096x128")
+                                      for s in (1, 2, 3, 4, 5) if str(s) in REF["runs"].get(c, {})])
 def test_device_training_run(cfg, seed):
     """One seeded device training run on the reference's env and hyperparameters (kept for the band
     test below): one rolling-mean point per update, finite, within CartPole-v1's [0, 500]."""
@@ -131,7 +141,7 @@ def test_episode_return_matches_reference(cfg):
       * the mean final deterministic 10-episode evaluation is within 50 of the reference's."""
     r_fin, r_auc, r_eval = _ref(cfg)
     fins, aucs, evals = [], [], []
-    for seed in (1, 2, 3, 4, 5):
+    for seed in _seeds(cfg):
         curve, ev = _device_result(cfg, seed)
         assert len(curve) == len(REF["runs"][cfg][str(seed)]["curve"])
         fins.append(curve[-1][1])
@@ -152,3 +162,48 @@ def test_episode_return_matches_reference(cfg):
     assert (fins >= r_fin.min() - 25).sum() >= 3, msg
     assert abs(aucs.mean() / r_auc.mean() - 1) <= 0.15, msg
     assert abs(evals.mean() - r_eval.mean()) <= 50, msg
+
+
+def _write_report(name, **kw):
+    rep = os.environ.get("RAI_TEST_REPORT_DIR")
+    if rep:  # the GPU runs keep the comparison (tools/gpu_check.sh)
+        os.makedirs(rep, exist_ok=True)
+        with open(os.path.join(rep, name), "w") as f:
+            json.dump(kw, f)
+
+
+@pytest.mark.gpu
+def test_episode_return_matches_reference_at_c2():
+    """The north star's "matching mean episode return" at the config it names: CartPole-v1 with
+    num_envs=4096, n_steps=128 (BASELINE configs[1]), the YAML's batch 256 x 20 epochs (40,960
+    optimizer steps per update) and lr / clip decaying linearly to 0 over 4 updates; the reference's
+    own PPO.learn, seeds 1-3 (make_golden_returns.py c2_4096x128), against the device trainer's fused
+    epoch kernel on the same env, seeds and schedule.  Population bands over the 3 seeds (reference
+    seed spreads: final rolling mean 102-137, its per-update points 21-23 / 32-36 / 61-75 / 102-137,
+    10-episode deterministic eval 257-465):
+      * every update's mean rolling mean (last 100 training episodes) within 30 % + 5 of the
+        reference's (the learning curve, update by update);
+      * the mean area under the curve within 20 %;
+      * every device seed improves monotonically over the 4 updates, as every reference seed does;
+      * the mean deterministic evaluation within 200 of the reference's (its seed std is ~100)."""
+    cfg = "c2_4096x128"
+    seeds = _seeds(cfg)
+    ref_curves = np.array([[p[1] for p in REF["runs"][cfg][str(s)]["curve"]] for s in seeds])
+    r_fin, r_auc, r_eval = _ref(cfg)
+    dev_curves, evals = [], []
+    for seed in seeds:
+        curve, ev = _device_result(cfg, seed)
+        assert len(curve) == ref_curves.shape[1]
+        dev_curves.append([p[1] for p in curve])
+        evals.append(ev)
+    dev_curves, evals = np.array(dev_curves), np.array(evals)
+    msg = (f"device curves {dev_curves.round(1).tolist()} eval {evals.round(1).tolist()}; reference curves "
+           f"{ref_curves.round(1).tolist()} eval {r_eval.round(1).tolist()}")
+    print(msg)
+    _write_report(f"returns_{cfg}.json", device_curves=dev_curves.tolist(), device_eval=evals.tolist(),
+                  reference_curves=ref_curves.tolist(), reference_eval=r_eval.tolist(), seeds=seeds)
+    dm, rm = dev_curves.mean(0), ref_curves.mean(0)
+    assert (np.abs(dm - rm) <= 0.3 * rm + 5).all(), msg
+    assert abs(dev_curves.mean() / ref_curves.mean() - 1) <= 0.2, msg
+    assert (np.diff(dev_curves, axis=1) > 0).all(), msg
+    assert abs(evals.mean() - r_eval.mean()) <= 200, msg
