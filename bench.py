@@ -287,6 +287,11 @@ def main():
 
     set_device_optimizations(dev, use_deterministic_algorithms=bool(args.deterministic))
     tunableop = torch.cuda.tunable.is_enabled()
+    # RAI_AUTOGRAD_MT=0 (profiling runs): autograd runs the backward on the calling thread instead of its
+    # device worker thread, so every dispatch of the update is submitted from one host thread (the
+    # rocprofv3 counter-collection crashes of r3zd / r3ze faulted with launches in flight on two)
+    if os.environ.get("RAI_AUTOGRAD_MT") == "0":
+        torch.autograd.set_multithreading_enabled(False)
     # MIOpen find mode for the CNN convolutions (C3 / C5): every candidate solver timed at the first call
     # of each problem, the fastest kept.  Measured C3: 1.10 s per update against 1.26 s with the default
     # immediate-mode choice (profiles/r2o_pong_find_mode_bench_line.json vs r2l)
@@ -419,22 +424,36 @@ def main():
                       "bytes_per_launch": large_bytes}
     del rl_, vl_, esl, advl, retl
     workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
-    pmc = {}
+    lib_sha = _lib.lib_sha256()
+    pmc, pmc_src = {}, None
     # the newest PMC summary (profiles/r<round><letter>_pmc.json, tools/pmc_summary.py) holding this workload
     for pmc_path in sorted((ROOT / "profiles").glob("r*_pmc.json"), reverse=True):
         pmc = json.loads(pmc_path.read_text()).get(workload, {})
         if pmc:
+            pmc_src = pmc_path.name
             break
 
     def traffic(kernel):
-        return pmc.get(kernel, {}).get("traffic_bytes_per_launch")
+        """HBM bytes per launch from the PMC summary, only when its counters were collected on the very
+        library this process loaded (lib_sha256); otherwise None (a stale figure is not reported)."""
+        e = pmc.get(kernel, {})
+        return e.get("traffic_bytes_per_launch") if e.get("lib_sha256") == lib_sha else None
+
+    def traffic_source(kernel):
+        e = pmc.get(kernel, {})
+        if not e:
+            return None
+        if e.get("lib_sha256") != lib_sha:
+            return f"{pmc_src}: measured on another librai_amd.so build (sha256 {str(e.get('lib_sha256'))[:12]}), not reported"
+        return f"{pmc_src} (2 x FETCH_SIZE + WRITE_SIZE per launch, same library sha256 {lib_sha[:12]})"
 
     # the instantiation rai_gae picks (csrc/gae.hip): columns per workgroup by column count
     C = N * K
     gae_name = "gae_kernel<double, %d>" % (64 if C >= 256 * 64 else (32 if C >= 256 * 32 else 16))
     roof_gae = {"kernel": gae_name, "bound": "hbm", "achieved": round(gae_bytes / (gae_us * 1e-6) / 1e9, 1),
                 "peak": 8000.0, "unit": "GB/s", "frac": round(gae_bytes / (gae_us * 1e-6) / 1e9 / 8000.0, 4),
-                "traffic": traffic(gae_name), "avg_us": round(gae_us, 3), "bytes_per_launch": gae_bytes}
+                "traffic": traffic(gae_name), "traffic_source": traffic_source(gae_name), "avg_us": round(gae_us, 3),
+                "bytes_per_launch": gae_bytes}
     if epoch_ms and args.config == "halfcheetah":
         # dominant kernel: the persistent wide-MLP epoch (rai_mlp_wide_epoch, csrc/mlp_wide_epoch.hip):
         # one launch = every minibatch step of one epoch = T*N samples of forward+backward at SURVEY.md
@@ -446,8 +465,8 @@ def main():
         kname = "mlp_wide_epoch_kernel<%d>" % head
         roofline = {"kernel": kname + " (rai_mlp_wide_epoch, 16 CUs per network)", "bound": "mfma",
                     "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
-                    "traffic": traffic(kname), "avg_ms": round(ms, 3), "flops_per_launch": flops,
-                    "launches_timed": len(epoch_ms)}
+                    "traffic": traffic(kname), "traffic_source": traffic_source(kname), "avg_ms": round(ms, 3),
+                    "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
         steps_per_launch = (T * N + algo.batch_size - 1) // algo.batch_size
         roof_lat = {"kernel": kname, "bound": "latency", "achieved": round(ms * 1e3 / steps_per_launch, 3),
                     "unit": "us per dependent optimizer step", "steps_per_launch": steps_per_launch}
@@ -464,7 +483,7 @@ def main():
         kname = "mlp_ppo_mc8_kernel<%d, %d>" % (act, G)
         roofline = {"kernel": kname + f" (rai_mlp_ppo_epoch, {G} CUs per network)", "bound": "mfma",
                     "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
-                    "traffic": traffic(kname), "avg_ms": round(ms, 3),
+                    "traffic": traffic(kname), "traffic_source": traffic_source(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
         roof_lat = latency_roofline(G, ms, (T * N + algo.batch_size - 1) // algo.batch_size, kname)
     elif args.config in UPDATE_FLOPS:
@@ -480,8 +499,11 @@ def main():
         for tp in sorted((ROOT / "profiles").glob(f"r*_{args.config}_traffic.json"), reverse=True):
             td = json.loads(tp.read_text())
             if td.get("workload", "").startswith(workload):
-                upd_traffic = td.get("bytes_per_update")
-                traffic_src = tp.name + (" (" + td["contractions"] + ")" if td.get("contractions") else "")
+                if td.get("lib_sha256") == lib_sha:  # counters collected on this very library
+                    upd_traffic = td.get("bytes_per_update")
+                    traffic_src = tp.name + (" (" + td["contractions"] + ")" if td.get("contractions") else "")
+                else:
+                    traffic_src = (f"{tp.name}: measured on another librai_amd.so build, not reported")
                 break
         kname = "whole update (MIOpen / hipBLASLt contractions + HIP epilogues)"
         if args.config == "pong":
@@ -531,6 +553,7 @@ def main():
             "roofline_gae": roof_gae,
             "roofline_gae_bandwidth_regime": roof_gae_large,
             "cpu_baseline": cpu,
+            "lib_sha256": lib_sha,
         }
         if args.dp_rehearsal or world > 1:
             if algo._xdp is not None:

@@ -229,6 +229,15 @@ def hip_runtimes_mapped() -> list[str]:
     return sorted(set(re.findall(r"\S*libamdhip64\.so\S*", maps)))
 
 
+def lib_sha256(path=None) -> str:
+    """sha256 of the C-ABI library file (default: the one lib() loads).  PMC summaries record it, and
+    bench.py reports a counter figure only when it was measured on this same binary."""
+    import hashlib
+
+    with open(path or lib_path(), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def lib() -> C.CDLL:
     """Load (once) and return the C-ABI library; raises if it is unavailable."""
     global _lib

@@ -11,7 +11,9 @@ GAE, per-epoch gathers) are added once.  The bench's own extra measurements in t
 bandwidth-regime GAE, gae_stream_kernel) and MIOpen find-mode trial kernels (present in the FETCH
 pass only: the WRITE pass reuses the find database) are excluded.
 """
+import hashlib
 import json
+import os
 import sys
 
 STEPS = 2048
@@ -37,7 +39,9 @@ def main():
         else:
             upd_b += tot
     top = sorted(kernels.items(), key=lambda kv: -kv[1]["bytes_per_launch"] * kv[1]["dispatches"])
-    doc = {"workload": "ppo pong num_envs=1024/rank n_steps=128 (eager, RAI_GRAPHS=0)",
+    libp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rl-algo-impls_amd", "lib", "librai_amd.so")
+    doc = {"workload": os.environ.get("C3_WORKLOAD", "ppo pong num_envs=1024/rank n_steps=128 (eager, RAI_GRAPHS=0)"),
+           "lib_sha256": hashlib.sha256(open(libp, "rb").read()).hexdigest(),
            "optimizer_steps_per_update": STEPS,
            "bytes_per_optimizer_step": round(step_b),
            "bytes_per_update": round(step_b * STEPS + upd_b),

@@ -29,6 +29,12 @@ for c in $CONFIGS; do
         python3 bench.py --config "$c" --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 $extra
     run "write_$c" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$c" -o run -- \
         python3 bench.py --config "$c" --steps 1 --warmup 0 --no-cpu-baseline --roofline-reps 20 $extra
+    # per-kernel medians + the library's sha256 (bench.py reports traffic only for the same binary)
+    wl=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['config']['workload'])" "$OUT/write_$c.log")
+    fcsv=$(find "$OUT/fetch_$c" -name "*counter_collection.csv" | head -1)
+    wcsv=$(find "$OUT/write_$c" -name "*counter_collection.csv" | head -1)
+    python3 tools/pmc_summary.py "$OUT/pmc.json" "$wl" "$fcsv" "$wcsv" > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc_summary failed"; exit 1; }
+    find "$OUT" -name "*counter_collection.csv" -size +20M -delete
   fi
   if [ -n "${MFMA_PMC:-}" ]; then
     run "mfma_$c" 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
