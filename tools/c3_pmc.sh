@@ -17,8 +17,8 @@ for C in FETCH_SIZE WRITE_SIZE; do
   echo "== $C" | tee -a "$OUT/steps.log"
   RAI_AUTOGRAD_MT=${AUTOGRAD_MT:-1} RAI_GRAPHS=${GRAPHS:-0} RAI_ROLLOUT_GRAPH=${GRAPHS:-0} RAI_GRAPH_EAGER=${GRAPH_EAGER:-0} timeout -s KILL 400 rocprofv3 --pmc $C ${KREGEX:+--kernel-include-regex "$KREGEX"} --output-format csv -d "$OUT/$C" -o run -- \
     python3 bench.py --config pong --no-cpu-baseline --roofline-reps 1 --steps 1 --warmup 0 > "$OUT/$C.log" 2>&1
-  sha256sum rl-algo-impls_amd/lib/librai_amd.so > "$OUT/lib_sha256.txt"  # the binary the crash frames map to
   rc=$?
+  sha256sum rl-algo-impls_amd/lib/librai_amd.so > "$OUT/lib_sha256.txt"  # the binary the crash frames map to
   echo "== $C rc=$rc" | tee -a "$OUT/steps.log"
   grep -v amdgpu.ids "$OUT/$C.log" | tail -3
   if [ $rc -ne 0 ]; then  # map the crash's PCs with the newest maps dump of that process
