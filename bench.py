@@ -132,6 +132,30 @@ def latency_roofline(G: int, avg_ms: float, steps_per_launch: int, kname: str) -
             "steps_per_launch": steps_per_launch}
 
 
+def latency_roofline_wide(avg_ms: float, steps_per_launch: int, kname: str) -> dict:
+    """Per-optimizer-step latency floor of the C4 whole-epoch kernel (csrc/mlp_wide_epoch.hip,
+    mlp_wide_epoch_kernel<1>) from the MI355X price list (/opt/skills/guides/MI355X_MICROARCH.md),
+    against the measured step time.  A launch is `steps_per_launch` DEPENDENT optimizer steps
+    (rl_algo_impls/ppo/ppo.py:375,441-447), so the bound is one step's critical path:
+      * MFMA issue: each of the 16 workgroups of a network issues ~270 v_mfma_f32_16x16x4f32 per step
+        (fwd2 64, dW2 64, dH1 64, dW1 16, small-parameter tiles 48, fwd1 5) over its
+        4 SIMDs at the 32-cycle issue rate: 2,160 cycles at 2.4 GHz;
+      * three all-to-all edges among the 16 workgroups (A: the H1 all-gather, B: the output-layer
+        partials, C: the dZ2 all-gather), each at least the price list's 'allgather' row at its cheapest
+        (8 KB published by 32 CUs, parked: 2.4 us);
+      * the norm-share exchange D as tagged 8-B granules: the 'handoff-1to1' row, idle, 8 B (0.8 us).
+    frac = floor / measured us per step."""
+    t_mfma = 270 * 32 / 4 / 2.4e3
+    t_edges = 3 * 2.4
+    t_gran = 0.8
+    floor_us = t_mfma + t_edges + t_gran
+    step_us = avg_ms * 1e3 / max(steps_per_launch, 1)
+    return {"kernel": kname, "bound": "latency", "achieved": round(step_us, 3), "peak": round(floor_us, 3),
+            "unit": "us per dependent optimizer step", "frac": round(floor_us / step_us, 4),
+            "floor_terms_us": {"mfma_issue": round(t_mfma, 3), "allgather_edges": t_edges, "granule_edge": t_gran},
+            "steps_per_launch": steps_per_launch}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -468,8 +492,7 @@ def main():
                     "traffic": traffic(kname), "traffic_source": traffic_source(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
         steps_per_launch = (T * N + algo.batch_size - 1) // algo.batch_size
-        roof_lat = {"kernel": kname, "bound": "latency", "achieved": round(ms * 1e3 / steps_per_launch, 3),
-                    "unit": "us per dependent optimizer step", "steps_per_launch": steps_per_launch}
+        roof_lat = latency_roofline_wide(ms, steps_per_launch, kname)
     elif epoch_ms:
         # dominant kernel: one fused PPO epoch per launch = T*N samples of forward+backward at
         # SURVEY.md 8(d)'s 52,352 FLOP/sample (CartPole MLP, torch.utils.flop_counter), f32 MFMA peak

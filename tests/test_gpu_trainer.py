@@ -494,6 +494,60 @@ def _graphed_vs_eager(kind, T, N, bs, extra):
         np.testing.assert_allclose(n1, n0, rtol=1e-4 if kind == "pong" else 1e-5)
 
 
+def test_wide_epoch_full_c4_horizon_drift(monkeypatch):
+    """Config C4's update at its per-GPU shape (256 envs x 512 steps = 131,072 rows; the YAML's batch 64
+    x 20 epochs = 2,048 dependent optimizer steps per rai_mlp_wide_epoch launch, 40,960 per update;
+    rl_algo_impls/hyperparams/ppo.yml:337-359) through the whole-epoch kernel vs the per-minibatch
+    kernels (RAI_WIDE_EPOCH=0: graph-replayed wide-MLP forward/backward + rai_ppo_loss +
+    rai_clip_optim_step), identical rollout and permutations.  The whole-epoch kernel reuses its
+    per-step publish / drain slots thousands of times per launch; this is the horizon at which a slot
+    reuse or drift bug would show.  Bound as test_fused_epoch_full_c2_horizon_drift: the per-minibatch
+    path re-run from weights perturbed by one ulp sets the noise floor."""
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    torch.manual_seed(3)
+    env = SyntheticVecEnv(256, "halfcheetah", seed=5)
+    policy = ActorCritic(env, pi_hidden_sizes=[256, 256], v_hidden_sizes=[256, 256], activation_fn="relu",
+                         log_std_init=-2, init_layers_orthogonal=False).to(DEV)
+    gen = SyncStepRolloutGenerator(policy, env, n_steps=512, seed=11)
+    r = gen.rollout(gamma=0.98, gae_lambda=0.92)
+    p0 = torch.nn.utils.parameters_to_vector(policy.parameters()).detach().clone()
+    runs = {}
+    for name, epoch, perturb in (("epoch", "1", False), ("minibatch", "0", False), ("minibatch_ulp", "0", True)):
+        monkeypatch.setenv("RAI_WIDE_EPOCH", epoch)
+        start = p0.clone()
+        if perturb:
+            start = torch.nextafter(start, torch.full_like(start, float("inf")))
+        torch.nn.utils.vector_to_parameters(start, policy.parameters())
+        algo = PPO(policy, DEV, None, batch_size=64, n_epochs=20, gamma=0.98, gae_lambda=0.92,
+                   ent_coef=0.000401762, max_grad_norm=0.8, vf_coef=0.58096, learning_rate=2.0633e-05,
+                   clip_range=0.1)
+        g = torch.Generator(device=DEV)
+        g.manual_seed(123)
+        r._perm_source = lambda n: torch.randperm(n, device=DEV, generator=g)
+        stats, norms, _ = algo.update(r)
+        torch.cuda.synchronize()
+        assert algo.optimizer.step_count == 40960
+        assert (getattr(algo, "_we_ws", None) is not None) == (epoch == "1"), "whole-epoch kernel use"
+        runs[name] = (algo.flat.flat.detach().cpu().double().numpy(), stats.astype(np.float64), norms)
+    pe, se, ne = runs["epoch"]
+    pm, sm, nm = runs["minibatch"]
+    pu, su, nu = runs["minibatch_ulp"]
+    rel = lambda a, b: float(np.linalg.norm(a - b) / np.linalg.norm(b))
+    drift, floor = rel(pe, pm), rel(pu, pm)
+    last = slice(-2048, None)
+    stat_drift = np.abs(se[last, :6].mean(0) - sm[last, :6].mean(0))
+    stat_floor = np.abs(su[last, :6].mean(0) - sm[last, :6].mean(0))
+    print(f"C4 horizon: |p_epoch - p_minibatch|/|p| = {drift:.3e}, ulp floor {floor:.3e}; max abs param diff "
+          f"{np.abs(pe - pm).max():.3e} floor {np.abs(pu - pm).max():.3e}; last-epoch mean stats diff {stat_drift} "
+          f"floor {stat_floor}; grad norms rel {rel(ne, nm):.3e} floor {rel(nu, nm):.3e}")
+    assert np.isfinite(pe).all() and np.isfinite(se).all() and np.isfinite(ne).all()
+    assert drift <= max(4 * floor, 1e-5), (drift, floor)
+    assert rel(ne, nm) <= max(4 * rel(nu, nm), 1e-4)
+    assert (stat_drift <= np.maximum(4 * stat_floor, 1e-4 * (1 + np.abs(sm[last, :6].mean(0))))).all()
+
+
 @pytest.mark.parametrize("kind,hidden,act,extra", [
     ("halfcheetah", 256, "relu", dict(ent_coef=0.01)),                     # the C4 policy
     ("halfcheetah", 128, "tanh", dict(clip_range_vf=0.2)),
