@@ -514,11 +514,12 @@ def test_wide_epoch_full_c4_horizon_drift(monkeypatch):
     r = gen.rollout(gamma=0.98, gae_lambda=0.92)
     p0 = torch.nn.utils.parameters_to_vector(policy.parameters()).detach().clone()
     runs = {}
-    for name, epoch, perturb in (("epoch", "1", False), ("minibatch", "0", False), ("minibatch_ulp", "0", True)):
+    for name, epoch, perturb in (("epoch", "1", 0), ("minibatch", "0", 0), ("minibatch_ulp", "0", 1),
+                                 ("minibatch_ulp_down", "0", -1)):
         monkeypatch.setenv("RAI_WIDE_EPOCH", epoch)
         start = p0.clone()
         if perturb:
-            start = torch.nextafter(start, torch.full_like(start, float("inf")))
+            start = torch.nextafter(start, torch.full_like(start, perturb * float("inf")))
         torch.nn.utils.vector_to_parameters(start, policy.parameters())
         algo = PPO(policy, DEV, None, batch_size=64, n_epochs=20, gamma=0.98, gae_lambda=0.92,
                    ent_coef=0.000401762, max_grad_norm=0.8, vf_coef=0.58096, learning_rate=2.0633e-05,
@@ -533,19 +534,25 @@ def test_wide_epoch_full_c4_horizon_drift(monkeypatch):
         runs[name] = (algo.flat.flat.detach().cpu().double().numpy(), stats.astype(np.float64), norms)
     pe, se, ne = runs["epoch"]
     pm, sm, nm = runs["minibatch"]
-    pu, su, nu = runs["minibatch_ulp"]
+    ulps = [runs["minibatch_ulp"], runs["minibatch_ulp_down"]]
     rel = lambda a, b: float(np.linalg.norm(a - b) / np.linalg.norm(b))
-    drift, floor = rel(pe, pm), rel(pu, pm)
+    drift, floor = rel(pe, pm), max(rel(pu, pm) for pu, _, _ in ulps)
     last = slice(-2048, None)
     stat_drift = np.abs(se[last, :6].mean(0) - sm[last, :6].mean(0))
-    stat_floor = np.abs(su[last, :6].mean(0) - sm[last, :6].mean(0))
+    stat_floor = np.max([np.abs(su[last, :6].mean(0) - sm[last, :6].mean(0)) for _, su, _ in ulps], axis=0)
+    norm_floor = max(rel(nu, nm) for _, _, nu in ulps)
     print(f"C4 horizon: |p_epoch - p_minibatch|/|p| = {drift:.3e}, ulp floor {floor:.3e}; max abs param diff "
-          f"{np.abs(pe - pm).max():.3e} floor {np.abs(pu - pm).max():.3e}; last-epoch mean stats diff {stat_drift} "
-          f"floor {stat_floor}; grad norms rel {rel(ne, nm):.3e} floor {rel(nu, nm):.3e}")
+          f"{np.abs(pe - pm).max():.3e}; last-epoch mean stats diff {stat_drift} floor {stat_floor}; "
+          f"grad norms rel {rel(ne, nm):.3e} floor {norm_floor:.3e}")
     assert np.isfinite(pe).all() and np.isfinite(se).all() and np.isfinite(ne).all()
     assert drift <= max(4 * floor, 1e-5), (drift, floor)
-    assert rel(ne, nm) <= max(4 * rel(nu, nm), 1e-4)
-    assert (stat_drift <= np.maximum(4 * stat_floor, 1e-4 * (1 + np.abs(sm[last, :6].mean(0))))).all()
+    assert rel(ne, nm) <= max(4 * norm_floor, 1e-4)
+    # clipped_frac (column 4) is a mean of 131,072 per-sample indicators: once the trajectories have
+    # decorrelated to the ulp floor, its difference is sampling noise, 3 binomial standard deviations
+    p_clip = float(sm[last, 4].mean())
+    tol = np.maximum(4 * stat_floor, 1e-4 * (1 + np.abs(sm[last, :6].mean(0))))
+    tol[4] = max(tol[4], 3 * np.sqrt(p_clip * (1 - p_clip) / (2048 * 64)))
+    assert (stat_drift <= tol).all(), (stat_drift, tol)
 
 
 @pytest.mark.parametrize("kind,hidden,act,extra", [
