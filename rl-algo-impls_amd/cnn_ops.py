@@ -14,8 +14,9 @@ Convolutions on hand-written MFMA kernels (round 3, csrc/conv.hip).  The forward
 conv -> ReLU pair is ONE launch, rai_conv2d_bias_relu_fwd (f32 MFMA implicit GEMM, bias + ReLU in its
 store, conv3 writing nn.Flatten's NCHW order directly), and the weight gradient is
 rai_conv2d_wgrad (f32 MFMA, fixed-order split reduction) added straight into the flat .grad view.
-The input gradient (conv2, conv3) is rai_conv2d_dgrad (f32 MFMA over same-parity pixel classes).  Shapes those kernels do not take fall back to
-MIOpen (still on the GPU); RAI_CONV_MFMA=0 selects MIOpen everywhere (same-box A/B).
+The input gradient (conv2, conv3) is rai_conv2d_dgrad (f32 MFMA: per image, a GEMM over its output
+pixels and a col2im in LDS).  Shapes those kernels do not take fall back to MIOpen (still on the GPU);
+RAI_CONV_MFMA=0 selects MIOpen everywhere (same-box A/B).
 
 Direct gradient accumulation.  Inside the trainer's update (`direct_grads(module)`), every
 parameter's .grad is a view into the flat gradient buffer (optim.FlatParams), zeroed by the
@@ -183,7 +184,9 @@ _WS = _Workspaces()
 _CONV_MFMA = os.environ.get("RAI_CONV_MFMA", "1") != "0"
 _FC_ADDMM_RELU = os.environ.get("RAI_FC_ADDMM_RELU", "1") != "0"  # +0.4 % C3 (r3zk)
 _CONV_FUSE_RELU_BWD = os.environ.get("RAI_CONV_FUSE_RELU_BWD", "1") != "0"  # +0.45 % C3 (r3z)
-_CONV_MFMA_DGRAD = os.environ.get("RAI_CONV_MFMA_DGRAD", "0") == "1"  # measured no faster than MIOpen (r3u)
+# the per-image input-gradient kernel (round 4): conv2 26.8 vs MIOpen 33.2 us, conv3 21.0 vs 27.7 us at B = 256,
+# C3 155.6-156.2k vs 150.9-152.9k env-steps/s same box (profiles/r4e_*); RAI_CONV_MFMA_DGRAD=0 restores MIOpen's dx
+_CONV_MFMA_DGRAD = os.environ.get("RAI_CONV_MFMA_DGRAD", "1") == "1"
 
 
 class _WgradWorkspaces:

@@ -766,6 +766,131 @@ int launch_dgrad_lds(const ConvDgradArgs& a, hipStream_t st) {
   return RAI_OK;
 }
 
+// The input gradient per IMAGE, as a GEMM over the image's output pixels followed by col2im in LDS
+// (round 4).  For image n: dxc[(tap, ci)][p] = sum_co W[co][tap][ci] * dz[n][p][co] over the OH*OW
+// output pixels p -- every (pixel, tap) product lands inside the input (no border taps computed as
+// zeros, unlike the pixel-class form above) -- then dx[n][p*S + tap] += dxc, summed over the taps in
+// a fixed (kh, kw) order.  The workgroup's waves own disjoint (16-ci block, tap-parity class (kh % S,
+// kw % S)) pairs: a class's taps write only input pixels of that parity, so no two waves touch the same
+// dx element and one wave's adds run in program order -- deterministic without atomics or barriers.
+// MFMA rows = ci, columns = output pixels, reduction = co (16 per quad, the 4-wide trick along co: one
+// float4 of dz per lane, four strided W loads per tap); a wave holds TC taps x MT pixel tiles of
+// accumulators.  The image's dx is assembled in LDS (pixel stride Ci + 4 floats: the 16 pixel lanes of
+// an add land on distinct banks) and written once, coalesced.  NatureCNN: conv2 (4x4/2, 64 -> 32 ch,
+// 9x9 -> 20x20) = 8 waves x 4 taps x 6 tiles, conv3 (3x3/1, 64 -> 64, 7x7 -> 9x9) = 4 waves x 9 x 4.
+template <int TC, int MT, int NT, int PF>
+__global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float dxl[];  // [H * W][Ci + 4]
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int NCB = a.Ci >> 4;
+  const int cb = wv % NCB, cls = wv / NCB;
+  const int ph = cls / a.S, pw = cls - ph * a.S;
+  const int TW = a.KW / a.S;
+  const int CP = a.Ci + 4;
+  const int HW = a.H * a.W, OHW = a.OH * a.OW;
+  for (int e = threadIdx.x; e < HW * CP / 4; e += NT) reinterpret_cast<f4*>(dxl)[e] = f4{0.f, 0.f, 0.f, 0.f};
+  const float* dzn = a.dz + (int64_t)n * OHW * a.Co;
+  const int64_t wco = (int64_t)a.KH * a.KW * a.Ci;  // W stride of one co
+  int woff[TC];
+#pragma unroll
+  for (int t = 0; t < TC; ++t) {
+    const int th = t / TW, tw = t - th * TW;
+    woff[t] = ((ph + a.S * th) * a.KW + pw + a.S * tw) * a.Ci + 16 * cb + li;
+  }
+  int poff[MT];
+  bool pv[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int p = 16 * mt + li;
+    pv[mt] = p < OHW;
+    poff[mt] = (pv[mt] ? p : 0) * a.Co;
+  }
+  f4 acc[TC][MT];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int q, float (&Wv)[TC][4], f4 (&Dv)[MT]) {
+    const int co0 = 4 * (4 * q + g);
+    const float* wq = a.w + (int64_t)co0 * wco;
+#pragma unroll
+    for (int t = 0; t < TC; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Wv[t][j] = wq[j * wco + woff[t]];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      Dv[mt] = pv[mt] ? *reinterpret_cast<const f4*>(dzn + poff[mt] + co0) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  const int nq = a.Co >> 4;
+  float Wv[PF][TC][4];
+  f4 Dv[PF][MT];
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nq) load(u, Wv[u], Dv[u]);
+  for (int q = 0; q < nq; q += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (q + u < nq) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int t = 0; t < TC; ++t)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+              acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wv[u][t][j], Dv[u][mt][j], acc[t][mt], 0, 0, 0);
+      }
+      if (q + u + PF < nq) load(q + u + PF, Wv[u], Dv[u]);
+    }
+  }
+  __syncthreads();  // LDS zeroed by every thread
+  // col2im: lane (i, g) holds ci rows 16 cb + 4g .. +3 of output pixel p = 16 mt + i; taps in order
+#pragma unroll
+  for (int t = 0; t < TC; ++t) {
+    const int th = t / TW, tw = t - th * TW;
+    const int kh = ph + a.S * th, kw = pw + a.S * tw;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      if (!pv[mt]) continue;
+      const int p = 16 * mt + li;
+      const int oh = p / a.OW, ow = p - oh * a.OW;
+      f4* d = reinterpret_cast<f4*>(dxl + ((oh * a.S + kh) * a.W + ow * a.S + kw) * CP + 16 * cb + 4 * g);
+      *d += acc[t][mt];
+    }
+  }
+  __syncthreads();
+  float* dxn = a.dx + (int64_t)n * HW * a.Ci;
+  const int c4 = a.Ci >> 2;
+  for (int e = threadIdx.x; e < HW * c4; e += NT) {
+    const int px = e / c4, c = e - px * c4;
+    reinterpret_cast<f4*>(dxn)[e] = *reinterpret_cast<const f4*>(dxl + px * CP + 4 * c);
+  }
+}
+
+template <int TC, int MT, int NT>
+int launch_dgrad_img(const ConvDgradArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)a.H * a.W * (a.Ci + 4) * sizeof(float);
+  if (lds > 160 * 1024) return RAI_E_SHAPE;
+  auto k = conv_dgrad_img_kernel<TC, MT, NT, 2>;
+  const int e = allow_lds(reinterpret_cast<const void*>(k));
+  if (e != RAI_OK) return e;
+  if (a.B > 0x7fffffffLL) return RAI_E_SHAPE;
+  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(NT), lds, st, a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+// the per-image form's instantiation for this shape: 1 = conv3-like, 2 = conv2-like, 0 = none
+static int dgrad_img_kind(const ConvDgradArgs& a) {
+  if (a.Ci % 16 || a.Co % 16 || a.KH % a.S || a.KW % a.S) return 0;
+  const int nw = (a.Ci / 16) * a.S * a.S, tc = (a.KH / a.S) * (a.KW / a.S), mt = (a.OH * a.OW + 15) / 16;
+  if ((size_t)a.H * a.W * (a.Ci + 4) * sizeof(float) > 160 * 1024) return 0;
+  if (nw == 4 && tc == 9 && mt == 4) return 1;
+  if (nw == 8 && tc == 4 && mt == 6) return 2;
+  return 0;
+}
+
 }  // namespace
 
 extern "C" int64_t rai_conv2d_wgrad_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
@@ -1043,6 +1168,14 @@ extern "C" int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, in
   a.OW = (W - KW) / stride + 1;
   const int64_t maxcls = B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
   hipStream_t st = rai_stream(stream);
+  // variant 0: the per-image GEMM + col2im form where it is instantiated (NatureCNN conv2 / conv3),
+  // else the pixel-class form; 3: the per-image form only (RAI_E_UNSUPPORTED where not instantiated)
+  const int kind = dgrad_img_kind(a);
+  if (variant == 0 || variant == 3) {
+    if (kind == 1) return launch_dgrad_img<9, 4, 256>(a, st);
+    if (kind == 2) return launch_dgrad_img<4, 6, 512>(a, st);
+    if (variant == 3) return RAI_E_UNSUPPORTED;
+  }
   if (variant == 1 && Ci == 32) return launch_dgrad_lds<2, 2, 1>(a, st);  // LDS weights, 32 ci x 32 px per wave
   if (variant == 2 && Ci == 32) return launch_dgrad_lds<2, 1, 1>(a, st);  // LDS weights, 32 ci x 16 px per wave
   if (variant == 1 && Ci == 64) return launch_dgrad_lds<2, 1, 2>(a, st);  // LDS weights, ci halves over waves

@@ -141,7 +141,7 @@ def main():
                     r = ref_dgrad()
                     row["dgrad_relerr"] = ((dx - r).abs().max() / r.abs().max()).item()
                     row["dgrad_us"] = round(timeit(mine_dgrad, args.reps), 2)
-                    for dv in (1, 2):
+                    for dv in (1, 2, 3):
                         def mine_dgrad_v():
                             return L.rai_conv2d_dgrad_v(dz.data_ptr(), wt.data_ptr(), B, H, H, Ci, Co, k, k, s,
                                                         dx.data_ptr(), dv, st)
