@@ -846,18 +846,35 @@ __global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs 
   }
   __syncthreads();  // LDS zeroed by every thread
   // col2im: lane (i, g) holds ci rows 16 cb + 4g .. +3 of output pixel p = 16 mt + i; taps in order
+  int pbase[MT];  // this lane's dx LDS offset of tap (0, 0) per pixel tile
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int p = 16 * mt + li;
+    const int oh = p / a.OW, ow = p - oh * a.OW;
+    pbase[mt] = ((oh * a.S + ph) * a.W + ow * a.S + pw) * CP + 16 * cb + 4 * g;
+  }
 #pragma unroll
   for (int t = 0; t < TC; ++t) {
     const int th = t / TW, tw = t - th * TW;
-    const int kh = ph + a.S * th, kw = pw + a.S * tw;
+    const int toff = (a.S * th * a.W + a.S * tw) * CP;
+#ifdef RAI_DGRAD_BATCH_COL2IM
+    // one tap's tiles touch distinct dx pixels: all their reads, then the adds, then the writes (one LDS
+    // round trip per tap instead of one per tile)
+    f4 cur[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      if (pv[mt]) cur[mt] = *reinterpret_cast<const f4*>(dxl + pbase[mt] + toff);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      if (pv[mt]) *reinterpret_cast<f4*>(dxl + pbase[mt] + toff) = cur[mt] + acc[t][mt];
+#else
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       if (!pv[mt]) continue;
-      const int p = 16 * mt + li;
-      const int oh = p / a.OW, ow = p - oh * a.OW;
-      f4* d = reinterpret_cast<f4*>(dxl + ((oh * a.S + kh) * a.W + ow * a.S + kw) * CP + 16 * cb + 4 * g);
+      f4* d = reinterpret_cast<f4*>(dxl + pbase[mt] + toff);
       *d += acc[t][mt];
     }
+#endif
   }
   __syncthreads();
   float* dxn = a.dx + (int64_t)n * HW * a.Ci;
@@ -866,6 +883,162 @@ __global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs 
     const int px = e / c4, c = e - px * c4;
     reinterpret_cast<f4*>(dxn)[e] = *reinterpret_cast<const f4*>(dxl + px * CP + 4 * c);
   }
+}
+
+// The same per-image input gradient with the weight operand staged through LDS, transposed to
+// [tap][ci][co] one 16-co quad at a time (double-buffered): per quad the workgroup loads the contiguous
+// 16 x KH*KW*Ci block of W with 16-B loads and writes it with 16-B LDS stores along co, and the MFMA's
+// weight operand is one ds_read_b128 per tap (instead of four strided 4-B global loads per tap).  Row
+// stride 16 + 4 floats: the 16 ci lanes of a read land on distinct banks.
+template <int TC, int MT, int NT, int SI>
+__global__ __launch_bounds__(NT) void conv_dgrad_img_lds_kernel(const ConvDgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int WR = 20;  // floats per (tap, ci) row of a staged quad
+  const int KK = a.KH * a.KW;
+  const int CP = a.Ci + 4;
+  const int HW = a.H * a.W, OHW = a.OH * a.OW;
+  float* const dxl = lds;                          // [HW][CP]
+  float* const wb0 = lds + ((HW * CP + 3) & ~3);  // [2][KK][Ci][WR]
+  const int wbuf = KK * a.Ci * WR;
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int NCB = a.Ci >> 4;
+  const int cb = wv % NCB, cls = wv / NCB;
+  const int ph = cls / a.S, pw = cls - ph * a.S;
+  const int TW = a.KW / a.S;
+  for (int e = threadIdx.x; e < HW * CP / 4; e += NT) reinterpret_cast<f4*>(dxl)[e] = f4{0.f, 0.f, 0.f, 0.f};
+  // staging items of a quad: (tap, 4-ci group, 4-co group): 4 global float4 (co m = 0..3) -> 4 LDS float4
+  const int ci4n = a.Ci >> 2;
+  const int nitems = KK * ci4n * 4;
+  const int64_t wco = (int64_t)KK * a.Ci;
+  auto stage_load = [&](int q, int item, f4 (&r)[4]) {
+    const int cg = item & 3, rest = item >> 2, c4 = rest % ci4n, tap = rest / ci4n;
+    const float* src = a.w + (int64_t)(16 * q + 4 * cg) * wco + tap * a.Ci + 4 * c4;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) r[m] = *reinterpret_cast<const f4*>(src + m * wco);
+  };
+  auto stage_store = [&](int buf, int item, const f4 (&r)[4]) {
+    const int cg = item & 3, rest = item >> 2, c4 = rest % ci4n, tap = rest / ci4n;
+    float* dst = wb0 + buf * wbuf + (tap * a.Ci + 4 * c4) * WR + 4 * cg;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      *reinterpret_cast<f4*>(dst + c * WR) = f4{r[0][c], r[1][c], r[2][c], r[3][c]};
+  };
+  const float* dzn = a.dz + (int64_t)n * OHW * a.Co;
+  int woff[TC];
+#pragma unroll
+  for (int t = 0; t < TC; ++t) {
+    const int th = t / TW, tw = t - th * TW;
+    woff[t] = (((ph + a.S * th) * a.KW + pw + a.S * tw) * a.Ci + 16 * cb + li) * WR + 4 * g;
+  }
+  int poff[MT];
+  bool pv[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int p = 16 * mt + li;
+    pv[mt] = p < OHW;
+    poff[mt] = (pv[mt] ? p : 0) * a.Co;
+  }
+  auto load_dz = [&](int q, f4 (&Dv)[MT]) {
+    const int co0 = 4 * (4 * q + g);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      Dv[mt] = pv[mt] ? *reinterpret_cast<const f4*>(dzn + poff[mt] + co0) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  f4 acc[TC][MT];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  const int nq = a.Co >> 4;
+  f4 sr[SI][4];
+#pragma unroll
+  for (int u = 0; u < SI; ++u) {
+    const int item = threadIdx.x + u * NT;
+    if (item < nitems) stage_load(0, item, sr[u]);
+  }
+  f4 Dv[MT];
+  load_dz(0, Dv);
+#pragma unroll
+  for (int u = 0; u < SI; ++u) {
+    const int item = threadIdx.x + u * NT;
+    if (item < nitems) stage_store(0, item, sr[u]);
+  }
+  __syncthreads();
+  for (int q = 0; q < nq; ++q) {
+    const int buf = q & 1;
+    if (q + 1 < nq) {
+#pragma unroll
+      for (int u = 0; u < SI; ++u) {
+        const int item = threadIdx.x + u * NT;
+        if (item < nitems) stage_load(q + 1, item, sr[u]);
+      }
+    }
+    f4 Dn[MT];
+    if (q + 1 < nq) load_dz(q + 1, Dn);
+    f4 A[TC];
+#pragma unroll
+    for (int t = 0; t < TC; ++t) A[t] = *reinterpret_cast<const f4*>(wb0 + buf * wbuf + woff[t]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][j], Dv[mt][j], acc[t][mt], 0, 0, 0);
+    if (q + 1 < nq) {
+#pragma unroll
+      for (int u = 0; u < SI; ++u) {
+        const int item = threadIdx.x + u * NT;
+        if (item < nitems) stage_store(buf ^ 1, item, sr[u]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) Dv[mt] = Dn[mt];
+    }
+    __syncthreads();
+  }
+  int pbase[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int p = 16 * mt + li;
+    const int oh = p / a.OW, ow = p - oh * a.OW;
+    pbase[mt] = ((oh * a.S + ph) * a.W + ow * a.S + pw) * CP + 16 * cb + 4 * g;
+  }
+#pragma unroll
+  for (int t = 0; t < TC; ++t) {
+    const int th = t / TW, tw = t - th * TW;
+    const int toff = (a.S * th * a.W + a.S * tw) * CP;
+    f4 cur[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      if (pv[mt]) cur[mt] = *reinterpret_cast<const f4*>(dxl + pbase[mt] + toff);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      if (pv[mt]) *reinterpret_cast<f4*>(dxl + pbase[mt] + toff) = cur[mt] + acc[t][mt];
+  }
+  __syncthreads();
+  float* dxn = a.dx + (int64_t)n * HW * a.Ci;
+  const int c4 = a.Ci >> 2;
+  for (int e = threadIdx.x; e < HW * c4; e += NT) {
+    const int px = e / c4, c = e - px * c4;
+    reinterpret_cast<f4*>(dxn)[e] = *reinterpret_cast<const f4*>(dxl + px * CP + 4 * c);
+  }
+}
+
+// SI: staging items per thread per quad (conv3: 576 items / 256 threads -> 3; conv2: 512 / 512 -> 1)
+template <int TC, int MT, int NT, int SI>
+int launch_dgrad_img_lds(const ConvDgradArgs& a, hipStream_t st) {
+  const int KK = a.KH * a.KW;
+  const size_t lds = ((size_t)a.H * a.W * (a.Ci + 4) + 3) / 4 * 4 * sizeof(float) + 2 * (size_t)KK * a.Ci * 20 * sizeof(float);
+  if (lds > 160 * 1024 || KK * (a.Ci / 4) * 4 > SI * NT || a.Co % 16) return RAI_E_SHAPE;
+  auto k = conv_dgrad_img_lds_kernel<TC, MT, NT, SI>;
+  const int e = allow_lds(reinterpret_cast<const void*>(k));
+  if (e != RAI_OK) return e;
+  if (a.B > 0x7fffffffLL) return RAI_E_SHAPE;
+  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(NT), lds, st, a);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
 }
 
 template <int TC, int MT, int NT>
@@ -1175,6 +1348,11 @@ extern "C" int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, in
     if (kind == 1) return launch_dgrad_img<9, 4, 256>(a, st);
     if (kind == 2) return launch_dgrad_img<4, 6, 512>(a, st);
     if (variant == 3) return RAI_E_UNSUPPORTED;
+  }
+  if (variant == 4) {  // the per-image form with the weight operand staged through LDS
+    if (kind == 1) return launch_dgrad_img_lds<9, 4, 256, 3>(a, st);
+    if (kind == 2) return launch_dgrad_img_lds<4, 6, 512, 1>(a, st);
+    return RAI_E_UNSUPPORTED;
   }
   if (variant == 1 && Ci == 32) return launch_dgrad_lds<2, 2, 1>(a, st);  // LDS weights, 32 ci x 32 px per wave
   if (variant == 2 && Ci == 32) return launch_dgrad_lds<2, 1, 1>(a, st);  // LDS weights, 32 ci x 16 px per wave
