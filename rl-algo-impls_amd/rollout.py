@@ -459,20 +459,21 @@ class SyncStepRolloutGenerator(RolloutGenerator):
     # an observation batch at least this large goes host -> device straight from the env's array
     _DIRECT_OBS_BYTES = 1 << 20
 
-    def _stage_obs(self, obs: np.ndarray) -> None:
+    def _stage_obs(self, obs: np.ndarray, dst: Optional[torch.Tensor] = None) -> None:
         """The next observation batch into next_obs_dev.  Large batches (C3 Pong: 1024 x 4x84x84 u8,
         29 MB) are copied straight from the env's pageable array: HIP's pageable path (~0.54 ms,
         ~53 GB/s, returns when the copy is done) is as fast as the DMA from pinned memory alone,
         while staging through the pinned buffer first costs a single-threaded host memcpy of the
         whole batch (1.35 ms; profiles/r2s_rollout_timing.txt).  Small batches keep the pinned
         buffer and an asynchronous copy."""
+        dst = self.next_obs_dev if dst is None else dst
         if (obs.nbytes >= self._DIRECT_OBS_BYTES and isinstance(obs, np.ndarray) and obs.flags.c_contiguous
                 and obs.flags.writeable and torch.from_numpy(obs[:0]).dtype == self.obs_dtype
-                and obs.shape == tuple(self.next_obs_dev.shape)):
-            self.next_obs_dev.copy_(torch.from_numpy(obs))
+                and obs.shape == tuple(dst.shape)):
+            dst.copy_(torch.from_numpy(obs))
             return
         np.copyto(self.h_obs.numpy(), obs, casting="same_kind")
-        self.next_obs_dev.copy_(self.h_obs, non_blocking=True)
+        dst.copy_(self.h_obs, non_blocking=True)
 
     def _sample(self, params: torch.Tensor, v: torch.Tensor, s: int) -> None:
         L = _lib.lib()
@@ -498,9 +499,14 @@ class SyncStepRolloutGenerator(RolloutGenerator):
     def _rollout(self, output_next_values: bool) -> Optional[torch.Tensor]:
         self.policy.eval()
         net = self.policy.network
+        # the fused CartPole-class step reads its slot directly: each step's next observations and episode
+        # starts go host -> device straight into slot s + 1 (two device copies per step fewer); the other
+        # policies' graph-replayed forwards read the fixed next_obs_dev buffer, so they keep the slot copy
+        direct = self.fused_step is not None and os.environ.get("RAI_ROLLOUT_DIRECT", "1") != "0"
         for s in range(self.n_steps):
-            self.obs[s].copy_(self.next_obs_dev)
-            self.episode_starts[s].copy_(self.next_episode_starts)
+            if not direct or s == 0:
+                self.obs[s].copy_(self.next_obs_dev)
+                self.episode_starts[s].copy_(self.next_episode_starts)
             if self.action_masks is not None:
                 self.action_masks[s].copy_(self.next_masks_dev)
             if self.fused_step is not None:
@@ -523,8 +529,10 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             np.copyto(self.h_rew.numpy(), rew, casting="same_kind")
             np.logical_or(term, trunc, out=self.h_done.numpy())
             self.rewards[s].copy_(self.h_rew, non_blocking=True)
-            self.next_episode_starts.copy_(self.h_done, non_blocking=True)
-            self._stage_obs(obs)
+            into_slot = direct and s + 1 < self.n_steps
+            (self.episode_starts[s + 1] if into_slot else self.next_episode_starts).copy_(self.h_done,
+                                                                                           non_blocking=True)
+            self._stage_obs(obs, self.obs[s + 1] if into_slot else None)
             self._stage_masks()
         next_values = None
         if output_next_values:

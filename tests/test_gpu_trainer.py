@@ -644,3 +644,32 @@ def test_wide_rollout_forward_matches_module(kind, N, monkeypatch):
     np.testing.assert_allclose(n1, n0, rtol=1e-4, atol=1e-5)
     same = (a1 == a0) if kind == "cartpole" else np.ones(l1.shape, dtype=bool)
     np.testing.assert_allclose(l1[same], l0[same], rtol=1e-4, atol=1e-5)
+
+
+def test_fused_rollout_direct_slot_staging_is_identical(monkeypatch):
+    """The CartPole-class rollout stages each step's next observations and episode starts straight into
+    slot s + 1 (RAI_ROLLOUT_DIRECT, default on) instead of through next_obs_dev / next_episode_starts
+    and a device copy: two seeded rollouts (two updates' worth, so the second starts from the first's
+    carried-over state), one each way, give bit-identical buffers and bootstrap values."""
+    from rl_algo_impls_amd.envs import SyntheticVecEnv
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    out = []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("RAI_ROLLOUT_DIRECT", direct)
+        torch.manual_seed(3)
+        env = SyntheticVecEnv(96, "cartpole", seed=5)
+        policy = ActorCritic(env).to(DEV)
+        gen = SyncStepRolloutGenerator(policy, env, n_steps=16, seed=9)
+        assert gen.fused_step is not None
+        res = []
+        for _ in range(2):
+            r = gen.rollout(gamma=0.98, gae_lambda=0.8)
+            torch.cuda.synchronize()
+            res.append([t.detach().cpu().numpy().copy() for t in (gen.obs, gen.actions, gen.rewards, gen.episode_starts,
+                                                                   gen.values, gen.logprobs, r.next_values,
+                                                                   r.next_episode_starts, r.advantages)])
+        out.append(res)
+    for a, b in zip(out[0], out[1]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
