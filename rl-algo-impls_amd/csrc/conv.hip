@@ -778,7 +778,7 @@ int launch_dgrad_lds(const ConvDgradArgs& a, hipStream_t st) {
 // accumulators.  The image's dx is assembled in LDS (pixel stride Ci + 4 floats: the 16 pixel lanes of
 // an add land on distinct banks) and written once, coalesced.  NatureCNN: conv2 (4x4/2, 64 -> 32 ch,
 // 9x9 -> 20x20) = 8 waves x 4 taps x 6 tiles, conv3 (3x3/1, 64 -> 64, 7x7 -> 9x9) = 4 waves x 9 x 4.
-template <int TC, int MT, int NT, int PF>
+template <int TC, int MT, int NT, int PF, bool BUF = false>
 __global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float dxl[];  // [H * W][Ci + 4]
   const int n = blockIdx.x;
@@ -812,7 +812,30 @@ __global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs 
   for (int t = 0; t < TC; ++t)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  // BUF: buffer loads with the lane-invariant part of every offset in a scalar register (no per-load
+  // 64-bit address arithmetic); a masked pixel's offset points past the image's dz, which reads 0
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.w), 0,
+                                                                       (int)(a.Co * wco * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dzn), 0,
+                                                                       OHW * a.Co * 4, 0x00020000);
+  int wvo[TC], dvo[MT];
+#pragma unroll
+  for (int t = 0; t < TC; ++t) wvo[t] = 4 * (int)(4 * g * wco + woff[t]);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) dvo[mt] = pv[mt] ? 4 * (poff[mt] + 4 * g) : OHW * a.Co * 4;
   auto load = [&](int q, float (&Wv)[TC][4], f4 (&Dv)[MT]) {
+    if (BUF) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int so = 4 * (int)((16 * q + j) * wco);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) Wv[t][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wrs, wvo[t], so, 0));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        Dv[mt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(drs, dvo[mt], 64 * q, 0));
+      return;
+    }
     const int co0 = 4 * (4 * q + g);
     const float* wq = a.w + (int64_t)co0 * wco;
 #pragma unroll
@@ -1041,11 +1064,12 @@ int launch_dgrad_img_lds(const ConvDgradArgs& a, hipStream_t st) {
   return RAI_OK;
 }
 
-template <int TC, int MT, int NT>
+template <int TC, int MT, int NT, int PF = 2, bool BUF = false>
 int launch_dgrad_img(const ConvDgradArgs& a, hipStream_t st) {
   const size_t lds = (size_t)a.H * a.W * (a.Ci + 4) * sizeof(float);
   if (lds > 160 * 1024) return RAI_E_SHAPE;
-  auto k = conv_dgrad_img_kernel<TC, MT, NT, 2>;
+  if (BUF && (int64_t)a.Co * a.KH * a.KW * a.Ci * 4 >= (1LL << 31)) return RAI_E_SHAPE;
+  auto k = conv_dgrad_img_kernel<TC, MT, NT, PF, BUF>;
   const int e = allow_lds(reinterpret_cast<const void*>(k));
   if (e != RAI_OK) return e;
   if (a.B > 0x7fffffffLL) return RAI_E_SHAPE;
@@ -1341,13 +1365,26 @@ extern "C" int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, in
   a.OW = (W - KW) / stride + 1;
   const int64_t maxcls = B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
   hipStream_t st = rai_stream(stream);
-  // variant 0: the per-image GEMM + col2im form where it is instantiated (NatureCNN conv2 / conv3),
-  // else the pixel-class form; 3: the per-image form only (RAI_E_UNSUPPORTED where not instantiated)
+  // variant 0: the per-image GEMM + col2im form where it is instantiated (NatureCNN conv2 / conv3), with
+  // buffer loads (B = 256: conv2 21.9 us with 2 quads in flight, conv3 18.2 us with 3, against 26.0 /
+  // 19.1 us with pointer loads and MIOpen's 33.2 / 27.7; profiles/r4f_dgrad_probe.txt), else the
+  // pixel-class form; 3: the per-image form with pointer loads (RAI_E_UNSUPPORTED where not instantiated)
   const int kind = dgrad_img_kind(a);
-  if (variant == 0 || variant == 3) {
+  if (variant == 0 && kind == 1) return launch_dgrad_img<9, 4, 256, 3, true>(a, st);
+  if (variant == 0 && kind == 2) return launch_dgrad_img<4, 6, 512, 2, true>(a, st);
+  if (variant == 3) {
     if (kind == 1) return launch_dgrad_img<9, 4, 256>(a, st);
     if (kind == 2) return launch_dgrad_img<4, 6, 512>(a, st);
     if (variant == 3) return RAI_E_UNSUPPORTED;
+  }
+  if (variant >= 5 && variant <= 7) {  // the per-image form: buffer loads (5), + 3 / 4 quads in flight (6 / 7)
+    if (kind == 1 && variant == 5) return launch_dgrad_img<9, 4, 256, 2, true>(a, st);
+    if (kind == 1 && variant == 6) return launch_dgrad_img<9, 4, 256, 3, true>(a, st);
+    if (kind == 1 && variant == 7) return launch_dgrad_img<9, 4, 256, 4, true>(a, st);
+    if (kind == 2 && variant == 5) return launch_dgrad_img<4, 6, 512, 2, true>(a, st);
+    if (kind == 2 && variant == 6) return launch_dgrad_img<4, 6, 512, 3, true>(a, st);
+    if (kind == 2 && variant == 7) return launch_dgrad_img<4, 6, 512, 4, true>(a, st);
+    return RAI_E_UNSUPPORTED;
   }
   if (variant == 4) {  // the per-image form with the weight operand staged through LDS
     if (kind == 1) return launch_dgrad_img_lds<9, 4, 256, 3>(a, st);

@@ -222,12 +222,13 @@ DGRAD_CASES = [  # (Ci, H, Co, k, stride): NatureCNN conv2 / conv3, odd sizes, a
 
 @pytest.mark.parametrize("case", DGRAD_CASES, ids=lambda c: "x".join(str(v) for v in c))
 @pytest.mark.parametrize("B", [1, 3, 64])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_conv_dgrad_matches_fp64(case, B, variant):
     """rai_conv2d_dgrad_v against fp64 autograd.  Variants: 0 = the shipped choice (the per-image
     GEMM + col2im form for NatureCNN conv2 / conv3, else the pixel-class form), 1 / 2 = the pixel-class
     form with LDS-resident weights, 3 = the per-image form only, 4 = the per-image form with the weight
-    operand staged through LDS (3 and 4: RAI_E_UNSUPPORTED on shapes they have no instantiation for)."""
+    operand staged through LDS, 5 / 6 / 7 = the per-image form with buffer loads and 2 / 3 / 4 quads in
+    flight (3-7: RAI_E_UNSUPPORTED on shapes they have no instantiation for)."""
     Ci, H, Co, k, s = case
     x, w, _ = _inputs(B, Ci, H, Co, k, seed=B + 31)
     OH = (H - k) // s + 1
@@ -237,7 +238,7 @@ def test_conv_dgrad_matches_fp64(case, B, variant):
     dx = torch.full((B, Ci, H, H), float("nan"), device=DEV).contiguous(memory_format=torch.channels_last)
     rc = _lib.lib().rai_conv2d_dgrad_v(dzd.data_ptr(), wd.data_ptr(), B, H, H, Ci, Co, k, k, s, dx.data_ptr(),
                                        variant, _lib.stream_handle(DEV))
-    if variant in (3, 4) and (Ci, H, Co, k, s) not in ((32, 20, 64, 4, 2), (64, 9, 64, 3, 1)):
+    if variant >= 3 and (Ci, H, Co, k, s) not in ((32, 20, 64, 4, 2), (64, 9, 64, 3, 1)):
         assert rc == -6  # RAI_E_UNSUPPORTED
         return
     _lib.check(rc, "rai_conv2d_dgrad")
