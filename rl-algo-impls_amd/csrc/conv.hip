@@ -175,7 +175,7 @@ static int allow_lds(const void* kernel) {
 // one per CU) copies its COT rows x K once (row stride K + 4 floats: the 16 lanes of a ds_read_b128
 // group land on distinct banks), then loops over pixel tiles; only the im2col operand is read from
 // L1/L2 per quad.
-template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF>
+template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF, bool BUF = false>
 __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) {
   static_assert(WCO * WPX == 8, "eight waves");
   constexpr int COT = 16 * TCO * WCO, PXT = 16 * TPX * WPX;
@@ -202,16 +202,21 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   for (int tc = 0; tc < TCO; ++tc) wrow[tc] = wl + (16 * (TCO * wco + tc) + li) * KP;
   const int64_t ntiles = (a.M + PXT - 1) / PXT;
   const int nq = nch >> 2;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x), 0, BUF ? (int)((a.M / (a.OH * a.OW)) * a.H * a.W * a.Ci * 4) : 0, 0x00020000);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t px0 = tile * PXT + 16 * TPX * wpx;
     const float* xb[TPX];
+    int xbo[TPX];  // BUF: the same base as an element offset into x (host: x < 2 GB)
 #pragma unroll
     for (int tp = 0; tp < TPX; ++tp) {
       int64_t p = px0 + 16 * tp + li;
       p = p < a.M ? p : a.M - 1;
       const int64_t n = p / OHW;
       const int r = (int)(p - n * OHW), oh = r / a.OW, ow = r - oh * a.OW;
-      xb[tp] = a.x + ((n * a.H + (int64_t)oh * a.S) * a.W + (int64_t)ow * a.S) * a.Ci;
+      const int64_t base = ((n * a.H + (int64_t)oh * a.S) * a.W + (int64_t)ow * a.S) * a.Ci;
+      xb[tp] = a.x + base;
+      xbo[tp] = (int)base;
     }
     f4 acc[TCO][TPX];
 #pragma unroll
@@ -221,6 +226,12 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
     f4 Br[PF][TPX];
     auto ldb = [&](int qd, f4(&Bv)[TPX]) {
       const int xo = xoff[4 * qd + g];
+      if (BUF) {
+#pragma unroll
+        for (int tp = 0; tp < TPX; ++tp)
+          Bv[tp] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, 4 * (xbo[tp] + xo), 0, 0));
+        return;
+      }
 #pragma unroll
       for (int tp = 0; tp < TPX; ++tp) Bv[tp] = *reinterpret_cast<const f4*>(xb[tp] + xo);
     };
@@ -272,10 +283,11 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   }
 }
 
-template <int TCO, int TPX, int WCO, int WPX, int PF>
+template <int TCO, int TPX, int WCO, int WPX, int PF, bool BUF = false>
 int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   constexpr int PXT = 16 * TPX * WPX, COT = 16 * TCO * WCO;
   if (a.Co % COT) return RAI_E_SHAPE;
+  if (BUF && (a.M / ((int64_t)a.OH * a.OW)) * a.H * a.W * a.Ci * 4 >= (1LL << 31)) return RAI_E_SHAPE;
   const size_t lds = (size_t)COT * (a.K + 4) * sizeof(float);
   if (lds + CV_MAXCHUNK * 4 > 160 * 1024) return RAI_E_SHAPE;
   const int64_t ntiles = (a.M + PXT - 1) / PXT;
@@ -285,12 +297,12 @@ int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   if (gx < 1) gx = 1;
   const dim3 grid((unsigned)gx, (unsigned)cot);
   if (nchw) {
-    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF>;
+    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF, BUF>;
     const int e = allow_lds(reinterpret_cast<const void*>(k));
     if (e != RAI_OK) return e;
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
   } else {
-    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, false, PF>;
+    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, false, PF, BUF>;
     const int e = allow_lds(reinterpret_cast<const void*>(k));
     if (e != RAI_OK) return e;
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
@@ -338,7 +350,7 @@ struct ConvWrwArgs {
   int H, W, Ci, Co, KW, S_, OH, OW, K;
 };
 
-template <int VC, int PF, bool RB>
+template <int VC, int PF, bool RB, bool BUF = false>
 __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs a) {
   constexpr int NB = VC * 4;  // 16x16 accumulator blocks per wave
   __shared__ float dbl[RB ? 4 * 16 * VC : 1];  // RB: the waves' bias-gradient sums
@@ -380,9 +392,29 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
     const float* dzc = a.dz + pbeg * a.Co + VC * li;
     const float* yc = RB ? a.y + pbeg * a.Co + VC * li : nullptr;
     const int nst = (hi - lo + 3) >> 2;
+    // BUF: 32-bit element offsets into buffer resources (host: x, dz < 2 GB) instead of 64-bit pointers
+    const int dzo = (int)(pbeg * a.Co) + VC * li, xco = (int)(n0 * a.H * a.W * a.Ci) + xo;
+    const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dz), 0,
+                                                                         BUF ? (int)(a.M * a.Co * 4) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(RB ? a.y : a.dz), 0,
+                                                                         BUF ? (int)(a.M * a.Co * 4) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x), 0, BUF ? (int)((a.M / (a.OH * a.OW)) * a.H * a.W * a.Ci * 4) : 0, 0x00020000);
+    auto ldz = [&](const __amdgpu_buffer_rsrc_t& rs, int off) -> fv {
+      if constexpr (VC == 4) return __builtin_bit_cast(fv, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * off, 0, 0));
+      else return __builtin_bit_cast(fv, __builtin_amdgcn_raw_buffer_load_b64(rs, 4 * off, 0, 0));
+    };
     auto ld = [&](int st, fv& dv, f4& xv) {
       const int pl = lo + 4 * st + g;
-      if (pl < hi) {
+      if (BUF && pl < hi) {
+        dv = ldz(zrs, dzo + pl * a.Co);
+        if (RB) {
+          const fv yv = ldz(yrs, dzo + pl * a.Co);
+#pragma unroll
+          for (int j = 0; j < VC; ++j) dv[j] = yv[j] > 0.f ? dv[j] : 0.f;
+        }
+        xv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, 4 * (xco + xbase_l[pl]), 0, 0));
+      } else if (pl < hi) {
         dv = *reinterpret_cast<const fv*>(dzc + (int64_t)pl * a.Co);
         if (RB) {
           const fv yv = *reinterpret_cast<const fv*>(yc + (int64_t)pl * a.Co);
@@ -1144,10 +1176,19 @@ static int wgrad_partials(const float* x, const float* dz, const float* y, int64
   if ((int64_t)(WR_MAXPX / (a.OH * a.OW) + 2) * H * W * Ci > 0x7fffffffLL) return RAI_E_SHAPE;
   const dim3 grid((unsigned)p.S, (unsigned)p.KT);
   if (pf <= 0) pf = 4;
+  const bool buf_ok = (int64_t)B * H * W * Ci * 4 < (1LL << 31) && a.M * Co * 4 < (1LL << 31);
+  if (pf >= 100 && !buf_ok) return RAI_E_SHAPE;
   if (y) {  // the ReLU backward and the bias gradient fused in (rai_conv2d_wgrad_relu_partials)
     if (((uintptr_t)y) & 15) return RAI_E_SHAPE;
-    if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true>), grid, dim3(CV_THREADS), 0, st, a);
+    if (pf == 104 && p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else if (pf == 104) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true>), grid, dim3(CV_THREADS), 0, st, a);
     else hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true>), grid, dim3(CV_THREADS), 0, st, a);
+  } else if (pf >= 100) {  // buffer loads, 4 or 8 pixel steps in flight (A/B)
+    if (p.VC == 2 && pf == 104) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, false, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 8, false, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else if (pf == 104) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, false, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((conv_wrw_kernel<4, 8, false, true>), grid, dim3(CV_THREADS), 0, st, a);
   } else if (p.VC == 2) {
     if (pf == 4) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, false>), grid, dim3(CV_THREADS), 0, st, a);
     else hipLaunchKernelGGL((conv_wrw_kernel<2, 8, false>), grid, dim3(CV_THREADS), 0, st, a);
@@ -1323,6 +1364,9 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
     case 13: return launch_fwd_lds<2, 1, 2, 4, 4>(a, nchw, st);  // LDS weights, 64 co x 64 px, 8 waves
     case 14: return launch_fwd_lds<2, 2, 1, 8, 3>(a, nchw, st);  // LDS weights, 32 co x 256 px, 8 waves
     case 15: return launch_fwd_lds<1, 2, 2, 4, 4>(a, nchw, st);  // LDS weights, 32 co x 128 px, 8 waves
+    case 16: return launch_fwd_lds<2, 2, 1, 8, 3, true>(a, nchw, st);  // variant 14, buffer loads
+    case 17: return launch_fwd_lds<2, 1, 2, 4, 4, true>(a, nchw, st);  // variant 13, buffer loads
+    case 18: return launch_fwd_lds<2, 2, 2, 4, 3, true>(a, nchw, st);  // variant 12, buffer loads
     default: return RAI_E_SHAPE;
   }
 }

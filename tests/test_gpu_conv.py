@@ -72,7 +72,7 @@ def test_conv_bias_relu_fwd_matches_fp64(case, B):
     assert (err <= tol).all(), float((err / tol).max())
 
 
-@pytest.mark.parametrize("variant", list(range(1, 16)))
+@pytest.mark.parametrize("variant", list(range(1, 19)))
 def test_conv_every_blocking_variant(variant):
     Ci, H, Co, k, s, flat = 32, 20, 64, 4, 2, False
     x, w, b = _inputs(9, Ci, H, Co, k, seed=3)
@@ -101,7 +101,7 @@ def test_conv_rejects_unsupported_shapes():
     assert L.rai_conv2d_bias_relu_fwd(None, None, None, 1, 8, 8, 8, 16, 2, 2, 1, 0, None, st) == -1
 
 
-def _wgrad(x, dz, KH, KW, stride, dw0=None):
+def _wgrad(x, dz, KH, KW, stride, dw0=None, pf=0):
     """rai_conv2d_wgrad: x (B, Ci, H, W), dz (B, Co, OH, OW) NCHW tensors on the CPU; returns dw in
     (Co, Ci, KH, KW) NCHW order.  dw0: accumulate onto it."""
     B, Ci, H, W = x.shape
@@ -113,8 +113,8 @@ def _wgrad(x, dz, KH, KW, stride, dw0=None):
     dw = dw.contiguous(memory_format=torch.channels_last)
     nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, stride))
     ws = torch.full((max(nb, 16) // 4,), float("nan"), device=DEV)  # needs no zeroing
-    rc = L.rai_conv2d_wgrad(xd.data_ptr(), dzd.data_ptr(), B, H, W, Ci, Co, KH, KW, stride, dw.data_ptr(),
-                            0 if dw0 is None else 1, ws.data_ptr(), nb, _lib.stream_handle(DEV))
+    rc = L.rai_conv2d_wgrad_v(xd.data_ptr(), dzd.data_ptr(), B, H, W, Ci, Co, KH, KW, stride, dw.data_ptr(),
+                              0 if dw0 is None else 1, ws.data_ptr(), nb, 0, pf, _lib.stream_handle(DEV))
     _lib.check(rc, "rai_conv2d_wgrad")
     torch.cuda.synchronize()
     return dw.cpu()
@@ -130,7 +130,8 @@ WGRAD_CASES = [  # (Ci, H, Co, k, stride): the three NatureCNN layers + a ragged
 
 @pytest.mark.parametrize("case", WGRAD_CASES, ids=lambda c: "x".join(str(v) for v in c))
 @pytest.mark.parametrize("B", [1, 5, 256])
-def test_conv_wgrad_matches_fp64(case, B):
+@pytest.mark.parametrize("pf", [0, 104, 108], ids=["default", "buf4", "buf8"])
+def test_conv_wgrad_matches_fp64(case, B, pf):
     Ci, H, Co, k, s = case
     if B == 256 and Ci == 4:
         B = 64  # conv1 at 64 samples keeps the fp64 CPU reference fast; 256 runs below at 16
@@ -138,7 +139,7 @@ def test_conv_wgrad_matches_fp64(case, B):
     OH = (H - k) // s + 1
     g = torch.Generator().manual_seed(B)
     dz = torch.randn(B, Co, OH, OH, generator=g) * (torch.rand(B, Co, OH, OH, generator=g) > 0.4)
-    dw = _wgrad(x, dz, k, k, s)
+    dw = _wgrad(x, dz, k, k, s, pf=pf)
     xd, dzd = x.double(), dz.double()
     ref = torch.ops.aten.convolution_backward(dzd, xd, w.double(), None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                               [False, True, False])[1]

@@ -49,7 +49,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--batches", default="256,1024")
-    ap.add_argument("--variants", default="0,1,10,11,12,13,14,15")
+    ap.add_argument("--variants", default="0,12,13,14,15,16,17,18")
     args = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     dev = torch.device("cuda:0")
@@ -117,7 +117,7 @@ def main():
                 row["wgrad_relerr"] = ((grad2 - grad).abs().max() / grad.abs().max()).item()
                 row["wgrad_us"] = round(timeit(mine_wgrad, args.reps), 2)
                 row["wgrad_tflops"] = round(row["flops"] / row["wgrad_us"] / 1e6, 1)
-                for tw, pf in ((256, 4), (256, 8), (512, 4), (768, 8), (1024, 8)):
+                for tw, pf in ((512, 4), (512, 8), (512, 104), (512, 108), (1024, 104), (1024, 108)):
                     row[f"wgrad_{tw}_{pf}_us"] = round(timeit(lambda: mine_wgrad(tw, pf), args.reps), 2)
                 row["wgrad_ws_mb"] = round(nb / 2**20, 2)
             else:
