@@ -1,0 +1,44 @@
+#!/bin/bash
+# C3 whole-update HBM traffic assembled from kernel-GROUP-restricted counter passes (the unrestricted
+# whole-update pass aborts inside rocprofiler-sdk: profiles/r3c/r3zd/r3ze/r4b_*_crash_mapped.txt).
+# Groups: ours (this repo's HIP kernels), gemm (hipBLASLt / rocBLAS), rest (everything else: torch
+# elementwise, copies, MIOpen if any).  Per group a FETCH_SIZE and a WRITE_SIZE pass over one eager C3
+# update (the product's graphed step body launched eagerly, RAI_GRAPH_EAGER=1), aggregated per kernel on
+# the box (tools/pmc_kernels.py); tools/c3_traffic.py then merges them.  Stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-r4}
+OUT=gpurun_out/c3grp_$TAG
+mkdir -p "$OUT"
+OURS='conv_|rai_|gather|bias_relu|heads|pg_loss|loss_|clip_optim|grad_sumsq|gae|sample|policy|minibatch|wrw'
+GEMM='Cijk|gemm|Gemm|GEMM'
+sha256sum rl-algo-impls_amd/lib/librai_amd.so > "$OUT/lib_sha256.txt"
+for grp in ours gemm rest; do
+  case $grp in
+    ours) sel=(--kernel-include-regex "$OURS") ;;
+    gemm) sel=(--kernel-include-regex "$GEMM") ;;
+    rest) sel=(--kernel-exclude-regex "$OURS|$GEMM") ;;
+  esac
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "== $grp $C" | tee -a "$OUT/steps.log"
+    RAI_GRAPHS=1 RAI_GRAPH_EAGER=1 timeout -s KILL 400 rocprofv3 --pmc $C "${sel[@]}" --output-format csv \
+      -d "$OUT/${grp}_$C" -o run -- python3 bench.py --config pong --no-cpu-baseline --roofline-reps 1 --steps 1 \
+      --warmup 0 > "$OUT/${grp}_$C.log" 2>&1
+    rc=$?
+    echo "== $grp $C rc=$rc" | tee -a "$OUT/steps.log"
+    [ $rc -eq 0 ] || { grep -v amdgpu.ids "$OUT/${grp}_$C.log" | tail -20; exit $rc; }
+    f=$(find "$OUT/${grp}_$C" -name "*counter_collection.csv" | head -1)
+    python3 tools/pmc_kernels.py "$f" "$OUT/${grp}_$C.json" --delete || exit 1
+  done
+done
+python3 - "$OUT" <<'PY'
+import json, sys
+out = sys.argv[1]
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    merged = {"kernels": {}}
+    for g in ("ours", "gemm", "rest"):
+        merged["kernels"].update(json.load(open(f"{out}/{g}_{c}.json"))["kernels"])
+    json.dump(merged, open(f"{out}/{c}.json", "w"), indent=1)
+PY
+exit 0
