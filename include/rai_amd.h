@@ -241,9 +241,16 @@ int rai_conv2d_wgrad_relu_partials(const float* dy, const float* y, const float*
 int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
                      int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream);
 /* The same with a fixed form (variant 0 = default; 1, 2 = weights resident in LDS, persistent workgroups;
- * tools/conv_bench.py A/B). */
+ * 3 = per image, pointer loads; 4 = per image, weights staged through LDS; 5 / 6 / 7 = per image, buffer
+ * loads, 2 / 3 / 4 quads in flight; tools/conv_bench.py, tools/dgrad_probe.py A/B). */
 int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,
                        int32_t KH, int32_t KW, int32_t stride, float* dx, int32_t variant, void* stream);
+/* The input gradient with the layer's ReLU backward folded in (round 4; NatureCNN conv2, whose dz also feeds
+ * rai_conv2d_wgrad_relu_partials): dz = y > 0 ? dy : 0 is formed on the fly from dy and the saved output y
+ * (both NHWC (B, OH, OW, Co)), so no rai_bias_relu_bwd pass materialises it.  The per-image form only:
+ * RAI_E_UNSUPPORTED for shapes it is not instantiated for. */
+int rai_conv2d_dgrad_relu(const float* dy, const float* y, const float* w, int64_t B, int32_t H, int32_t W,
+                          int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream);
 /* The same with a fixed launch shape for same-box A/B (tools/conv_bench.py): target_wgs workgroups
  * (0 = 512, at most 1024), pf pixel steps in flight per wave (0 = 4; 4 or 8). */
 int rai_conv2d_wgrad_v(const float* x, const float* dz, int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co,

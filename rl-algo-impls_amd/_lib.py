@@ -183,6 +183,7 @@ _SIGNATURES = {
     "rai_conv2d_wgrad_relu_partials": (C.c_int, [_vp, _vp, _vp, _i64] + [_i32] * 7 + [_vp, _i64, _vp]),
     "rai_conv2d_dgrad": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _vp]),
     "rai_conv2d_dgrad_v": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _i32, _vp]),
+    "rai_conv2d_dgrad_relu": (C.c_int, [_vp, _vp, _vp, _i64] + [_i32] * 7 + [_vp, _vp]),
     "rai_bias_relu_bwd_nchw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_mlp_ppo_workspace_bytes": (_i64, [C.c_int64, C.c_int32]),
     "rai_mlp_ppo_grads": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _i32,

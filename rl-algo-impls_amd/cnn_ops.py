@@ -258,6 +258,23 @@ def _conv_dgrad(x, dz, w, stride) -> torch.Tensor:
                                                [True, False, False])[0]
 
 
+def _conv_dgrad_relu(x, dy, y, w, stride):
+    """dx with the layer's ReLU backward folded in (rai_conv2d_dgrad_relu: dz = y > 0 ? dy : 0 formed on the
+    fly); None where that kernel has no instantiation for the shape (the caller then materialises dz)."""
+    B, Ci, H, W = (int(v) for v in x.shape)
+    Co, _, KH, KW = (int(v) for v in w.shape)
+    s = _pair(stride)[0]
+    if not (dy.is_contiguous(memory_format=torch.channels_last) and dy.data_ptr() % 16 == 0):
+        return None
+    dx = torch.empty((B, Ci, H, W), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    rc = _lib.lib().rai_conv2d_dgrad_relu(dy.data_ptr(), y.data_ptr(), w.data_ptr(), B, H, W, Ci, Co, KH, KW, s,
+                                          dx.data_ptr(), _lib.stream_handle(x.device))
+    if rc == -6:  # RAI_E_UNSUPPORTED
+        return None
+    _lib.check(rc, "rai_conv2d_dgrad_relu")
+    return dx
+
+
 def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, pending: "_PendingGrads", y=None, db=None):
     """rai_conv2d_wgrad_partials for this layer (with y: rai_conv2d_wgrad_relu_partials, dz being the ReLU
     output's gradient dy, and the bias gradient reduced into db); returns (job, workspace) for the
@@ -358,15 +375,21 @@ class ConvBiasReLU(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, b, y = ctx.saved_tensors
         stride, padding, key, direct_b, direct_w, flatten, zshape, mfma = ctx.conf
-        if (mfma and _CONV_FUSE_RELU_BWD and not ctx.needs_input_grad[0] and not flatten and direct_b and direct_w
+        if (mfma and _CONV_FUSE_RELU_BWD and not flatten and direct_b and direct_w
+                and (not ctx.needs_input_grad[0] or _CONV_MFMA_DGRAD)
                 and w.grad.is_contiguous(memory_format=torch.channels_last) and w.grad.data_ptr() % 16 == 0
                 and b.grad.data_ptr() % 16 == 0 and y.is_contiguous(memory_format=torch.channels_last)):
-            # the layer's dz has no consumer but the weight gradient (conv1: its input needs no gradient):
-            # the bias + ReLU backward and the bias gradient are folded into the weight-gradient partials
+            # the bias + ReLU backward folded into its consumers, dz never materialised: the weight-gradient
+            # partials (with the bias gradient) and, where the input needs a gradient (conv2), the input
+            # gradient form dz = y > 0 ? dy : 0 on the fly (conv1's input needs none)
             dy = dy.contiguous(memory_format=torch.channels_last)
-            job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, ctx.pending, y=y, db=b.grad)
-            ctx.pending.add_wgrad(job, wsp, w)
-            return None, None, None, None, None, None, None
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = _conv_dgrad_relu(x, dy, y, w, stride)
+            if dx is not None or not ctx.needs_input_grad[0]:
+                job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, ctx.pending, y=y, db=b.grad)
+                ctx.pending.add_wgrad(job, wsp, w)
+                return dx, None, None, None, None, None, None
         ws = _WS.get(key, zshape[1], y.device)
         if flatten:
             dz, db = _bias_relu_bwd_nchw(dy.contiguous(), y, b, ws, direct_b, zshape)

@@ -581,7 +581,8 @@ static WrwPlan wrw_plan(int64_t M, int Co, int K, int target_wgs) {
 // TQ column blocks; invalid taps (outside the output) load zeros.  Every dx element is written once
 // (no split, no zero-fill, deterministic).
 struct ConvDgradArgs {
-  const float* dz;  // (B, OH, OW, Co)
+  const float* dz;  // (B, OH, OW, Co); with a ReLU folded in: dy, the gradient of the ReLU's output
+  const float* y;   // ReLU folded in: the forward output (dz = y > 0 ? dz : 0), else unused
   const float* w;   // (Co, KH, KW, Ci)
   float* dx;        // (B, H, W, Ci)
   int64_t B;
@@ -810,7 +811,7 @@ int launch_dgrad_lds(const ConvDgradArgs& a, hipStream_t st) {
 // accumulators.  The image's dx is assembled in LDS (pixel stride Ci + 4 floats: the 16 pixel lanes of
 // an add land on distinct banks) and written once, coalesced.  NatureCNN: conv2 (4x4/2, 64 -> 32 ch,
 // 9x9 -> 20x20) = 8 waves x 4 taps x 6 tiles, conv3 (3x3/1, 64 -> 64, 7x7 -> 9x9) = 4 waves x 9 x 4.
-template <int TC, int MT, int NT, int PF, bool BUF = false>
+template <int TC, int MT, int NT, int PF, bool BUF = false, bool RELU = false>
 __global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float dxl[];  // [H * W][Ci + 4]
   const int n = blockIdx.x;
@@ -850,6 +851,8 @@ __global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs 
                                                                        (int)(a.Co * wco * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dzn), 0,
                                                                        OHW * a.Co * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(RELU ? a.y + (int64_t)n * OHW * a.Co : dzn), 0, OHW * a.Co * 4, 0x00020000);
   int wvo[TC], dvo[MT];
 #pragma unroll
   for (int t = 0; t < TC; ++t) wvo[t] = 4 * (int)(4 * g * wco + woff[t]);
@@ -864,8 +867,14 @@ __global__ __launch_bounds__(NT) void conv_dgrad_img_kernel(const ConvDgradArgs 
         for (int t = 0; t < TC; ++t) Wv[t][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wrs, wvo[t], so, 0));
       }
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt) {
         Dv[mt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(drs, dvo[mt], 64 * q, 0));
+        if (RELU) {  // threshold_backward on the saved output: dz = y > 0 ? dy : 0
+          const f4 yv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(yrs, dvo[mt], 64 * q, 0));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Dv[mt][j] = yv[j] > 0.f ? Dv[mt][j] : 0.f;
+        }
+      }
       return;
     }
     const int co0 = 4 * (4 * q + g);
@@ -1096,12 +1105,13 @@ int launch_dgrad_img_lds(const ConvDgradArgs& a, hipStream_t st) {
   return RAI_OK;
 }
 
-template <int TC, int MT, int NT, int PF = 2, bool BUF = false>
+template <int TC, int MT, int NT, int PF = 2, bool BUF = false, bool RELU = false>
 int launch_dgrad_img(const ConvDgradArgs& a, hipStream_t st) {
+  static_assert(BUF || !RELU, "the ReLU-folded form uses buffer loads");
   const size_t lds = (size_t)a.H * a.W * (a.Ci + 4) * sizeof(float);
   if (lds > 160 * 1024) return RAI_E_SHAPE;
   if (BUF && (int64_t)a.Co * a.KH * a.KW * a.Ci * 4 >= (1LL << 31)) return RAI_E_SHAPE;
-  auto k = conv_dgrad_img_kernel<TC, MT, NT, PF, BUF>;
+  auto k = conv_dgrad_img_kernel<TC, MT, NT, PF, BUF, RELU>;
   const int e = allow_lds(reinterpret_cast<const void*>(k));
   if (e != RAI_OK) return e;
   if (a.B > 0x7fffffffLL) return RAI_E_SHAPE;
@@ -1395,6 +1405,7 @@ extern "C" int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, in
   if (((uintptr_t)dz | (uintptr_t)w | (uintptr_t)dx) & 15) return RAI_E_SHAPE;
   ConvDgradArgs a;
   a.dz = dz;
+  a.y = nullptr;
   a.w = w;
   a.dx = dx;
   a.B = B;
@@ -1455,4 +1466,35 @@ extern "C" int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, in
 extern "C" int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci,
                                 int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx, void* stream) {
   return rai_conv2d_dgrad_v(dz, w, B, H, W, Ci, Co, KH, KW, stride, dx, 0, stream);
+}
+
+extern "C" int rai_conv2d_dgrad_relu(const float* dy, const float* y, const float* w, int64_t B, int32_t H, int32_t W,
+                                     int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx,
+                                     void* stream) {
+  if (B < 0 || H < 1 || W < 1 || Ci < 16 || Co < 16 || Co % 16 || KH < 1 || KW < 1 || stride < 1 || KH > H ||
+      KW > W || KH % stride || KW % stride)
+    return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!dy || !y || !w || !dx) return RAI_E_NULLPTR;
+  if (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)w | (uintptr_t)dx) & 15) return RAI_E_SHAPE;
+  ConvDgradArgs a;
+  a.dz = dy;
+  a.y = y;
+  a.w = w;
+  a.dx = dx;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.KH = KH;
+  a.KW = KW;
+  a.S = stride;
+  a.OH = (H - KH) / stride + 1;
+  a.OW = (W - KW) / stride + 1;
+  hipStream_t st = rai_stream(stream);
+  const int kind = dgrad_img_kind(a);
+  if (kind == 1) return launch_dgrad_img<9, 4, 256, 3, true, true>(a, st);
+  if (kind == 2) return launch_dgrad_img<4, 6, 512, 2, true, true>(a, st);
+  return RAI_E_UNSUPPORTED;
 }

@@ -321,3 +321,50 @@ def test_same_conv_twice_in_one_backward_accumulates_both_uses():
         got = got.detach().cpu().double()
         assert torch.isfinite(got).all()
         assert ((got - ref).abs() <= 1e-4 * ref.abs().max() + 1e-6).all(), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("case", [(32, 20, 64, 4, 2), (64, 9, 64, 3, 1)], ids=["conv2", "conv3"])
+@pytest.mark.parametrize("B", [3, 256])
+def test_conv_dgrad_relu_folds_the_relu_backward(case, B):
+    """rai_conv2d_dgrad_relu: the input gradient of dz = (y > 0 ? dy : 0) formed on the fly from dy and the
+    saved output y -- against fp64 autograd on the materialised dz (bound as test_conv_dgrad_matches_fp64),
+    and bit-identical to rai_conv2d_dgrad on that dz (the same kernel, same summation order).  A shape the
+    per-image form has no instantiation for returns RAI_E_UNSUPPORTED."""
+    Ci, H, Co, k, s = case
+    x, w, _ = _inputs(B, Ci, H, Co, k, seed=B + 3)
+    OH = (H - k) // s + 1
+    gen = torch.Generator().manual_seed(B + 9)
+    dy = torch.randn(B, Co, OH, OH, generator=gen)
+    y = torch.relu(torch.randn(B, Co, OH, OH, generator=gen))
+    dz = torch.where(y > 0, dy, torch.zeros_like(dy))
+    cl = lambda t: t.to(DEV).contiguous(memory_format=torch.channels_last)
+    dyd, yd, dzd, wd = cl(dy), cl(y), cl(dz), cl(w)
+    dx = torch.full((B, Ci, H, H), float("nan"), device=DEV).contiguous(memory_format=torch.channels_last)
+    dx2 = torch.full_like(dx, float("nan"))
+    L = _lib.lib()
+    st = _lib.stream_handle(DEV)
+    _lib.check(L.rai_conv2d_dgrad_relu(dyd.data_ptr(), yd.data_ptr(), wd.data_ptr(), B, H, H, Ci, Co, k, k, s,
+                                       dx.data_ptr(), st), "rai_conv2d_dgrad_relu")
+    _lib.check(L.rai_conv2d_dgrad(dzd.data_ptr(), wd.data_ptr(), B, H, H, Ci, Co, k, k, s, dx2.data_ptr(), st),
+               "rai_conv2d_dgrad")
+    torch.cuda.synchronize()
+    assert torch.equal(dx.cpu(), dx2.cpu())
+    ref = torch.ops.aten.convolution_backward(dz.double(), x.double(), w.double(), None, [s, s], [0, 0], [1, 1],
+                                              False, [0, 0], 1, [True, False, False])[0]
+    bound = torch.ops.aten.convolution_backward(dz.double().abs(), x.double(), w.double().abs(), None, [s, s],
+                                                [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    got = dx.cpu().double()
+    tol = (Co * k * k + 2) * 2.0 ** -24 * bound + 1e-30
+    assert ((got - ref).abs() <= tol).all()
+
+
+def test_conv_dgrad_relu_rejects_shapes_without_an_instantiation():
+    """Argument checks only (nothing is launched): a shape the per-image form is not instantiated for
+    returns RAI_E_UNSUPPORTED, null pointers RAI_E_NULLPTR, B = 0 is a no-op."""
+    L = _lib.lib()
+    st = _lib.stream_handle(DEV)
+    buf = torch.zeros(64, device=DEV)
+    p = buf.data_ptr()
+    assert L.rai_conv2d_dgrad_relu(p, p, p, 2, 11, 11, 32, 16, 2, 2, 2, p, st) == -6
+    assert L.rai_conv2d_dgrad_relu(None, p, p, 2, 20, 20, 32, 64, 4, 4, 2, p, st) == -1
+    assert L.rai_conv2d_dgrad_relu(None, None, None, 0, 20, 20, 32, 64, 4, 4, 2, None, st) == 0
