@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .optim import FlatOptimizer, FlatParams
 from .pg_common import (DeviceBlocks, launch_loss, load_optimizer, log_scalars, make_hparams, num_or_array,
-                        save_optimizer, unsupported, value_columns)
+                        save_optimizer, scale_logp_by_num_actions, unsupported, value_columns)
 
 
 class A2CTrainStats:  # rl_algo_impls/a2c/train_stats.py
@@ -41,7 +41,8 @@ class A2C:
                  multi_reward_weights: Optional[List[float]] = None, scale_loss_by_num_actions: bool = False,
                  gradient_accumulation: bool = False, autocast_loss: bool = False,
                  num_minibatches: Optional[int] = None):
-        unsupported(scale_loss_by_num_actions=scale_loss_by_num_actions, autocast_loss=autocast_loss)
+        unsupported(autocast_loss=autocast_loss)
+        self.scale_loss_by_num_actions = scale_loss_by_num_actions
         self.policy = policy
         self.device = torch.device(device)
         self.tb_writer = tb_writer
@@ -91,6 +92,8 @@ class A2C:
             K = None
             for mb in r.minibatches(r.total_steps // nmb, shuffle=not self.gradient_accumulation):
                 logp, ent, v = self.policy(mb.obs, mb.actions, action_masks=mb.action_masks)
+                if self.scale_loss_by_num_actions:  # a2c.py:144-147
+                    logp = scale_logp_by_num_actions(logp, mb.num_actions)
                 if K is None:
                     K = value_columns(v)
                     hp = make_hparams(loss_kind=1, K=K, ent_coef=self.ent_coef, vf_coef=self.vf_coef,

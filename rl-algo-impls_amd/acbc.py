@@ -6,7 +6,7 @@ The third algorithm over the same hot path: the device rollout with its GAE retu
 rl_algo_impls/rollout/vec_rollout.py:78-88), minibatches of the HBM rollout, one fused loss
 launch and the fused clip_grad_norm_ + Adam.  Per minibatch (acbc.py:94-128):
 
-    pi_loss = -mean(logp(a))                         (or / num_actions: not supported)
+    pi_loss = -mean(logp(a))                         (or of logp / num_actions, scale_loss_by_num_actions)
     v_loss  = mean((v - R)^2) per value column
     loss    = pi_loss + sum(vf_coef * v_loss)        (/ num_minibatches under gradient accumulation)
 
@@ -24,7 +24,7 @@ import torch
 
 from .optim import FlatOptimizer, FlatParams
 from .pg_common import (DeviceBlocks, launch_loss, load_optimizer, log_scalars, make_hparams, num_or_array,
-                        save_optimizer, unsupported, value_columns)
+                        save_optimizer, scale_logp_by_num_actions, unsupported, value_columns)
 
 
 class ACBCTrainStats:
@@ -50,7 +50,7 @@ class ACBC:
     def __init__(self, policy, device: torch.device, tb_writer, learning_rate: float = 3e-4, batch_size: int = 64,
                  n_epochs: int = 10, gamma=0.99, gae_lambda=0.95, vf_coef=0.25, max_grad_norm: float = 0.5,
                  gradient_accumulation: bool = False, scale_loss_by_num_actions: bool = False):
-        unsupported(scale_loss_by_num_actions=scale_loss_by_num_actions)
+        self.scale_loss_by_num_actions = scale_loss_by_num_actions
         self.policy = policy
         self.device = torch.device(device)
         self.tb_writer = tb_writer
@@ -116,6 +116,8 @@ class ACBC:
         for _ in range(self.n_epochs):
             for mb in r.minibatches(self.batch_size, shuffle=not self.gradient_accumulation):
                 logp, ent, v = self.policy(mb.obs, mb.actions, action_masks=mb.action_masks)
+                if self.scale_loss_by_num_actions:  # acbc.py:114-117
+                    logp = scale_logp_by_num_actions(logp, mb.num_actions)
                 if K is None:
                     K = value_columns(v)
                     hp = make_hparams(loss_kind=1, K=K, ent_coef=0.0, vf_coef=self.vf_coef,

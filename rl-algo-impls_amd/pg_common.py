@@ -159,6 +159,16 @@ def launch_loss(blocks: DeviceBlocks, logp, ent, v, old_logp, old_values, adv, r
     return d_logp, d_ent, d_v
 
 
+def scale_logp_by_num_actions(logp: torch.Tensor, num_actions: Optional[torch.Tensor]) -> torch.Tensor:
+    """scale_loss_by_num_actions (rl_algo_impls/a2c/a2c.py:144-147, rl_algo_impls/acbc/acbc.py:114-117): the
+    policy term uses logp / num_actions where num_actions > 0, else 0 -- the reference's expression, on the
+    device, differentiated by autograd (the loss kernel then sees the scaled log-probabilities).  The
+    rollout's Batch.num_actions exists for action-masked (GridNet) rollouts only."""
+    if num_actions is None:
+        raise ValueError("scale_loss_by_num_actions needs Batch.num_actions (an action-masked GridNet rollout)")
+    return torch.where(num_actions > 0, logp / num_actions, 0)
+
+
 def value_columns(v: torch.Tensor) -> int:
     return 1 if v.dim() == 1 else int(v.shape[1])
 
