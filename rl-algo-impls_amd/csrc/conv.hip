@@ -1185,8 +1185,10 @@ static int wgrad_partials(const float* x, const float* dz, const float* y, int64
   // a split's offsets from its first sample fit int32
   if ((int64_t)(WR_MAXPX / (a.OH * a.OW) + 2) * H * W * Ci > 0x7fffffffLL) return RAI_E_SHAPE;
   const dim3 grid((unsigned)p.S, (unsigned)p.KT);
-  if (pf <= 0) pf = 4;
   const bool buf_ok = (int64_t)B * H * W * Ci * 4 < (1LL << 31) && a.M * Co * 4 < (1LL << 31);
+  // default: buffer loads with 4 pixel steps in flight where the operands fit 2 GB buffers (NatureCNN
+  // B = 256: 2-4 % faster than pointer loads, B = 1024: 8-21 %; profiles/r4g_conv_bench.txt)
+  if (pf <= 0) pf = buf_ok ? 104 : 4;
   if (pf >= 100 && !buf_ok) return RAI_E_SHAPE;
   if (y) {  // the ReLU backward and the bias gradient fused in (rai_conv2d_wgrad_relu_partials)
     if (((uintptr_t)y) & 15) return RAI_E_SHAPE;
@@ -1350,11 +1352,14 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
     // measured (profiles/r3v_conv_bench.txt): the LDS-resident-weight forms win wherever the weight rows
     // fit (<= ~150 KB); 32 co x 256 px tiles once they give >= 256 workgroup tiles, else 64 co x 64 px
     const size_t lds32 = (size_t)32 * (K + 4) * 4, lds64 = (size_t)64 * (K + 4) * 4;
+    // buffer-load forms (16 / 17 = 14 / 13 with raw_buffer_load, scalar offsets) where the input fits a
+    // 2 GB buffer: 3-6 % faster at B = 256 and 1024 (profiles/r4g_conv_bench.txt)
     const int64_t t14 = (a.M + 255) / 256 * (Co / 32);
+    const bool buf = B * H * W * (int64_t)Ci * 4 < (1LL << 31);
     if (Co % 32 == 0 && lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && (t14 >= 256 || Co % 64 != 0))
-      variant = 14;
+      variant = buf ? 16 : 14;
     else if (Co % 64 == 0 && lds64 + CV_MAXCHUNK * 4 <= 160 * 1024)
-      variant = 13;
+      variant = buf ? 17 : 13;
     else
       variant = (Co % 64 == 0) ? 10 : (Co % 32 == 0) ? 11 : 7;
   }
