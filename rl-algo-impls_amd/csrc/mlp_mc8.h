@@ -590,7 +590,9 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
     }
+    STAMP(9);
     __syncthreads();
+    STAMP(10);
     if (tid == 0) {
       __hip_atomic_fetch_add(&sync[M8_CNT1 + net], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!m8_wait2(sync, M8_CNT1 + net, M8_CNT1 + net, (unsigned long long)G * (mb + 1), MC_WAIT_LOCAL)) {
@@ -679,6 +681,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         }
         s = sum;
       }
+      STAMP(11);
       // ---- round 2: publish the summed share and its squared norm ----
       const int s2 = (int)M8_S2_OFF + ((net * 2 + par) * WL_N + 4 * chl) * (int)sizeof(float);
       if (own) __builtin_amdgcn_raw_buffer_store_b128(as_u4(s), srs, s2, 0, 16);
@@ -698,7 +701,9 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    STAMP(12);
     __syncthreads();
+    STAMP(13);
     if (tid == 0) {
       __hip_atomic_fetch_add(&sync[M8_CNT2 + net], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!m8_wait2(sync, M8_CNT2, M8_CNT2 + 1, (unsigned long long)G * (mb + 1), MC_WAIT_LOCAL)) {
@@ -731,6 +736,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       const double sq = ((d2a[0] + d2a[1]) + d2b[0]) + d2b[1];
       const double tot = wave_sum_v(lane < 2 * G ? sq : 0.0);
       const float total_norm = (float)sqrt(tot);
+      STAMP(14);
       float coef = 1.f;
       if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
 #pragma unroll
