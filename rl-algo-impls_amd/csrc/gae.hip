@@ -355,6 +355,88 @@ __global__ __launch_bounds__(NT) void gae_stream_kernel(const GaeArgs a) {
   }
 }
 
+// Fast mode (RAI_GAE_FAST, fp32) at latency-bound shapes: a chunked affine
+// scan over T instead of T serial steps per column.  Row t's step is the affine map
+// x -> delta_t + c_t x (c_t = gamma*lambda*next_nonterminal); a 512-thread block owns COLS columns and
+// cuts T into P = 512 / COLS segments of L <= GAE_SCAN_LMAX rows, one thread per (segment, column):
+//   (1) each thread loads its L rows, forms delta_t / c_t (gae_delta<float>: the serial fast mode's
+//       per-row arithmetic) and composes its segment's map (D, Cc) bottom-up, to LDS;
+//   (2) the carry entering segment s is the composition of the segments above it applied to 0
+//       (at most P - 1 dependent multiply-adds, operands from LDS);
+//   (3) each thread re-runs its rows from that carry (the serial chain's own operations) and stores
+//       adv and returns = adv + V.
+// The dependent chain is 2 L + P steps instead of T (C2, T = 128 at 4096 columns: 4 + 32 + 4).  Only
+// the grouping of the fp32 chain differs from the serial fast mode; the tolerance is fast mode's
+// (tests/test_gpu_kernels.py: rtol 1e-5 against the exact oracle).
+constexpr int GAE_SCAN_LMAX = 32;
+
+template <int COLS, int LM>
+__global__ __launch_bounds__(512) void gae_scan_kernel(const GaeArgs a) {
+  constexpr int P = 512 / COLS;
+  __shared__ float seg_d[P][COLS], seg_c[P][COLS];
+  const int tid = threadIdx.x;
+  const int lane = tid % COLS;
+  const int s = tid / COLS;  // segment
+  // XCD-aware column groups (as gae_kernel)
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  const int grp = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int64_t c = (int64_t)grp * COLS + lane;
+  const int64_t C = a.C, N = a.N, T = a.T;
+  const bool valid = c < C;
+  const int64_t cc = valid ? c : 0;
+  const int64_t n = cc / a.K;
+  const int k = (int)(cc - n * a.K);
+  const float g32 = a.gamma32[k], gl = a.gl32[k];
+  const int64_t L = (T + P - 1) / P;
+  const int64_t t_lo = (int64_t)s * L;
+  const int64_t t_hi = t_lo + L < T ? t_lo + L : T;  // rows [t_lo, t_hi); empty when t_lo >= T
+  float d[LM], cf[LM], vv[LM];
+#pragma unroll
+  for (int i = 0; i < LM; ++i) {
+    const int64_t t = t_lo + i;
+    d[i] = 0.f;
+    cf[i] = 1.f;
+    vv[i] = 0.f;
+    if (t < t_hi) {
+      const bool last = t == T - 1;
+      const float r = a.rewards[t * C + cc];
+      const float v = a.values[t * C + cc];
+      const float vn = last ? a.next_values[cc] : a.values[(t + 1) * C + cc];
+      const uint8_t e = last ? a.next_es[n] : a.es[(t + 1) * N + n];
+      d[i] = gae_delta<float>(r, v, vn, e, false, g32, 0.0);
+      cf[i] = e ? 0.f : gl;
+      vv[i] = v;
+    }
+  }
+  // (1) the segment's map, composed from its last row upwards: x -> D + Cc x
+  float D = 0.f, Cc = 1.f;
+#pragma unroll
+  for (int i = LM - 1; i >= 0; --i) {
+    if (t_lo + i < t_hi) {
+      D = d[i] + cf[i] * D;
+      Cc = cf[i] * Cc;
+    }
+  }
+  seg_d[s][lane] = D;
+  seg_c[s][lane] = Cc;
+  __syncthreads();
+  // (2) carry entering the segment from below it in time order (rows >= t_hi)
+  float x = 0.f;
+  for (int q = P - 1; q > s; --q) x = seg_d[q][lane] + seg_c[q][lane] * x;
+  // (3) the segment's rows from that carry
+#pragma unroll
+  for (int i = LM - 1; i >= 0; --i) {
+    const int64_t t = t_lo + i;
+    if (t < t_hi) {
+      x = d[i] + cf[i] * x;
+      if (valid) {
+        a.adv[t * C + c] = x;
+        if (a.ret) a.ret[t * C + c] = x + vv[i];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t* episode_starts,
@@ -439,6 +521,27 @@ extern "C" int rai_gae(const float* rewards, const float* values, const uint8_t*
 #undef RAI_GAE_STREAM_LAUNCH
     RAI_LAUNCH_CHECK();
     return RAI_OK;
+  }
+  // fast mode: the chunked affine scan where T fits its segments (RAI_GAE_SCAN=0: the serial fp32 chain)
+  const char* sc = getenv("RAI_GAE_SCAN");
+  if (mode == RAI_GAE_FAST && !(sc && sc[0] == '0')) {
+    // columns per block: the widest of 64 / 32 / 16 that still gives >= 256 blocks; P = 512 / cols segments
+    const int scols = a.C >= 256LL * 64 ? 64 : (a.C >= 256LL * 32 ? 32 : 16);
+    const int64_t L = (T + 512 / scols - 1) / (512 / scols);  // rows per segment
+    if (L <= GAE_SCAN_LMAX) {
+      const dim3 grid((unsigned)((a.C + scols - 1) / scols)), block(512);
+#define RAI_GAE_SCAN_LAUNCH(CO)                                                                    \
+  do {                                                                                             \
+    if (L <= 8) hipLaunchKernelGGL((gae_scan_kernel<CO, 8>), grid, block, 0, st, a);              \
+    else hipLaunchKernelGGL((gae_scan_kernel<CO, GAE_SCAN_LMAX>), grid, block, 0, st, a);         \
+  } while (0)
+      if (scols == 64) RAI_GAE_SCAN_LAUNCH(64);
+      else if (scols == 32) RAI_GAE_SCAN_LAUNCH(32);
+      else RAI_GAE_SCAN_LAUNCH(16);
+#undef RAI_GAE_SCAN_LAUNCH
+      RAI_LAUNCH_CHECK();
+      return RAI_OK;
+    }
   }
   // columns per block: the widest of 64 / 32 / 16 that still gives >= 256 blocks (one per CU)
   int cols = 64;

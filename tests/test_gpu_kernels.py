@@ -98,6 +98,34 @@ def test_gae_fast_mode_tolerance():
     np.testing.assert_allclose(adv.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("T,N,K", [(1, 1, 1), (5, 7, 1), (128, 4096, 1), (33, 200, 1), (1024, 100, 1),
+                                   (1025, 100, 1), (128, 700, 3), (64, 20000, 1), (200, 9000, 1)])
+def test_gae_fast_mode_affine_scan(T, N, K, monkeypatch):
+    """Fast mode's chunked affine scan (gae_scan_kernel: segments of <= 32 rows, 16 / 32 / 64 columns per
+    block; T = 1025 at 100 columns falls back to the serial fp32 chain) against the exact C oracle and
+    against the serial fp32 chain (RAI_GAE_SCAN=0), at fast mode's tolerance; episode starts dense enough
+    to cut every segment, and none in some columns (long carries)."""
+    rng = np.random.default_rng(T * 7 + N + K)
+    shp = (T, N) if K == 1 else (T, N, K)
+    r = rng.standard_normal(shp, dtype=np.float32)
+    v = rng.standard_normal(shp, dtype=np.float32)
+    es = rng.random((T, N)) < 0.05
+    es[:, : N // 3] = False
+    nes = rng.random(N) < 0.05
+    nv = rng.standard_normal(shp[1:], dtype=np.float32)
+    g = 0.99 if K == 1 else np.array([0.99, 0.995, 0.999])
+    lam = 0.95 if K == 1 else np.array([0.95, 0.9, 0.99])
+    adv_ref, ret_ref = oracle.gae_c(r, v, es, nes, nv, g, lam)
+    tol = dict(rtol=1e-5, atol=1e-5 * max(1.0, float(np.abs(adv_ref).max())))
+    fast, fret = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), g, lam, mode=FAST,
+                                           want_returns=True)
+    np.testing.assert_allclose(fast.cpu().numpy(), adv_ref, **tol)
+    np.testing.assert_allclose(fret.cpu().numpy(), ret_ref, **tol)
+    monkeypatch.setenv("RAI_GAE_SCAN", "0")
+    serial, _ = compute_advantages_device(dev(r), dev(v), dev(es), dev(nes), dev(nv), g, lam, mode=FAST)
+    np.testing.assert_allclose(fast.cpu().numpy(), serial.cpu().numpy(), **tol)
+
+
 def test_gae_edge_cases():
     # T=1, N=1; all starts; no starts; ragged column count (not a multiple of 64)
     for T, N in [(1, 1), (1, 65), (33, 63), (64, 129)]:

@@ -39,7 +39,9 @@ for (T, N, K, vname, venv) in [c + v for c in CASES for v in (VARIANTS if c[1] >
     ret = torch.empty_like(v)
     g = 0.99 if K == 1 else __import__("numpy").array([0.99, 0.995, 0.999])
     byts = 16 * T * N * K + T * N + 4 * N * K + N
-    for mode, name in ((EXACT, "exact"), (FAST, "fast")):
+    # fast: the chunked affine scan where it applies; fast_serial: the serial fp32 chain (RAI_GAE_SCAN=0)
+    for mode, name, scan in ((EXACT, "exact", "1"), (FAST, "fast", "1"), (FAST, "fast_serial", "0")):
+        os.environ["RAI_GAE_SCAN"] = scan
         for _ in range(5):
             compute_advantages_device(r, v, es, nes, nv, g, 0.95, mode=mode, advantages_out=adv, returns_out=ret)
         reps = 200
@@ -54,5 +56,5 @@ for (T, N, K, vname, venv) in [c + v for c in CASES for v in (VARIANTS if c[1] >
         e1.record()
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps
-        print(f"T={T:4d} N={N:8d} K={K} {vname:9s} {name:5s}: {us:9.2f} us  {byts / us / 1e3:8.1f} GB/s  "
+        print(f"T={T:4d} N={N:8d} K={K} {vname:9s} {name:11s}: {us:9.2f} us  {byts / us / 1e3:8.1f} GB/s  "
               f"({100 * byts / us / 1e3 / 8000:.1f}% of 8 TB/s)", flush=True)
