@@ -234,6 +234,20 @@ int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, in
 int rai_conv2d_wgrad_relu_partials(const float* dy, const float* y, const float* x, int64_t B, int32_t H, int32_t W,
                                    int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
                                    int64_t workspace_bytes, void* stream);
+/* The first NatureCNN layer on uint8 frames (round 4): x is the gathered uint8 NHWC minibatch (B, H, W, 4)
+ * (RAI_XFORM_U8_CHW_TO_U8_HWC) and the kernels read x = u8 / x_divisor (IEEE division: the value
+ * cnn.py:24-27's obs.float() / range_size and RAI_XFORM_U8_CHW_TO_F32_HWC give), so the float32 input is
+ * never materialised.  Ci == 4, x 4-B aligned, B * H * W * 4 < 2^31; otherwise as the float32 forms.
+ * The forward is the LDS-weight form (RAI_E_UNSUPPORTED if the weight rows do not fit LDS). */
+int rai_conv2d_bias_relu_fwd_u8(const uint8_t* x, float x_divisor, const float* w, const float* b, int64_t B,
+                                int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride,
+                                int32_t out_nchw, float* y, void* stream);
+int rai_conv2d_wgrad_partials_u8(const uint8_t* x, float x_divisor, const float* dz, int64_t B, int32_t H, int32_t W,
+                                 int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
+                                 int64_t workspace_bytes, void* stream);
+int rai_conv2d_wgrad_relu_partials_u8(const float* dy, const float* y, const uint8_t* x, float x_divisor, int64_t B,
+                                      int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW,
+                                      int32_t stride, void* workspace, int64_t workspace_bytes, void* stream);
 /* Input gradient of the same convolution (Conv2d's autograd dx; NatureCNN conv2 / conv3): dx (B, H, W, Ci)
  * NHWC = the transposed convolution of dz (B, OH, OW, Co) NHWC with w (Co, KH, KW, Ci) channels_last,
  * every element written (no accumulate, no zero-fill).  Ci 32 or 64, Co % 16 == 0, KH and KW multiples
@@ -423,11 +437,15 @@ int rai_categorical_critic_heads_bwd(const float* enc, const float* wpi, const f
  *     out = (float)u8 / divisor (IEEE division).  This is the NatureCNN input prescale
  *     `obs.float() / range_size` of rl_algo_impls/shared/encoder/cnn.py:24-27 plus the channels_last
  *     conversion, fused into the gather of rl_algo_impls/rollout/rollout.py:56-69.
+ *   RAI_XFORM_U8_CHW_TO_U8_HWC (round 4): the same source row (channels == 4), transposed only: dst
+ *     receives hw x 4 uint8 (a channels_last uint8 tensor, 16-B aligned) for the uint8-input
+ *     convolution (rai_conv2d_bias_relu_fwd_u8), which applies the prescale itself.
  * rai_gather_minibatch_x: rai_gather_minibatch (advance == 0) / _next (advance != 0) with one
  * rai_gather_xform per field (xform NULL: all copies).  Errors: RAI_E_SHAPE for a transform whose
  * shape or alignment does not fit, RAI_E_MODE for an unknown kind. */
 #define RAI_XFORM_COPY 0
 #define RAI_XFORM_U8_CHW_TO_F32_HWC 1
+#define RAI_XFORM_U8_CHW_TO_U8_HWC 2
 typedef struct rai_gather_xform {
   int32_t kind;
   int32_t channels;

@@ -72,6 +72,7 @@ class MinibatchDesc(C.Structure):
 
 RAI_XFORM_COPY = 0
 RAI_XFORM_U8_CHW_TO_F32_HWC = 1
+RAI_XFORM_U8_CHW_TO_U8_HWC = 2
 
 
 class GatherXform(C.Structure):
@@ -181,6 +182,9 @@ _SIGNATURES = {
     "rai_conv2d_wgrad_partials": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _i64, _vp]),
     "rai_conv2d_wgrad_reduce": (C.c_int, [_vp, _i32, _i32, _vp]),
     "rai_conv2d_wgrad_relu_partials": (C.c_int, [_vp, _vp, _vp, _i64] + [_i32] * 7 + [_vp, _i64, _vp]),
+    "rai_conv2d_bias_relu_fwd_u8": (C.c_int, [_vp, C.c_float, _vp, _vp, _i64] + [_i32] * 8 + [_vp, _vp]),
+    "rai_conv2d_wgrad_partials_u8": (C.c_int, [_vp, C.c_float, _vp, _i64] + [_i32] * 7 + [_vp, _i64, _vp]),
+    "rai_conv2d_wgrad_relu_partials_u8": (C.c_int, [_vp, _vp, _vp, C.c_float, _i64] + [_i32] * 7 + [_vp, _i64, _vp]),
     "rai_conv2d_dgrad": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _vp]),
     "rai_conv2d_dgrad_v": (C.c_int, [_vp, _vp, _i64] + [_i32] * 7 + [_vp, _i32, _vp]),
     "rai_conv2d_dgrad_relu": (C.c_int, [_vp, _vp, _vp, _i64] + [_i32] * 7 + [_vp, _vp]),

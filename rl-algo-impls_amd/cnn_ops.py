@@ -187,6 +187,10 @@ _CONV_FUSE_RELU_BWD = os.environ.get("RAI_CONV_FUSE_RELU_BWD", "1") != "0"  # +0
 # the per-image input-gradient kernel (round 4): conv2 26.8 vs MIOpen 33.2 us, conv3 21.0 vs 27.7 us at B = 256,
 # C3 155.6-156.2k vs 150.9-152.9k env-steps/s same box (profiles/r4e_*); RAI_CONV_MFMA_DGRAD=0 restores MIOpen's dx
 _CONV_MFMA_DGRAD = os.environ.get("RAI_CONV_MFMA_DGRAD", "1") == "1"
+# the first layer on the uint8 frames (round 4): the gather writes the minibatch as uint8 NHWC and conv1's
+# forward / weight gradient read x = u8 / range_size in-kernel (rai_conv2d_bias_relu_fwd_u8,
+# rai_conv2d_wgrad_*partials_u8); RAI_CONV_U8=0 keeps the float32 prescale in the gather
+_CONV_U8 = os.environ.get("RAI_CONV_U8", "1") == "1"
 
 
 class _WgradWorkspaces:
@@ -215,20 +219,32 @@ _WG_WS = _WgradWorkspaces()
 
 def _mfma_conv_ok(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride, padding) -> bool:
     """The shapes and layouts csrc/conv.hip takes: NHWC fp32 input, channels_last weight, no padding,
-    Ci % 4 == 0, Co 32 / 64, KH * KW * Ci % 64 == 0, 16-B aligned pointers."""
+    Ci % 4 == 0, Co 32 / 64, KH * KW * Ci % 64 == 0, 16-B aligned pointers; or a uint8 NHWC input with
+    Ci == 4 (4-B aligned, under 2^31 bytes: the _u8 kernels)."""
     if not _CONV_MFMA or tuple(_pair(padding)) != (0, 0):
         return False
     Co, Ci, KH, KW = (int(v) for v in w.shape)
     # operand shapes must agree (the kernels take Ci, H, W from x): mismatches go to F.conv2d, which raises
     if x.dim() != 4 or int(x.shape[1]) != Ci or int(x.shape[2]) < KH or int(x.shape[3]) < KW:
         return False
-    return (x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+    if x.dtype == torch.uint8:
+        x_ok = (Ci == 4 and x.data_ptr() % 4 == 0 and x.numel() < 2 ** 31)
+    else:
+        x_ok = x.dtype == torch.float32 and x.data_ptr() % 16 == 0
+    return (x_ok and x.is_contiguous(memory_format=torch.channels_last)
             and w.is_contiguous(memory_format=torch.channels_last) and Ci % 4 == 0 and Co in (32, 64)
             and (KH * KW * Ci) % 64 == 0 and KH * KW * Ci <= 8192 and b.is_contiguous()
-            and all(t.data_ptr() % 16 == 0 for t in (x, w, b)))
+            and all(t.data_ptr() % 16 == 0 for t in (w, b)))
 
 
-def _conv_fwd_mfma(x, w, b, stride, flatten) -> torch.Tensor:
+def _u8_to_f32(x: torch.Tensor, x_div: float) -> torch.Tensor:
+    """x.float() / x_div, channels_last: IEEE division by a device scalar (as the gather's prescale; a
+    Python-scalar divisor would be a multiply by the rounded reciprocal on the GPU)."""
+    d = torch.tensor(float(x_div), dtype=torch.float32, device=x.device)
+    return (x.float() / d).contiguous(memory_format=torch.channels_last)
+
+
+def _conv_fwd_mfma(x, w, b, stride, flatten, x_div=None) -> torch.Tensor:
     B, Ci, H, W = (int(v) for v in x.shape)
     Co, _, KH, KW = (int(v) for v in w.shape)
     s = _pair(stride)[0]
@@ -237,9 +253,15 @@ def _conv_fwd_mfma(x, w, b, stride, flatten) -> torch.Tensor:
         y = torch.empty((B, Co * OH * OW), dtype=torch.float32, device=x.device)
     else:
         y = torch.empty((B, Co, OH, OW), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-    _lib.check(_lib.lib().rai_conv2d_bias_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), B, H, W, Ci, Co, KH,
-                                                   KW, s, 1 if flatten else 0, y.data_ptr(),
-                                                   _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd")
+    L = _lib.lib()
+    if x.dtype == torch.uint8:
+        _lib.check(L.rai_conv2d_bias_relu_fwd_u8(x.data_ptr(), float(x_div), w.data_ptr(), b.data_ptr(), B, H, W, Ci,
+                                                 Co, KH, KW, s, 1 if flatten else 0, y.data_ptr(),
+                                                 _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd_u8")
+        return y
+    _lib.check(L.rai_conv2d_bias_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), B, H, W, Ci, Co, KH,
+                                          KW, s, 1 if flatten else 0, y.data_ptr(),
+                                          _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd")
     return y
 
 
@@ -275,10 +297,12 @@ def _conv_dgrad_relu(x, dy, y, w, stride):
     return dx
 
 
-def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, pending: "_PendingGrads", y=None, db=None):
+def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, pending: "_PendingGrads", y=None, db=None,
+                         x_div=None):
     """rai_conv2d_wgrad_partials for this layer (with y: rai_conv2d_wgrad_relu_partials, dz being the ReLU
-    output's gradient dy, and the bias gradient reduced into db); returns (job, workspace) for the
-    deferred reduction.  A reduction still pending on the layer's workspace runs first (pending.reserve)."""
+    output's gradient dy, and the bias gradient reduced into db; a uint8 x: the _u8 forms, x / x_div);
+    returns (job, workspace) for the deferred reduction.  A reduction still pending on the layer's
+    workspace runs first (pending.reserve)."""
     B, Ci, H, W = (int(v) for v in x.shape)
     Co, _, KH, KW = (int(v) for v in w.shape)
     s = _pair(stride)[0]
@@ -287,7 +311,14 @@ def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, pending: 
     ws = _WG_WS.get(module, nb, x.device)
     pending.reserve(ws)
     st = _lib.stream_handle(x.device)
-    if y is None:
+    if x.dtype == torch.uint8 and y is None:
+        _lib.check(L.rai_conv2d_wgrad_partials_u8(x.data_ptr(), float(x_div), dz.data_ptr(), B, H, W, Ci, Co, KH, KW,
+                                                  s, ws.data_ptr(), nb, st), "rai_conv2d_wgrad_partials_u8")
+    elif x.dtype == torch.uint8:
+        _lib.check(L.rai_conv2d_wgrad_relu_partials_u8(dz.data_ptr(), y.data_ptr(), x.data_ptr(), float(x_div), B, H,
+                                                       W, Ci, Co, KH, KW, s, ws.data_ptr(), nb, st),
+                   "rai_conv2d_wgrad_relu_partials_u8")
+    elif y is None:
         _lib.check(L.rai_conv2d_wgrad_partials(x.data_ptr(), dz.data_ptr(), B, H, W, Ci, Co, KH, KW, s, ws.data_ptr(),
                                                nb, st), "rai_conv2d_wgrad_partials")
     else:
@@ -354,10 +385,14 @@ class ConvBiasReLU(torch.autograd.Function):
     torch.flatten(., 1) of it (NCHW order, (B, C*H*W)) by the transposing epilogue pair."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, key, flatten=False):
+    def forward(ctx, x, w, b, stride, padding, key, flatten=False, x_div=None):
         mfma = _mfma_conv_ok(x, w, b, stride, padding) and len(set(_pair(stride))) == 1
+        if x.dtype == torch.uint8 and not mfma:  # uint8 frames outside the _u8 kernels: the prescale here
+            x = _u8_to_f32(x, x_div)
+            mfma = _mfma_conv_ok(x, w, b, stride, padding) and len(set(_pair(stride))) == 1
+        ctx.x_div = x_div
         if mfma:
-            y = _conv_fwd_mfma(x, w, b, stride, flatten)
+            y = _conv_fwd_mfma(x, w, b, stride, flatten, x_div)
             B, _, H, W = x.shape
             s = _pair(stride)[0]
             zshape = (int(B), int(w.shape[0]), (int(H) - int(w.shape[2])) // s + 1, (int(W) - int(w.shape[3])) // s + 1)
@@ -375,6 +410,7 @@ class ConvBiasReLU(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, b, y = ctx.saved_tensors
         stride, padding, key, direct_b, direct_w, flatten, zshape, mfma = ctx.conf
+        u8 = x.dtype == torch.uint8  # (never needs an input gradient)
         if (mfma and _CONV_FUSE_RELU_BWD and not flatten and direct_b and direct_w
                 and (not ctx.needs_input_grad[0] or _CONV_MFMA_DGRAD)
                 and w.grad.is_contiguous(memory_format=torch.channels_last) and w.grad.data_ptr() % 16 == 0
@@ -387,9 +423,10 @@ class ConvBiasReLU(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 dx = _conv_dgrad_relu(x, dy, y, w, stride)
             if dx is not None or not ctx.needs_input_grad[0]:
-                job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, ctx.pending, y=y, db=b.grad)
+                job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, ctx.pending, y=y, db=b.grad,
+                                                x_div=ctx.x_div)
                 ctx.pending.add_wgrad(job, wsp, w)
-                return dx, None, None, None, None, None, None
+                return dx, None, None, None, None, None, None, None
         ws = _WS.get(key, zshape[1], y.device)
         if flatten:
             dz, db = _bias_relu_bwd_nchw(dy.contiguous(), y, b, ws, direct_b, zshape)
@@ -397,6 +434,10 @@ class ConvBiasReLU(torch.autograd.Function):
             dy = dy.contiguous(memory_format=torch.channels_last)
             dz, db = _bias_relu_bwd(dy, y, b, ws, direct_b)
         need_dx = ctx.needs_input_grad[0]
+        if u8 and not (mfma and direct_w and w.grad.is_contiguous(memory_format=torch.channels_last)
+                       and w.grad.data_ptr() % 16 == 0 and dz.is_contiguous(memory_format=torch.channels_last)
+                       and dz.data_ptr() % 16 == 0):
+            x = _u8_to_f32(x, ctx.x_div)  # the float32 forms below (outside the trainer's direct gradients)
         if mfma and dz.is_contiguous(memory_format=torch.channels_last) and dz.data_ptr() % 16 == 0:
             dx = None
             if need_dx:
@@ -405,7 +446,7 @@ class ConvBiasReLU(torch.autograd.Function):
             if (direct_w and g.is_contiguous(memory_format=torch.channels_last) and g.data_ptr() % 16 == 0):
                 # partial tiles now; their reduction into the flat .grad joins the other layers' in one
                 # launch at direct_grads() exit
-                job, ws = _conv_wgrad_partials(key, x, dz, w, stride, g, ctx.pending)
+                job, ws = _conv_wgrad_partials(key, x, dz, w, stride, g, ctx.pending, x_div=ctx.x_div)
                 ctx.pending.add_wgrad(job, ws, w)
                 dw = None
             else:
@@ -414,13 +455,13 @@ class ConvBiasReLU(torch.autograd.Function):
                 if direct_w:
                     ctx.pending.add(w, dw)
                     dw = None
-            return dx, dw, db, None, None, None, None
+            return dx, dw, db, None, None, None, None, None
         dx, dw, _ = torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), _pair(padding), [1, 1],
                                                         False, [0, 0], 1, [need_dx, True, False])
         if direct_w:  # accumulated with the other layers' at direct_grads() exit
             ctx.pending.add(w, dw)
             dw = None
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 class LinearBiasReLU(torch.autograd.Function):
@@ -460,10 +501,16 @@ def _pair(v):
 _BRT_MAX_ELEMS = 8192  # csrc/se_block.hip BRT_MAX_ELEMS: (C + 1) * H * W of the transposing pair
 
 
-def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor, flatten: bool = False) -> torch.Tensor:
+def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor, flatten: bool = False, x_div=None) -> torch.Tensor:
     """relu(conv(x)) for an NHWC fp32 GPU activation (fused epilogue), else the module path.
-    flatten: return torch.flatten(relu(conv(x)), 1) (NCHW order), transposed inside the epilogue."""
-    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.bias is not None and conv.groups == 1
+    flatten: return torch.flatten(relu(conv(x)), 1) (NCHW order), transposed inside the epilogue.
+    x_div: x is uint8 frames and the layer's input is x / x_div (the NatureCNN prescale)."""
+    if x.dtype == torch.uint8 and (x_div is None or not x.is_cuda):
+        if x_div is None:
+            raise ValueError("conv_relu: a uint8 input needs its divisor (x_div)")
+        x = x.float() / x_div  # CPU: IEEE division
+        x_div = None
+    if (x.is_cuda and (x.dtype == torch.float32 or x.dtype == torch.uint8) and x.dim() == 4 and conv.bias is not None and conv.groups == 1
             and tuple(conv.dilation) == (1, 1) and conv.padding_mode == "zeros" and isinstance(conv.padding, tuple)
             and conv.out_channels % 4 == 0 and 256 % (conv.out_channels // 4) == 0):
         if flatten:
@@ -472,10 +519,12 @@ def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor, flatten: bool = False) -> 
                 hw *= (int(x.shape[2 + d]) + 2 * conv.padding[d] - conv.kernel_size[d]) // conv.stride[d] + 1
             flatten = (conv.out_channels + 1) * hw <= _BRT_MAX_ELEMS
             if not flatten:
-                return torch.flatten(conv_relu(conv, x), 1)
+                return torch.flatten(conv_relu(conv, x, x_div=x_div), 1)
         _WS.prewarm(conv, conv.out_channels, x.device)
         return ConvBiasReLU.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), conv,
-                                  flatten)
+                                  flatten, x_div)
+    if x.dtype == torch.uint8:
+        x = _u8_to_f32(x, x_div)
     y = F.relu(conv(x))
     return torch.flatten(y, 1) if flatten else y
 

@@ -40,6 +40,8 @@ constexpr int CV_MAXCHUNK = 2048;  // K <= 8192
 
 struct ConvFwdArgs {
   const float* x;
+  const uint8_t* xu8;  // U8 forms: the uint8 NHWC input (Ci = 4), read as x = u8 / xdiv
+  float xdiv;
   const float* w;
   const float* b;
   float* y;
@@ -175,12 +177,16 @@ static int allow_lds(const void* kernel) {
 // one per CU) copies its COT rows x K once (row stride K + 4 floats: the 16 lanes of a ds_read_b128
 // group land on distinct banks), then loops over pixel tiles; only the im2col operand is read from
 // L1/L2 per quad.
-template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF, bool BUF = false>
+template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF, bool BUF = false, bool U8 = false>
 __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) {
   static_assert(WCO * WPX == 8, "eight waves");
+  static_assert(!U8 || BUF, "the uint8 input is read through a buffer resource");
   constexpr int COT = 16 * TCO * WCO, PXT = 16 * TPX * WPX;
   extern __shared__ __attribute__((aligned(16))) float wl[];  // [COT][K + 4]
   __shared__ int xoff[CV_MAXCHUNK];
+  __shared__ float lut[U8 ? 256 : 1];  // U8: lut[u] = u / xdiv (IEEE division, as the gather's prescale)
+  if (U8)
+    for (int i = threadIdx.x; i < 256; i += 512) lut[i] = (float)i / a.xdiv;
   const int K = a.K, KP = K + 4;
   const int nch = K >> 2;
   const int co_wg = blockIdx.y * COT;
@@ -203,7 +209,8 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   const int64_t ntiles = (a.M + PXT - 1) / PXT;
   const int nq = nch >> 2;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.x), 0, BUF ? (int)((a.M / (a.OH * a.OW)) * a.H * a.W * a.Ci * 4) : 0, 0x00020000);
+      U8 ? (void*)const_cast<uint8_t*>(a.xu8) : (void*)const_cast<float*>(a.x), 0,
+      BUF ? (int)((a.M / (a.OH * a.OW)) * a.H * a.W * a.Ci * (U8 ? 1 : 4)) : 0, 0x00020000);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t px0 = tile * PXT + 16 * TPX * wpx;
     const float* xb[TPX];
@@ -226,6 +233,14 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
     f4 Br[PF][TPX];
     auto ldb = [&](int qd, f4(&Bv)[TPX]) {
       const int xo = xoff[4 * qd + g];
+      if (U8) {  // one pixel's 4 channels per chunk (Ci = 4): one dword, four table reads
+#pragma unroll
+        for (int tp = 0; tp < TPX; ++tp) {
+          const unsigned u = __builtin_amdgcn_raw_buffer_load_b32(xrs, xbo[tp] + xo, 0, 0);
+          Bv[tp] = f4{lut[u & 255u], lut[(u >> 8) & 255u], lut[(u >> 16) & 255u], lut[u >> 24]};
+        }
+        return;
+      }
       if (BUF) {
 #pragma unroll
         for (int tp = 0; tp < TPX; ++tp)
@@ -283,11 +298,11 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   }
 }
 
-template <int TCO, int TPX, int WCO, int WPX, int PF, bool BUF = false>
+template <int TCO, int TPX, int WCO, int WPX, int PF, bool BUF = false, bool U8 = false>
 int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   constexpr int PXT = 16 * TPX * WPX, COT = 16 * TCO * WCO;
   if (a.Co % COT) return RAI_E_SHAPE;
-  if (BUF && (a.M / ((int64_t)a.OH * a.OW)) * a.H * a.W * a.Ci * 4 >= (1LL << 31)) return RAI_E_SHAPE;
+  if (BUF && (a.M / ((int64_t)a.OH * a.OW)) * a.H * a.W * a.Ci * (U8 ? 1 : 4) >= (1LL << 31)) return RAI_E_SHAPE;
   const size_t lds = (size_t)COT * (a.K + 4) * sizeof(float);
   if (lds + CV_MAXCHUNK * 4 > 160 * 1024) return RAI_E_SHAPE;
   const int64_t ntiles = (a.M + PXT - 1) / PXT;
@@ -297,12 +312,12 @@ int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   if (gx < 1) gx = 1;
   const dim3 grid((unsigned)gx, (unsigned)cot);
   if (nchw) {
-    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF, BUF>;
+    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF, BUF, U8>;
     const int e = allow_lds(reinterpret_cast<const void*>(k));
     if (e != RAI_OK) return e;
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
   } else {
-    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, false, PF, BUF>;
+    auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, false, PF, BUF, U8>;
     const int e = allow_lds(reinterpret_cast<const void*>(k));
     if (e != RAI_OK) return e;
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
@@ -342,6 +357,8 @@ constexpr int WR_MAXPX = 8192;  // pixels per split (their base offsets sit in L
 
 struct ConvWrwArgs {
   const float* x;
+  const uint8_t* xu8;  // U8 forms: uint8 NHWC input (Ci = 4), x = u8 / xdiv
+  float xdiv;
   const float* dz;  // RB: dy, the gradient of the ReLU's output
   const float* y;   // RB: the forward output (dz = y > 0 ? dy : 0, as threshold_backward)
   float* part;      // [S][Co][K], then (RB) the bias-gradient partials [S][Co]
@@ -350,10 +367,13 @@ struct ConvWrwArgs {
   int H, W, Ci, Co, KW, S_, OH, OW, K;
 };
 
-template <int VC, int PF, bool RB, bool BUF = false>
+template <int VC, int PF, bool RB, bool BUF = false, bool U8 = false>
 __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs a) {
+  static_assert(!U8 || BUF, "the uint8 input is read through a buffer resource");
   constexpr int NB = VC * 4;  // 16x16 accumulator blocks per wave
   __shared__ float dbl[RB ? 4 * 16 * VC : 1];  // RB: the waves' bias-gradient sums
+  __shared__ float lut[U8 ? 256 : 1];          // U8: lut[u] = u / xdiv
+  if (U8) lut[threadIdx.x] = (float)threadIdx.x / a.xdiv;  // CV_THREADS == 256
   // LDS: the split's pixel -> input offset table, later reused for the cross-wave sum of the tiles
   constexpr int TAB_BYTES = WR_MAXPX * 4, RED_BYTES = 3 * NB * 64 * 16;
   __shared__ __attribute__((aligned(16))) unsigned char lds[TAB_BYTES > RED_BYTES ? TAB_BYTES : RED_BYTES];
@@ -399,7 +419,8 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(RB ? a.y : a.dz), 0,
                                                                          BUF ? (int)(a.M * a.Co * 4) : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.x), 0, BUF ? (int)((a.M / (a.OH * a.OW)) * a.H * a.W * a.Ci * 4) : 0, 0x00020000);
+        U8 ? (void*)const_cast<uint8_t*>(a.xu8) : (void*)const_cast<float*>(a.x), 0,
+        BUF ? (int)((a.M / (a.OH * a.OW)) * a.H * a.W * a.Ci * (U8 ? 1 : 4)) : 0, 0x00020000);
     auto ldz = [&](const __amdgpu_buffer_rsrc_t& rs, int off) -> fv {
       if constexpr (VC == 4) return __builtin_bit_cast(fv, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * off, 0, 0));
       else return __builtin_bit_cast(fv, __builtin_amdgcn_raw_buffer_load_b64(rs, 4 * off, 0, 0));
@@ -413,7 +434,12 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
 #pragma unroll
           for (int j = 0; j < VC; ++j) dv[j] = yv[j] > 0.f ? dv[j] : 0.f;
         }
-        xv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, 4 * (xco + xbase_l[pl]), 0, 0));
+        if (U8) {
+          const unsigned u = __builtin_amdgcn_raw_buffer_load_b32(xrs, xco + xbase_l[pl], 0, 0);
+          xv = f4{lut[u & 255u], lut[(u >> 8) & 255u], lut[(u >> 16) & 255u], lut[u >> 24]};
+        } else {
+          xv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, 4 * (xco + xbase_l[pl]), 0, 0));
+        }
       } else if (pl < hi) {
         dv = *reinterpret_cast<const fv*>(dzc + (int64_t)pl * a.Co);
         if (RB) {
@@ -1158,14 +1184,22 @@ static bool wgrad_shape_ok(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t 
 // the first launch of rai_conv2d_wgrad: every workgroup's partial tile into workspace (B >= 1)
 static int wgrad_partials(const float* x, const float* dz, const float* y, int64_t B, int32_t H, int32_t W,
                           int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, void* workspace,
-                          int64_t workspace_bytes, int32_t target_wgs, int32_t pf, hipStream_t st) {
+                          int64_t workspace_bytes, int32_t target_wgs, int32_t pf, hipStream_t st,
+                          const uint8_t* xu8 = nullptr, float xdiv = 1.f) {
   const int64_t K = (int64_t)KH * KW * Ci;
+  if (xu8) {  // uint8 input: one dword per pixel (Ci = 4), buffer loads
+    if (Ci != 4 || !(xdiv > 0.f) || (int64_t)B * H * W * Ci >= (1LL << 31)) return RAI_E_SHAPE;
+    if ((uintptr_t)xu8 & 3) return RAI_E_SHAPE;
+    x = reinterpret_cast<const float*>(xu8);  // never dereferenced as float
+  }
   if (!x || !dz || !workspace) return RAI_E_NULLPTR;
-  if (((uintptr_t)x | (uintptr_t)dz | (uintptr_t)workspace) & 15) return RAI_E_SHAPE;
+  if (((uintptr_t)(xu8 ? nullptr : x) | (uintptr_t)dz | (uintptr_t)workspace) & 15) return RAI_E_SHAPE;
   if ((int64_t)H * W * Ci > (1LL << 30)) return RAI_E_SHAPE;  // per-chunk offsets are int32
   if (workspace_bytes < rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, stride)) return RAI_E_WORKSPACE;
   ConvWrwArgs a;
   a.x = x;
+  a.xu8 = xu8;
+  a.xdiv = xdiv;
   a.dz = dz;
   a.y = y;
   a.part = static_cast<float*>(workspace);
@@ -1190,7 +1224,14 @@ static int wgrad_partials(const float* x, const float* dz, const float* y, int64
   // B = 256: 2-4 % faster than pointer loads, B = 1024: 8-21 %; profiles/r4g_conv_bench.txt)
   if (pf <= 0) pf = buf_ok ? 104 : 4;
   if (pf >= 100 && !buf_ok) return RAI_E_SHAPE;
-  if (y) {  // the ReLU backward and the bias gradient fused in (rai_conv2d_wgrad_relu_partials)
+  if (xu8) {  // buffer loads, 4 pixel steps in flight (the default form), uint8 input
+    if (!buf_ok) return RAI_E_SHAPE;
+    if (y && (((uintptr_t)y) & 15)) return RAI_E_SHAPE;
+    if (y && p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true, true, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else if (y) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true, true, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, false, true, true>), grid, dim3(CV_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((conv_wrw_kernel<4, 4, false, true, true>), grid, dim3(CV_THREADS), 0, st, a);
+  } else if (y) {  // the ReLU backward and the bias gradient fused in (rai_conv2d_wgrad_relu_partials)
     if (((uintptr_t)y) & 15) return RAI_E_SHAPE;
     if (pf == 104 && p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true, true>), grid, dim3(CV_THREADS), 0, st, a);
     else if (pf == 104) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true, true>), grid, dim3(CV_THREADS), 0, st, a);
@@ -1311,6 +1352,28 @@ extern "C" int rai_conv2d_wgrad_relu_partials(const float* dy, const float* y, c
                         rai_stream(stream));
 }
 
+// uint8-input forms of the two partial passes (the first NatureCNN layer: x = u8 / x_divisor, Ci = 4)
+extern "C" int rai_conv2d_wgrad_partials_u8(const uint8_t* x, float x_divisor, const float* dz, int64_t B, int32_t H,
+                                            int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride,
+                                            void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!wgrad_shape_ok(B, H, W, Ci, Co, KH, KW, stride) || Ci != 4) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!x) return RAI_E_NULLPTR;
+  return wgrad_partials(nullptr, dz, nullptr, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, 0, 0,
+                        rai_stream(stream), x, x_divisor);
+}
+
+extern "C" int rai_conv2d_wgrad_relu_partials_u8(const float* dy, const float* y, const uint8_t* x, float x_divisor,
+                                                 int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH,
+                                                 int32_t KW, int32_t stride, void* workspace, int64_t workspace_bytes,
+                                                 void* stream) {
+  if (!wgrad_shape_ok(B, H, W, Ci, Co, KH, KW, stride) || Ci != 4) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!x || !y) return RAI_E_NULLPTR;
+  return wgrad_partials(nullptr, dy, y, B, H, W, Ci, Co, KH, KW, stride, workspace, workspace_bytes, 0, 0,
+                        rai_stream(stream), x, x_divisor);
+}
+
 extern "C" int rai_conv2d_wgrad_reduce(const rai_conv2d_wgrad_job* jobs, int32_t n_jobs, int32_t accumulate,
                                        void* stream) {
   if (n_jobs < 0 || n_jobs > RAI_WGRAD_MAX_JOBS) return RAI_E_SHAPE;
@@ -1332,6 +1395,8 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
   if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y) & 15) return RAI_E_SHAPE;
   ConvFwdArgs a;
   a.x = x;
+  a.xu8 = nullptr;
+  a.xdiv = 1.f;
   a.w = w;
   a.b = b;
   a.y = y;
@@ -1384,6 +1449,48 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
     case 18: return launch_fwd_lds<2, 2, 2, 4, 3, true>(a, nchw, st);  // variant 12, buffer loads
     default: return RAI_E_SHAPE;
   }
+}
+
+// The first NatureCNN layer on the rollout's uint8 frames (NHWC, Ci = 4): x = u8 / x_divisor formed in the
+// kernel (IEEE division, the value the gather's prescale writes), so the f32 input tensor (4x the
+// bytes) is never written or read.  The LDS-weight forms with buffer loads (variants 16 / 17's blocking).
+extern "C" int rai_conv2d_bias_relu_fwd_u8(const uint8_t* x, float x_divisor, const float* w, const float* b,
+                                          int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH,
+                                          int32_t KW, int32_t stride, int32_t out_nchw, float* y, void* stream) {
+  if (B < 0 || H < 1 || W < 1 || Ci != 4 || Co < 16 || Co % 16 || KH < 1 || KW < 1 || stride < 1 || KH > H ||
+      KW > W || !(x_divisor > 0.f))
+    return RAI_E_SHAPE;
+  const int64_t K = (int64_t)KH * KW * Ci;
+  if (K % 32 || K / 4 > CV_MAXCHUNK) return RAI_E_SHAPE;
+  if (B == 0) return RAI_OK;
+  if (!x || !w || !b || !y) return RAI_E_NULLPTR;
+  if ((((uintptr_t)w | (uintptr_t)b | (uintptr_t)y) & 15) || ((uintptr_t)x & 3)) return RAI_E_SHAPE;
+  if (B * H * W * (int64_t)Ci >= (1LL << 31)) return RAI_E_SHAPE;
+  ConvFwdArgs a;
+  a.x = nullptr;
+  a.xu8 = x;
+  a.xdiv = x_divisor;
+  a.w = w;
+  a.b = b;
+  a.y = y;
+  a.H = H;
+  a.W = W;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.KW = KW;
+  a.S = stride;
+  a.OH = (H - KH) / stride + 1;
+  a.OW = (W - KW) / stride + 1;
+  a.K = (int)K;
+  a.M = B * a.OH * a.OW;
+  hipStream_t st = rai_stream(stream);
+  const bool nchw = out_nchw != 0;
+  const size_t lds32 = (size_t)32 * (K + 4) * 4, lds64 = (size_t)64 * (K + 4) * 4;
+  const int64_t t14 = (a.M + 255) / 256 * (Co / 32);
+  if (Co % 32 == 0 && lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && (t14 >= 256 || Co % 64 != 0))
+    return launch_fwd_lds<2, 2, 1, 8, 3, true, true>(a, nchw, st);
+  if (Co % 64 == 0 && lds64 + CV_MAXCHUNK * 4 <= 160 * 1024) return launch_fwd_lds<2, 1, 2, 4, 4, true, true>(a, nchw, st);
+  return RAI_E_UNSUPPORTED;
 }
 
 extern "C" int rai_conv2d_bias_relu_fwd(const float* x, const float* w, const float* b, int64_t B, int32_t H,

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
 struct MbDst {
   uint8_t* dst[RAI_MAX_FIELDS];
   int64_t units[RAI_MAX_FIELDS];
-  int32_t gran[RAI_MAX_FIELDS];  // 16 / 4 / 1: copy; 0: frame quads
+  int32_t gran[RAI_MAX_FIELDS];  // 16 / 4 / 1: copy; 0: frame quads -> f32; -1: frame quads -> u8 (4 planes)
   int32_t planes[RAI_MAX_FIELDS];
   int64_t hw[RAI_MAX_FIELDS];
   float divisor[RAI_MAX_FIELDS];
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(NT) void gather_minibatch_kernel(rai_minibatch_desc
         while (j >= (int)o.units[f]) j -= (int)o.units[f++];
         fk[k] = f;
         const uint8_t* src = static_cast<const uint8_t*>(d->src[f]);
-        if (o.gran[f] == 0) {  // frame quad j of row sr: one word per plane
+        if (o.gran[f] <= 0) {  // frame quad j of row sr: one word per plane
           const int C = o.planes[f];
           const int64_t hw4 = o.hw[f] >> 2;
           const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src) + sr * C * hw4 + j;
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(NT) void gather_minibatch_kernel(rai_minibatch_desc
           v[k].y = C > 1 ? s32[hw4] : 0u;
           v[k].z = C > 2 ? s32[2 * hw4] : 0u;
           v[k].w = C > 3 ? s32[3 * hw4] : 0u;
-          doff[k] = (r * o.hw[f] + 4LL * j) * C;  // float index of the quad's first pixel
+          doff[k] = (r * o.hw[f] + 4LL * j) * C;  // element (float or byte) index of the quad's first pixel
         } else {
           const int64_t so = sr * o.units[f] + j;
           doff[k] = r * o.units[f] + j;
@@ -140,6 +140,14 @@ __global__ __launch_bounds__(NT) void gather_minibatch_kernel(rai_minibatch_desc
           }
           out[q] = make_float4(e[0], e[1], e[2], e[3]);
         }
+      } else if (o.gran[f] == -1) {  // 4 pixels x 4 planes of bytes, transposed to pixel-major (NHWC)
+        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        uint32_t px[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          px[p] = ((w[0] >> (8 * p)) & 0xffu) | (((w[1] >> (8 * p)) & 0xffu) << 8) |
+                  (((w[2] >> (8 * p)) & 0xffu) << 16) | (((w[3] >> (8 * p)) & 0xffu) << 24);
+        *reinterpret_cast<uint4*>(o.dst[f] + doff[k]) = make_uint4(px[0], px[1], px[2], px[3]);
       } else if (o.gran[f] == 16) {
         reinterpret_cast<uint4*>(o.dst[f])[doff[k]] = v[k];
       } else if (o.gran[f] == 4) {
@@ -312,6 +320,15 @@ static int gather_minibatch(rai_minibatch_desc* desc, int32_t n_fields, void* co
       o.planes[i] = x.channels;
       o.hw[i] = x.hw;
       o.divisor[i] = x.divisor;
+      o.units[i] = x.hw / 4;
+    } else if (kind == RAI_XFORM_U8_CHW_TO_U8_HWC) {
+      const rai_gather_xform& x = xform[i];
+      // exactly 4 planes (one 16-B pixel-major quad per unit), 16-B aligned output
+      if (x.channels != 4 || x.hw < 4 || x.hw % 4 || 4 * x.hw != row_bytes[i] || ((uintptr_t)dst[i] & 15))
+        return RAI_E_SHAPE;
+      o.gran[i] = -1;
+      o.planes[i] = 4;
+      o.hw[i] = x.hw;
       o.units[i] = x.hw / 4;
     } else if (kind == RAI_XFORM_COPY) {
       const int gran = (row_bytes[i] % 16 == 0) ? 16 : ((row_bytes[i] % 4 == 0) ? 4 : 1);

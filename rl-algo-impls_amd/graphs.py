@@ -84,12 +84,14 @@ class MinibatchStepGraph:
 
 def static_buffers(fields: List[torch.Tensor], rows: int, device, xforms: Optional[list]) -> List[torch.Tensor]:
     """Minibatch destination buffers: the fields' own row shape and dtype, except a transformed
-    frame field (RAI_XFORM_U8_CHW_TO_F32_HWC), which is float32 channels_last."""
+    frame field: float32 channels_last (RAI_XFORM_U8_CHW_TO_F32_HWC) or uint8 channels_last
+    (RAI_XFORM_U8_CHW_TO_U8_HWC)."""
     out = []
     for i, f in enumerate(fields):
         x = xforms[i] if xforms is not None else None
-        if x is not None and x.kind == _lib.RAI_XFORM_U8_CHW_TO_F32_HWC:
-            out.append(torch.empty((rows,) + tuple(f.shape[1:]), dtype=torch.float32, device=device,
+        if x is not None and x.kind in (_lib.RAI_XFORM_U8_CHW_TO_F32_HWC, _lib.RAI_XFORM_U8_CHW_TO_U8_HWC):
+            dt = torch.float32 if x.kind == _lib.RAI_XFORM_U8_CHW_TO_F32_HWC else torch.uint8
+            out.append(torch.empty((rows,) + tuple(f.shape[1:]), dtype=dt, device=device,
                                    memory_format=torch.channels_last))
         else:
             out.append(torch.empty((rows,) + tuple(f.shape[1:]), dtype=f.dtype, device=device))

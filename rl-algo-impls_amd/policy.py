@@ -126,31 +126,43 @@ class NatureCnnEncoder(nn.Module):
         # the divisor as a device scalar (non-persistent: not in the state_dict), see forward()
         self.register_buffer("_range", torch.tensor(self.range_size, dtype=torch.float32), persistent=False)
 
+    def _u8_input(self, obs: torch.Tensor) -> bool:
+        """conv1 reads the uint8 frames itself (cnn_ops RAI_CONV_U8): 4 channels, the fused ReLU path."""
+        from . import cnn_ops
+
+        return (cnn_ops._CONV_U8 and cnn_ops._CONV_MFMA and _CHANNELS_LAST and _FUSED_EPILOGUES and self._relu
+                and obs.is_cuda and obs.dtype == torch.uint8 and int(obs.shape[-3]) == 4)
+
     def obs_transform(self, obs: torch.Tensor):
         """The rai_gather_xform that turns a gathered uint8 frame row into this encoder's input
-        (obs.float() / range_size, channels_last), or None when the fused path does not apply."""
+        (obs.float() / range_size, channels_last; or, where conv1 reads uint8 itself, the uint8 frames
+        in channels_last), or None when the fused path does not apply."""
         from . import _lib
 
         C, H, W = (int(d) for d in obs.shape[-3:])
         if not (_CHANNELS_LAST and _FUSED_EPILOGUES and obs.is_cuda and obs.dtype == torch.uint8 and C <= 4
                 and (H * W) % 4 == 0):
             return None
-        return _lib.GatherXform(kind=_lib.RAI_XFORM_U8_CHW_TO_F32_HWC, channels=C, hw=H * W,
-                                divisor=self.range_size)
+        kind = _lib.RAI_XFORM_U8_CHW_TO_U8_HWC if self._u8_input(obs) else _lib.RAI_XFORM_U8_CHW_TO_F32_HWC
+        return _lib.GatherXform(kind=kind, channels=C, hw=H * W, divisor=self.range_size)
 
     def forward(self, obs: torch.Tensor, prepared: bool = False) -> torch.Tensor:
-        """prepared: obs is already obs.float() / range_size in channels_last (the minibatch gather's
-        RAI_XFORM_U8_CHW_TO_F32_HWC output)."""
+        """prepared: obs is already the encoder's input in channels_last (the minibatch gather's output:
+        obs.float() / range_size, or the uint8 frames when conv1 applies the prescale itself)."""
         if obs.dim() == 3:
             obs = obs.unsqueeze(0)
         if prepared:
             x = obs
+        elif self._u8_input(obs):
+            x = obs.contiguous(memory_format=torch.channels_last)  # uint8: conv1 divides in-kernel
         elif obs.is_cuda:
             # IEEE division, as the reference's CPU path and the fused gather: torch divides a CUDA
             # tensor by a Python scalar as a multiply by the rounded reciprocal
             x = obs.float() / self._range
         else:
             x = obs.float() / self.range_size
+        if x.dtype == torch.uint8:  # prepared uint8 frames: only the fused path takes them
+            return self._forward_fused(x.contiguous(memory_format=torch.channels_last))
         if _CHANNELS_LAST and x.is_cuda:
             x = x.contiguous(memory_format=torch.channels_last)
             if _FUSED_EPILOGUES and self._relu:
@@ -162,8 +174,8 @@ class NatureCnnEncoder(nn.Module):
         cnn_ops (same modules, same parameters, same state_dict)."""
         from .cnn_ops import conv_relu, linear_relu
 
-        for i in (0, 2):
-            x = conv_relu(self.cnn[i], x)
+        x = conv_relu(self.cnn[0], x, x_div=self.range_size if x.dtype == torch.uint8 else None)
+        x = conv_relu(self.cnn[2], x)
         # conv3's epilogue writes the flattened (NCHW-order) fc input itself: no layout copies
         return linear_relu(self.fc[1], conv_relu(self.cnn[4], x, flatten=True))
 
