@@ -428,6 +428,16 @@ int rai_categorical_critic_heads_bwd(const float* enc, const float* wpi, const f
                                      const float* d_v, float* d_enc, float* g_wpi, float* g_bpi, float* g_wv,
                                      float* g_bv, int32_t accumulate, void* workspace, int64_t workspace_bytes,
                                      void* stream);
+/* The same backward with the ReLU backward of the layer that produced enc folded in (round 4; NatureCNN's
+ * fc -> ReLU, rl_algo_impls/shared/encoder/cnn.py:44-53): dz = enc <= 0 ? 0 : d_enc (threshold_backward on
+ * the saved ReLU output) is written in place of d_enc, and g_benc (D floats) receives that layer's bias
+ * gradient (the column sums of dz, fixed order; accumulate != 0 adds).  Replaces rai_bias_relu_bwd there. */
+int rai_categorical_critic_heads_bwd_relu(const float* enc, const float* wpi, const float* bpi, const float* wv,
+                                          const float* bv, const int64_t* actions, const float* logits, int64_t B,
+                                          int32_t D, int32_t A, const float* d_logp, const float* d_entropy,
+                                          const float* d_v, float* dz, float* g_wpi, float* g_bpi, float* g_wv,
+                                          float* g_bv, float* g_benc, int32_t accumulate, void* workspace,
+                                          int64_t workspace_bytes, void* stream);
 
 /* Per-field output transform of the minibatch gather.
  *   RAI_XFORM_COPY: the row's bytes are copied (as above).

@@ -171,6 +171,8 @@ _SIGNATURES = {
     "rai_categorical_critic_heads_workspace_bytes": (_i64, [_i64, _i32]),
     "rai_categorical_critic_heads_bwd": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp,
                                                    _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
+    "rai_categorical_critic_heads_bwd_relu": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp,
+                                                        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_bias_relu_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "rai_bias_relu_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_bias_relu_fwd_nchw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),

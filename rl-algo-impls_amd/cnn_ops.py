@@ -584,14 +584,92 @@ class CategoricalCriticHeads(torch.autograd.Function):
         return (d_enc,) + grads + (None,)
 
 
+class FcReluHeads(torch.autograd.Function):
+    """The fc layer -> ReLU and the Categorical + critic heads over its output as ONE autograd node
+    (round 4): forward = the fc GEMM with its bias + ReLU epilogue, then rai_categorical_critic_heads_fwd;
+    backward = rai_categorical_critic_heads_bwd_relu, which writes the fc's dz (its ReLU backward folded
+    into the heads' input gradient) and the fc's bias gradient, then dx = dz W and W.grad += dz^T x.  One
+    node, so no other consumer of the fc output can add an unmasked gradient behind the fold.  Used inside
+    direct_grads() only (every parameter gradient accumulated in place)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wpi, bpi, wv, bv, actions):
+        if _FC_ADDMM_RELU:
+            y = torch._addmm_activation(b, x, w.t(), use_gelu=False)
+        else:
+            y = _bias_relu_fwd(torch.mm(x, w.t()), b)
+        B, D = int(y.shape[0]), int(y.shape[1])
+        A = int(wpi.shape[0])
+        logits = torch.empty((B, A), dtype=torch.float32, device=y.device)
+        logp = torch.empty(B, dtype=torch.float32, device=y.device)
+        ent = torch.empty_like(logp)
+        v = torch.empty_like(logp)
+        _lib.check(_lib.lib().rai_categorical_critic_heads_fwd(
+            y.data_ptr(), wpi.data_ptr(), bpi.data_ptr(), wv.data_ptr(), bv.data_ptr(), actions.data_ptr(), B, D, A,
+            logits.data_ptr(), logp.data_ptr(), ent.data_ptr(), v.data_ptr(), _lib.stream_handle(y.device)),
+            "rai_categorical_critic_heads_fwd")
+        ctx.save_for_backward(x, w, b, y, wpi, bpi, wv, bv, actions, logits)
+        ctx.mark_non_differentiable(logits)
+        return logp, ent, v
+
+    @staticmethod
+    def backward(ctx, d_logp, d_ent, d_v):
+        x, w, b, y, wpi, bpi, wv, bv, actions, logits = ctx.saved_tensors
+        B, D, A = int(y.shape[0]), int(y.shape[1]), int(wpi.shape[0])
+        dev = y.device
+        z = lambda t: t.contiguous() if t is not None else torch.zeros(B, dtype=torch.float32, device=dev)
+        d_logp, d_ent, d_v = z(d_logp), z(d_ent), z(d_v)
+        dz = torch.empty_like(y)
+        L = _lib.lib()
+        ws = torch.empty(int(L.rai_categorical_critic_heads_workspace_bytes(B, A)), dtype=torch.uint8, device=dev)
+        _lib.check(L.rai_categorical_critic_heads_bwd_relu(
+            y.data_ptr(), wpi.data_ptr(), bpi.data_ptr(), wv.data_ptr(), bv.data_ptr(), actions.data_ptr(),
+            logits.data_ptr(), B, D, A, d_logp.data_ptr(), d_ent.data_ptr(), d_v.data_ptr(), dz.data_ptr(),
+            wpi.grad.data_ptr(), bpi.grad.data_ptr(), wv.grad.data_ptr(), bv.grad.data_ptr(), b.grad.data_ptr(), 1,
+            ws.data_ptr(), ws.numel(), _lib.stream_handle(dev)), "rai_categorical_critic_heads_bwd_relu")
+        dx = torch.mm(dz, w) if ctx.needs_input_grad[0] else None
+        w.grad.addmm_(dz.t(), x)  # beta = 1: the GEMM accumulates into the flat gradient view
+        notify_grad_written(w)  # data parallel: this layer's gradient bucket may go (dp_buckets)
+        return dx, None, None, None, None, None, None, None
+
+
+# the fc ReLU backward folded into the heads' backward (FcReluHeads); RAI_FC_HEADS_FOLD=0: separate nodes
+_FC_HEADS_FOLD = os.environ.get("RAI_FC_HEADS_FOLD", "1") == "1"
+
+
+def fc_relu_heads_fusable(network, lin: torch.nn.Linear, x: torch.Tensor, action_masks) -> bool:
+    """FcReluHeads applies: the heads are fusable over the fc output, the fc is a GPU fp32 Linear with a
+    bias, and every parameter involved accumulates its gradient in place (inside direct_grads())."""
+    if not (_FC_HEADS_FOLD and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and lin.bias is not None
+            and int(x.shape[1]) == lin.in_features):
+        return False
+    if not _heads_ok(network, action_masks):
+        return False
+    params = [lin.bias, network._pi._fc[0].weight, network._pi._fc[0].bias, network._v._fc[0][0].weight,
+              network._v._fc[0][0].bias]
+    return (all(_direct(p, raw=True) for p in params) and _direct(lin.weight)
+            and lin.weight.grad.is_contiguous())
+
+
+def fc_relu_heads(network, lin: torch.nn.Linear, x: torch.Tensor, actions: torch.Tensor):
+    lin_pi = network._pi._fc[0]
+    lin_v = network._v._fc[0][0]
+    return FcReluHeads.apply(x.contiguous(), lin.weight, lin.bias, lin_pi.weight, lin_pi.bias, lin_v.weight,
+                             lin_v.bias, actions.long().contiguous())
+
+
 def heads_fusable(network, enc: torch.Tensor, action_masks) -> bool:
     """A ConnectedTrio network whose actor head is Categorical Linear(D, A) and critic head
     Linear(D, 1), no hidden layers, no action masks, fp32 on the GPU (the NatureCNN policy)."""
+    return enc.is_cuda and enc.dtype == torch.float32 and enc.dim() == 2 and _heads_ok(network, action_masks)
+
+
+def _heads_ok(network, action_masks) -> bool:
     from .policy import CategoricalActorHead
 
     pi = network._pi
-    if not (enc.is_cuda and enc.dtype == torch.float32 and enc.dim() == 2 and action_masks is None
-            and isinstance(pi, CategoricalActorHead) and network.pi_hidden_sizes == () and network.v_hidden_sizes == ()):
+    if not (action_masks is None and isinstance(pi, CategoricalActorHead) and network.pi_hidden_sizes == ()
+            and network.v_hidden_sizes == ()):
         return False
     A = pi.act_dim
     return (2 <= A <= 10 or A == 12) and isinstance(pi._fc[0], torch.nn.Linear)

@@ -87,8 +87,10 @@ __global__ __launch_bounds__(HD_THREADS) void heads_fwd_kernel(const HeadsArgs a
   }
 }
 
-// (1) per row: dlogits and d_enc; dlogits (B, A) and dv (B) stored for pass (2)
-template <int A>
+// (1) per row: dlogits and d_enc; dlogits (B, A) and dv (B) stored for pass (2).  RELU (round 4): enc is
+// the output of the layer's ReLU and d_enc is written as that layer's dz = enc <= 0 ? 0 : d_enc (torch's
+// threshold_backward on the saved result), so the ReLU backward needs no pass of its own
+template <int A, bool RELU = false>
 __global__ __launch_bounds__(HD_THREADS) void heads_bwd_rows_kernel(const HeadsArgs a, const float* __restrict__ logits,
                                                                    const float* __restrict__ d_logp,
                                                                    const float* __restrict__ d_ent,
@@ -133,26 +135,32 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_rows_kernel(const HeadsA
     float s = gv * a.wv[d];
 #pragma unroll
     for (int o = 0; o < A; ++o) s = fmaf(dq[o], a.wpi[o * D + d], s);
+    if (RELU) s = a.enc[b * D + d] <= 0.f ? 0.f : s;
     d_enc[b * D + d] = s;
   }
 }
 
 // (2) weight gradients: workgroup j owns columns [16 j, 16 j + 16) of Wpi / Wv; its 256 threads are
 // 16 columns x 16 row lanes; each lane sums rows lane, lane + 16, ... (row order), then the 16 row
-// lanes are added in order through LDS.  Workgroup 0 also sums the bias gradients.
-template <int A>
+// lanes are added in order through LDS.  Workgroup 0 also sums the bias gradients.  FCB (round 4): the
+// same column sums of pass (1)'s dz give the bias gradient of the layer whose ReLU output enc is
+// (g_benc[d] = sum over rows of dz[:, d], row lanes in order, as the weights)
+template <int A, bool FCB = false>
 __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const HeadsArgs a,
                                                                       const float* __restrict__ dlogits,
                                                                       const float* __restrict__ dvv,
                                                                       float* __restrict__ g_wpi, float* __restrict__ g_bpi,
                                                                       float* __restrict__ g_wv, float* __restrict__ g_bv,
-                                                                      int accumulate) {
+                                                                      int accumulate, const float* __restrict__ dz = nullptr,
+                                                                      float* __restrict__ g_benc = nullptr) {
   __shared__ float red[A + 1][16][17];
+  __shared__ float redb[FCB ? 16 : 1][17];
   const int tid = threadIdx.x, col = tid & 15, rl = tid >> 4;
   const int d = blockIdx.x * 16 + col;
   const int D = a.D;
   const int64_t B = a.B;
   float acc[A + 1];
+  float accb = 0.f;
 #pragma unroll
   for (int o = 0; o <= A; ++o) acc[o] = 0.f;
   if (d < D) {
@@ -161,11 +169,20 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const Hea
 #pragma unroll
       for (int o = 0; o < A; ++o) acc[o] = fmaf(dlogits[b * A + o], x, acc[o]);
       acc[A] = fmaf(dvv[b], x, acc[A]);
+      if (FCB) accb += dz[b * D + d];
     }
   }
 #pragma unroll
   for (int o = 0; o <= A; ++o) red[o][rl][col] = acc[o];
+  if (FCB) redb[rl][col] = accb;
   __syncthreads();
+  if (FCB && tid < 16) {
+    const int dd = blockIdx.x * 16 + tid;
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += redb[r][tid];
+    if (dd < D) g_benc[dd] = accumulate ? g_benc[dd] + s : s;
+  }
   if (tid < 16 * (A + 1)) {
     const int o = tid >> 4, c = tid & 15;
     const int dd = blockIdx.x * 16 + c;
@@ -239,6 +256,14 @@ extern "C" int rai_categorical_critic_heads_fwd(const float* enc, const float* w
   return RAI_OK;
 }
 
+extern "C" int rai_categorical_critic_heads_bwd_relu(const float* enc, const float* wpi, const float* bpi,
+                                                     const float* wv, const float* bv, const int64_t* actions,
+                                                     const float* logits, int64_t B, int32_t D, int32_t A,
+                                                     const float* d_logp, const float* d_entropy, const float* d_v,
+                                                     float* dz, float* g_wpi, float* g_bpi, float* g_wv, float* g_bv,
+                                                     float* g_benc, int32_t accumulate, void* workspace,
+                                                     int64_t workspace_bytes, void* stream);
+
 extern "C" int64_t rai_categorical_critic_heads_workspace_bytes(int64_t B, int32_t A) {
   return B < 0 || A < 1 ? 0 : B * (int64_t)(A + 1) * 4;
 }
@@ -272,6 +297,51 @@ extern "C" int rai_categorical_critic_heads_bwd(const float* enc, const float* w
     RAI_HD_B(2) RAI_HD_B(3) RAI_HD_B(4) RAI_HD_B(5) RAI_HD_B(6) RAI_HD_B(7) RAI_HD_B(8) RAI_HD_B(9) RAI_HD_B(10)
     RAI_HD_B(12)
 #undef RAI_HD_B
+    default: return RAI_E_SHAPE;
+  }
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+// The heads' backward with the ReLU backward of the layer that produced enc folded in (round 4; NatureCNN's
+// fc -> ReLU, nature_cnn.py / cnn.py:44-53): dz = enc <= 0 ? 0 : d_enc is written instead of d_enc, and
+// g_benc (D floats) receives (accumulate: += ) that layer's bias gradient, the column sums of dz; the
+// separate rai_bias_relu_bwd pass over the (B, D) gradient is gone.
+extern "C" int rai_categorical_critic_heads_bwd_relu(const float* enc, const float* wpi, const float* bpi,
+                                                     const float* wv, const float* bv, const int64_t* actions,
+                                                     const float* logits, int64_t B, int32_t D, int32_t A,
+                                                     const float* d_logp, const float* d_entropy, const float* d_v,
+                                                     float* dz, float* g_wpi, float* g_bpi, float* g_wv, float* g_bv,
+                                                     float* g_benc, int32_t accumulate, void* workspace,
+                                                     int64_t workspace_bytes, void* stream) {
+  if (B < 0 || D < 1 || !a_ok(A)) return RAI_E_SHAPE;
+  if (!enc || !wpi || !bpi || !wv || !bv || !actions || !logits || !d_logp || !d_entropy || !d_v || !dz || !g_wpi ||
+      !g_bpi || !g_wv || !g_bv || !g_benc || !workspace)
+    return RAI_E_NULLPTR;
+  if (workspace_bytes < rai_categorical_critic_heads_workspace_bytes(B, A)) return RAI_E_WORKSPACE;
+  hipStream_t st = rai_stream(stream);
+  if (B == 0) {
+    if (!accumulate) {
+      const hipError_t e = hipMemsetAsync(g_benc, 0, (size_t)D * 4, st);
+      if (e != hipSuccess) return (int)e;
+    }
+    return RAI_OK;
+  }
+  const HeadsArgs a = make_args(enc, wpi, bpi, wv, bv, actions, B, D, A);
+  float* dlogits = static_cast<float*>(workspace);
+  float* dvv = dlogits + B * A;
+  const dim3 grid1((unsigned)((B + 3) / 4)), grid2((unsigned)((D + 15) / 16));
+  switch (A) {
+#define RAI_HD_BR(n)                                                                                            \
+  case n:                                                                                                       \
+    hipLaunchKernelGGL((heads_bwd_rows_kernel<n, true>), grid1, dim3(HD_THREADS), 0, st, a, logits, d_logp,      \
+                       d_entropy, d_v, dlogits, dvv, dz);                                                       \
+    hipLaunchKernelGGL((heads_bwd_weights_kernel<n, true>), grid2, dim3(HD_THREADS), 0, st, a, dlogits, dvv,     \
+                       g_wpi, g_bpi, g_wv, g_bv, accumulate, dz, g_benc);                                       \
+    break;
+    RAI_HD_BR(2) RAI_HD_BR(3) RAI_HD_BR(4) RAI_HD_BR(5) RAI_HD_BR(6) RAI_HD_BR(7) RAI_HD_BR(8) RAI_HD_BR(9)
+    RAI_HD_BR(10) RAI_HD_BR(12)
+#undef RAI_HD_BR
     default: return RAI_E_SHAPE;
   }
   RAI_LAUNCH_CHECK();

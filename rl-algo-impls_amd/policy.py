@@ -172,12 +172,36 @@ class NatureCnnEncoder(nn.Module):
     def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
         """Bias-free MIOpen convolutions / hipBLASLt GEMM with the bias + ReLU epilogues of
         cnn_ops (same modules, same parameters, same state_dict)."""
-        from .cnn_ops import conv_relu, linear_relu
+        return self.fc_relu(self._trunk_fused(x))
+
+    def _trunk_fused(self, x: torch.Tensor) -> torch.Tensor:
+        """The three conv -> ReLU layers; conv3's epilogue writes the flattened (NCHW-order) fc input
+        itself: no layout copies."""
+        from .cnn_ops import conv_relu
 
         x = conv_relu(self.cnn[0], x, x_div=self.range_size if x.dtype == torch.uint8 else None)
         x = conv_relu(self.cnn[2], x)
-        # conv3's epilogue writes the flattened (NCHW-order) fc input itself: no layout copies
-        return linear_relu(self.fc[1], conv_relu(self.cnn[4], x, flatten=True))
+        return conv_relu(self.cnn[4], x, flatten=True)
+
+    def fc_relu(self, flat: torch.Tensor) -> torch.Tensor:
+        from .cnn_ops import linear_relu
+
+        return linear_relu(self.fc[1], flat)
+
+    def forward_trunk(self, obs: torch.Tensor, prepared: bool = False):
+        """The flattened conv3 output (the fc layer's input) where the fused GPU path applies, else None
+        (the caller then runs forward())."""
+        if obs.dim() == 3:
+            obs = obs.unsqueeze(0)
+        if not (obs.is_cuda and _CHANNELS_LAST and _FUSED_EPILOGUES and self._relu):
+            return None
+        if prepared:
+            x = obs
+        elif self._u8_input(obs):
+            x = obs
+        else:
+            x = obs.float() / self._range
+        return self._trunk_fused(x.contiguous(memory_format=torch.channels_last))
 
 
 class Encoder(nn.Module):  # shared/encoder/encoder.py:25-73
@@ -326,7 +350,20 @@ class ConnectedTrioNetwork(nn.Module):
         self.v_hidden_sizes = tuple(v_hidden_sizes)
 
     def forward(self, obs, action, action_masks=None, obs_prepared: bool = False):
-        enc = self._feature_extractor(obs, obs_prepared)
+        if _FUSED_EPILOGUES and self._feature_extractor.kind == "cnn":
+            fe = self._feature_extractor.feature_extractor
+            trunk = fe.forward_trunk(obs, obs_prepared)  # conv3's flattened output, or None
+            if trunk is not None:
+                from .cnn_ops import fc_relu_heads, fc_relu_heads_fusable
+
+                # the fc -> ReLU and both heads as one node: the ReLU backward folded into the heads' backward
+                if fc_relu_heads_fusable(self, fe.fc[1], trunk, action_masks):
+                    return fc_relu_heads(self, fe.fc[1], trunk, action)
+                enc = fe.fc_relu(trunk)
+            else:
+                enc = self._feature_extractor(obs, obs_prepared)
+        else:
+            enc = self._feature_extractor(obs, obs_prepared)
         if _FUSED_EPILOGUES and self._feature_extractor.kind == "cnn":
             from .cnn_ops import categorical_critic_heads, heads_fusable
 

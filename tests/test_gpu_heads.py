@@ -53,3 +53,98 @@ def test_heads_match_module_path(B, D, A):
     for p, b in zip(params, gref[1:]):
         np.testing.assert_allclose((p.grad - 0.25).cpu().numpy(), b.reshape(p.shape).cpu().numpy(), rtol=2e-4,
                                    atol=2e-5 * float(b.abs().max()) + 1e-6)
+
+
+@pytest.mark.parametrize("B,A", [(256, 6), (37, 2), (1, 3)])
+def test_fc_relu_heads_fold_matches_the_separate_nodes(B, A):
+    """cnn_ops.FcReluHeads (the fc -> ReLU and both heads as one node; the ReLU backward folded into
+    rai_categorical_critic_heads_bwd_relu, which also writes the fc's bias gradient) against the unfused
+    module path (Linear -> ReLU -> CategoricalActorHead / CriticHead, torch autograd): outputs, the fc
+    input's gradient and every parameter gradient, accumulated into existing .grad views as in the
+    trainer.  Dead ReLU units (some fc outputs <= 0) are part of the input."""
+    torch.manual_seed(B * 7 + A)
+    D, F = 512, 3136
+    fc = torch.nn.Linear(F, D).to(DEV)
+    pi = CategoricalActorHead(A, D, (), torch.nn.ReLU).to(DEV)
+    v = CriticHead(D, (), torch.nn.ReLU).to(DEV)
+    with torch.no_grad():
+        pi._fc[0].weight.mul_(30.0)
+
+    class Net:  # the attributes fc_relu_heads reads from a ConnectedTrio network
+        pass
+
+    net = Net()
+    net._pi, net._v, net.pi_hidden_sizes, net.v_hidden_sizes = pi, v, (), ()
+    x = torch.randn(B, F, device=DEV) * 0.05
+    act = torch.randint(0, A, (B,), device=DEV)
+    up = [torch.randn(B, device=DEV) for _ in range(3)]
+    params = [fc.weight, fc.bias, pi._fc[0].weight, pi._fc[0].bias, v._fc[0][0].weight, v._fc[0][0].bias]
+
+    x1 = x.clone().requires_grad_(True)
+    enc = torch.relu(fc(x1))
+    assert (enc == 0).any() and (enc > 0).any()
+    d = torch.distributions.Categorical(logits=pi._fc(enc))
+    ref = (d.log_prob(act), d.entropy(), v(enc))
+    gref = torch.autograd.grad(ref, [x1] + params, up)
+
+    for p in params:
+        p.grad = torch.full_like(p, 0.25)
+    x2 = x.clone().requires_grad_(True)
+    with cnn_ops.direct_grads():
+        assert cnn_ops.fc_relu_heads_fusable(net, fc, x2, None)
+        out = cnn_ops.fc_relu_heads(net, fc, x2, act)
+    for o, r in zip(out, ref):
+        np.testing.assert_allclose(o.detach().cpu().numpy(), r.detach().cpu().numpy(), rtol=2e-5, atol=2e-5)
+    torch.autograd.backward(out, up)
+    np.testing.assert_allclose(x2.grad.cpu().numpy(), gref[0].cpu().numpy(), rtol=2e-4,
+                               atol=2e-5 * float(gref[0].abs().max()))
+    for name, p, b in zip(("w_fc", "b_fc", "wpi", "bpi", "wv", "bv"), params, gref[1:]):
+        np.testing.assert_allclose((p.grad - 0.25).cpu().numpy(), b.reshape(p.shape).cpu().numpy(), rtol=2e-4,
+                                   atol=2e-5 * float(b.abs().max()) + 1e-6, err_msg=name)
+    # outside direct_grads() the fold does not apply (autograd-returned gradients keep the separate nodes)
+    assert not cnn_ops.fc_relu_heads_fusable(net, fc, x2, None)
+
+
+def test_heads_bwd_relu_equals_heads_bwd_then_relu_bwd():
+    """rai_categorical_critic_heads_bwd_relu's dz is bit-identical to rai_categorical_critic_heads_bwd's
+    d_enc masked by threshold_backward (enc <= 0 -> 0), its head gradients are identical, and the fc bias
+    gradient equals the column sums of dz (fp32, fixed order)."""
+    import ctypes as C
+
+    from rl_algo_impls_amd import _lib
+    B, D, A = 256, 512, 6
+    g = torch.Generator(device="cpu").manual_seed(4)
+    enc = torch.relu(torch.randn(B, D, generator=g)).to(DEV)
+    wpi, bpi = (torch.randn(A, D, generator=g) * 0.1).to(DEV), torch.randn(A, generator=g).to(DEV)
+    wv, bv = (torch.randn(1, D, generator=g) * 0.1).to(DEV), torch.randn(1, generator=g).to(DEV)
+    act = torch.randint(0, A, (B,), generator=g).to(DEV)
+    dl, de, dv = (torch.randn(B, generator=g).to(DEV) for _ in range(3))
+    L, st = _lib.lib(), _lib.stream_handle(DEV)
+    logits, lp, en, vv = (torch.empty(B, A, device=DEV), torch.empty(B, device=DEV), torch.empty(B, device=DEV),
+                          torch.empty(B, device=DEV))
+    _lib.check(L.rai_categorical_critic_heads_fwd(enc.data_ptr(), wpi.data_ptr(), bpi.data_ptr(), wv.data_ptr(),
+                                                  bv.data_ptr(), act.data_ptr(), B, D, A, logits.data_ptr(),
+                                                  lp.data_ptr(), en.data_ptr(), vv.data_ptr(), st), "fwd")
+    ws = torch.empty(int(L.rai_categorical_critic_heads_workspace_bytes(B, A)), dtype=torch.uint8, device=DEV)
+    outs = []
+    for relu in (False, True):
+        grads = [torch.zeros_like(t) for t in (wpi, bpi, wv, bv)]
+        d_enc = torch.empty_like(enc)
+        gb = torch.full((D,), 0.5, device=DEV)
+        args = [enc.data_ptr(), wpi.data_ptr(), bpi.data_ptr(), wv.data_ptr(), bv.data_ptr(), act.data_ptr(),
+                logits.data_ptr(), B, D, A, dl.data_ptr(), de.data_ptr(), dv.data_ptr(), d_enc.data_ptr()]
+        args += [t.data_ptr() for t in grads]
+        if relu:
+            rc = L.rai_categorical_critic_heads_bwd_relu(*args, gb.data_ptr(), 1, ws.data_ptr(), ws.numel(), st)
+        else:
+            rc = L.rai_categorical_critic_heads_bwd(*args, 1, ws.data_ptr(), ws.numel(), st)
+        _lib.check(rc, "bwd")
+        torch.cuda.synchronize()
+        outs.append((d_enc.cpu(), [t.cpu() for t in grads], gb.cpu()))
+    dz_ref = torch.where(enc.cpu() <= 0, torch.zeros(()), outs[0][0])
+    assert torch.equal(outs[1][0], dz_ref)
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert torch.equal(a, b)
+    db_ref = 0.5 + dz_ref.double().sum(0)
+    bound = 0.5 + dz_ref.double().abs().sum(0)
+    assert ((outs[1][2].double() - db_ref).abs() <= (B + 2) * 2.0 ** -24 * bound).all()

@@ -69,19 +69,21 @@ def _fixture_rollout(z, meta):
 
 
 @pytest.mark.parametrize("graphs", [True, False], ids=["graph_replay", "eager"])
-@pytest.mark.parametrize("layout", ["nhwc_fused", "nhwc_fused_f32", "nhwc", "nchw"])
+@pytest.mark.parametrize("layout", ["nhwc_fused", "nhwc_fused_f32", "nhwc_fused_unfolded", "nhwc", "nchw"])
 def test_pong_minibatch_steps_match_reference(layout, graphs, monkeypatch):
     """nhwc_fused (the default): frames gathered as uint8 channels_last and read by conv1 itself
     (x = u8 / 255 in-kernel, cnn_ops RAI_CONV_U8) and the cnn_ops bias + ReLU epilogues with in-place
     gradient accumulation; nhwc_fused_f32: the same with the gather's uint8 -> float / 255 transform;
-    nhwc: the modules' own kernels on channels_last; nchw: plain NCHW."""
+    nhwc_fused_unfolded: the fc ReLU backward as its own pass instead of folded into the heads' backward
+    (RAI_FC_HEADS_FOLD=0); nhwc: the modules' own kernels on channels_last; nchw: plain NCHW."""
     from rl_algo_impls_amd import cnn_ops
 
     z = np.load(GOLDEN / "pong_steps.npz", allow_pickle=False)
     meta = json.loads(str(z["index"]))
     monkeypatch.setattr(policy_mod, "_CHANNELS_LAST", layout != "nchw")
     monkeypatch.setattr(policy_mod, "_FUSED_EPILOGUES", layout.startswith("nhwc_fused"))
-    monkeypatch.setattr(cnn_ops, "_CONV_U8", layout == "nhwc_fused")
+    monkeypatch.setattr(cnn_ops, "_CONV_U8", layout in ("nhwc_fused", "nhwc_fused_unfolded"))
+    monkeypatch.setattr(cnn_ops, "_FC_HEADS_FOLD", layout != "nhwc_fused_unfolded")
     pol = _pong_policy(meta["shapes"])
     nets.load_flat(pol, pong_init([tuple(s) for s in meta["shapes"]], meta["init_seed"]))
     pol = pol.to(DEV)
@@ -98,8 +100,8 @@ def test_pong_minibatch_steps_match_reference(layout, graphs, monkeypatch):
         assert fused_gather == layout.startswith("nhwc_fused")
         if fused_gather:
             kinds = {x.kind for g in algo._graphed.graphs.values() if g.xforms for x in g.xforms if x is not None}
-            assert kinds == {_lib.RAI_XFORM_U8_CHW_TO_U8_HWC if layout == "nhwc_fused"
-                             else _lib.RAI_XFORM_U8_CHW_TO_F32_HWC}
+            assert kinds == {_lib.RAI_XFORM_U8_CHW_TO_F32_HWC if layout == "nhwc_fused_f32"
+                             else _lib.RAI_XFORM_U8_CHW_TO_U8_HWC}
     lr = float(kw["learning_rate"])
     # pre-clip gradient norms (each step clips to 0.5): fp32, different conv summation order
     np.testing.assert_allclose(norms, z["norms"], rtol=2e-4)
