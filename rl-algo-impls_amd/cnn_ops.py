@@ -79,17 +79,49 @@ class _WgradJob(C.Structure):
 _MAX_JOBS = 4  # RAI_WGRAD_MAX_JOBS
 
 
+# Weight-gradient partials on a side stream (round 4): a layer's partials depend only on its dz (or dy, y)
+# and x, not on the input gradient the backward computes next, so they run beside the dgrad chain
+# (conv3 wgrad || conv3 dgrad -> conv2 dgrad, conv2 wgrad || ...) instead of after it; the reduction joins
+# the side stream first.  Inside a graph capture the fork and join are captured edges.  The operands are
+# kept referenced by the pending job until that join, so the caching allocator cannot hand their memory
+# to later work on the main stream while the side stream still reads it.  RAI_WGRAD_OVERLAP=0: in order.
+_WGRAD_OVERLAP = os.environ.get("RAI_WGRAD_OVERLAP", "1") == "1"
+_SIDE: Dict[str, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(device):
+    """The device's weight-gradient side stream (created outside any capture), or None."""
+    if not _WGRAD_OVERLAP or torch.device(device).type != "cuda":
+        return None
+    k = str(device)
+    s = _SIDE.get(k)
+    if s is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        s = torch.cuda.Stream(device)
+        _SIDE[k] = s
+    return s
+
+
+def _join_side(device) -> None:
+    s = _SIDE.get(str(device))
+    if s is not None:
+        torch.cuda.current_stream(device).wait_stream(s)
+
+
 def _reduce_wgrad_jobs(jobs: list, device) -> None:
     """One rai_conv2d_wgrad_reduce launch per RAI_WGRAD_MAX_JOBS layers: each layer's partial tiles
-    summed in a fixed order and added into its flat .grad view."""
+    summed in a fixed order and added into its flat .grad view (after joining the side stream the
+    partials ran on)."""
+    _join_side(device)
     L = _lib.lib()
     for i in range(0, len(jobs), _MAX_JOBS):
         chunk = jobs[i:i + _MAX_JOBS]
-        arr = (_WgradJob * len(chunk))(*[j for j, _ws, _w in chunk])
+        arr = (_WgradJob * len(chunk))(*[j[0] for j in chunk])
         _lib.check(L.rai_conv2d_wgrad_reduce(C.cast(arr, C.c_void_p), len(chunk), 1, _lib.stream_handle(device)),
                    "rai_conv2d_wgrad_reduce")
-    for _j, _ws, w in jobs:
-        notify_grad_written(w)
+    for j in jobs:
+        notify_grad_written(j[2])
 
 
 class _PendingGrads:
@@ -110,18 +142,19 @@ class _PendingGrads:
         else:
             self.items.append((w, dw))
 
-    def add_wgrad(self, job: "_WgradJob", ws: torch.Tensor, w: torch.Tensor) -> None:
+    def add_wgrad(self, job: "_WgradJob", ws: torch.Tensor, w: torch.Tensor, keep=()) -> None:
+        """keep: the partials' operands, referenced until the reduction has joined the side stream."""
         if self.closed:
-            _reduce_wgrad_jobs([(job, ws, w)], ws.device)
+            _reduce_wgrad_jobs([(job, ws, w, keep)], ws.device)
             return
-        assert not any(ws is other for _j, other, _w in self.jobs), "reserve(ws) before writing its partials"
-        self.jobs.append((job, ws, w))
+        assert not any(ws is j[1] for j in self.jobs), "reserve(ws) before writing its partials"
+        self.jobs.append((job, ws, w, keep))
 
     def reserve(self, ws: torch.Tensor) -> None:
         """Called BEFORE a weight-gradient partials launch writes `ws`: a job still pending on that
         workspace (the same layer run twice in one backward) is reduced first, while its partials are
         intact (stream order puts that reduction ahead of the overwrite)."""
-        if not self.closed and any(ws is other for _j, other, _w in self.jobs):
+        if not self.closed and any(ws is j[1] for j in self.jobs):
             self.flush_jobs()
 
     def flush_jobs(self) -> None:
@@ -133,6 +166,8 @@ class _PendingGrads:
         self.closed = True
         if flush:
             self.flush_jobs()
+        elif self.jobs:  # dropped unreduced: still join the side stream before their operands are released
+            _join_side(self.jobs[0][1].device)
         self.jobs = []
         items, self.items = self.items, []
         if flush and items:
@@ -310,6 +345,18 @@ def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, pending: 
     nb = int(L.rai_conv2d_wgrad_workspace_bytes(B, H, W, Ci, Co, KH, KW, s))
     ws = _WG_WS.get(module, nb, x.device)
     pending.reserve(ws)
+    side = _side_stream(x.device) if pending is not None and not pending.closed else None
+    if side is not None:  # fork: the side stream waits for everything queued so far (dz / dy, y, x)
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(side):
+            _launch_wgrad_partials(L, x, dz, y, x_div, B, H, W, Ci, Co, KH, KW, s, ws, nb)
+    else:
+        _launch_wgrad_partials(L, x, dz, y, x_div, B, H, W, Ci, Co, KH, KW, s, ws, nb)
+    return _WgradJob(ws.data_ptr(), grad.data_ptr(), None if db is None else db.data_ptr(), B, H, W, Ci, Co, KH, KW,
+                     s, 0), ws
+
+
+def _launch_wgrad_partials(L, x, dz, y, x_div, B, H, W, Ci, Co, KH, KW, s, ws, nb) -> None:
     st = _lib.stream_handle(x.device)
     if x.dtype == torch.uint8 and y is None:
         _lib.check(L.rai_conv2d_wgrad_partials_u8(x.data_ptr(), float(x_div), dz.data_ptr(), B, H, W, Ci, Co, KH, KW,
@@ -324,8 +371,6 @@ def _conv_wgrad_partials(module, x, dz, w, stride, grad: torch.Tensor, pending: 
     else:
         _lib.check(L.rai_conv2d_wgrad_relu_partials(dz.data_ptr(), y.data_ptr(), x.data_ptr(), B, H, W, Ci, Co, KH, KW,
                                                     s, ws.data_ptr(), nb, st), "rai_conv2d_wgrad_relu_partials")
-    return _WgradJob(ws.data_ptr(), grad.data_ptr(), None if db is None else db.data_ptr(), B, H, W, Ci, Co, KH, KW,
-                     s, 0), ws
 
 
 def _conv_wgrad_mfma(module, x, dz, w, stride, out: torch.Tensor, accumulate: bool) -> None:
@@ -425,7 +470,7 @@ class ConvBiasReLU(torch.autograd.Function):
             if dx is not None or not ctx.needs_input_grad[0]:
                 job, wsp = _conv_wgrad_partials(key, x, dy, w, stride, w.grad, ctx.pending, y=y, db=b.grad,
                                                 x_div=ctx.x_div)
-                ctx.pending.add_wgrad(job, wsp, w)
+                ctx.pending.add_wgrad(job, wsp, w, keep=(x, dy, y))
                 return dx, None, None, None, None, None, None, None
         ws = _WS.get(key, zshape[1], y.device)
         if flatten:
@@ -447,7 +492,7 @@ class ConvBiasReLU(torch.autograd.Function):
                 # partial tiles now; their reduction into the flat .grad joins the other layers' in one
                 # launch at direct_grads() exit
                 job, ws = _conv_wgrad_partials(key, x, dz, w, stride, g, ctx.pending, x_div=ctx.x_div)
-                ctx.pending.add_wgrad(job, ws, w)
+                ctx.pending.add_wgrad(job, ws, w, keep=(x, dz))
                 dw = None
             else:
                 dw = torch.empty_like(w, memory_format=torch.channels_last)
