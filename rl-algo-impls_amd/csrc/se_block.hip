@@ -371,6 +371,10 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_fwd_nchw_kernel(const fl
   }
 }
 
+// VEC (round 4, 16-B aligned dy / y): the sample's NCHW plane is read as float4s, all of a thread's loads
+// issued before the first use (one memory round trip per sample instead of one per loop trip), and the
+// channel of element e is e * ceil(2^32 / HW) >> 32 (exact for e < 8192) instead of an integer division.
+template <bool VEC = false>
 __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_nchw_kernel(const float* __restrict__ dy,
                                                                        const float* __restrict__ y, int64_t B, int HW,
                                                                        int C, float* __restrict__ dx, float* partial,
@@ -381,15 +385,42 @@ __global__ __launch_bounds__(BR_THREADS) void bias_relu_bwd_nchw_kernel(const fl
   __shared__ int last;
   const int tid = threadIdx.x, C4 = C / 4, lanes = BR_THREADS / C4, c4 = tid % C4, lane = tid / C4;
   const int n = HW * C, ld = C + 1;
+  const unsigned magic = (unsigned)((0x100000000ULL + (unsigned)HW - 1) / (unsigned)HW);
   float db0[4] = {0.f, 0.f, 0.f, 0.f};
   br_load_db(db, accumulate, C4, db0);
   f4 wsum = f4{0.f, 0.f, 0.f, 0.f};  // thread tid < C4: this workgroup's samples, in sample order
   for (int64_t s = blockIdx.x; s < B; s += gridDim.x) {
     const float* dys = dy + s * n;
     const float* ys = y + s * n;
-    for (int e = tid; e < n; e += BR_THREADS) {  // NCHW element e = c * HW + p
-      const int c = e / HW, p = e - c * HW;
-      t[p * ld + c] = ys[e] <= 0.f ? 0.f : dys[e];
+    if (VEC) {
+      constexpr int NV = BRT_MAX_ELEMS / 4 / BR_THREADS;  // float4s per thread at most
+      const int n4 = n >> 2;
+      f4 yv[NV], gv[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int m4 = tid + i * BR_THREADS;
+        if (m4 < n4) {
+          yv[i] = reinterpret_cast<const f4*>(ys)[m4];
+          gv[i] = reinterpret_cast<const f4*>(dys)[m4];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int m4 = tid + i * BR_THREADS;
+        if (m4 < n4) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // NCHW element e = c * HW + p
+            const unsigned e = 4u * (unsigned)m4 + q;
+            const int c = (int)__umulhi(e, magic), p = (int)e - c * HW;
+            t[p * ld + c] = yv[i][q] <= 0.f ? 0.f : gv[i][q];
+          }
+        }
+      }
+    } else {
+      for (int e = tid; e < n; e += BR_THREADS) {  // NCHW element e = c * HW + p
+        const int c = e / HW, p = e - c * HW;
+        t[p * ld + c] = ys[e] <= 0.f ? 0.f : dys[e];
+      }
     }
     __syncthreads();
     float* dxs = dx + s * n;
@@ -468,8 +499,13 @@ extern "C" int rai_bias_relu_bwd_nchw(const float* dy, const float* y, int64_t B
   const int64_t blocks = B < BR_MAX_BLOCKS ? B : BR_MAX_BLOCKS;
   float* partial = static_cast<float*>(workspace);
   int* counter = reinterpret_cast<int*>(static_cast<uint8_t*>(workspace) + (int64_t)BR_MAX_BLOCKS * C * 4);
-  hipLaunchKernelGGL(bias_relu_bwd_nchw_kernel, dim3((unsigned)blocks), dim3(BR_THREADS), 0, st, dy, y, B, HW, C, dx,
-                     partial, counter, db, accumulate);
+  const char* bv = getenv("RAI_BRT_VEC");  // A/B: 0 keeps the scalar form
+  if ((((uintptr_t)dy | (uintptr_t)y) & 15) == 0 && !(bv && bv[0] == '0'))
+    hipLaunchKernelGGL(bias_relu_bwd_nchw_kernel<true>, dim3((unsigned)blocks), dim3(BR_THREADS), 0, st, dy, y, B, HW,
+                       C, dx, partial, counter, db, accumulate);
+  else
+    hipLaunchKernelGGL(bias_relu_bwd_nchw_kernel<false>, dim3((unsigned)blocks), dim3(BR_THREADS), 0, st, dy, y, B,
+                       HW, C, dx, partial, counter, db, accumulate);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

@@ -647,6 +647,18 @@ def test_bias_relu_nchw_pair_matches_torch_flatten(B, H, W, C):
         dbs.append(db - (0.5 if acc else 0.0))
     assert torch.equal(dbs[0], dbs[2])
     assert bool((ws[-576:].view(torch.int32) == 0).all())
+    # the scalar form (RAI_BRT_VEC=0; also taken for misaligned dy / y) gives the same bits as the float4 form
+    import os
+    os.environ["RAI_BRT_VEC"] = "0"
+    try:
+        dx = torch.empty(B, C, H, W, device=DEV, memory_format=torch.channels_last)
+        db = torch.empty(C, device=DEV)
+        _lib.check(L.rai_bias_relu_bwd_nchw(dy.data_ptr(), y.data_ptr(), B, H * W, C, dx.data_ptr(), db.data_ptr(),
+                                            0, ws.data_ptr(), ws.numel(), st), "bwd_nchw scalar")
+    finally:
+        del os.environ["RAI_BRT_VEC"]
+    assert torch.equal(dx, dx_ref)
+    assert torch.equal(db, dbs[0])
     # shapes the pair does not take: C not a multiple of 4, (C + 1) * HW over the LDS plane
     assert L.rai_bias_relu_fwd_nchw(z.data_ptr(), b.data_ptr(), B, H * W, 6, y.data_ptr(), st) == -2
     assert L.rai_bias_relu_fwd_nchw(z.data_ptr(), b.data_ptr(), 1, 4096, 64, y.data_ptr(), st) == -2
