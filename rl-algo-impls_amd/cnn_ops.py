@@ -85,7 +85,10 @@ _MAX_JOBS = 4  # RAI_WGRAD_MAX_JOBS
 # the side stream first.  Inside a graph capture the fork and join are captured edges.  The operands are
 # kept referenced by the pending job until that join, so the caching allocator cannot hand their memory
 # to later work on the main stream while the side stream still reads it.  RAI_WGRAD_OVERLAP=0: in order.
-_WGRAD_OVERLAP = os.environ.get("RAI_WGRAD_OVERLAP", "1") == "1"
+# Measured SLOWER on C3 (161k vs 169k env-steps/s with it off, same box: profiles/r4j_ab_c3_wgrad_overlap.txt):
+# the weight-gradient and input-gradient kernels each fill the GPU, and the fork / join add dependencies to the
+# captured step.  Off by default; RAI_WGRAD_OVERLAP=1 turns it on.
+_WGRAD_OVERLAP = os.environ.get("RAI_WGRAD_OVERLAP", "0") == "1"
 _SIDE: Dict[str, "torch.cuda.Stream"] = {}
 
 
@@ -275,7 +278,7 @@ def _mfma_conv_ok(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride, pad
 def _u8_to_f32(x: torch.Tensor, x_div: float) -> torch.Tensor:
     """x.float() / x_div, channels_last: IEEE division by a device scalar (as the gather's prescale; a
     Python-scalar divisor would be a multiply by the rounded reciprocal on the GPU)."""
-    d = torch.tensor(float(x_div), dtype=torch.float32, device=x.device)
+    d = torch.full((), float(x_div), dtype=torch.float32, device=x.device)  # a fill kernel: graph-capturable
     return (x.float() / d).contiguous(memory_format=torch.channels_last)
 
 

@@ -533,15 +533,16 @@ def test_nature_cnn_encoder_uint8_path_equals_float32_path(monkeypatch):
     obs = torch.randint(0, 256, (64, 4, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
     assert enc.obs_transform(obs).kind == _lib.RAI_XFORM_U8_CHW_TO_U8_HWC
     outs = []
-    for u8 in (True, False):
+    for u8 in (False, True, False):  # the first pass settles the fc GEMMs' tuned solutions (TunableOp)
         monkeypatch.setattr(cnn_ops, "_CONV_U8", u8)
         for p in enc.parameters():
             p.grad = None
         f = enc(obs)
         f.square().sum().backward()
         outs.append((f.detach().cpu(), [p.grad.detach().cpu().clone() for p in enc.parameters()]))
+    outs = outs[1:]
     assert torch.equal(outs[0][0], outs[1][0])
     for a, b in zip(outs[0][1], outs[1][1]):
-        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+        assert torch.equal(a, b)
     monkeypatch.setattr(cnn_ops, "_CONV_U8", False)
     assert enc.obs_transform(obs).kind == _lib.RAI_XFORM_U8_CHW_TO_F32_HWC
