@@ -519,16 +519,20 @@ def test_gather_uint8_frames_transposed_to_nhwc(n, B):
 
 def test_nature_cnn_encoder_uint8_path_equals_float32_path(monkeypatch):
     """The encoder on uint8 frames: conv1 reading the frames itself (RAI_CONV_U8, default) gives the same
-    features, bit for bit, as the float32 prescale path, for the rollout's unprepared frames and for the
-    gather's prepared minibatch (obs_transform's kind); the gradients of the layers above agree too."""
+    features, bit for bit, as the float32 prescale path, and -- inside direct_grads(), as in the trainer,
+    where conv1's weight gradient runs rai_conv2d_wgrad_relu_partials_u8 -- the same parameter gradients.
+    The conv weights are channels_last as the trainer's flat buffer stores them (the MFMA kernels' layout;
+    MIOpen's weight gradient would not be bit-reproducible)."""
     import make_golden_networks as nets
     from rl_algo_impls_amd import cnn_ops
-
     from rl_algo_impls_amd.policy import ActorCritic
 
     torch.manual_seed(0)
     pol = ActorCritic(nets.pong_env(), activation_fn="relu").to(DEV)
     enc = pol.network._feature_extractor.feature_extractor
+    for m in enc.cnn:
+        if isinstance(m, torch.nn.Conv2d):
+            m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
     g = torch.Generator().manual_seed(9)
     obs = torch.randint(0, 256, (64, 4, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
     assert enc.obs_transform(obs).kind == _lib.RAI_XFORM_U8_CHW_TO_U8_HWC
@@ -536,13 +540,15 @@ def test_nature_cnn_encoder_uint8_path_equals_float32_path(monkeypatch):
     for u8 in (False, True, False):  # the first pass settles the fc GEMMs' tuned solutions (TunableOp)
         monkeypatch.setattr(cnn_ops, "_CONV_U8", u8)
         for p in enc.parameters():
-            p.grad = None
-        f = enc(obs)
-        f.square().sum().backward()
+            p.grad = torch.zeros_like(p)  # conv weights: channels_last like their data
+        with cnn_ops.direct_grads():
+            f = enc(obs)
+            f.square().sum().backward()
+        torch.cuda.synchronize()
         outs.append((f.detach().cpu(), [p.grad.detach().cpu().clone() for p in enc.parameters()]))
     outs = outs[1:]
     assert torch.equal(outs[0][0], outs[1][0])
-    for a, b in zip(outs[0][1], outs[1][1]):
-        assert torch.equal(a, b)
+    for (name, _), a, b in zip(enc.named_parameters(), outs[0][1], outs[1][1]):
+        assert torch.equal(a, b), name
     monkeypatch.setattr(cnn_ops, "_CONV_U8", False)
     assert enc.obs_transform(obs).kind == _lib.RAI_XFORM_U8_CHW_TO_F32_HWC
