@@ -317,6 +317,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         for (int r = 0; r < 4; ++r) S.H1[16 * T_ + g * 4 + r][16 * t + li] = act_f(relu, z[tt][r] + bj);
       }
     }
+    STAMP(15);  // work done; the barrier wait follows
     lds_barrier();
     STAMP(1);
     // ============ F2: H2 = act(H1 W2^T + b2), own columns; output-layer partial sums ============
@@ -363,6 +364,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         if (li < 4) S.Zp[hf_][16 * T_ + g * 4 + li][o] = sel;
       }
     }
+    STAMP(16);  // work done; the barrier wait follows
     lds_barrier();
     STAMP(2);
     // ============ loss (both halves, identical), dZ2 on own columns ============
@@ -416,6 +418,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         }
       }
     }
+    STAMP(17);  // work done; the barrier wait follows
     lds_barrier();
     STAMP(3);
     // ============ dH1 = dZ2 W2 (own columns), dZ1, per-tile partials ============
@@ -508,6 +511,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         }
       }
     }
+    STAMP(18);  // work done; the barrier wait follows
     lds_barrier();
     STAMP(4);
     // ============ P_B: dW2 partial over the CU's RC rows (wave w: dW2 rows [16w, 16w + 16)) =====
@@ -574,6 +578,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       }
       }
     }
+    STAMP(19);  // work done; the barrier wait follows
     lds_barrier();
     STAMP(5);
     // ============ round 1: publish the partial (sc1), arrive; sum share c over the G slots ============

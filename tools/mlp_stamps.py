@@ -59,6 +59,9 @@ for net in range(2):
     print(f"--- workgroup {net} ({'actor' if net == 0 else 'critic'}): {tot / nmb:.0f} stamp-ticks/mb")
     for i, n in enumerate(NAMES):
         print(f"  {n:28s} {st[net, i + 1] / nmb:10.1f} ticks/mb  {100 * st[net, i + 1] / tot:5.1f}%")
+    if LAYOUT == "mc8":  # compute phases split into work and barrier wait (STAMP 15-19: work, phases 1-5: wait)
+        for i, n in ((15, "F1 work"), (16, "F2 work"), (17, "loss work"), (18, "dH1 work"), (19, "P_B work")):
+            print(f"  {n:34s} {st[net, i] / nmb:10.1f} ticks/mb (+ barrier {st[net, i - 14] / nmb:.1f})")
     if LAYOUT == "mc8":  # sub-phases (STAMP 9-14 split phases 6-8 above)
         for i, n in ((9, "  r1: wave-0 partial stores + drain"), (10, "  r1: barrier (other waves' drains)"),
                      (11, "  r2: share-sum loads (+ xGMI)"), (12, "  r2: share store + norm + drain"),
