@@ -33,6 +33,14 @@
 // to fp32 tolerance against the per-minibatch path and the reference (tests/test_gpu_trainer.py).
 #include "common.h"
 
+// RAI_WE_NO_DEFER (A/B builds only): the W2 Adam at the end of its own step instead of in the next
+// step's A wait
+#ifdef RAI_WE_NO_DEFER
+constexpr bool WE_DEFER_W2 = false;
+#else
+constexpr bool WE_DEFER_W2 = true;
+#endif
+
 namespace {
 
 constexpr int WE_NT = 256;                  // threads per workgroup (4 waves)
@@ -474,6 +482,31 @@ __device__ __forceinline__ bool we_arrive_wait(unsigned long long* ctr, int ci, 
   return !bail;
 }
 
+// we_arrive_wait split in two, so the workgroup can work between its own arrival and the wait for the
+// others' (the deferred W2 Adam below): every wave's stores were drained before the barrier that precedes
+// the arrival (as in we_arrive_wait), and the wait's closing barrier releases the waves.
+__device__ __forceinline__ void we_arrive(unsigned long long* ctr, int ci) {
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(&ctr[ci * (WE_CTR_STRIDE / 8)], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool we_wait(unsigned long long* ctr, int ci, unsigned long long want,
+                                        rai_train_state* state, int& bail) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = rai_clock();
+    while (__hip_atomic_load(&ctr[ci * (WE_CTR_STRIDE / 8)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      if (rai_expired(t0, RAI_SPIN_LOCAL)) {
+        __hip_atomic_store(&state->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bail = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  return !bail;
+}
+
 template <int HEAD>  // 0 Categorical, 1 Gaussian
 __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j) {
   const rai_mlp_wide_desc& d = a.d;
@@ -592,6 +625,30 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 #ifdef RAI_STAMPS
   unsigned long long st_acc[24] = {0}, t_last = __builtin_amdgcn_s_memtime();
 #endif
+  // clip + Adam on this workgroup's W2 row slice with the last D phase's clip coefficient and bias
+  // corrections (S.coef / S.adamc, rewritten only by the next D phase) and the gradient rows g_r
+  float g_r[4][4];  // this step's W2-row gradient, kept for the deferred Adam
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g_r[t][r] = 0.f;
+  auto adam_w2 = [&]() {
+    const float coef = S.coef;
+    const float inv_c3 = S.adamc[0], c4 = S.adamc[1];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ct = 4 * w + t;
+      if (ct < G) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float& p = S.W2r[4 * g + r][WE_SL * ct + li];
+          float pv = p;
+          adam_fast(pv, m_r[t][r], v_r[t][r], g_r[t][r] * coef, c1, c2, beta2, inv_c3, c4, eps);
+          p = pv;
+        }
+      }
+    }
+  };
 
   for (int mb = 0; mb < nmb; ++mb) {
     const int par = mb & 1;
@@ -668,7 +725,13 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     WSTAMP(0);
-    if (!we_arrive_wait(ctr, WE_CA + net, want, a.state, S.bail, w, side_a)) break;
+    // A: arrive, then -- while the other workgroups' H1 slices land -- the previous step's Adam on this
+    // workgroup's W2 rows (deferred from its D phase: only fwd2 and the W2 publish below read them), then
+    // wait.  Same values as applying it at the end of the previous step.
+    we_arrive(ctr, WE_CA + net);
+    if (w == 1) side_a();
+    if (WE_DEFER_W2 && mb > 0) adam_w2();
+    if (!we_wait(ctr, WE_CA + net, want, a.state, S.bail)) break;
     WSTAMP(1);
     we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // H1 -> Act
     // W2 rows j (as updated by the last Adam step) for this step's column owners: issued after the
@@ -987,7 +1050,6 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     WSTAMP(10);
     f4 g_rv[4];
     we_dw2_tiles4<0, WE_SL>(&S.Z2j[0][0], WE_SP, &S.Act[0][WE_SL * 4 * w], WE_HP, lane, g_rv);
-    float g_r[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1144,20 +1206,8 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     {
       const float coef = S.coef;
       const float inv_c3 = S.adamc[0], c4 = S.adamc[1];
-      // W2 row slice
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int ct = 4 * w + t;
-        if (ct < G) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float& p = S.W2r[4 * g + r][WE_SL * ct + li];
-            float pv = p;
-            adam_fast(pv, m_r[t][r], v_r[t][r], g_r[t][r] * coef, c1, c2, beta2, inv_c3, c4, eps);
-            p = pv;
-          }
-        }
-      }
+      // (the W2 row slice: deferred to the next step's A wait, adam_w2)
+      if (!WE_DEFER_W2) adam_w2();
       if (WE_SL * w + li < IN) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1175,6 +1225,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
     lds_barrier();
     WSTAMP(21);
+  }
+  if (WE_DEFER_W2 && !S.bail && nmb > 0) {  // the last step's deferred W2 Adam
+    adam_w2();
+    lds_barrier();
   }
 #ifdef RAI_STAMPS
   if (j == 0 && tid == 0)
