@@ -1447,6 +1447,10 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
     case 16: return launch_fwd_lds<2, 2, 1, 8, 3, true>(a, nchw, st);  // variant 14, buffer loads
     case 17: return launch_fwd_lds<2, 1, 2, 4, 4, true>(a, nchw, st);  // variant 13, buffer loads
     case 18: return launch_fwd_lds<2, 2, 2, 4, 3, true>(a, nchw, st);  // variant 12, buffer loads
+    // 64 co x 32 px (one 16 x 16 block per wave): twice variant 17's pixel tiles, for grids whose tile
+    // count is just above the CU count (NatureCNN conv2 at B = 256: 648 tiles instead of 324 on 256 CUs)
+    case 19: return launch_fwd_lds<1, 1, 4, 2, 4, true>(a, nchw, st);
+    case 20: return launch_fwd_lds<1, 1, 4, 2, 8, true>(a, nchw, st);
     default: return RAI_E_SHAPE;
   }
 }

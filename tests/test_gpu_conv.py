@@ -72,7 +72,7 @@ def test_conv_bias_relu_fwd_matches_fp64(case, B):
     assert (err <= tol).all(), float((err / tol).max())
 
 
-@pytest.mark.parametrize("variant", list(range(1, 19)))
+@pytest.mark.parametrize("variant", list(range(1, 21)))
 def test_conv_every_blocking_variant(variant):
     Ci, H, Co, k, s, flat = 32, 20, 64, 4, 2, False
     x, w, b = _inputs(9, Ci, H, Co, k, seed=3)

@@ -49,7 +49,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--batches", default="256,1024")
-    ap.add_argument("--variants", default="0,12,13,14,15,16,17,18")
+    ap.add_argument("--variants", default="0,12,13,14,15,16,17,18,19,20")
     args = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     dev = torch.device("cuda:0")
