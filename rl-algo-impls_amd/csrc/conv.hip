@@ -1418,10 +1418,17 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
     // fit (<= ~150 KB); 32 co x 256 px tiles once they give >= 256 workgroup tiles, else 64 co x 64 px
     const size_t lds32 = (size_t)32 * (K + 4) * 4, lds64 = (size_t)64 * (K + 4) * 4;
     // buffer-load forms (16 / 17 = 14 / 13 with raw_buffer_load, scalar offsets) where the input fits a
-    // 2 GB buffer: 3-6 % faster at B = 256 and 1024 (profiles/r4g_conv_bench.txt)
-    const int64_t t14 = (a.M + 255) / 256 * (Co / 32);
+    // 2 GB buffer: 3-6 % faster at B = 256 and 1024 (profiles/r4g_conv_bench.txt).  Between the 32 x 256
+    // and the 64 x 64 tile: the fewer rounds of tiles over the persistent workgroups (one per CU), a
+    // 32 x 256 tile costing two 64 x 64 ones, ties to the wider tile (it measured faster at equal rounds:
+    // conv2 at B = 256 24.2 vs 26.1 us, conv2 / conv3 at B = 1024; conv3 at B = 256 takes the 64 x 64
+    // tile, 17.6 vs 24.8 us; profiles/r4n_conv_bench.txt)
+    const int ncu = num_cus();
+    const int64_t wg32 = ncu / (Co / 32 > 0 ? Co / 32 : 1), wg64 = ncu / (Co / 64 > 0 ? Co / 64 : 1);
+    const int64_t rounds32 = ((a.M + 255) / 256 + wg32 - 1) / (wg32 > 0 ? wg32 : 1);
+    const int64_t rounds64 = ((a.M + 63) / 64 + wg64 - 1) / (wg64 > 0 ? wg64 : 1);
     const bool buf = B * H * W * (int64_t)Ci * 4 < (1LL << 31);
-    if (Co % 32 == 0 && lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && (t14 >= 256 || Co % 64 != 0))
+    if (Co % 32 == 0 && lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && (Co % 64 != 0 || 2 * rounds32 <= rounds64))
       variant = buf ? 16 : 14;
     else if (Co % 64 == 0 && lds64 + CV_MAXCHUNK * 4 <= 160 * 1024)
       variant = buf ? 17 : 13;
