@@ -69,21 +69,24 @@ def _fixture_rollout(z, meta):
 
 
 @pytest.mark.parametrize("graphs", [True, False], ids=["graph_replay", "eager"])
-@pytest.mark.parametrize("layout", ["nhwc_fused", "nhwc_fused_f32", "nhwc_fused_unfolded", "nhwc", "nchw"])
+@pytest.mark.parametrize("layout", ["nhwc_fused", "nhwc_fused_f32", "nhwc_fused_unfolded", "nhwc_fused_overlap", "nhwc",
+                                    "nchw"])
 def test_pong_minibatch_steps_match_reference(layout, graphs, monkeypatch):
     """nhwc_fused (the default): frames gathered as uint8 channels_last and read by conv1 itself
     (x = u8 / 255 in-kernel, cnn_ops RAI_CONV_U8) and the cnn_ops bias + ReLU epilogues with in-place
     gradient accumulation; nhwc_fused_f32: the same with the gather's uint8 -> float / 255 transform;
     nhwc_fused_unfolded: the fc ReLU backward as its own pass instead of folded into the heads' backward
-    (RAI_FC_HEADS_FOLD=0); nhwc: the modules' own kernels on channels_last; nchw: plain NCHW."""
+    (RAI_FC_HEADS_FOLD=0); nhwc_fused_overlap: the weight-gradient partials on a side stream
+    (RAI_WGRAD_OVERLAP=1, an option); nhwc: the modules' own kernels on channels_last; nchw: plain NCHW."""
     from rl_algo_impls_amd import cnn_ops
 
     z = np.load(GOLDEN / "pong_steps.npz", allow_pickle=False)
     meta = json.loads(str(z["index"]))
     monkeypatch.setattr(policy_mod, "_CHANNELS_LAST", layout != "nchw")
     monkeypatch.setattr(policy_mod, "_FUSED_EPILOGUES", layout.startswith("nhwc_fused"))
-    monkeypatch.setattr(cnn_ops, "_CONV_U8", layout in ("nhwc_fused", "nhwc_fused_unfolded"))
+    monkeypatch.setattr(cnn_ops, "_CONV_U8", layout in ("nhwc_fused", "nhwc_fused_unfolded", "nhwc_fused_overlap"))
     monkeypatch.setattr(cnn_ops, "_FC_HEADS_FOLD", layout != "nhwc_fused_unfolded")
+    monkeypatch.setattr(cnn_ops, "_WGRAD_OVERLAP", layout == "nhwc_fused_overlap")
     pol = _pong_policy(meta["shapes"])
     nets.load_flat(pol, pong_init([tuple(s) for s in meta["shapes"]], meta["init_seed"]))
     pol = pol.to(DEV)
