@@ -584,7 +584,13 @@ static WrwPlan wrw_plan(int64_t M, int Co, int K, int target_wgs) {
   WrwPlan p;
   p.VC = Co / 16;
   p.KT = K / 64;  // k tiles (grid.y)
-  if (target_wgs <= 0) target_wgs = 512;  // measured best of 256 / 512 / 768 / 1024 at B = 256 (r3r)
+  // default: 512 workgroups (measured best of 256 / 512 / 768 / 1024 at B = 256, r3r), 1024 for K <= 256
+  // (NatureCNN conv1: 26.5 vs 28.6 us at B = 256, 71.3 vs 84.4 at B = 1024; profiles/r4g_conv_bench.txt)
+  static const int env_wgs = [] {  // A/B: RAI_WRW_WGS=512 restores the single default (read once)
+    const char* e = getenv("RAI_WRW_WGS");
+    return e ? atoi(e) : 0;
+  }();
+  if (target_wgs <= 0) target_wgs = env_wgs > 0 && env_wgs <= 1024 ? env_wgs : (K <= 256 ? 1024 : 512);
   int64_t S = target_wgs / p.KT;
   S = S < 16 ? 16 : (S / 16) * 16;
   while (S > 16 && (M + S - 1) / S < 64) S -= 16;
