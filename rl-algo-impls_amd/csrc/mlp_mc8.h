@@ -637,10 +637,22 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
       const int chl = min(ch, WL_CH - 1);
       const int pbase = (net * 2 + par) * G * WL_N * (int)sizeof(float);
       f4 v[G];
+#ifdef RAI_M8_ALL_LOAD  // A/B builds only: every lane loads (clamped), as before round 4
+      const bool ld = true;
+#else
+      // only the share's owner lanes load (tid < SH: 75 of 256 at G = 16): the other lanes' clamped loads
+      // were a second copy of the request stream through the CU's address unit, results unused
+      const bool ld = tid < SH;
+#endif
+      if (ld) {
 #pragma unroll
-      for (int cc = 0; cc < G; ++cc)
-        v[cc] = as_f4(__builtin_amdgcn_raw_buffer_load_b128(srs, pbase + (cc * WL_N + 4 * chl) * (int)sizeof(float),
-                                                            0, 16));
+        for (int cc = 0; cc < G; ++cc)
+          v[cc] = as_f4(__builtin_amdgcn_raw_buffer_load_b128(srs, pbase + (cc * WL_N + 4 * chl) * (int)sizeof(float),
+                                                              0, 16));
+      } else {
+#pragma unroll
+        for (int cc = 0; cc < G; ++cc) v[cc] = f4{0.f, 0.f, 0.f, 0.f};
+      }
       f4 s = v[0];
 #pragma unroll
       for (int cc = 1; cc < G; ++cc) s += v[cc];
