@@ -42,12 +42,48 @@ struct ConvFwdArgs {
   const float* x;
   const uint8_t* xu8;  // U8 forms: the uint8 NHWC input (Ci = 4), read as x = u8 / xdiv
   float xdiv;
+  float xinv;          // U8 == 2: the rounded 1 / xdiv of the multiply + fma-correction quotient
   const float* w;
   const float* b;
   float* y;
   int64_t M;  // B * OH * OW output pixels
   int H, W, Ci, Co, KW, S, OH, OW, K;
 };
+
+// The uint8 forms' x = u / d for the four bytes of a dword.  U8 == 1: a 256-entry LDS table of the IEEE
+// quotients (four dependent, bank-conflicting LDS reads per dword).  U8 == 2: the quotient q0 = u * inv
+// corrected by one fused multiply-add step, q = q0 + (u - q0 d) inv (two FMAs, exact residual) — four
+// VALU operations per byte and no LDS; the host launches it only when u8_div_valu_exact(d) has
+// checked it equal, bit for bit, to u / d for all 256 bytes (true for d = 255).
+__device__ __forceinline__ f4 u8x4_div(unsigned u, float d, float inv) {
+  f4 r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float x = (float)((u >> (8 * q)) & 255u);
+    const float q0 = x * inv;
+    r[q] = __builtin_fmaf(__builtin_fmaf(-q0, d, x), inv, q0);
+  }
+  return r;
+}
+
+// host: does the U8 == 2 quotient equal the IEEE u / d for every byte?  (RAI_CONV_U8_LUT=1: the table)
+static bool u8_div_valu_exact(float d, float* inv_out) {
+  static const bool force_lut = [] {
+    const char* e = getenv("RAI_CONV_U8_LUT");
+    return e && e[0] == '1';
+  }();
+  if (force_lut || !(d > 0.f)) return false;
+  const float inv = 1.f / d;
+  for (int i = 0; i < 256; ++i) {
+    const float x = (float)i;
+    volatile float q0 = x * inv;  // a rounded product, as the device's v_mul_f32
+    const float q = std::fmaf(std::fmaf(-q0, d, x), inv, q0);
+    const float ref = x / d;
+    if (__builtin_bit_cast(uint32_t, q) != __builtin_bit_cast(uint32_t, ref)) return false;
+  }
+  *inv_out = inv;
+  return true;
+}
 
 template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF>
 __global__ __launch_bounds__(CV_THREADS) void conv_fwd_kernel(const ConvFwdArgs a) {
@@ -177,15 +213,15 @@ static int allow_lds(const void* kernel) {
 // one per CU) copies its COT rows x K once (row stride K + 4 floats: the 16 lanes of a ds_read_b128
 // group land on distinct banks), then loops over pixel tiles; only the im2col operand is read from
 // L1/L2 per quad.
-template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF, bool BUF = false, bool U8 = false>
+template <int TCO, int TPX, int WCO, int WPX, bool NCHW, int PF, bool BUF = false, int U8 = 0>
 __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) {
   static_assert(WCO * WPX == 8, "eight waves");
   static_assert(!U8 || BUF, "the uint8 input is read through a buffer resource");
   constexpr int COT = 16 * TCO * WCO, PXT = 16 * TPX * WPX;
   extern __shared__ __attribute__((aligned(16))) float wl[];  // [COT][K + 4]
   __shared__ int xoff[CV_MAXCHUNK];
-  __shared__ float lut[U8 ? 256 : 1];  // U8: lut[u] = u / xdiv (IEEE division, as the gather's prescale)
-  if (U8)
+  __shared__ float lut[U8 == 1 ? 256 : 1];  // U8 == 1: lut[u] = u / xdiv (IEEE division, as the gather's prescale)
+  if (U8 == 1)
     for (int i = threadIdx.x; i < 256; i += 512) lut[i] = (float)i / a.xdiv;
   const int K = a.K, KP = K + 4;
   const int nch = K >> 2;
@@ -231,14 +267,13 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
 #pragma unroll
       for (int tp = 0; tp < TPX; ++tp) acc[tc][tp] = f4{0.f, 0.f, 0.f, 0.f};
     f4 Br[PF][TPX];
-    auto ldb = [&](int qd, f4(&Bv)[TPX]) {
+    unsigned Ur[U8 ? PF : 1][TPX];  // U8: the raw dwords, converted when the stage is consumed (no early wait)
+    auto ldb = [&](int qd, int slot) {
+      f4(&Bv)[TPX] = Br[slot];
       const int xo = xoff[4 * qd + g];
-      if (U8) {  // one pixel's 4 channels per chunk (Ci = 4): one dword, four table reads
+      if (U8) {  // one pixel's 4 channels per chunk (Ci = 4): one dword
 #pragma unroll
-        for (int tp = 0; tp < TPX; ++tp) {
-          const unsigned u = __builtin_amdgcn_raw_buffer_load_b32(xrs, xbo[tp] + xo, 0, 0);
-          Bv[tp] = f4{lut[u & 255u], lut[(u >> 8) & 255u], lut[(u >> 16) & 255u], lut[u >> 24]};
-        }
+        for (int tp = 0; tp < TPX; ++tp) Ur[slot][tp] = __builtin_amdgcn_raw_buffer_load_b32(xrs, xbo[tp] + xo, 0, 0);
         return;
       }
       if (BUF) {
@@ -250,13 +285,25 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
 #pragma unroll
       for (int tp = 0; tp < TPX; ++tp) Bv[tp] = *reinterpret_cast<const f4*>(xb[tp] + xo);
     };
+    // BUF: every ring load is issued (a chunk index past the end re-reads the last chunk, an L1 hit), so
+    // the loop's loads are straight-line code and each wait leaves the PF - 1 younger stages in flight
 #pragma unroll
-    for (int u = 0; u < PF; ++u)
-      if (u < nq) ldb(u, Br[u]);
+    for (int u = 0; u < PF; ++u) {
+      if (BUF || u < nq) ldb(BUF ? min(u, nq - 1) : u, u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     for (int qd = 0; qd < nq; qd += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         if (qd + u < nq) {
+          if (U8) {
+#pragma unroll
+            for (int tp = 0; tp < TPX; ++tp) {
+              const unsigned w4 = Ur[u][tp];
+              if (U8 == 2) Br[u][tp] = u8x4_div(w4, a.xdiv, a.xinv);
+              else Br[u][tp] = f4{lut[w4 & 255u], lut[(w4 >> 8) & 255u], lut[(w4 >> 16) & 255u], lut[w4 >> 24]};
+            }
+          }
           f4 A[TCO];
 #pragma unroll
           for (int tc = 0; tc < TCO; ++tc) A[tc] = *reinterpret_cast<const f4*>(wrow[tc] + 4 * (4 * (qd + u) + g));
@@ -268,7 +315,7 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
               for (int tp = 0; tp < TPX; ++tp)
                 acc[tc][tp] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[tc][j], Br[u][tp][j], acc[tc][tp], 0, 0, 0);
         }
-        if (qd + u + PF < nq) ldb(qd + u + PF, Br[u]);
+        if (BUF || qd + u + PF < nq) ldb(BUF ? min(qd + u + PF, nq - 1) : qd + u + PF, u);
       }
     }
 #pragma unroll
@@ -298,7 +345,7 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   }
 }
 
-template <int TCO, int TPX, int WCO, int WPX, int PF, bool BUF = false, bool U8 = false>
+template <int TCO, int TPX, int WCO, int WPX, int PF, bool BUF = false, int U8 = 0>
 int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   constexpr int PXT = 16 * TPX * WPX, COT = 16 * TCO * WCO;
   if (a.Co % COT) return RAI_E_SHAPE;
@@ -359,6 +406,7 @@ struct ConvWrwArgs {
   const float* x;
   const uint8_t* xu8;  // U8 forms: uint8 NHWC input (Ci = 4), x = u8 / xdiv
   float xdiv;
+  float xinv;          // U8 == 2: the rounded 1 / xdiv (see u8x4_div)
   const float* dz;  // RB: dy, the gradient of the ReLU's output
   const float* y;   // RB: the forward output (dz = y > 0 ? dy : 0, as threshold_backward)
   float* part;      // [S][Co][K], then (RB) the bias-gradient partials [S][Co]
@@ -367,13 +415,13 @@ struct ConvWrwArgs {
   int H, W, Ci, Co, KW, S_, OH, OW, K;
 };
 
-template <int VC, int PF, bool RB, bool BUF = false, bool U8 = false>
+template <int VC, int PF, bool RB, bool BUF = false, int U8 = 0>
 __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs a) {
   static_assert(!U8 || BUF, "the uint8 input is read through a buffer resource");
   constexpr int NB = VC * 4;  // 16x16 accumulator blocks per wave
   __shared__ float dbl[RB ? 4 * 16 * VC : 1];  // RB: the waves' bias-gradient sums
-  __shared__ float lut[U8 ? 256 : 1];          // U8: lut[u] = u / xdiv
-  if (U8) lut[threadIdx.x] = (float)threadIdx.x / a.xdiv;  // CV_THREADS == 256
+  __shared__ float lut[U8 == 1 ? 256 : 1];     // U8 == 1: lut[u] = u / xdiv
+  if (U8 == 1) lut[threadIdx.x] = (float)threadIdx.x / a.xdiv;  // CV_THREADS == 256
   // LDS: the split's pixel -> input offset table, later reused for the cross-wave sum of the tiles
   constexpr int TAB_BYTES = WR_MAXPX * 4, RED_BYTES = 3 * NB * 64 * 16;
   __shared__ __attribute__((aligned(16))) unsigned char lds[TAB_BYTES > RED_BYTES ? TAB_BYTES : RED_BYTES];
@@ -425,32 +473,32 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
       if constexpr (VC == 4) return __builtin_bit_cast(fv, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * off, 0, 0));
       else return __builtin_bit_cast(fv, __builtin_amdgcn_raw_buffer_load_b64(rs, 4 * off, 0, 0));
     };
-    auto ld = [&](int st, fv& dv, f4& xv) {
+    // the PF-deep ring holds the loads as they arrive (raw dz, y, the uint8 dword): the ReLU mask and the
+    // byte conversion are applied when a step is consumed, so no load is waited for PF - 1 steps early
+    fv dv[PF];
+    fv yv[RB ? PF : 1];
+    f4 xv[PF];
+    unsigned xu[U8 ? PF : 1];
+    auto ld = [&](int st, int u) {
       const int pl = lo + 4 * st + g;
-      if (BUF && pl < hi) {
-        dv = ldz(zrs, dzo + pl * a.Co);
-        if (RB) {
-          const fv yv = ldz(yrs, dzo + pl * a.Co);
-#pragma unroll
-          for (int j = 0; j < VC; ++j) dv[j] = yv[j] > 0.f ? dv[j] : 0.f;
-        }
-        if (U8) {
-          const unsigned u = __builtin_amdgcn_raw_buffer_load_b32(xrs, xco + xbase_l[pl], 0, 0);
-          xv = f4{lut[u & 255u], lut[(u >> 8) & 255u], lut[(u >> 16) & 255u], lut[u >> 24]};
-        } else {
-          xv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, 4 * (xco + xbase_l[pl]), 0, 0));
-        }
+      if (BUF) {
+        // unconditional, so the loop's loads are straight-line code and each wait leaves the PF - 1 younger
+        // steps in flight: a lane past the wave's pixels re-reads its last pixel (an L1 hit), zeroed when
+        // consumed
+        const int plc = min(min(pl, max(hi - 1, lo)), WR_MAXPX - 1);
+        dv[u] = ldz(zrs, dzo + plc * a.Co);
+        if (RB) yv[u] = ldz(yrs, dzo + plc * a.Co);
+        if (U8) xu[u] = __builtin_amdgcn_raw_buffer_load_b32(xrs, xco + xbase_l[plc], 0, 0);
+        else xv[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, 4 * (xco + xbase_l[plc]), 0, 0));
       } else if (pl < hi) {
-        dv = *reinterpret_cast<const fv*>(dzc + (int64_t)pl * a.Co);
-        if (RB) {
-          const fv yv = *reinterpret_cast<const fv*>(yc + (int64_t)pl * a.Co);
-#pragma unroll
-          for (int j = 0; j < VC; ++j) dv[j] = yv[j] > 0.f ? dv[j] : 0.f;
-        }
-        xv = *reinterpret_cast<const f4*>(xc + xbase_l[pl]);
+        dv[u] = *reinterpret_cast<const fv*>(dzc + (int64_t)pl * a.Co);
+        if (RB) yv[u] = *reinterpret_cast<const fv*>(yc + (int64_t)pl * a.Co);
+        xv[u] = *reinterpret_cast<const f4*>(xc + xbase_l[pl]);
       } else {
-        dv = fv{};
-        xv = f4{0.f, 0.f, 0.f, 0.f};
+        dv[u] = fv{};
+        if (RB) yv[u] = fv{};
+        if (U8) xu[u] = 0u;
+        else xv[u] = f4{0.f, 0.f, 0.f, 0.f};
       }
     };
     auto mma = [&](const fv& dv, const f4& xv) {
@@ -460,19 +508,35 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
         for (int jj = 0; jj < 4; ++jj)
           acc[j][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[j], xv[jj], acc[j][jj], 0, 0, 0);
     };
-    fv dv[PF];
-    f4 xv[PF];
     fv dsum = fv{};  // RB: this lane's bias-gradient sum (its pixels, in step order)
+    // prologue loads in slot order (the scheduler may not interleave them): the loop-entry wait state then
+    // matches the back edge's, and each step waits for its own slot only
 #pragma unroll
-    for (int u = 0; u < PF; ++u) ld(u, dv[u], xv[u]);
+    for (int u = 0; u < PF; ++u) {
+      ld(u, u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     for (int st = 0; st < nst; st += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         if (st + u < nst) {
-          mma(dv[u], xv[u]);
-          if (RB) dsum += dv[u];
+          fv d = dv[u];
+          if (RB) {
+#pragma unroll
+            for (int j = 0; j < VC; ++j) d[j] = yv[u][j] > 0.f ? d[j] : 0.f;
+          }
+          f4 x;
+          if (U8 == 2) x = u8x4_div(xu[u], a.xdiv, a.xinv);
+          else if (U8 == 1) x = f4{lut[xu[u] & 255u], lut[(xu[u] >> 8) & 255u], lut[(xu[u] >> 16) & 255u], lut[xu[u] >> 24]};
+          else x = xv[u];
+          if (BUF && lo + 4 * (st + u) + g >= hi) {  // past the wave's pixels: zero, as the pointer form loads
+            d = fv{};
+            x = f4{0.f, 0.f, 0.f, 0.f};
+          }
+          mma(d, x);
+          if (RB) dsum += d;
         }
-        if (st + u + PF < nst) ld(st + u + PF, dv[u], xv[u]);
+        if (BUF || st + u + PF < nst) ld(st + u + PF, u);
       }
     }
     if (RB) {  // the four lane groups (rows of the step), then the waves in order through LDS
@@ -1206,6 +1270,7 @@ static int wgrad_partials(const float* x, const float* dz, const float* y, int64
   a.x = x;
   a.xu8 = xu8;
   a.xdiv = xdiv;
+  a.xinv = 0.f;
   a.dz = dz;
   a.y = y;
   a.part = static_cast<float*>(workspace);
@@ -1233,10 +1298,17 @@ static int wgrad_partials(const float* x, const float* dz, const float* y, int64
   if (xu8) {  // buffer loads, 4 pixel steps in flight (the default form), uint8 input
     if (!buf_ok) return RAI_E_SHAPE;
     if (y && (((uintptr_t)y) & 15)) return RAI_E_SHAPE;
-    if (y && p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true, true, true>), grid, dim3(CV_THREADS), 0, st, a);
-    else if (y) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true, true, true>), grid, dim3(CV_THREADS), 0, st, a);
-    else if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, false, true, true>), grid, dim3(CV_THREADS), 0, st, a);
-    else hipLaunchKernelGGL((conv_wrw_kernel<4, 4, false, true, true>), grid, dim3(CV_THREADS), 0, st, a);
+    if (u8_div_valu_exact(xdiv, &a.xinv)) {
+      if (y && p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true, true, 2>), grid, dim3(CV_THREADS), 0, st, a);
+      else if (y) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true, true, 2>), grid, dim3(CV_THREADS), 0, st, a);
+      else if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, false, true, 2>), grid, dim3(CV_THREADS), 0, st, a);
+      else hipLaunchKernelGGL((conv_wrw_kernel<4, 4, false, true, 2>), grid, dim3(CV_THREADS), 0, st, a);
+    } else {
+      if (y && p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true, true, 1>), grid, dim3(CV_THREADS), 0, st, a);
+      else if (y) hipLaunchKernelGGL((conv_wrw_kernel<4, 4, true, true, 1>), grid, dim3(CV_THREADS), 0, st, a);
+      else if (p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, false, true, 1>), grid, dim3(CV_THREADS), 0, st, a);
+      else hipLaunchKernelGGL((conv_wrw_kernel<4, 4, false, true, 1>), grid, dim3(CV_THREADS), 0, st, a);
+    }
   } else if (y) {  // the ReLU backward and the bias gradient fused in (rai_conv2d_wgrad_relu_partials)
     if (((uintptr_t)y) & 15) return RAI_E_SHAPE;
     if (pf == 104 && p.VC == 2) hipLaunchKernelGGL((conv_wrw_kernel<2, 4, true, true>), grid, dim3(CV_THREADS), 0, st, a);
@@ -1403,6 +1475,7 @@ extern "C" int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const 
   a.x = x;
   a.xu8 = nullptr;
   a.xdiv = 1.f;
+  a.xinv = 1.f;
   a.w = w;
   a.b = b;
   a.y = y;
@@ -1487,6 +1560,8 @@ extern "C" int rai_conv2d_bias_relu_fwd_u8(const uint8_t* x, float x_divisor, co
   a.x = nullptr;
   a.xu8 = x;
   a.xdiv = x_divisor;
+  a.xinv = 0.f;
+  const bool valu = u8_div_valu_exact(x_divisor, &a.xinv);
   a.w = w;
   a.b = b;
   a.y = y;
@@ -1505,8 +1580,9 @@ extern "C" int rai_conv2d_bias_relu_fwd_u8(const uint8_t* x, float x_divisor, co
   const size_t lds32 = (size_t)32 * (K + 4) * 4, lds64 = (size_t)64 * (K + 4) * 4;
   const int64_t t14 = (a.M + 255) / 256 * (Co / 32);
   if (Co % 32 == 0 && lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && (t14 >= 256 || Co % 64 != 0))
-    return launch_fwd_lds<2, 2, 1, 8, 3, true, true>(a, nchw, st);
-  if (Co % 64 == 0 && lds64 + CV_MAXCHUNK * 4 <= 160 * 1024) return launch_fwd_lds<2, 1, 2, 4, 4, true, true>(a, nchw, st);
+    return valu ? launch_fwd_lds<2, 2, 1, 8, 3, true, 2>(a, nchw, st) : launch_fwd_lds<2, 2, 1, 8, 3, true, 1>(a, nchw, st);
+  if (Co % 64 == 0 && lds64 + CV_MAXCHUNK * 4 <= 160 * 1024)
+    return valu ? launch_fwd_lds<2, 1, 2, 4, 4, true, 2>(a, nchw, st) : launch_fwd_lds<2, 1, 2, 4, 4, true, 1>(a, nchw, st);
   return RAI_E_UNSUPPORTED;
 }
 

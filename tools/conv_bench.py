@@ -88,6 +88,15 @@ def main():
                 err = (y[:8].double().cpu() - yd).abs().max().item() / max(yd.abs().max().item(), 1e-30)
                 t = timeit(mine, args.reps)
                 row[f"v{v}"] = {"us": round(t, 2), "tflops": round(row["flops"] / t / 1e6, 1), "relerr": err}
+            if Ci == 4:  # conv1 on the uint8 frames (the product's C3 path): the same forward with the /255 in-kernel
+                xu = torch.randint(0, 256, (B, Ci, H, H), generator=g, dtype=torch.uint8).to(dev)
+                xu = xu.contiguous(memory_format=torch.channels_last)
+
+                def mine_u8():
+                    return L.rai_conv2d_bias_relu_fwd_u8(xu.data_ptr(), C.c_float(255.0), w.data_ptr(), b.data_ptr(), B,
+                                                         H, H, Ci, Co, k, k, s, 1 if flat else 0, y.data_ptr(), st)
+                rc = mine_u8()
+                row["u8_us"] = round(timeit(mine_u8, args.reps), 2) if rc == 0 else f"rc={rc}"
             # weight gradient: MIOpen (find mode) + the accumulate into .grad vs rai_conv2d_wgrad
             dz = (torch.randn(B, Co, OH, OH, generator=g) * 0.01).to(dev).contiguous(memory_format=torch.channels_last)
             grad = torch.zeros_like(w)
