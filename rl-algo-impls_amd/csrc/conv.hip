@@ -68,11 +68,8 @@ __device__ __forceinline__ f4 u8x4_div(unsigned u, float d, float inv) {
 
 // host: does the U8 == 2 quotient equal the IEEE u / d for every byte?  (RAI_CONV_U8_LUT=1: the table)
 static bool u8_div_valu_exact(float d, float* inv_out) {
-  static const bool force_lut = [] {
-    const char* e = getenv("RAI_CONV_U8_LUT");
-    return e && e[0] == '1';
-  }();
-  if (force_lut || !(d > 0.f)) return false;
+  const char* e = getenv("RAI_CONV_U8_LUT");  // read per launch (the tests switch it in-process)
+  if ((e && e[0] == '1') || !(d > 0.f)) return false;
   const float inv = 1.f / d;
   for (int i = 0; i < 256; ++i) {
     const float x = (float)i;
@@ -292,30 +289,46 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
       if (BUF || u < nq) ldb(BUF ? min(u, nq - 1) : u, u);
       __builtin_amdgcn_sched_barrier(0);
     }
-    for (int qd = 0; qd < nq; qd += PF) {
+    auto stage = [&](int q, int u) {  // chunk quad q from ring slot u
+      if (U8) {
 #pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        if (qd + u < nq) {
-          if (U8) {
-#pragma unroll
-            for (int tp = 0; tp < TPX; ++tp) {
-              const unsigned w4 = Ur[u][tp];
-              if (U8 == 2) Br[u][tp] = u8x4_div(w4, a.xdiv, a.xinv);
-              else Br[u][tp] = f4{lut[w4 & 255u], lut[(w4 >> 8) & 255u], lut[(w4 >> 16) & 255u], lut[w4 >> 24]};
-            }
-          }
-          f4 A[TCO];
-#pragma unroll
-          for (int tc = 0; tc < TCO; ++tc) A[tc] = *reinterpret_cast<const f4*>(wrow[tc] + 4 * (4 * (qd + u) + g));
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int tc = 0; tc < TCO; ++tc)
-#pragma unroll
-              for (int tp = 0; tp < TPX; ++tp)
-                acc[tc][tp] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[tc][j], Br[u][tp][j], acc[tc][tp], 0, 0, 0);
+        for (int tp = 0; tp < TPX; ++tp) {
+          const unsigned w4 = Ur[u][tp];
+          if (U8 == 2) Br[u][tp] = u8x4_div(w4, a.xdiv, a.xinv);
+          else Br[u][tp] = f4{lut[w4 & 255u], lut[(w4 >> 8) & 255u], lut[(w4 >> 16) & 255u], lut[w4 >> 24]};
         }
-        if (BUF || qd + u + PF < nq) ldb(BUF ? min(qd + u + PF, nq - 1) : qd + u + PF, u);
+      }
+      f4 A[TCO];
+#pragma unroll
+      for (int tc = 0; tc < TCO; ++tc) A[tc] = *reinterpret_cast<const f4*>(wrow[tc] + 4 * (4 * q + g));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tc = 0; tc < TCO; ++tc)
+#pragma unroll
+          for (int tp = 0; tp < TPX; ++tp)
+            acc[tc][tp] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[tc][j], Br[u][tp][j], acc[tc][tp], 0, 0, 0);
+    };
+    if (BUF) {  // full PF blocks as straight-line code (stages interleave), then the remainder
+      int qd = 0;
+      for (; qd + PF <= nq; qd += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          stage(qd + u, u);
+          ldb(min(qd + u + PF, nq - 1), u);
+          __builtin_amdgcn_sched_barrier(0);  // slot u's reload right behind its MFMAs, not clustered at the end
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u)
+        if (qd + u < nq) stage(qd + u, u);
+    } else {
+      for (int qd = 0; qd < nq; qd += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          if (qd + u < nq) stage(qd + u, u);
+          if (qd + u + PF < nq) ldb(qd + u + PF, u);
+        }
       }
     }
 #pragma unroll
@@ -516,27 +529,43 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
       ld(u, u);
       __builtin_amdgcn_sched_barrier(0);
     }
-    for (int st = 0; st < nst; st += PF) {
+    auto step = [&](int sq, int u) {  // pixel step sq from ring slot u
+      fv d = dv[u];
+      if (RB) {
 #pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        if (st + u < nst) {
-          fv d = dv[u];
-          if (RB) {
+        for (int j = 0; j < VC; ++j) d[j] = yv[u][j] > 0.f ? d[j] : 0.f;
+      }
+      f4 x;
+      if (U8 == 2) x = u8x4_div(xu[u], a.xdiv, a.xinv);
+      else if (U8 == 1) x = f4{lut[xu[u] & 255u], lut[(xu[u] >> 8) & 255u], lut[(xu[u] >> 16) & 255u], lut[xu[u] >> 24]};
+      else x = xv[u];
+      if (BUF && lo + 4 * sq + g >= hi) {  // past the wave's pixels: zero, as the pointer form loads
+        d = fv{};
+        x = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      mma(d, x);
+      if (RB) dsum += d;
+    };
+    if (BUF) {  // full PF blocks as straight-line code (steps interleave), then the remainder
+      int st = 0;
+      for (; st + PF <= nst; st += PF) {
 #pragma unroll
-            for (int j = 0; j < VC; ++j) d[j] = yv[u][j] > 0.f ? d[j] : 0.f;
-          }
-          f4 x;
-          if (U8 == 2) x = u8x4_div(xu[u], a.xdiv, a.xinv);
-          else if (U8 == 1) x = f4{lut[xu[u] & 255u], lut[(xu[u] >> 8) & 255u], lut[(xu[u] >> 16) & 255u], lut[xu[u] >> 24]};
-          else x = xv[u];
-          if (BUF && lo + 4 * (st + u) + g >= hi) {  // past the wave's pixels: zero, as the pointer form loads
-            d = fv{};
-            x = f4{0.f, 0.f, 0.f, 0.f};
-          }
-          mma(d, x);
-          if (RB) dsum += d;
+        for (int u = 0; u < PF; ++u) {
+          step(st + u, u);
+          ld(st + u + PF, u);
+          __builtin_amdgcn_sched_barrier(0);  // slot u's reload right behind its MFMAs, not clustered at the end
         }
-        if (BUF || st + u + PF < nst) ld(st + u + PF, u);
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u)
+        if (st + u < nst) step(st + u, u);
+    } else {
+      for (int st = 0; st < nst; st += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          if (st + u < nst) step(st + u, u);
+          if (st + u + PF < nst) ld(st + u + PF, u);
+        }
       }
     }
     if (RB) {  // the four lane groups (rows of the step), then the waves in order through LDS

@@ -378,14 +378,22 @@ def _u8_frames(B, H, seed):
     return u
 
 
+U8_QUOTIENTS = [("fma", 255.0), ("table", 255.0), ("fma", 7.0)]
+
+
+@pytest.mark.parametrize("quot,divisor", U8_QUOTIENTS)
 @pytest.mark.parametrize("B", [1, 7, 256, 1024])
-def test_conv1_uint8_forward_is_the_float32_forward_of_the_prescaled_frames(B):
+def test_conv1_uint8_forward_is_the_float32_forward_of_the_prescaled_frames(B, quot, divisor, monkeypatch):
     """rai_conv2d_bias_relu_fwd_u8 on uint8 NHWC frames (conv1 of NatureCNN, x = u8 / 255 formed in the
     kernel) is bit-identical to rai_conv2d_bias_relu_fwd on the float32 frames u8 / 255 (IEEE division, as
-    the gather's prescale writes them): same blocking and summation order, only the operand load differs."""
+    the gather's prescale writes them): same blocking and summation order, only the operand load differs.
+    Both in-kernel quotients: the multiply + fma correction (default where the host has checked it exact
+    for the divisor) and the LDS table (RAI_CONV_U8_LUT=1)."""
+    if quot == "table":
+        monkeypatch.setenv("RAI_CONV_U8_LUT", "1")
     u = _u8_frames(B, 84, seed=B)
     _, w, b = _inputs(1, 4, 84, 32, 8, seed=3)
-    div = torch.tensor(255.0)
+    div = torch.tensor(divisor)
     xf = (u.float() / div).to(DEV).contiguous(memory_format=torch.channels_last)
     ud = u.to(DEV).contiguous(memory_format=torch.channels_last)
     wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
@@ -397,8 +405,8 @@ def test_conv1_uint8_forward_is_the_float32_forward_of_the_prescaled_frames(B):
     y8 = torch.full_like(y32, float("nan"))
     _lib.check(L.rai_conv2d_bias_relu_fwd(xf.data_ptr(), wd.data_ptr(), bd.data_ptr(), B, 84, 84, 4, 32, 8, 8, 4, 0,
                                           y32.data_ptr(), st), "fwd f32")
-    _lib.check(L.rai_conv2d_bias_relu_fwd_u8(ud.data_ptr(), 255.0, wd.data_ptr(), bd.data_ptr(), B, 84, 84, 4, 32, 8,
-                                             8, 4, 0, y8.data_ptr(), st), "fwd u8")
+    _lib.check(L.rai_conv2d_bias_relu_fwd_u8(ud.data_ptr(), divisor, wd.data_ptr(), bd.data_ptr(), B, 84, 84, 4, 32,
+                                             8, 8, 4, 0, y8.data_ptr(), st), "fwd u8")
     torch.cuda.synchronize()
     assert torch.equal(y8.cpu(), y32.cpu())
     if B <= 7:  # and against fp64 (bound as test_conv_bias_relu_fwd_matches_fp64)
@@ -407,12 +415,15 @@ def test_conv1_uint8_forward_is_the_float32_forward_of_the_prescaled_frames(B):
         assert ((got - ref).abs() <= 256 * 2.0 ** -24 * bound + 1e-30).all()
 
 
+@pytest.mark.parametrize("quot", ["fma", "table"])
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("B", [3, 256])
-def test_conv1_uint8_weight_gradient_partials_match_the_float32_ones(relu, B):
+def test_conv1_uint8_weight_gradient_partials_match_the_float32_ones(relu, B, quot, monkeypatch):
     """rai_conv2d_wgrad_partials_u8 / rai_conv2d_wgrad_relu_partials_u8 + the reduce: bit-identical dW (and
-    db) to the float32 forms on the prescaled frames."""
+    db) to the float32 forms on the prescaled frames, with either in-kernel quotient."""
     from rl_algo_impls_amd.cnn_ops import _WgradJob
+    if quot == "table":
+        monkeypatch.setenv("RAI_CONV_U8_LUT", "1")
     u = _u8_frames(B, 84, seed=11 + B)
     gen = torch.Generator().manual_seed(B)
     dy = torch.randn(B, 32, 20, 20, generator=gen)
