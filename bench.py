@@ -532,8 +532,10 @@ def main():
         if args.config == "pong":
             from rl_algo_impls_amd import cnn_ops as _cnn
             if _cnn._CONV_MFMA:
-                kname = ("whole update (hand-written MFMA convolution forward + weight gradient, MIOpen input "
-                         "gradient, hipBLASLt fc GEMMs, HIP epilogues)")
+                dgrad = ("weight + input gradients" if _cnn._CONV_MFMA_DGRAD
+                         else "weight gradient, MIOpen input gradient")
+                kname = (f"whole update (hand-written MFMA convolution forward + {dgrad}, hipBLASLt fc GEMMs, "
+                         "HIP epilogues)")
         roofline = {"kernel": kname, "bound": "mfma",
                     "achieved": round(tf, 3), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 4),
                     "traffic": upd_traffic, "traffic_source": traffic_src, "traffic_unit": "bytes per update",
