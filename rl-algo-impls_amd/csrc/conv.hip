@@ -56,14 +56,19 @@ struct ConvFwdArgs {
 // VALU operations per byte and no LDS; the host launches it only when u8_div_valu_exact(d) has
 // checked it equal, bit for bit, to u / d for all 256 bytes (true for d = 255).
 __device__ __forceinline__ f4 u8x4_div(unsigned u, float d, float inv) {
-  f4 r;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float x = (float)((u >> (8 * q)) & 255u);
-    const float q0 = x * inv;
-    r[q] = __builtin_fmaf(__builtin_fmaf(-q0, d, x), inv, q0);
-  }
-  return r;
+#ifdef RAI_U8_FAKE_CVT  // diagnostic builds only (wrong values): the dword operand path without the quotient
+  return f4{__uint_as_float(u), __uint_as_float(u >> 8), __uint_as_float(u >> 16), __uint_as_float(u >> 24)};
+#endif
+  // packed-fp32 pairs (v_pk_mul_f32 / v_pk_fma_f32: two lanes' worth per VALU op, per-element IEEE results
+  // identical to the scalar ops the host check runs)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const f2v iv = {inv, inv}, dv = {d, d};
+  const f2v x01 = {(float)(u & 255u), (float)((u >> 8) & 255u)};
+  const f2v x23 = {(float)((u >> 16) & 255u), (float)(u >> 24)};
+  const f2v q01 = x01 * iv, q23 = x23 * iv;
+  const f2v r01 = __builtin_elementwise_fma(__builtin_elementwise_fma(-q01, dv, x01), iv, q01);
+  const f2v r23 = __builtin_elementwise_fma(__builtin_elementwise_fma(-q23, dv, x23), iv, q23);
+  return f4{r01.x, r01.y, r23.x, r23.y};
 }
 
 // host: does the U8 == 2 quotient equal the IEEE u / d for every byte?  (RAI_CONV_U8_LUT=1: the table)
