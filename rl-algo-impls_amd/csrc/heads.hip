@@ -53,11 +53,30 @@ __global__ __launch_bounds__(HD_THREADS) void heads_fwd_kernel(const HeadsArgs a
   float acc[A + 1];
 #pragma unroll
   for (int o = 0; o <= A; ++o) acc[o] = 0.f;
-  for (int d = lane; d < D; d += 64) {
-    const float x = e[d];
+  constexpr int NPL = 8;
+  if (D <= 64 * NPL) {  // NatureCNN (D = 512): all of the lane's loads first (one round trip, not eight)
+    float xs[NPL], ws[NPL][A + 1];
 #pragma unroll
-    for (int o = 0; o < A; ++o) acc[o] = fmaf(x, a.wpi[o * D + d], acc[o]);
-    acc[A] = fmaf(x, a.wv[d], acc[A]);
+    for (int k = 0; k < NPL; ++k) {
+      const int d = min(lane + 64 * k, D - 1);
+      xs[k] = e[d];
+#pragma unroll
+      for (int o = 0; o < A; ++o) ws[k][o] = a.wpi[o * D + d];
+      ws[k][A] = a.wv[d];
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const bool in = lane + 64 * k < D;  // the same fma sequence as the loop below
+#pragma unroll
+      for (int o = 0; o <= A; ++o) acc[o] = in ? fmaf(xs[k], ws[k][o], acc[o]) : acc[o];
+    }
+  } else {
+    for (int d = lane; d < D; d += 64) {
+      const float x = e[d];
+#pragma unroll
+      for (int o = 0; o < A; ++o) acc[o] = fmaf(x, a.wpi[o * D + d], acc[o]);
+      acc[A] = fmaf(x, a.wv[d], acc[A]);
+    }
   }
   float z[A];
 #pragma unroll
@@ -131,6 +150,26 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_rows_kernel(const HeadsA
     dvv[b] = gv;
   }
   const int D = a.D;
+  constexpr int NPL = 8;  // D <= 512 (NatureCNN): every load of the row first, then the stores (the
+                          // stores may alias the weights for the compiler, so a fused loop serialises)
+  if (D <= 64 * NPL) {
+    float sv[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int d = min(lane + 64 * k, D - 1);  // branch-free (all loads batch); d >= D lanes are not stored
+      float s = gv * a.wv[d];
+#pragma unroll
+      for (int o = 0; o < A; ++o) s = fmaf(dq[o], a.wpi[o * D + d], s);
+      if (RELU) s = a.enc[b * D + d] <= 0.f ? 0.f : s;
+      sv[k] = s;
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int d = lane + 64 * k;
+      if (d < D) d_enc[b * D + d] = sv[k];
+    }
+    return;
+  }
   for (int d = lane; d < D; d += 64) {
     float s = gv * a.wv[d];
 #pragma unroll
@@ -164,6 +203,7 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const Hea
 #pragma unroll
   for (int o = 0; o <= A; ++o) acc[o] = 0.f;
   if (d < D) {
+#pragma unroll 8  // B = 256: 16 rows per lane, their loads in two batches (same accumulation order)
     for (int64_t b = rl; b < B; b += 16) {
       const float x = a.enc[b * D + d];
 #pragma unroll
