@@ -72,9 +72,9 @@ __device__ __forceinline__ void block_sum_small(double (&v)[NV], double* sc) {
 
 // KM: compile-time bound on the value columns (1 or RAI_MAX_K) so every per-column array is
 // register-resident (indices unrolled; a runtime-indexed array would live in scratch).
-template <int KM>
+template <int KM, class AdvF>
 __device__ __forceinline__ float row_adv(const LossArgs& a, const rai_ppo_hparams& hp, const AdvNorm& nm,
-                                         int64_t b) {
+                                         int64_t b, AdvF adv) {
 #pragma clang fp contract(off)
   const int K = a.K;
   if (hp.normalize_after_scaling) {
@@ -83,14 +83,14 @@ __device__ __forceinline__ float row_adv(const LossArgs& a, const rai_ppo_hparam
       x = 0.f;
 #pragma unroll
       for (int k = 0; k < KM; ++k)
-        if (k < K) x += a.adv[b * K + k] * hp.multi_reward_weights[k];
+        if (k < K) x += adv(b, k) * hp.multi_reward_weights[k];
     } else {
-      x = a.adv[b * K];
+      x = adv(b, 0);
     }
     return (x - nm.smean) / nm.sden;
   }
   if (KM == 1 || (K == 1 && !hp.has_multi_reward_weights)) {
-    const float x = a.adv[b * K];
+    const float x = adv(b, 0);
     float y = x;
     if (hp.normalize_advantage) y = (x - nm.mean[0]) / nm.den[0];
     else if (hp.standardize_advantage) y = x / nm.den[0];
@@ -100,7 +100,7 @@ __device__ __forceinline__ float row_adv(const LossArgs& a, const rai_ppo_hparam
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     if (k < K) {
-      float x = a.adv[b * K + k];
+      float x = adv(b, k);
       if (hp.normalize_advantage) x = (x - nm.mean[k]) / nm.den[k];
       else if (hp.standardize_advantage) x = x / nm.den[k];
       s += x * (hp.has_multi_reward_weights ? hp.multi_reward_weights[k] : 1.f);
@@ -117,11 +117,44 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
   constexpr int NR = 4 + 2 * KM;  // pi_sum, kl_sum, clip_cnt, ent_sum, vloss[KM], vclip[KM]
   __shared__ double red[NR * (LOSS_THREADS / 64 + 1)];
   __shared__ AdvNorm nm_s;
-  const rai_ppo_hparams& hp = *a.hp;
+  // by value: one scalar load batch at entry (through a reference every field read after a barrier is a
+  // fresh global load on the critical path); likewise the train-state words, which only thread 0 writes,
+  // at the very end
+  const rai_ppo_hparams hp = *a.hp;
+  const int st_stat_index = a.state->stat_index, st_pi_coef_zero = a.state->pi_coef_zero;
   const int K = a.K;
   const int64_t B = a.B;
   const int tid = threadIdx.x, NT = blockDim.x;
   const bool ppo = hp.loss_kind == 0;
+
+  // one row per thread (B <= blockDim.x: C3's 256-row minibatch): the row's inputs are loaded once, all
+  // together, and every pass below reads them from registers -- one memory round trip instead of one per
+  // pass.  Otherwise the accessors read memory, as before.  Same values, same arithmetic.
+  const bool one_row = B <= NT;
+  float c_adv[KM], c_v[KM], c_R[KM], c_vo[KM];
+  float c_nl = 0.f, c_ol = 0.f, c_ent = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) c_adv[k] = c_v[k] = c_R[k] = c_vo[k] = 0.f;
+  if (one_row && tid < B) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (k < K) {
+        c_adv[k] = a.adv[tid * K + k];
+        c_v[k] = a.new_values[tid * K + k];
+        c_R[k] = a.ret[tid * K + k];
+        c_vo[k] = a.old_values[tid * K + k];
+      }
+    c_nl = a.new_logp[tid];
+    c_ol = a.old_logp[tid];
+  }
+  const bool one_ent = a.n_entropy <= NT;
+  if (one_ent && tid < a.n_entropy) c_ent = a.entropy[tid];
+  auto ADV = [&](int64_t b, int k) -> float { return one_row ? c_adv[k] : a.adv[b * K + k]; };
+  auto NV = [&](int64_t b, int k) -> float { return one_row ? c_v[k] : a.new_values[b * K + k]; };
+  auto RET = [&](int64_t b, int k) -> float { return one_row ? c_R[k] : a.ret[b * K + k]; };
+  auto OV = [&](int64_t b, int k) -> float { return one_row ? c_vo[k] : a.old_values[b * K + k]; };
+  auto NL = [&](int64_t b) -> float { return one_row ? c_nl : a.new_logp[b]; };
+  auto OL = [&](int64_t b) -> float { return one_row ? c_ol : a.old_logp[b]; };
 
   // ---- pass 0: advantage moments (two-pass, fp64 accumulation; ppo.py:307-318) ---------
   const bool need_cols = !hp.normalize_after_scaling && (hp.normalize_advantage || hp.standardize_advantage);
@@ -130,7 +163,7 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
     // over the union of the ranks' minibatch slices).  Row si holds K (mean, den) pairs per column,
     // or one pair of the weighted advantage under normalize_advantages_after_scaling.
     if (tid == 0) {
-      const int si = a.state->stat_index;
+      const int si = st_stat_index;
       if (hp.normalize_after_scaling) {
         nm_s.smean = hp.ext_moments[2 * si];
         nm_s.sden = hp.ext_moments[2 * si + 1];
@@ -151,9 +184,9 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
         x = 0.f;
 #pragma unroll
         for (int k = 0; k < KM; ++k)
-          if (k < K) x += a.adv[b * K + k] * hp.multi_reward_weights[k];
+          if (k < K) x += ADV(b, k) * hp.multi_reward_weights[k];
       } else {
-        x = a.adv[b * K];
+        x = ADV(b, 0);
       }
       acc[0] += (double)x;
     }
@@ -166,9 +199,9 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
         x = 0.f;
 #pragma unroll
         for (int k = 0; k < KM; ++k)
-          if (k < K) x += a.adv[b * K + k] * hp.multi_reward_weights[k];
+          if (k < K) x += ADV(b, k) * hp.multi_reward_weights[k];
       } else {
-        x = a.adv[b * K];
+        x = ADV(b, 0);
       }
       const double d = (double)x - (double)mean;
       acc[0] += d * d;
@@ -185,7 +218,7 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
     for (int64_t b = tid; b < B; b += NT) {
 #pragma unroll
       for (int k = 0; k < KM; ++k)
-        if (k < K) acc[k] += (double)a.adv[b * K + k];
+        if (k < K) acc[k] += (double)ADV(b, k);
     }
     block_sum_small<KM>(acc, red);
     float mean[KM];
@@ -198,7 +231,7 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         if (k < K) {
-          const double d = (double)a.adv[b * K + k] - (double)mean[k];
+          const double d = (double)ADV(b, k) - (double)mean[k];
           acc[k] += d * d;
         }
       }
@@ -224,24 +257,24 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
 #pragma unroll
   for (int i = 0; i < NR; ++i) acc[i] = 0.0;
   for (int64_t b = tid; b < B; b += NT) {
-    const float A = row_adv<KM>(a, hp, nm, b);
+    const float A = row_adv<KM>(a, hp, nm, b, ADV);
     if (ppo) {
-      const float logratio = a.new_logp[b] - a.old_logp[b];
+      const float logratio = NL(b) - OL(b);
       const float ratio = expf(logratio);
       const float cr = fminf(fmaxf(ratio, lo), hi);
       acc[0] += (double)fminf(ratio * A, cr * A);
       acc[1] += (double)((ratio - 1.f) - logratio);
       acc[2] += (fabsf(ratio - 1.f) > hp.clip_range) ? 1.0 : 0.0;
     } else {
-      acc[0] += (double)(A * a.new_logp[b]);
+      acc[0] += (double)(A * NL(b));
     }
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       if (k < K) {
-        const float v = a.new_values[b * K + k], R = a.ret[b * K + k];
+        const float v = NV(b, k), R = RET(b, k);
         float l = vf_elem_loss(vfn, v - R);
         if (vclip_on) {
-          const float vo = a.old_values[b * K + k];
+          const float vo = OV(b, k);
           const float vc = vo + fminf(fmaxf(v - vo, -vclip), vclip);
           l = fmaxf(l, vf_elem_loss(vfn, vc - R));
           acc[4 + KM + k] += (fabsf(v - vo) > vclip) ? 1.0 : 0.0;
@@ -250,12 +283,16 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
       }
     }
   }
-  for (int64_t i = tid; i < a.n_entropy; i += NT) acc[3] += (double)a.entropy[i];
+  if (one_ent) {
+    if (tid < a.n_entropy) acc[3] += (double)c_ent;
+  } else {
+    for (int64_t i = tid; i < a.n_entropy; i += NT) acc[3] += (double)a.entropy[i];
+  }
   block_sum_small<NR>(acc, red);
 
   const float invB = 1.f / (float)B;
   const float approx_kl = (float)(acc[1] / (double)B);
-  int latched = a.state->pi_coef_zero;
+  int latched = st_pi_coef_zero;
   if (ppo && hp.has_kl_cutoff && approx_kl > hp.kl_cutoff) latched = 1;
   const float pi_coef = (ppo && latched) ? 0.f : 1.f;
   const float halve = hp.ppo2_vf_coef_halving ? 0.5f : 1.f;
@@ -267,9 +304,9 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
 #pragma unroll
   for (int k = 0; k < KM; ++k) gl[k] = ((hp.vf_coef[k] * halve) * invB) * gs;  // d loss / d l_bk
   for (int64_t b = tid; b < B; b += NT) {
-    const float A = row_adv<KM>(a, hp, nm, b);
+    const float A = row_adv<KM>(a, hp, nm, b, ADV);
     if (ppo) {
-      const float logratio = a.new_logp[b] - a.old_logp[b];
+      const float logratio = NL(b) - OL(b);
       const float ratio = expf(logratio);
       const float cr = fminf(fmaxf(ratio, lo), hi);
       const float s1 = ratio * A, s2 = cr * A;
@@ -286,10 +323,10 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       if (k < K) {
-        const float v = a.new_values[b * K + k], R = a.ret[b * K + k];
+        const float v = NV(b, k), R = RET(b, k);
         float dv;
         if (vclip_on) {
-          const float vo = a.old_values[b * K + k];
+          const float vo = OV(b, k);
           const float dvo = v - vo;
           const float vc = vo + fminf(fmaxf(dvo, -vclip), vclip);
           const float l1 = vf_elem_loss(vfn, v - R);
@@ -315,7 +352,7 @@ __device__ __forceinline__ void pg_loss_body(const LossArgs& a) {
     const float pi_loss = (float)(-acc[0] / (double)B);
     const float ent_loss = (float)(-acc[3] / (double)a.n_entropy);
     float vsum = 0.f;
-    const int idx = a.state->stat_index;
+    const int idx = st_stat_index;
     float* row = (a.stats && idx < a.max_stats) ? a.stats + (int64_t)idx * RAI_STAT_STRIDE : nullptr;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
