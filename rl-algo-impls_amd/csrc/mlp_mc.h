@@ -134,6 +134,24 @@ __device__ __forceinline__ void adam_update_fast(float& p, float& m, float& v, f
   p = p + neg_step * (m * __builtin_amdgcn_rcpf(denom));
 }
 
+// The same update on an element pair in packed fp32 (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32: two
+// elements per VALU op; per element the identical IEEE operations, so identical results), the square
+// root and reciprocal per element.  The 8-CU epoch kernel's whole-network Adam is on every step's
+// critical path.
+typedef float f2a __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void adam_update_fast2(f2a& p, f2a& m, f2a& v, f2a g, float w1, float w2, float beta2,
+                                                  float inv_bc2_sqrt, float neg_step, float eps) {
+  const f2a W1 = {w1, w1}, W2 = {w2, w2}, B2 = {beta2, beta2}, IB = {inv_bc2_sqrt, inv_bc2_sqrt}, EP = {eps, eps},
+            NS = {neg_step, neg_step};
+  m = m + W1 * (g - m);
+  v = v * B2;
+  v = v + (W2 * g) * g;
+  const f2a sq = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+  const f2a denom = sq * IB + EP;
+  const f2a rc = {__builtin_amdgcn_rcpf(denom.x), __builtin_amdgcn_rcpf(denom.y)};
+  p = p + NS * (m * rc);
+}
+
 // Branch-free gather: the load is issued unconditionally (clamped index) and masked after, so
 // a run of them stays in one basic block with all loads in flight (a guarded load becomes a
 // branch, and the wait for its data is then placed before the next one is issued).

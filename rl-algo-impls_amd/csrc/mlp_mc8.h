@@ -761,6 +761,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
         const int ch = tid + M8_NT * i;
         if (ch < WL_CH) {
           f4 p = *reinterpret_cast<const f4*>(&S.Wt[4 * ch]);
+#ifdef RAI_M8_SCALAR_ADAM  // A/B builds only: one element per VALU op
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float pq = p[q], mq = mreg[i][q], vq = vreg[i][q];
@@ -769,6 +770,22 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
             mreg[i][q] = mq;
             vreg[i][q] = vq;
           }
+#else
+          const f2a C2 = {coef, coef};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // element pairs (0, 1), (2, 3)
+            f2a pp = {p[2 * h], p[2 * h + 1]}, mm = {mreg[i][2 * h], mreg[i][2 * h + 1]},
+                vv = {vreg[i][2 * h], vreg[i][2 * h + 1]};
+            const f2a gg = f2a{gr[i][2 * h], gr[i][2 * h + 1]} * C2;
+            adam_update_fast2(pp, mm, vv, gg, w1, w2, beta2, inv_bc2_sqrt, neg_step, adam_eps);
+            p[2 * h] = pp.x;
+            p[2 * h + 1] = pp.y;
+            mreg[i][2 * h] = mm.x;
+            mreg[i][2 * h + 1] = mm.y;
+            vreg[i][2 * h] = vv.x;
+            vreg[i][2 * h + 1] = vv.y;
+          }
+#endif
           *reinterpret_cast<f4*>(&S.Wt[4 * ch]) = p;
         }
       }
