@@ -179,11 +179,13 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_rows_kernel(const HeadsA
   }
 }
 
-// (2) weight gradients: workgroup j owns columns [16 j, 16 j + 16) of Wpi / Wv; its 256 threads are
-// 16 columns x 16 row lanes; each lane sums rows lane, lane + 16, ... (row order), then the 16 row
-// lanes are added in order through LDS.  Workgroup 0 also sums the bias gradients.  FCB (round 4): the
-// same column sums of pass (1)'s dz give the bias gradient of the layer whose ReLU output enc is
-// (g_benc[d] = sum over rows of dz[:, d], row lanes in order, as the weights)
+// (2) weight gradients: workgroup j owns columns [C j, C j + C) of Wpi / Wv (C = HW_COLS); its 256
+// threads are C columns x HW_RL row lanes; each lane sums rows lane, lane + HW_RL, ... (row order), then
+// the row lanes are added in order through LDS.  Workgroup 0 also sums the bias gradients.  FCB (round
+// 4): the same column sums of pass (1)'s dz give the bias gradient of the layer whose ReLU output enc is
+// (g_benc[d] = sum over rows of dz[:, d], row lanes in order, as the weights).  Round 4: 8 columns x 32
+// row lanes (64 workgroups at D = 512, 8 rows per lane in one load batch) instead of 16 x 16 over 32.
+constexpr int HW_COLS = 8, HW_RL = HD_THREADS / HW_COLS;
 template <int A, bool FCB = false>
 __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const HeadsArgs a,
                                                                       const float* __restrict__ dlogits,
@@ -192,10 +194,11 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const Hea
                                                                       float* __restrict__ g_wv, float* __restrict__ g_bv,
                                                                       int accumulate, const float* __restrict__ dz = nullptr,
                                                                       float* __restrict__ g_benc = nullptr) {
-  __shared__ float red[A + 1][16][17];
-  __shared__ float redb[FCB ? 16 : 1][17];
-  const int tid = threadIdx.x, col = tid & 15, rl = tid >> 4;
-  const int d = blockIdx.x * 16 + col;
+  __shared__ float red[A + 1][HW_RL][HW_COLS + 1];
+  __shared__ float redb[FCB ? HW_RL : 1][HW_COLS + 1];
+  __shared__ float redbias[A + 1][17];
+  const int tid = threadIdx.x, col = tid % HW_COLS, rl = tid / HW_COLS;
+  const int d = blockIdx.x * HW_COLS + col;
   const int D = a.D;
   const int64_t B = a.B;
   float acc[A + 1];
@@ -203,8 +206,8 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const Hea
 #pragma unroll
   for (int o = 0; o <= A; ++o) acc[o] = 0.f;
   if (d < D) {
-#pragma unroll 8  // B = 256: 16 rows per lane, their loads in two batches (same accumulation order)
-    for (int64_t b = rl; b < B; b += 16) {
+#pragma unroll 8  // B = 256: 8 rows per lane, their loads in one batch
+    for (int64_t b = rl; b < B; b += HW_RL) {
       const float x = a.enc[b * D + d];
 #pragma unroll
       for (int o = 0; o < A; ++o) acc[o] = fmaf(dlogits[b * A + o], x, acc[o]);
@@ -216,19 +219,19 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const Hea
   for (int o = 0; o <= A; ++o) red[o][rl][col] = acc[o];
   if (FCB) redb[rl][col] = accb;
   __syncthreads();
-  if (FCB && tid < 16) {
-    const int dd = blockIdx.x * 16 + tid;
+  if (FCB && tid < HW_COLS) {
+    const int dd = blockIdx.x * HW_COLS + tid;
     float s = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s += redb[r][tid];
+    for (int r = 0; r < HW_RL; ++r) s += redb[r][tid];
     if (dd < D) g_benc[dd] = accumulate ? g_benc[dd] + s : s;
   }
-  if (tid < 16 * (A + 1)) {
-    const int o = tid >> 4, c = tid & 15;
-    const int dd = blockIdx.x * 16 + c;
+  if (tid < HW_COLS * (A + 1)) {
+    const int o = tid / HW_COLS, c = tid % HW_COLS;
+    const int dd = blockIdx.x * HW_COLS + c;
     float s = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s += red[o][r][c];
+    for (int r = 0; r < HW_RL; ++r) s += red[o][r][c];
     if (dd < D) {
       float* dst = o < A ? g_wpi + o * D + dd : g_wv + dd;
       *dst = accumulate ? *dst + s : s;
@@ -240,12 +243,12 @@ __global__ __launch_bounds__(HD_THREADS) void heads_bwd_weights_kernel(const Hea
     float s = 0.f;
     if (o <= A)
       for (int64_t b = l; b < B; b += 16) s += o < A ? dlogits[b * A + o] : dvv[b];
-    if (o <= A) red[o][l][16] = s;
+    if (o <= A) redbias[o][l] = s;
     __syncthreads();
     if (tid <= A) {
       float t = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) t += red[tid][r][16];
+      for (int r = 0; r < 16; ++r) t += redbias[tid][r];
       float* dst = tid < A ? g_bpi + tid : g_bv;
       *dst = accumulate ? *dst + t : t;
     }
@@ -325,7 +328,7 @@ extern "C" int rai_categorical_critic_heads_bwd(const float* enc, const float* w
   float* dlogits = static_cast<float*>(workspace);
   float* dvv = dlogits + B * A;
   hipStream_t st = rai_stream(stream);
-  const dim3 grid1((unsigned)((B + 3) / 4)), grid2((unsigned)((D + 15) / 16));
+  const dim3 grid1((unsigned)((B + 3) / 4)), grid2((unsigned)((D + HW_COLS - 1) / HW_COLS));
   switch (A) {
 #define RAI_HD_B(n)                                                                                          \
   case n:                                                                                                    \
@@ -370,7 +373,7 @@ extern "C" int rai_categorical_critic_heads_bwd_relu(const float* enc, const flo
   const HeadsArgs a = make_args(enc, wpi, bpi, wv, bv, actions, B, D, A);
   float* dlogits = static_cast<float*>(workspace);
   float* dvv = dlogits + B * A;
-  const dim3 grid1((unsigned)((B + 3) / 4)), grid2((unsigned)((D + 15) / 16));
+  const dim3 grid1((unsigned)((B + 3) / 4)), grid2((unsigned)((D + HW_COLS - 1) / HW_COLS));
   switch (A) {
 #define RAI_HD_BR(n)                                                                                            \
   case n:                                                                                                       \
