@@ -511,7 +511,14 @@ int rai_mlp_policy_step(const float* const* pi_params, const float* const* v_par
  * Stats rows: [0] holds the policy+entropy part of the loss; the caller adds
  * vf_coef * v_loss ([5]).
  * ------------------------------------------------------------------------ */
-/* Workspace: the inter-workgroup exchange words plus one (mean, den) pair per minibatch. */
+/* batch_size > 256 (SURVEY 8(d) batch policy (b), e.g. batch = n_steps * num_envs / 4; in_dim <= 4,
+ * n_actions == 2, else RAI_E_UNSUPPORTED): the throughput-bound large-minibatch form.  Per epoch two
+ * small launches compute every minibatch's advantage moments; per minibatch three launches: forward,
+ * loss and backward partial gradients over all CUs (256 workgroups, 16-row MFMA tiles), a fixed-order
+ * reduction of the 128 partials per network into the gradient + the stats row, clip_grad_norm_ + Adam.
+ * Deterministic.  rai_mlp_ppo_grads takes the same form for batch_size > 256 (mb_count == 1).
+ * Workspace: the inter-workgroup exchange words plus one (mean, den) pair per minibatch (<= 256
+ * rows); the moments, partial gradients (~4.7 MB) and norm partials (> 256 rows). */
 int64_t rai_mlp_ppo_workspace_bytes(int64_t n_rows, int32_t batch_size);
 int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
                       const int64_t* actions, const float* old_logp, const float* old_values,
@@ -610,6 +617,12 @@ int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_
                        const rai_ppo_hparams* hp, const rai_optim_hparams* ohp, rai_train_state* state,
                        float* stats, int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
                        int64_t workspace_bytes, void* stream);
+
+/* Timing hook of the large-minibatch form (bench.py's roofline): rai_mlp_large_timing(n) arms HIP
+ * events around the next n gradient-kernel launches (0 disarms); rai_mlp_large_timing_read writes the
+ * launches' durations in ms (in launch order, waiting for them) and their count. */
+int rai_mlp_large_timing(int32_t capacity);
+int rai_mlp_large_timing_read(float* ms_out, int32_t max_out, int32_t* count_out);
 
 /* --------------------------------------------------------------------------
  * Data-parallel runtime: one process per GPU, an RCCL

@@ -20,6 +20,7 @@ RAI_MAX_FIELDS = 8
 RAI_GRID_MAX_G = 8
 RAI_GRID_MAX_A = 256
 RAI_WIDE_MAX_B = 256
+RAI_MLP_EPOCH_MAX_B = 256  # rai_mlp_ppo_epoch's one-launch epoch kernels; larger minibatches: mlp_large.hip
 RAI_WIDE_MAX_H = 256
 RAI_WIDE_MAX_IN = 64
 RAI_WIDE_MAX_OUT = 8
@@ -196,6 +197,8 @@ _SIGNATURES = {
                                     _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_mlp_ppo_epoch": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
                                     _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
+    "rai_mlp_large_timing": (C.c_int, [_i32]),
+    "rai_mlp_large_timing_read": (C.c_int, [_vp, _i32, _vp]),
     "rai_categorical_sample": (C.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp, _vp, _vp, _i32, _vp]),
     "rai_gaussian_sample": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp,
                                       _i32, _vp]),

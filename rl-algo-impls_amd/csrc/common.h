@@ -34,6 +34,21 @@ __device__ __forceinline__ bool rai_expired(unsigned long long t0, long long lim
   return (long long)(rai_clock() - t0) > limit;
 }
 
+// Branch-free tanh (libm's tanhf branches on |x| ranges, which diverges across a wave):
+// |x| < 0.3: odd Taylor series to x^9 (truncation < 1e-7 relative); otherwise
+// 1 - 2 / (exp(2|x|) + 1) with the sign restored (absolute error ~1 ulp of 1).
+__device__ __forceinline__ float rai_tanh_bf(float x) {
+  const float ax = fabsf(x);
+  const float x2 = x * x;
+  float p = fmaf(x2, 62.f / 2835.f, -17.f / 315.f);
+  p = fmaf(x2, p, 2.f / 15.f);
+  p = fmaf(x2, p, -1.f / 3.f);
+  const float small = fmaf(x * x2, p, x);
+  const float e = __builtin_amdgcn_exp2f(ax * 2.885390081777927f);  // exp(2|x|)
+  const float big = fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+  return ax < 0.3f ? small : copysignf(big, x);
+}
+
 // ---- wave64 reductions (fixed order -> deterministic) ----------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -1,0 +1,809 @@
+// Large-minibatch PPO step for CartPole-class MLP actor-critics (SURVEY 8(d) batch policy (b):
+// batch_size = n_steps * num_envs / 4, i.e. 131,072 rows per optimizer step at config C2).
+//
+// Replaces rl_algo_impls/ppo/ppo.py:290-411 (minibatch forward, ppo.py:326-371 loss, ppo.py:375
+// backward, ppo.py:441-447 clip_grad_norm_ + Adam) for the policy of
+// rl_algo_impls/shared/policy/actor_critic_network/connected_trio.py with Flatten encoder and
+// [in -> 64 -> 64 -> out] actor (Categorical, shared/actor/categorical.py:57-87) and critic
+// (shared/policy/critic.py:11-41) MLPs, when a minibatch no longer fits the one-launch epoch kernels
+// (<= 256 rows, mlp_mc8.h).  At this size one optimizer step is ~6.9 GFLOP of 64-wide contractions:
+// throughput-bound, so the work spreads over every CU instead of a latency-bound dependent chain.
+//
+// Per minibatch, three launches on the caller's stream:
+//  1. lb_grads_kernel: 256 persistent workgroups of 8 waves (128 per network; actor and critic share
+//     no parameter and their loss terms are separable, ppo.py:361-371).  Each wave walks 16-row tiles
+//     of the minibatch with no workgroup barrier:
+//       layer 1, layer 2, dH1 = W2^T dZ2 on v_mfma_f32_16x16x4_f32 in the "hidden x rows" orientation,
+//       so every layer's accumulator tile is the next layer's B operand in place (no data movement on
+//       the forward / backward chain; the A operands are W2 permutations staged once in LDS);
+//       the output layer and its backward as lane-group sums (v_permlane16/32_swap) in the epilogue;
+//       the per-row loss and its gradient w.r.t. the head outputs (the arithmetic of mlp_ppo.hip);
+//       dW2 += dZ2^T H1 and [dW1 | db1] += dZ1^T [x | 1] on MFMA with the rows as the reduction axis
+//       (dZ2, H1, dZ1 transposed through a per-wave LDS tile; the x operand is loaded transposed);
+//       dW3, db2, db3 as per-lane partial sums.
+//     Accumulators persist over the wave's tiles; the 8 waves add their partials in LDS in wave order
+//     and the workgroup writes ONE partial gradient (its network's parameter block) + loss-statistic
+//     partials.  Tiles are dealt to waves statically: the summation order is fixed (deterministic).
+//  2. lb_reduce_kernel: every parameter's 128 workgroup partials summed in workgroup order -> the flat
+//     gradient; per-block fp64 squared-norm partials; block 0 writes the minibatch's stats row.
+//  3. optim.hip's clip_optim_kernel over those partials (clip_grad_norm_ + Adam, torch's formulas).
+// Epoch mode adds, once per epoch, the per-minibatch advantage moments (ppo.py:313-316: mean and
+// unbiased std, fp64 sums) in two small launches.
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+#include "internal.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int HID = 64;
+constexpr int LB_NT = 512;            // 8 waves: two per SIMD
+constexpr int LB_NW = LB_NT / 64;
+constexpr int LB_WG_PER_NET = 128;    // fixed: the partial-gradient summation order depends on it
+constexpr int LB_GRID = 2 * LB_WG_PER_NET;
+constexpr int LB_WAVES_PER_NET = LB_WG_PER_NET * LB_NW;
+constexpr int LB_TS = 24;             // transpose-tile row stride (floats): conflict-free b128 reads
+constexpr int LB_PSTRIDE = 4612;      // >= actor block 64*4+64+64*64+64+2*64+2 = 4610, multiple of 4
+constexpr int LB_MOMP = 64;           // advantage-moment partial chunks per minibatch
+constexpr int LB_RED_NT = 64;         // reduce kernel: one parameter per thread, many CUs
+constexpr float F32_MIN = -3.4028234663852886e38f;
+
+struct LbSmem {
+  float w2f[4][4][64][4];  // forward A operands   [m2][blk][lane][i] = W2[16 m2 + j][16 blk + 4 g + i]
+  float w2b[4][4][64][4];  // backward A operands  [m1][blk][lane][i] = W2[16 blk + 4 g + i][16 m1 + j]
+  float w1[HID][4];        // W1, inputs zero-padded to 4
+  float b1[HID];
+  float b2[HID];
+  float w3[2][HID];        // W3 rows (critic: row 1 zero)
+  float b3[4];
+  double st[LB_NW][4];     // per-wave loss-statistic partials
+  float tt[LB_NW][2][HID][LB_TS];  // per-wave transposes [c][row]: [0] dZ2, [1] H1 then dZ1; later the
+                                   // workgroup's partial-gradient accumulator
+};
+static_assert(sizeof(float) * LB_NW * 2 * HID * LB_TS >= sizeof(float) * LB_PSTRIDE, "accumulator fits");
+
+struct LbArgs {
+  const float* params;
+  const float* obs;
+  const int64_t* actions;
+  const float* old_logp;
+  const float* old_values;
+  const float* adv;
+  const float* ret;
+  const float* moments;  // this minibatch's (mean, den): A = (adv - mean) / den
+  const rai_ppo_hparams* hp;
+  float* part;           // [LB_GRID][LB_PSTRIDE] per-workgroup partial gradients (network-local order)
+  double* statp;         // [LB_GRID][4]
+  int64_t row0;          // first rollout row of the minibatch
+  int32_t rows;          // rows in the minibatch
+  int32_t in_dim;
+  float inv_n;           // 1 / (rows * world)
+};
+
+template <int RELU>
+__device__ __forceinline__ float lb_act(float z) {
+  return RELU ? fmaxf(z, 0.f) : rai_tanh_bf(z);
+}
+template <int RELU>
+__device__ __forceinline__ float lb_act_d(float h) {  // derivative from the activation's output
+  return RELU ? (h > 0.f ? 1.f : 0.f) : 1.f - h * h;
+}
+
+// Sum over the four 16-lane groups at the same lane & 15 (every lane receives the same bits).
+__device__ __forceinline__ float lb_sum_groups(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ float lb_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes of a DPP row (every lane of the row receives the same bits).
+__device__ __forceinline__ float lb_row_sum16(float v) {
+  v += lb_dpp<0xB1>(v);
+  v += lb_dpp<0x4E>(v);
+  v += lb_dpp<0x141>(v);
+  v += lb_dpp<0x140>(v);
+  return v;
+}
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// One tile's inputs for one lane (prefetched a tile ahead).
+struct LbIn {
+  float xb;     // layer-1 B operand: x[row j][feature g]
+  float xw[4];  // [dW1 | db1] B operand: [x | 1][row 4g + s][column j]
+  float u0, u1; // actor: old logp, advantage; critic: old value, return
+  int act;      // actor: action
+};
+
+template <bool ACTOR>
+__device__ __forceinline__ void lb_load(const LbArgs& a, int t, int g, int j, LbIn& in) {
+  const int IN = a.in_dim;
+  const int r = t * 16 + j;
+  const int64_t row = a.row0 + r;
+  const bool valid = r < a.rows;
+  in.xb = (valid && g < IN) ? a.obs[row * IN + g] : 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int rs = t * 16 + 4 * g + s;
+    const bool vs = rs < a.rows;
+    in.xw[s] = (vs && j < IN) ? a.obs[(a.row0 + rs) * IN + j] : ((vs && j == 4) ? 1.f : 0.f);
+  }
+  if (ACTOR) {
+    in.act = valid ? (int)a.actions[row] : 0;
+    in.u0 = valid ? a.old_logp[row] : 0.f;
+    in.u1 = valid ? a.adv[row] : 0.f;
+  } else {
+    in.act = 0;
+    in.u0 = valid ? a.old_values[row] : 0.f;
+    in.u1 = valid ? a.ret[row] : 0.f;
+  }
+}
+
+template <int RELU, bool ACTOR>
+__device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
+  constexpr int OUT = ACTOR ? 2 : 1;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int IN = a.in_dim;
+  const int szA = HID * IN + HID + HID * HID + HID + 2 * HID + 2;
+  const int base = ACTOR ? 0 : szA;
+  // network-local offsets (the partial-gradient layout) and flat offsets (base + local)
+  const int oW1 = 0, ob1 = HID * IN, oW2 = ob1 + HID, ob2 = oW2 + HID * HID, oW3 = ob2 + HID,
+            ob3 = oW3 + OUT * HID, P_net = ob3 + OUT;
+
+  // ---- stage the weights in LDS (operand permutations for the MFMA chains) -------------------
+  for (int e = tid; e < 4 * 4 * 64 * 4; e += LB_NT) {
+    const int i = e & 3, l = (e >> 2) & 63, blk = (e >> 8) & 3, m = e >> 10;
+    const int lg = l >> 4, lj = l & 15;
+    S.w2f[m][blk][l][i] = a.params[base + oW2 + (16 * m + lj) * HID + 16 * blk + 4 * lg + i];
+    S.w2b[m][blk][l][i] = a.params[base + oW2 + (16 * blk + 4 * lg + i) * HID + 16 * m + lj];
+  }
+  for (int e = tid; e < HID * 4; e += LB_NT) {
+    const int c = e >> 2, f = e & 3;
+    S.w1[c][f] = f < IN ? a.params[base + oW1 + c * IN + f] : 0.f;
+  }
+  if (tid < HID) {
+    S.b1[tid] = a.params[base + ob1 + tid];
+    S.b2[tid] = a.params[base + ob2 + tid];
+  }
+  if (tid < 2 * HID) {
+    const int o = tid >> 6, c = tid & 63;
+    S.w3[o][c] = o < OUT ? a.params[base + oW3 + o * HID + c] : 0.f;
+  }
+  if (tid < 4) S.b3[tid] = tid < OUT ? a.params[base + ob3 + tid] : 0.f;
+
+  const rai_ppo_hparams* hp = a.hp;
+  const float clip_range = hp->clip_range, ent_coef = hp->ent_coef, vf_coef0 = hp->vf_coef[0];
+  const float clip_range_vf = hp->clip_range_vf;
+  const int has_vclip = hp->has_clip_range_vf, vf_fn = hp->vf_loss_fn;
+  const float halve = hp->ppo2_vf_coef_halving ? 0.5f : 1.f;
+  const float amean = a.moments[0], aden = a.moments[1];
+  const float inv_n = a.inv_n;
+  __syncthreads();
+
+  // constant per-lane operands: layer-1 A = W1[16 m + j][g]
+  float w1a[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) w1a[m] = S.w1[16 * m + j][g];
+
+  f4 acc2[4][4];  // dW2 tile [mc][mk]: lane (g, j), reg i -> dW2[16 mc + 4 g + i][16 mk + j]
+  f4 acc1[4];     // [dW1 | db1] [mj]: lane (g, j = column), reg i -> row 16 mj + 4 g + i
+  float aw3[OUT][16], ab2[16], ab3[OUT];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    acc1[x] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc2[x][y] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    ab2[k] = 0.f;
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) aw3[o][k] = 0.f;
+  }
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) ab3[o] = 0.f;
+  double st0 = 0.0, st1 = 0.0, st2 = 0.0, st3 = 0.0;
+
+  float(*tdz)[LB_TS] = S.tt[w][0];
+  float(*th)[LB_TS] = S.tt[w][1];
+  const int n_tiles = (a.rows + 15) >> 4;
+  const int wave_id = wgn * LB_NW + w;
+  LbIn nx;
+  if (wave_id < n_tiles) lb_load<ACTOR>(a, wave_id, g, j, nx);
+
+  for (int t = wave_id; t < n_tiles; t += LB_WAVES_PER_NET) {
+    const LbIn in = nx;
+    if (t + LB_WAVES_PER_NET < n_tiles) lb_load<ACTOR>(a, t + LB_WAVES_PER_NET, g, j, nx);
+    const bool valid = t * 16 + j < a.rows;
+
+    // ---- layer 1: Z1^T[c][row] = W1 x^T; H1 = act(Z1 + b1) ----------------------------------
+    f4 h1[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f4 z = mfma4(w1a[m], in.xb, f4{0.f, 0.f, 0.f, 0.f});
+      const f4 bb = *reinterpret_cast<const f4*>(&S.b1[16 * m + 4 * g]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h1[m][i] = lb_act<RELU>(z[i] + bb[i]);
+    }
+    // H1 transposed for dW2's B operand
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) th[16 * m + 4 * g + i][j] = h1[m][i];
+
+    // ---- layer 2: Z2^T = W2 H1^T (B operand = the lane's own H1 registers) ---------------------
+    f4 z2[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) z2[m] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+      f4 wv[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) wv[m] = *reinterpret_cast<const f4*>(&S.w2f[m][blk][lane][0]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) z2[m] = mfma4(wv[m][i], h1[blk][i], z2[m]);
+    }
+    f4 h2[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f4 bb = *reinterpret_cast<const f4*>(&S.b2[16 * m + 4 * g]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h2[m][i] = lb_act<RELU>(z2[m][i] + bb[i]);
+    }
+
+    // ---- output layer: lane partials over its 16 hidden units, summed over the lane groups -------
+    float zo[OUT];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      float p = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const f4 wv = *reinterpret_cast<const f4*>(&S.w3[o][16 * m + 4 * g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p = fmaf(h2[m][i], wv[i], p);
+      }
+      zo[o] = lb_sum_groups(p) + S.b3[o];
+    }
+
+    // ---- loss per row (ppo.py:326-371; the tie rules of mlp_ppo.hip / loss.hip) -----------------
+    float d0 = 0.f, d1 = 0.f;
+    if (valid) {
+      if (ACTOR) {
+        const float z0 = zo[0], z1 = zo[OUT - 1];
+        const float mx = fmaxf(z0, z1);
+        const float se = expf(z0 - mx) + expf(z1 - mx);
+        const float lse = mx + logf(se);
+        const float n0 = z0 - lse, n1 = z1 - lse;
+        const float p0 = expf(n0), p1 = expf(n1);
+        float H = 0.f;
+        H -= fmaxf(n0, F32_MIN) * p0;
+        H -= fmaxf(n1, F32_MIN) * p1;
+        const int act = in.act == 1 ? 1 : 0;
+        const float logp = (act ? z1 : z0) - lse;
+        const float A = (in.u1 - amean) / aden;
+        const float logratio = logp - in.u0;
+        const float ratio = expf(logratio);
+        const float lo = 1.f - clip_range, hi = 1.f + clip_range;
+        const float cr = fminf(fmaxf(ratio, lo), hi);
+        const float s1 = ratio * A, s2 = cr * A;
+        const float gpi = -inv_n;
+        float g1, g2;
+        if (s1 < s2) { g1 = gpi; g2 = 0.f; }
+        else if (s1 > s2) { g1 = 0.f; g2 = gpi; }
+        else { g1 = gpi * 0.5f; g2 = gpi * 0.5f; }
+        const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float dlogp = (g1 * A + (g2 * A) * in_clip) * ratio;
+        const float dent = -ent_coef * inv_n;
+        d0 = dlogp * ((act == 0 ? 1.f : 0.f) - p0) + dent * (-p0 * (n0 + H));
+        d1 = dlogp * ((act == 1 ? 1.f : 0.f) - p1) + dent * (-p1 * (n1 + H));
+        if (g == 0) {
+          st0 += (double)fminf(s1, s2);
+          st1 += (double)((ratio - 1.f) - logratio);
+          st2 += (fabsf(ratio - 1.f) > clip_range) ? 1.0 : 0.0;
+          st3 += (double)H;
+        }
+      } else {
+        const float v = zo[0], R = in.u1, vo = in.u0;
+        const float gl = (vf_coef0 * halve) * inv_n;
+        float l = v - R;
+        float dv;
+        auto vloss = [&](float x) -> float {
+          if (vf_fn == 0) return x * x;
+          const float z = fabsf(x);
+          return z < 1.f ? 0.5f * z * z : (z - 0.5f);
+        };
+        auto vgrad = [&](float x) -> float {
+          if (vf_fn == 0) return 2.f * x;
+          return x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x);
+        };
+        float lv = vloss(l);
+        float vcl_cnt = 0.f;
+        if (has_vclip) {
+          const float dvo = v - vo;
+          const float vcl = vo + fminf(fmaxf(dvo, -clip_range_vf), clip_range_vf);
+          const float l2 = vloss(vcl - R);
+          float w1, w2;
+          if (lv > l2) { w1 = gl; w2 = 0.f; }
+          else if (lv < l2) { w1 = 0.f; w2 = gl; }
+          else { w1 = gl * 0.5f; w2 = gl * 0.5f; }
+          const float inside = (dvo >= -clip_range_vf && dvo <= clip_range_vf) ? 1.f : 0.f;
+          dv = w1 * vgrad(l) + (w2 * vgrad(vcl - R)) * inside;
+          vcl_cnt = (fabsf(v - vo) > clip_range_vf) ? 1.f : 0.f;
+          lv = fmaxf(lv, l2);
+        } else {
+          dv = gl * vgrad(l);
+        }
+        d0 = dv;
+        if (g == 0) {
+          st0 += (double)lv;
+          st1 += (double)vcl_cnt;
+        }
+      }
+    }
+
+    // ---- backward through the output layer: dZ2 = (W3^T d) * act'(H2); dW3, db2, db3 partials ----
+    f4 dz2[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f4 wa = *reinterpret_cast<const f4*>(&S.w3[0][16 * m + 4 * g]);
+      const f4 wb = *reinterpret_cast<const f4*>(&S.w3[1][16 * m + 4 * g]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float h = h2[m][i];
+        const float dh = ACTOR ? fmaf(d1, wb[i], d0 * wa[i]) : d0 * wa[i];
+        aw3[0][4 * m + i] = fmaf(d0, h, aw3[0][4 * m + i]);
+        if (ACTOR) aw3[OUT - 1][4 * m + i] = fmaf(d1, h, aw3[OUT - 1][4 * m + i]);
+        const float dz = dh * lb_act_d<RELU>(h);
+        dz2[m][i] = dz;
+        ab2[4 * m + i] += dz;
+      }
+    }
+    ab3[0] += d0;
+    if (ACTOR) ab3[OUT - 1] += d1;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tdz[16 * m + 4 * g + i][j] = dz2[m][i];
+
+    // ---- dH1^T = W2^T dZ2^T (B operand = the lane's own dZ2 registers); dZ1 = dH1 * act'(H1) ------
+    f4 dh1[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) dh1[m] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+      f4 wv[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) wv[m] = *reinterpret_cast<const f4*>(&S.w2b[m][blk][lane][0]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) dh1[m] = mfma4(wv[m][i], dz2[blk][i], dh1[m]);
+    }
+
+    // ---- dW2 += dZ2^T H1 over the tile's rows (row 4 g + s of k-step s in both operands) ---------
+    {
+      f4 ar[4], br[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        ar[m] = *reinterpret_cast<const f4*>(&tdz[16 * m + j][4 * g]);
+        br[m] = *reinterpret_cast<const f4*>(&th[16 * m + j][4 * g]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int mc = 0; mc < 4; ++mc)
+#pragma unroll
+          for (int mk = 0; mk < 4; ++mk) acc2[mc][mk] = mfma4(ar[mc][s], br[mk][s], acc2[mc][mk]);
+    }
+
+    // ---- [dW1 | db1] += dZ1^T [x | 1] (dZ1 transposed over H1's tile, read after it in order) -----
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) th[16 * m + 4 * g + i][j] = dh1[m][i] * lb_act_d<RELU>(h1[m][i]);
+    {
+      f4 az[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) az[m] = *reinterpret_cast<const f4*>(&th[16 * m + j][4 * g]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc1[m] = mfma4(az[m][s], in.xw[s], acc1[m]);
+    }
+  }
+
+  // ---- per-wave sums over the 16 row lanes, then the workgroup's partial in wave order -----------
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    ab2[k] = lb_row_sum16(ab2[k]);
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) aw3[o][k] = lb_row_sum16(aw3[o][k]);
+  }
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) ab3[o] = lb_row_sum16(ab3[o]);
+  {
+    double s[4] = {st0, st1, st2, st3};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = wave_sum(s[q]);
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) S.st[w][q] = s[q];
+    }
+  }
+  float* accv = &S.tt[0][0][0][0];
+  __syncthreads();  // every wave is past its last tile: the transpose tiles become the accumulator
+  for (int r = 0; r < LB_NW; ++r) {
+    if (w == r) {
+      const bool first = r == 0;
+      auto put = [&](int idx, float v) { accv[idx] = first ? v : accv[idx] + v; };
+#pragma unroll
+      for (int mc = 0; mc < 4; ++mc)
+#pragma unroll
+        for (int mk = 0; mk < 4; ++mk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) put(oW2 + (16 * mc + 4 * g + i) * HID + 16 * mk + j, acc2[mc][mk][i]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * m + 4 * g + i;
+          if (j < IN) put(oW1 + c * IN + j, acc1[m][i]);
+          else if (j == 4) put(ob1 + c, acc1[m][i]);
+        }
+      if (j == 0) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int c = 16 * m + 4 * g + i;
+            put(ob2 + c, ab2[4 * m + i]);
+#pragma unroll
+            for (int o = 0; o < OUT; ++o) put(oW3 + o * HID + c, aw3[o][4 * m + i]);
+          }
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) put(ob3 + o, ab3[o]);
+      }
+    }
+    __syncthreads();
+  }
+  const int slot = (ACTOR ? 0 : LB_WG_PER_NET) + wgn;
+  float* dst = a.part + (int64_t)slot * LB_PSTRIDE;
+  for (int e = tid; e < P_net; e += LB_NT) dst[e] = accv[e];
+  if (tid < 4) {
+    double s = 0.0;
+    for (int r = 0; r < LB_NW; ++r) s += S.st[r][tid];
+    a.statp[slot * 4 + tid] = s;
+  }
+}
+
+template <int RELU>
+__global__ __launch_bounds__(LB_NT, 1) void lb_grads_kernel(LbArgs a) {
+  extern __shared__ __align__(16) unsigned char lb_lds[];
+  LbSmem& S = *reinterpret_cast<LbSmem*>(lb_lds);
+  const int net = blockIdx.x & 1, wgn = blockIdx.x >> 1;
+  if (net == 0) lb_net<RELU, true>(a, S, wgn);
+  else lb_net<RELU, false>(a, S, wgn);
+}
+
+struct LbRed {
+  const float* part;
+  const double* statp;
+  float* grad;           // the minibatch gradient (flat parameter order)
+  double* sq_part;       // per-block fp64 squared-norm partials (epoch mode), or nullptr
+  rai_train_state* state;
+  float* stats;
+  const rai_ppo_hparams* hp;
+  int32_t P;
+  int32_t szA;
+  int32_t max_stats;
+  int32_t bump_step;     // epoch mode: advance state->opt_step (read by the optimizer launch)
+  double n_total;        // rows * world
+};
+
+// Every parameter's LB_WG_PER_NET workgroup partials in workgroup order; block 0 also writes the
+// minibatch's stats row (ppo.py:379-396 means; row[0] is the policy + entropy part, the host adds the
+// value term, as for rai_mlp_ppo_epoch).
+__global__ __launch_bounds__(LB_RED_NT) void lb_reduce_kernel(LbRed r) {
+  const int p = blockIdx.x * LB_RED_NT + threadIdx.x;
+  double sq = 0.0;
+  if (p < r.P) {
+    const int net = p >= r.szA ? 1 : 0;
+    const int loc = p - (net ? r.szA : 0);
+    const float* src = r.part + (int64_t)net * LB_WG_PER_NET * LB_PSTRIDE + loc;
+    float s[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < LB_WG_PER_NET; k += 8)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += src[(int64_t)(k + q) * LB_PSTRIDE];
+    const float v = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    r.grad[p] = v;
+    sq = (double)v * (double)v;
+  }
+  if (r.sq_part) {
+    sq = wave_sum(sq);  // one wave per block
+    if (threadIdx.x == 0) r.sq_part[blockIdx.x] = sq;
+  }
+  if (blockIdx.x != 0) return;
+  // stats: threads 0..3 the actor's four sums, 4..5 the critic's two, each in workgroup order
+  __shared__ double tot[6];
+  if (threadIdx.x < 6) {
+    const int net = threadIdx.x < 4 ? 0 : 1, q = threadIdx.x < 4 ? threadIdx.x : threadIdx.x - 4;
+    double t = 0.0;
+    for (int k = 0; k < LB_WG_PER_NET; ++k) t += r.statp[(net * LB_WG_PER_NET + k) * 4 + q];
+    tot[threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int idx = r.state->stat_index;
+    if (r.stats && idx < r.max_stats) {
+      const float halve = r.hp->ppo2_vf_coef_halving ? 0.5f : 1.f;
+      const double Bd = r.n_total;
+      float* row = r.stats + (int64_t)idx * RAI_STAT_STRIDE;
+      const float pi_loss = (float)(-tot[0] / Bd);
+      const float ent_loss = (float)(-tot[3] / Bd);
+      row[0] = pi_loss + r.hp->ent_coef * ent_loss;  // host adds the value term
+      row[1] = pi_loss;
+      row[2] = ent_loss;
+      row[3] = (float)(tot[1] / Bd);
+      row[4] = (float)(tot[2] / Bd);
+      row[5] = (float)(tot[4] / Bd) * halve;
+      row[5 + RAI_MAX_K] = r.hp->has_clip_range_vf ? (float)(tot[5] / Bd) : 0.f;
+    }
+    r.state->stat_index = idx + 1;
+    if (r.bump_step) r.state->opt_step += 1;
+  }
+}
+
+// Advantage moments of every minibatch of the epoch: fp64 (sum, sum of squares) per chunk, then per
+// minibatch mean (rounded to f32, as torch's f32 A.mean()) and unbiased std + 1e-8, encoded with the
+// normalize / standardize choice as adv_moments_kernel (mlp_ppo.hip) does.
+__global__ __launch_bounds__(256) void lb_moments_part_kernel(const float* __restrict__ adv, int64_t n_rows, int B,
+                                                              double* mp) {
+  __shared__ double red[2 * 4];
+  const int mb = blockIdx.y, ch = blockIdx.x;
+  const int64_t row0 = (int64_t)mb * B;
+  const int64_t rows = min((int64_t)B, n_rows - row0);
+  const int64_t lo = rows * ch / LB_MOMP, hi = rows * (ch + 1) / LB_MOMP;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+    const double x = (double)adv[row0 + i];
+    s1 += x;
+    s2 += x * x;
+  }
+  double v[2] = {s1, s2};
+  block_sum<2>(v, red);
+  if (threadIdx.x == 0) {
+    mp[((int64_t)mb * LB_MOMP + ch) * 2] = v[0];
+    mp[((int64_t)mb * LB_MOMP + ch) * 2 + 1] = v[1];
+  }
+}
+
+__global__ __launch_bounds__(64) void lb_moments_final_kernel(const double* __restrict__ mp, int64_t n_rows, int B,
+                                                              const rai_ppo_hparams* hp, float* moments) {
+  const int mb = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  const int64_t rows = min((int64_t)B, n_rows - (int64_t)mb * B);
+  double s1 = 0.0, s2 = 0.0;
+  for (int c = 0; c < LB_MOMP; ++c) {
+    s1 += mp[((int64_t)mb * LB_MOMP + c) * 2];
+    s2 += mp[((int64_t)mb * LB_MOMP + c) * 2 + 1];
+  }
+  const double n = (double)rows;
+  const double md = s1 / n;
+  const float mean = (float)md;
+  const double var = fmax(s2 - n * md * md, 0.0) / (n - 1.0);
+  const float den = (float)sqrt(var) + 1e-8f;
+  float m0 = 0.f, m1 = 1.f;
+  if (hp->normalize_advantage) { m0 = mean; m1 = den; }
+  else if (hp->standardize_advantage) { m1 = den; }
+  moments[2 * mb] = m0;
+  moments[2 * mb + 1] = m1;
+}
+
+// ---- workspace -------------------------------------------------------------------------------
+int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
+struct LbWs {
+  float* moments;
+  double* momp;
+  double* statp;
+  double* sq;
+  float* grad;
+  float* part;
+};
+constexpr int LB_MAX_P = 2 * LB_PSTRIDE;
+constexpr int LB_RED_MAX_BLOCKS = (LB_MAX_P + LB_RED_NT - 1) / LB_RED_NT;
+LbWs lb_carve(void* ws, int64_t nmb) {
+  unsigned char* p = static_cast<unsigned char*>(ws);
+  LbWs w;
+  w.moments = reinterpret_cast<float*>(p);
+  p += align256(8 * nmb);
+  w.momp = reinterpret_cast<double*>(p);
+  p += align256(16 * nmb * LB_MOMP);
+  w.statp = reinterpret_cast<double*>(p);
+  p += align256(8 * 4 * LB_GRID);
+  w.sq = reinterpret_cast<double*>(p);
+  p += align256(8 * LB_RED_MAX_BLOCKS);
+  w.grad = reinterpret_cast<float*>(p);
+  p += align256(4 * LB_MAX_P);
+  w.part = reinterpret_cast<float*>(p);
+  return w;
+}
+
+int lb_allow_lds(const void* kernel) {
+  static std::mutex mu;
+  static std::vector<const void*> done;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const void* k : done)
+    if (k == kernel) return RAI_OK;
+  const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(LbSmem));
+  if (e != hipSuccess) return (int)e;
+  done.push_back(kernel);
+  return RAI_OK;
+}
+
+// Timing hook (bench.py's roofline): HIP events around every lb_grads_kernel launch while armed.
+struct LbTiming {
+  std::mutex mu;
+  std::vector<hipEvent_t> ev;  // pairs
+  int next = 0;
+  int cap = 0;
+};
+LbTiming& lb_timing() {
+  static LbTiming t;
+  return t;
+}
+
+}  // namespace
+
+bool rai_internal::mlp_large_supported(int32_t in_dim, int32_t n_act, int32_t hidden) {
+  return hidden == HID && in_dim >= 1 && in_dim <= 4 && n_act == 2;
+}
+
+int64_t rai_internal::mlp_large_workspace_bytes(int64_t n_rows, int32_t batch) {
+  const int64_t nmb = batch > 0 ? (n_rows + batch - 1) / batch : 0;
+  return align256(8 * nmb) + align256(16 * nmb * LB_MOMP) + align256(8 * 4 * LB_GRID) +
+         align256(8 * LB_RED_MAX_BLOCKS) + align256(4 * LB_MAX_P) + (int64_t)LB_GRID * LB_PSTRIDE * 4;
+}
+
+int rai_internal::mlp_large(float* params, float* exp_avg, float* exp_avg_sq, const float* obs,
+                            const int64_t* actions, const float* old_logp, const float* old_values, const float* adv,
+                            const float* ret, int64_t n_rows, int32_t batch, int32_t in_dim, int32_t n_act,
+                            int32_t act_fn, int32_t mb_begin, int32_t mb_count, const float* moments, int32_t world,
+                            const rai_ppo_hparams* hp, const rai_optim_hparams* ohp, rai_train_state* state,
+                            float* stats, int32_t max_stats, float* norms, int32_t max_norms, float* grad_out,
+                            void* workspace, int64_t workspace_bytes, hipStream_t s) {
+  if (!mlp_large_supported(in_dim, n_act, HID)) return RAI_E_UNSUPPORTED;
+  if (batch < 2 || n_rows < 1 || world < 1 || (act_fn != 0 && act_fn != 1)) return RAI_E_SHAPE;
+  if (!params || !obs || !actions || !old_logp || !old_values || !adv || !ret || !hp || !state || !workspace)
+    return RAI_E_NULLPTR;
+  const bool grads_mode = grad_out != nullptr;
+  if (!grads_mode && (!exp_avg || !exp_avg_sq || !ohp)) return RAI_E_NULLPTR;
+  if (workspace_bytes < mlp_large_workspace_bytes(n_rows, batch)) return RAI_E_WORKSPACE;
+  const int64_t nmb = (n_rows + batch - 1) / batch;
+  if (grads_mode && (mb_count != 1 || mb_begin < 0 || mb_begin >= nmb || !moments)) return RAI_E_SHAPE;
+  if (!moments && n_rows % batch == 1) return RAI_E_SHAPE;  // a 1-row minibatch has no unbiased std
+  const int szA = HID * in_dim + HID + HID * HID + HID + 2 * HID + 2;
+  const int P = szA + HID * in_dim + HID + HID * HID + HID + HID + 1;
+  LbWs w = lb_carve(workspace, nmb);
+  int e = act_fn ? lb_allow_lds(reinterpret_cast<const void*>(&lb_grads_kernel<1>))
+                 : lb_allow_lds(reinterpret_cast<const void*>(&lb_grads_kernel<0>));
+  if (e != RAI_OK) return e;
+  const float* mom = moments;
+  if (!mom) {
+    hipLaunchKernelGGL(lb_moments_part_kernel, dim3(LB_MOMP, (unsigned)nmb), dim3(256), 0, s, adv, n_rows, batch,
+                       w.momp);
+    RAI_LAUNCH_CHECK();
+    hipLaunchKernelGGL(lb_moments_final_kernel, dim3((unsigned)nmb), dim3(64), 0, s, w.momp, n_rows, batch, hp,
+                       w.moments);
+    RAI_LAUNCH_CHECK();
+    mom = w.moments;
+  }
+  const int red_blocks = (P + LB_RED_NT - 1) / LB_RED_NT;
+  const int64_t mb_end = grads_mode ? mb_begin + 1 : nmb;
+  for (int64_t mb = grads_mode ? mb_begin : 0; mb < mb_end; ++mb) {
+    LbArgs a;
+    a.params = params;
+    a.obs = obs;
+    a.actions = actions;
+    a.old_logp = old_logp;
+    a.old_values = old_values;
+    a.adv = adv;
+    a.ret = ret;
+    a.moments = mom + 2 * mb;
+    a.hp = hp;
+    a.part = w.part;
+    a.statp = w.statp;
+    a.row0 = mb * batch;
+    a.rows = (int32_t)std::min<int64_t>(batch, n_rows - mb * batch);
+    a.in_dim = in_dim;
+    a.inv_n = 1.f / (float)((int64_t)a.rows * world);
+    LbTiming& tm = lb_timing();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    {
+      std::lock_guard<std::mutex> lock(tm.mu);
+      if (tm.next < tm.cap) {
+        e0 = tm.ev[2 * tm.next];
+        e1 = tm.ev[2 * tm.next + 1];
+        ++tm.next;
+      }
+    }
+    if (e0) (void)hipEventRecord(e0, s);
+    if (act_fn) hipLaunchKernelGGL(lb_grads_kernel<1>, dim3(LB_GRID), dim3(LB_NT), sizeof(LbSmem), s, a);
+    else hipLaunchKernelGGL(lb_grads_kernel<0>, dim3(LB_GRID), dim3(LB_NT), sizeof(LbSmem), s, a);
+    RAI_LAUNCH_CHECK();
+    if (e1) (void)hipEventRecord(e1, s);
+    LbRed r;
+    r.part = w.part;
+    r.statp = w.statp;
+    r.grad = grads_mode ? grad_out : w.grad;
+    r.sq_part = grads_mode ? nullptr : w.sq;
+    r.state = state;
+    r.stats = stats;
+    r.hp = hp;
+    r.P = P;
+    r.szA = szA;
+    r.max_stats = max_stats;
+    r.bump_step = grads_mode ? 0 : 1;
+    r.n_total = (double)a.rows * (double)world;
+    hipLaunchKernelGGL(lb_reduce_kernel, dim3(red_blocks), dim3(LB_RED_NT), 0, s, r);
+    RAI_LAUNCH_CHECK();
+    if (!grads_mode) {
+      e = rai_internal::optim_apply_partials(params, w.grad, exp_avg, exp_avg_sq, P, ohp, state, w.sq, red_blocks,
+                                             norms, max_norms, s);
+      if (e != RAI_OK) return e;
+    }
+  }
+  return RAI_OK;
+}
+
+extern "C" int rai_mlp_large_timing(int32_t capacity) {
+  LbTiming& t = lb_timing();
+  std::lock_guard<std::mutex> lock(t.mu);
+  if (capacity < 0) return RAI_E_SHAPE;
+  for (hipEvent_t ev : t.ev) (void)hipEventDestroy(ev);
+  t.ev.clear();
+  t.next = 0;
+  t.cap = 0;
+  for (int i = 0; i < 2 * capacity; ++i) {
+    hipEvent_t ev;
+    const hipError_t e = hipEventCreate(&ev);
+    if (e != hipSuccess) return (int)e;
+    t.ev.push_back(ev);
+  }
+  t.cap = capacity;
+  return RAI_OK;
+}
+
+extern "C" int rai_mlp_large_timing_read(float* ms_out, int32_t max_out, int32_t* count_out) {
+  if (!ms_out || !count_out) return RAI_E_NULLPTR;
+  LbTiming& t = lb_timing();
+  std::lock_guard<std::mutex> lock(t.mu);
+  const int n = std::min(t.next, (int)max_out);
+  for (int i = 0; i < n; ++i) {
+    hipError_t e = hipEventSynchronize(t.ev[2 * i + 1]);
+    if (e != hipSuccess) return (int)e;
+    e = hipEventElapsedTime(&ms_out[i], t.ev[2 * i], t.ev[2 * i + 1]);
+    if (e != hipSuccess) return (int)e;
+  }
+  *count_out = n;
+  return RAI_OK;
+}

@@ -30,6 +30,7 @@
 // The kernel is instantiated for padded (in_dim, n_actions) of (4, 2) — CartPole —
 // and (8, 8); padded rows/columns carry zeros.
 #include "common.h"
+#include "internal.h"
 
 #include <cstdlib>
 #include <cstring>
@@ -1634,6 +1635,7 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
 }  // namespace
 
 extern "C" int64_t rai_mlp_ppo_workspace_bytes(int64_t n_rows, int32_t batch_size) {
+  if (batch_size > MAXB) return rai_internal::mlp_large_workspace_bytes(n_rows, batch_size);
   return XCHG_BYTES + SCRATCH_BYTES + moments_bytes(n_rows, batch_size) + statp_bytes(n_rows, batch_size);
 }
 
@@ -1645,6 +1647,13 @@ extern "C" int rai_mlp_ppo_epoch(float* params, float* exp_avg, float* exp_avg_s
                                  rai_train_state* state, float* stats, int32_t max_stats, float* norms,
                                  int32_t max_norms, void* workspace, int64_t workspace_bytes,
                                  void* stream) {
+  if (batch_size > MAXB) {  // SURVEY 8(d) batch policy (b): the all-CU large-minibatch step (mlp_large.hip)
+    if (!rai_internal::mlp_large_supported(in_dim, n_actions, hidden)) return RAI_E_UNSUPPORTED;
+    return rai_internal::mlp_large(params, exp_avg, exp_avg_sq, obs, actions, old_logp, old_values, advantages,
+                                   returns, n_rows, batch_size, in_dim, n_actions, activation, 0, 1 << 30, nullptr,
+                                   1, hp, ohp, state, stats, max_stats, norms, max_norms, nullptr, workspace,
+                                   workspace_bytes, rai_stream(stream));
+  }
   MlpArgs a = {};
   a.params = params; a.exp_avg = exp_avg; a.exp_avg_sq = exp_avg_sq;
   a.obs = obs; a.actions = actions; a.old_logp = old_logp; a.old_values = old_values;
@@ -1667,7 +1676,8 @@ extern "C" int rai_mlp_ppo_epoch_xdp(float* params, float* exp_avg, float* exp_a
                                      const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
                                      int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
                                      int64_t workspace_bytes, void* stream) {
-  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3))) return RAI_E_UNSUPPORTED;
+  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3)) || batch_size > MAXB)
+    return RAI_E_UNSUPPORTED;
   if (!moments || !peers) return RAI_E_NULLPTR;
   if (world < 2 || world > XDP_MAXW || rank < 0 || rank >= world || step_base < 0) return RAI_E_SHAPE;
   MlpArgs a = {};
@@ -1743,7 +1753,8 @@ int rai_mlp_ppo_dp_step(float* params, float* exp_avg, float* exp_avg_sq, const 
                         const rai_optim_hparams* ohp, rai_train_state* state, float* grad_out, float* stats,
                         int32_t max_stats, float* norms, int32_t max_norms, int32_t sync_base, void* workspace,
                         int64_t workspace_bytes, void* stream) {
-  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3))) return RAI_E_UNSUPPORTED;
+  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3)) || batch_size > MAXB)
+    return RAI_E_UNSUPPORTED;
   if (!grad_out || !moments || !exp_avg || !exp_avg_sq) return RAI_E_NULLPTR;
   if (mb < 0 || mb_count < 0 || sync_base < 0) return RAI_E_SHAPE;
   MlpArgs a = {};
@@ -1770,6 +1781,13 @@ extern "C" int rai_mlp_ppo_grads(const float* params, const float* obs, const in
                                  int64_t workspace_bytes, void* stream) {
   if (!grad_out) return RAI_E_NULLPTR;
   if (mb_begin < 0 || mb_count < 1) return RAI_E_SHAPE;
+  if (batch_size > MAXB) {  // large minibatches: one minibatch per call (mlp_large.hip)
+    if (!rai_internal::mlp_large_supported(in_dim, n_actions, hidden)) return RAI_E_UNSUPPORTED;
+    return rai_internal::mlp_large(const_cast<float*>(params), nullptr, nullptr, obs, actions, old_logp, old_values,
+                                   advantages, returns, n_rows, batch_size, in_dim, n_actions, activation, mb_begin,
+                                   mb_count, moments, world, hp, ohp, state, stats, max_stats, nullptr, 0, grad_out,
+                                   workspace, workspace_bytes, rai_stream(stream));
+  }
   MlpArgs a = {};
   a.grad_in = nullptr; a.P_total = 0; a.sync_base = 0;
   a.params = const_cast<float*>(params);

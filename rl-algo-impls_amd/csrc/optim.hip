@@ -17,6 +17,7 @@
 // The step counter and grad-norm slot live in device memory (rai_train_state)
 // so a captured graph replays correctly.
 #include "common.h"
+#include "internal.h"
 
 #pragma clang fp contract(off)
 
@@ -195,6 +196,20 @@ extern "C" int rai_clip_optim_step(float* params, float* grads, float* state1, f
   hipLaunchKernelGGL(clip_optim_kernel, dim3(blocks), dim3(OPT_THREADS), 0, rai_stream(stream),
                      params, grads, state1, state2, P, hp, state, partial, blocks, norms,
                      max_norms, vec);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+int rai_internal::optim_apply_partials(float* params, float* grads, float* state1, float* state2, int64_t P,
+                                       const rai_optim_hparams* hp, rai_train_state* state, const double* partial,
+                                       int nparts, float* norms, int32_t max_norms, hipStream_t stream) {
+  if (P < 1 || nparts < 1) return RAI_E_SHAPE;
+  if (!params || !grads || !state1 || !hp || !state || !partial) return RAI_E_NULLPTR;
+  if (!state2) state2 = state1;
+  const int vec = ((uintptr_t)grads % 16) == 0 && ((uintptr_t)params % 16) == 0 && ((uintptr_t)state1 % 16) == 0 &&
+                  ((uintptr_t)state2 % 16) == 0;
+  hipLaunchKernelGGL(clip_optim_kernel, dim3(opt_blocks(P)), dim3(OPT_THREADS), 0, stream, params, grads, state1,
+                     state2, P, hp, state, partial, nparts, norms, max_norms, vec);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

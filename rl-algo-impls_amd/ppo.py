@@ -144,7 +144,7 @@ class PPO:
             xdp = os.environ.get("RAI_XDP", "1") != "0"
         spec = self.fused_mlp_spec()
         if (xdp and self.flat.flat.is_cuda and self.world > 1 and spec is not None and spec["in_dim"] <= 4
-                and spec["n_act"] <= 2 and self.world <= 8):
+                and spec["n_act"] <= 2 and self.world <= 8 and self.batch_size <= _lib.RAI_MLP_EPOCH_MAX_B):
             try:
                 self._xdp = self._setup_xdp(group)
             except RuntimeError as e:  # e.g. IPC unavailable: fall back to the per-step RCCL loop
@@ -469,7 +469,11 @@ class PPO:
         if self.force_generic:
             return None
         spec = mlp_actor_critic_spec(self.policy)
-        if spec is None or not (2 <= self.batch_size <= 256):
+        if spec is None or self.batch_size < 2:
+            return None
+        # > 256 rows per minibatch (SURVEY 8(d) batch policy (b)): the all-CU large-minibatch kernels of
+        # rai_mlp_ppo_epoch / rai_mlp_ppo_grads (csrc/mlp_large.hip) cover in_dim <= 4, two actions
+        if self.batch_size > _lib.RAI_MLP_EPOCH_MAX_B and not (spec["in_dim"] <= 4 and spec["n_act"] == 2):
             return None
         if (self.gradient_accumulation or self.kl_cutoff is not None or self.multi_reward_weights is not None
                 or self.vf_weights is not None or self.normalize_advantages_after_scaling

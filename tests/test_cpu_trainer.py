@@ -59,3 +59,25 @@ def test_cpu_trainer_pong_steps_match_reference(golden):
     ref = z["stats"]
     np.testing.assert_allclose(rows[:, [0, 1, 3, 4, 5, 2]], ref[:, :6], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(cpu_trainer.flat_params(pol), z["params"], rtol=1e-5, atol=1e-8)
+
+
+def test_cpu_trainer_scaled_batch_matches_reference(golden):
+    """SURVEY 8(d) batch policy (b) (batch = T*N/4): the CPU leg against the reference's own learn_epoch
+    at four minibatches per epoch (learn_epoch_scaled.npz, make_golden_scaled.py)."""
+    z = golden("learn_epoch_scaled.npz")
+    p = "scaled/"
+    kw = json.loads(str(z[p + "kw"]))
+    adv = oracle.compute_advantages(z[p + "rewards"], z[p + "values"], z[p + "episode_starts"],
+                                    z[p + "next_episode_starts"], z[p + "next_values"], kw["gamma"], kw["gae_lambda"])
+    np.testing.assert_array_equal(adv, z[p + "advantages"])
+    pol = cpu_trainer.MLPActorCritic()
+    cpu_trainer.load_flat(pol, z[p + "init"])
+    ppo = cpu_trainer.CpuPPO(pol, lr=kw["learning_rate"], batch_size=kw["batch_size"], n_epochs=kw["n_epochs"],
+                             clip_range=kw["clip_range"], ent_coef=kw["ent_coef"])
+    fl = lambda a: torch.as_tensor(np.asarray(a).reshape((-1,) + np.asarray(a).shape[2:]))
+    b = dict(obs=fl(z[p + "obs"]), logprobs=fl(z[p + "logprobs"]), actions=fl(z[p + "actions"]),
+             values=fl(z[p + "values"]), advantages=fl(adv), returns=fl(adv + z[p + "values"]))
+    rows, means = ppo.update(b, perms=list(z[p + "perms"]))
+    assert len(rows) == 8  # 2 epochs x 4 minibatches
+    np.testing.assert_allclose(rows[:, 6], z[p + "grad_norms"], rtol=1e-5)
+    np.testing.assert_allclose(cpu_trainer.flat_params(pol), z[p + "params"], rtol=2e-4, atol=1e-6)
