@@ -370,6 +370,11 @@ def main():
                   f"(this update: rollout {getattr(algo, 'last_rollout_seconds', 0.0):.3f} s of "
                   f"{getattr(algo, 'last_update_seconds', 0.0):.3f} s)", file=sys.stderr, flush=True)
 
+    # SURVEY 8(d) batch policy (b) on the CartPole-class MLP: the large-minibatch kernels (csrc/mlp_large.hip);
+    # their gradient kernel is the dominant one, timed per launch by the library's HIP-event hook
+    large = (args.config == "cartpole" and algo.fused_mlp_spec() is not None
+             and algo.batch_size > _lib.RAI_MLP_EPOCH_MAX_B)
+    nmb = (T * N + algo.batch_size - 1) // algo.batch_size
     _diagnostics("setup")
     for i in range(args.warmup):
         tw = time.perf_counter()
@@ -377,6 +382,8 @@ def main():
         progress("warmup", i, tw)
     barrier()
     algo.kernel_events = []  # HIP events around every fused epoch launch (same stream as the kernel)
+    if large:
+        _lib.check(_lib.lib().rai_mlp_large_timing(args.steps * algo_kw["n_epochs"] * nmb), "rai_mlp_large_timing")
     t0 = time.perf_counter()
     for i in range(args.steps):
         algo.learn_epoch(0, 1, gen, None)
@@ -387,6 +394,15 @@ def main():
     elapsed = time.perf_counter() - t0
     epoch_ms = [e0.elapsed_time(e1) for e0, e1 in algo.kernel_events]
     algo.kernel_events = None
+    large_ms = []
+    if large:
+        import ctypes as C
+
+        cap = args.steps * algo_kw["n_epochs"] * nmb
+        buf, cnt = (C.c_float * cap)(), C.c_int32(0)
+        _lib.check(_lib.lib().rai_mlp_large_timing_read(buf, cap, C.byref(cnt)), "rai_mlp_large_timing_read")
+        large_ms = list(buf[:cnt.value])
+        _lib.check(_lib.lib().rai_mlp_large_timing(0), "rai_mlp_large_timing")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -448,6 +464,8 @@ def main():
                       "bytes_per_launch": large_bytes}
     del rl_, vl_, esl, advl, retl
     workload = f"ppo {args.config} num_envs={N}/rank n_steps={T}"
+    if args.batch_policy == "scaled":
+        workload += f" batch_policy=scaled batch={algo.batch_size}"
     lib_sha = _lib.lib_sha256()
     pmc, pmc_src = {}, None
     # the newest PMC summary (profiles/r<round><letter>_pmc.json, tools/pmc_summary.py) holding this workload
@@ -493,6 +511,24 @@ def main():
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
         steps_per_launch = (T * N + algo.batch_size - 1) // algo.batch_size
         roof_lat = latency_roofline_wide(ms, steps_per_launch, kname)
+    elif large_ms:
+        # dominant kernel: the large-minibatch gradient kernel (csrc/mlp_large.hip, lb_grads_kernel), one launch
+        # per optimizer step = one minibatch of forward + loss + backward at SURVEY.md 8(d)'s 52,352 FLOP per
+        # sample (CartPole MLP, torch.utils.flop_counter), f32 MFMA peak.  Throughput-bound: the minibatch's
+        # rows are spread over every CU (there is no dependent chain inside a launch)
+        rows = T * N / nmb
+        flops = 52352.0 * rows
+        ms = float(np.mean(large_ms))
+        tf = flops / (ms * 1e-3) / 1e12
+        act = int(cfg["policy"].get("activation_fn", "tanh") == "relu")
+        kname = "lb_grads_kernel<%d>" % act
+        roofline = {"kernel": kname + " (rai_mlp_ppo_epoch, batch > 256: all-CU large-minibatch step)",
+                    "bound": "mfma", "achieved": round(tf, 3), "peak": 157.3, "unit": "TFLOP/s",
+                    "frac": round(tf / 157.3, 4), "traffic": traffic(kname), "traffic_source": traffic_source(kname),
+                    "avg_ms": round(ms, 4), "flops_per_launch": flops, "rows_per_launch": rows,
+                    "launches_timed": len(large_ms),
+                    "epoch_ms": round(float(np.mean(epoch_ms)), 4) if epoch_ms else None}
+        roof_lat = None
     elif epoch_ms:
         # dominant kernel: one fused PPO epoch per launch = T*N samples of forward+backward at
         # SURVEY.md 8(d)'s 52,352 FLOP/sample (CartPole MLP, torch.utils.flop_counter), f32 MFMA peak

@@ -309,11 +309,13 @@ def _conv_dgrad(x, dz, w, stride) -> torch.Tensor:
     B, Ci, H, W = (int(v) for v in x.shape)
     Co, _, KH, KW = (int(v) for v in w.shape)
     s = _pair(stride)[0]
-    if _CONV_MFMA_DGRAD and Ci in (32, 64) and KH % s == 0 and KW % s == 0:
+    if _CONV_MFMA_DGRAD and Ci in (32, 64) and Co % 16 == 0 and KH % s == 0 and KW % s == 0:
         dx = torch.empty((B, Ci, H, W), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-        _lib.check(_lib.lib().rai_conv2d_dgrad(dz.data_ptr(), w.data_ptr(), B, H, W, Ci, Co, KH, KW, s, dx.data_ptr(),
-                                               _lib.stream_handle(x.device)), "rai_conv2d_dgrad")
-        return dx
+        rc = _lib.lib().rai_conv2d_dgrad(dz.data_ptr(), w.data_ptr(), B, H, W, Ci, Co, KH, KW, s, dx.data_ptr(),
+                                         _lib.stream_handle(x.device))
+        if rc != -6:  # RAI_E_UNSUPPORTED: no instantiation for the shape, MIOpen below
+            _lib.check(rc, "rai_conv2d_dgrad")
+            return dx
     return torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), [0, 0], [1, 1], False, [0, 0], 1,
                                                [True, False, False])[0]
 

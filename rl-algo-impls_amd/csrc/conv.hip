@@ -1324,7 +1324,7 @@ static int wgrad_partials(const float* x, const float* dz, const float* y, int64
   // a split's offsets from its first sample fit int32
   if ((int64_t)(WR_MAXPX / (a.OH * a.OW) + 2) * H * W * Ci > 0x7fffffffLL) return RAI_E_SHAPE;
   const dim3 grid((unsigned)p.S, (unsigned)p.KT);
-  const bool buf_ok = (int64_t)B * H * W * Ci * 4 < (1LL << 31) && a.M * Co * 4 < (1LL << 31);
+  const bool buf_ok = (int64_t)B * H * W * Ci * (xu8 ? 1 : 4) < (1LL << 31) && a.M * Co * 4 < (1LL << 31);
   // default: buffer loads with 4 pixel steps in flight where the operands fit 2 GB buffers (NatureCNN
   // B = 256: 2-4 % faster than pointer loads, B = 1024: 8-21 %; profiles/r4g_conv_bench.txt)
   if (pf <= 0) pf = buf_ok ? 104 : 4;
@@ -1636,9 +1636,10 @@ extern "C" int rai_conv2d_wgrad(const float* x, const float* dz, int64_t B, int3
 extern "C" int rai_conv2d_dgrad_v(const float* dz, const float* w, int64_t B, int32_t H, int32_t W, int32_t Ci,
                                   int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx, int32_t variant,
                                   void* stream) {
-  if (B < 0 || H < 1 || W < 1 || (Ci != 32 && Ci != 64) || Co < 16 || Co % 16 || KH < 1 || KW < 1 || stride < 1 ||
-      KH > H || KW > W || KH % stride || KW % stride)
-    return RAI_E_SHAPE;
+  if (B < 0 || H < 1 || W < 1 || Ci < 1 || Co < 1 || KH < 1 || KW < 1 || stride < 1 || KH > H || KW > W)
+    return RAI_E_SHAPE;  // not a convolution
+  if ((Ci != 32 && Ci != 64) || Co % 16 || KH % stride || KW % stride)
+    return RAI_E_UNSUPPORTED;  // a valid shape these kernels are not instantiated for (the caller falls back)
   if (B == 0) return RAI_OK;
   if (!dz || !w || !dx) return RAI_E_NULLPTR;
   if (((uintptr_t)dz | (uintptr_t)w | (uintptr_t)dx) & 15) return RAI_E_SHAPE;
@@ -1710,9 +1711,9 @@ extern "C" int rai_conv2d_dgrad(const float* dz, const float* w, int64_t B, int3
 extern "C" int rai_conv2d_dgrad_relu(const float* dy, const float* y, const float* w, int64_t B, int32_t H, int32_t W,
                                      int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, float* dx,
                                      void* stream) {
-  if (B < 0 || H < 1 || W < 1 || Ci < 16 || Co < 16 || Co % 16 || KH < 1 || KW < 1 || stride < 1 || KH > H ||
-      KW > W || KH % stride || KW % stride)
-    return RAI_E_SHAPE;
+  if (B < 0 || H < 1 || W < 1 || Ci < 1 || Co < 1 || KH < 1 || KW < 1 || stride < 1 || KH > H || KW > W)
+    return RAI_E_SHAPE;  // not a convolution
+  if (Ci < 16 || Co % 16 || KH % stride || KW % stride) return RAI_E_UNSUPPORTED;  // not instantiated: fall back
   if (B == 0) return RAI_OK;
   if (!dy || !y || !w || !dx) return RAI_E_NULLPTR;
   if (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)w | (uintptr_t)dx) & 15) return RAI_E_SHAPE;

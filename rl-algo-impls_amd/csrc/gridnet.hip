@@ -20,6 +20,8 @@
 // mask bytes are one contiguous span, loaded coalesced into LDS; the 64*G (cell, group) items are
 // spread over the threads; the backward writes dz into the LDS tile in place and stores the span
 // coalesced.  Sums over a sample's items are fixed-order block reductions (deterministic).
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -389,7 +391,7 @@ constexpr int NA_THREADS = 256;
 constexpr int NA_CELLS = 256;
 
 __global__ void __launch_bounds__(NA_THREADS) gridnet_num_actions_kernel(GridArgs a, int per_group, int out_bytes,
-                                                                         void* out) {
+                                                                         int tile_cells, void* out) {
   extern __shared__ uint8_t na_tile[];
   __shared__ int na_part[NA_THREADS / RAI_WAVE];
   const int64_t b = blockIdx.x;
@@ -397,8 +399,8 @@ __global__ void __launch_bounds__(NA_THREADS) gridnet_num_actions_kernel(GridArg
   const uint8_t* row = a.mask + b * (int64_t)C * A;
   const bool dw = ((reinterpret_cast<uintptr_t>(row) | (uintptr_t)((int64_t)C * A)) & 3) == 0;
   int count = 0;
-  for (int c0 = 0; c0 < C; c0 += NA_CELLS) {
-    const int nc = min(NA_CELLS, C - c0);
+  for (int c0 = 0; c0 < C; c0 += tile_cells) {
+    const int nc = min(tile_cells, C - c0);
     const int nbytes = nc * A;
     const uint8_t* src = row + (int64_t)c0 * A;
     __syncthreads();
@@ -454,8 +456,10 @@ extern "C" int rai_gridnet_num_actions(const uint8_t* mask, const int64_t* actio
   bool gated = false;
   for (int g = 0; g < G; ++g) gated |= a.sub_ref[g] >= 0;
   if (per_group && gated && !actions) return RAI_E_NULLPTR;
-  hipLaunchKernelGGL(gridnet_num_actions_kernel, dim3((unsigned)B), dim3(NA_THREADS), (size_t)NA_CELLS * a.A,
-                     rai_stream(stream), a, (int)per_group, (int)out_bytes, out);
+  // the cell tile fits the default 64 KiB of LDS beside the kernel's static words for any A <= RAI_GRID_MAX_A
+  const int tile_cells = std::min(NA_CELLS, (65536 - 256) / a.A);
+  hipLaunchKernelGGL(gridnet_num_actions_kernel, dim3((unsigned)B), dim3(NA_THREADS), (size_t)tile_cells * a.A,
+                     rai_stream(stream), a, (int)per_group, (int)out_bytes, tile_cells, out);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
 }

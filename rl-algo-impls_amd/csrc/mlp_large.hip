@@ -10,7 +10,7 @@
 // throughput-bound, so the work spreads over every CU instead of a latency-bound dependent chain.
 //
 // Per minibatch, three launches on the caller's stream:
-//  1. lb_grads_kernel: 256 persistent workgroups of 8 waves (128 per network; actor and critic share
+//  1. lb_grads_kernel: 256 persistent workgroups of 4 waves (128 per network; actor and critic share
 //     no parameter and their loss terms are separable, ppo.py:361-371).  Each wave walks 16-row tiles
 //     of the minibatch with no workgroup barrier:
 //       layer 1, layer 2, dH1 = W2^T dZ2 on v_mfma_f32_16x16x4_f32 in the "hidden x rows" orientation,
@@ -43,7 +43,7 @@ namespace {
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int HID = 64;
-constexpr int LB_NT = 512;            // 8 waves: two per SIMD
+constexpr int LB_NT = 256;            // 4 waves: one per SIMD (each pipelines two tiles)
 constexpr int LB_NW = LB_NT / 64;
 constexpr int LB_WG_PER_NET = 128;    // fixed: the partial-gradient summation order depends on it
 constexpr int LB_GRID = 2 * LB_WG_PER_NET;
@@ -63,10 +63,14 @@ struct LbSmem {
   float w3[2][HID];        // W3 rows (critic: row 1 zero)
   float b3[4];
   double st[LB_NW][4];     // per-wave loss-statistic partials
-  float tt[LB_NW][2][HID][LB_TS];  // per-wave transposes [c][row]: [0] dZ2, [1] H1 then dZ1; later the
-                                   // workgroup's partial-gradient accumulator
+  // per-wave transpose tiles [c][row], two pipeline slots: H1 (then dZ1) and dZ2; after the tile loop
+  // the workgroup's partial-gradient accumulator (hs0 onward)
+  float hs0[LB_NW][HID][LB_TS];   // H1 of the slot's tile
+  float tdz0[LB_NW][HID][LB_TS];  // dZ2 (and the other slot's dH1 in passing)
+  float hs1[LB_NW][HID][LB_TS];
+  float tdz1[LB_NW][HID][LB_TS];
 };
-static_assert(sizeof(float) * LB_NW * 2 * HID * LB_TS >= sizeof(float) * LB_PSTRIDE, "accumulator fits");
+static_assert(sizeof(float) * LB_NW * 4 * HID * LB_TS >= sizeof(float) * LB_PSTRIDE, "accumulator fits");
 
 struct LbArgs {
   const float* params;
@@ -86,14 +90,21 @@ struct LbArgs {
   float inv_n;           // 1 / (rows * world)
 };
 
+// tanh without the small-|x| series: 1 - 2 / (exp(2|x|) + 1), sign restored.  Absolute error ~2 ulp of 1
+// everywhere (relative error grows below |x| ~ 1e-3, where tanh(x) ~ x is consumed only through sums of
+// O(1) terms, so the absolute error is what reaches the outputs); 6 instructions, no branch.
 template <int RELU>
 __device__ __forceinline__ float lb_act(float z) {
-  return RELU ? fmaxf(z, 0.f) : rai_tanh_bf(z);
+  if (RELU) return fmaxf(z, 0.f);
+  const float e = __builtin_amdgcn_exp2f(fabsf(z) * 2.885390081777927f);  // exp(2|z|)
+  return copysignf(fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f), z);
 }
 template <int RELU>
 __device__ __forceinline__ float lb_act_d(float h) {  // derivative from the activation's output
   return RELU ? (h > 0.f ? 1.f : 0.f) : 1.f - h * h;
 }
+__device__ __forceinline__ float lb_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float lb_log(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
 
 // Sum over the four 16-lane groups at the same lane & 15 (every lane receives the same bits).
 __device__ __forceinline__ float lb_sum_groups(float v) {
@@ -115,39 +126,91 @@ __device__ __forceinline__ float lb_row_sum16(float v) {
   return v;
 }
 
+#ifdef RAI_STAMPS
+// Diagnostic build only (never the shipped library): shader-clock stamps of every wave at the kernel's
+// phase boundaries (last launch), plus the constant-rate clock at start / end; rai_mlp_large_debug_stamps
+__device__ unsigned long long g_lb_stamps[LB_GRID][LB_NW][16];
+#define LB_STAMP(k)                                                                               \
+  do {                                                                                            \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
+    if ((threadIdx.x & 63) == 0) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] = t_;               \
+  } while (0)
+#define LB_ACC(k, t0)                                                                             \
+  do {                                                                                            \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
+    if ((threadIdx.x & 63) == 0) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] += t_ - (t0);       \
+    t0 = t_;                                                                                      \
+  } while (0)
+#define LB_RSTAMP(k)                                                                              \
+  do {                                                                                            \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                               \
+    if ((threadIdx.x & 63) == 0) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] = t_;               \
+  } while (0)
+#else
+#define LB_STAMP(k) do { } while (0)
+#define LB_RSTAMP(k) do { } while (0)
+#define LB_ACC(k, t0) do { } while (0)
+#endif
+
+// Interleave an MFMA-heavy phase with a VALU-heavy one inside a scheduling region: N groups of one MFMA
+// followed by V VALU instructions (the compiler otherwise clusters the MFMAs and exposes the VALU chain).
+template <int N, int V>
+__device__ __forceinline__ void lb_interleave() {
+#ifndef LB_NO_IGLP
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+  }
+#endif
+}
+
+#ifdef LB_NO_FENCE  // A/B builds only
+#define LB_FENCE() do { } while (0)
+#else
+#define LB_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// One tile's inputs for one lane (prefetched a tile ahead).
 struct LbIn {
   float xb;     // layer-1 B operand: x[row j][feature g]
-  float xw[4];  // [dW1 | db1] B operand: [x | 1][row 4g + s][column j]
   float u0, u1; // actor: old logp, advantage; critic: old value, return
   int act;      // actor: action
+  bool valid;   // row j of the tile is inside the minibatch
 };
 
+// One tile's forward inputs for one lane (prefetched a tile ahead).  Loads are unconditional (row
+// indices clamped into the minibatch) and masked afterwards, so the tile body is one basic block.
 template <bool ACTOR>
 __device__ __forceinline__ void lb_load(const LbArgs& a, int t, int g, int j, LbIn& in) {
-  const int IN = a.in_dim;
+  const int IN = a.in_dim, last = a.rows - 1;
   const int r = t * 16 + j;
-  const int64_t row = a.row0 + r;
-  const bool valid = r < a.rows;
-  in.xb = (valid && g < IN) ? a.obs[row * IN + g] : 0.f;
+  const bool valid = r <= last;
+  const int64_t row = a.row0 + min(r, last);
+  const float xb = a.obs[row * IN + min(g, IN - 1)];
+  in.xb = (valid && g < IN) ? xb : 0.f;
+  if (ACTOR) {
+    in.act = (int)a.actions[row];
+    in.u0 = a.old_logp[row];
+    in.u1 = a.adv[row];
+  } else {
+    in.act = 0;
+    in.u0 = a.old_values[row];
+    in.u1 = a.ret[row];
+  }
+  in.valid = valid;
+}
+// [dW1 | db1]'s B operand of tile t: [x | 1][row 4g + s][column j] (zero past the minibatch)
+__device__ __forceinline__ void lb_load_xw(const LbArgs& a, int t, int g, int j, float (&xw)[4]) {
+  const int IN = a.in_dim, last = a.rows - 1;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int rs = t * 16 + 4 * g + s;
-    const bool vs = rs < a.rows;
-    in.xw[s] = (vs && j < IN) ? a.obs[(a.row0 + rs) * IN + j] : ((vs && j == 4) ? 1.f : 0.f);
-  }
-  if (ACTOR) {
-    in.act = valid ? (int)a.actions[row] : 0;
-    in.u0 = valid ? a.old_logp[row] : 0.f;
-    in.u1 = valid ? a.adv[row] : 0.f;
-  } else {
-    in.act = 0;
-    in.u0 = valid ? a.old_values[row] : 0.f;
-    in.u1 = valid ? a.ret[row] : 0.f;
+    const float x = a.obs[(a.row0 + min(rs, last)) * IN + min(j, IN - 1)];
+    xw[s] = rs <= last ? (j < IN ? x : (j == 4 ? 1.f : 0.f)) : 0.f;
   }
 }
 
@@ -163,6 +226,12 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
   const int oW1 = 0, ob1 = HID * IN, oW2 = ob1 + HID, ob2 = oW2 + HID * HID, oW3 = ob2 + HID,
             ob3 = oW3 + OUT * HID, P_net = ob3 + OUT;
 
+  LB_RSTAMP(8);
+  LB_STAMP(0);
+#ifdef RAI_STAMPS
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 10; k < 16; ++k) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] = 0;
+#endif
   // ---- stage the weights in LDS (operand permutations for the MFMA chains) -------------------
   for (int e = tid; e < 4 * 4 * 64 * 4; e += LB_NT) {
     const int i = e & 3, l = (e >> 2) & 63, blk = (e >> 8) & 3, m = e >> 10;
@@ -187,17 +256,24 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
   const rai_ppo_hparams* hp = a.hp;
   const float clip_range = hp->clip_range, ent_coef = hp->ent_coef, vf_coef0 = hp->vf_coef[0];
   const float clip_range_vf = hp->clip_range_vf;
-  const int has_vclip = hp->has_clip_range_vf, vf_fn = hp->vf_loss_fn;
+  const bool has_vclip = hp->has_clip_range_vf != 0, huber = hp->vf_loss_fn != 0;
   const float halve = hp->ppo2_vf_coef_halving ? 0.5f : 1.f;
   const float amean = a.moments[0], aden = a.moments[1];
   const float inv_n = a.inv_n;
   __syncthreads();
+  LB_STAMP(1);
 
-  // constant per-lane operands: layer-1 A = W1[16 m + j][g]
+  // constant per-lane operands: layer-1 A = W1[16 m + j][g].  The W2 permutations (layer 2 / dH1 A
+  // operands) stay in LDS; each pipeline phase reads the next phase's block (lb_w2).
   float w1a[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) w1a[m] = S.w1[16 * m + j][g];
+  auto lb_w2 = [&](const float (&t)[4][4][64][4], int blk, f4 (&wv)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) wv[m] = *reinterpret_cast<const f4*>(&t[m][blk][lane][0]);
+  };
 
+  LB_STAMP(2);
   f4 acc2[4][4];  // dW2 tile [mc][mk]: lane (g, j), reg i -> dW2[16 mc + 4 g + i][16 mk + j]
   f4 acc1[4];     // [dW1 | db1] [mj]: lane (g, j = column), reg i -> row 16 mj + 4 g + i
   float aw3[OUT][16], ab2[16], ab3[OUT];
@@ -215,218 +291,279 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
   }
 #pragma unroll
   for (int o = 0; o < OUT; ++o) ab3[o] = 0.f;
-  double st0 = 0.0, st1 = 0.0, st2 = 0.0, st3 = 0.0;
+  float st0 = 0.f, st1 = 0.f, st2 = 0.f, st3 = 0.f;  // per-lane sums over its rows (<= a few hundred)
 
-  float(*tdz)[LB_TS] = S.tt[w][0];
-  float(*th)[LB_TS] = S.tt[w][1];
-  const int n_tiles = (a.rows + 15) >> 4;
-  const int wave_id = wgn * LB_NW + w;
-  LbIn nx;
-  if (wave_id < n_tiles) lb_load<ACTOR>(a, wave_id, g, j, nx);
-
-  for (int t = wave_id; t < n_tiles; t += LB_WAVES_PER_NET) {
-    const LbIn in = nx;
-    if (t + LB_WAVES_PER_NET < n_tiles) lb_load<ACTOR>(a, t + LB_WAVES_PER_NET, g, j, nx);
-    const bool valid = t * 16 + j < a.rows;
-
-    // ---- layer 1: Z1^T[c][row] = W1 x^T; H1 = act(Z1 + b1) ----------------------------------
-    f4 h1[4];
+  // ---- the tile pipeline's phases.  Forward (tile k + 1, VALU-heavy): layer 1, layer 2, output layer,
+  // loss, backward through the output layer; H1^T and dZ2^T go to the slot's LDS tiles (and dZ2 also in
+  // registers to the next step).  Backward (tile k, MFMA-heavy): dH1^T = W2^T dZ2^T, dW2 += dZ2^T H1,
+  // [dW1 | db1] += dZ1^T [x | 1] with the rows as the MFMA reduction axis (row 4 g + s of k-step s).
+  // Branch-free (invalid rows carry zero gradients).
+  auto l1_mfma = [&](const LbIn& in, f4 (&z1)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) z1[m] = mfma4(w1a[m], in.xb, f4{0.f, 0.f, 0.f, 0.f});
+  };
+  auto act_rows = [&](const f4& z, const float* bias, int m, f4& h) {  // h = act(z + b[16 m + 4 g + i])
+    const f4 bb = *reinterpret_cast<const f4*>(&bias[16 * m + 4 * g]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = lb_act<RELU>(z[i] + bb[i]);
+  };
+  auto put_t = [&](float(*t)[LB_TS], const f4& v, int m) {  // T-layout registers -> [c][row] tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[16 * m + 4 * g + i][j] = v[i];
+  };
+  auto dh1_blk = [&](const f4 (&dz2)[4], int blk, const f4 (&wv)[4], f4 (&dh1)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) dh1[m] = mfma4(wv[m][i], dz2[blk][i], dh1[m]);
+  };
+  auto l2_blk = [&](const f4 (&h1)[4], int blk, const f4 (&wv)[4], f4 (&z2)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) z2[m] = mfma4(wv[m][i], h1[blk][i], z2[m]);
+  };
+  auto dw2_s = [&](const f4 (&ar)[4], const f4 (&br)[4], int s) {
+#pragma unroll
+    for (int mc = 0; mc < 4; ++mc)
+#pragma unroll
+      for (int mk = 0; mk < 4; ++mk) acc2[mc][mk] = mfma4(ar[mc][s], br[mk][s], acc2[mc][mk]);
+  };
+  auto out_layer = [&](const f4 (&h2)[4], float (&zo)[OUT]) {
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      float p[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {  // four independent chains, summed in a fixed order
+        const f4 wv = *reinterpret_cast<const f4*>(&S.w3[o][16 * m + 4 * g]);
+        p[m] = h2[m][0] * wv[0];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) p[m] = fmaf(h2[m][i], wv[i], p[m]);
+      }
+      zo[o] = lb_sum_groups((p[0] + p[1]) + (p[2] + p[3])) + S.b3[o];
+    }
+  };
+  // loss per row (ppo.py:326-371; the min/max tie rules of loss.hip): gradient w.r.t. the outputs
+  auto loss = [&](const LbIn& in, const float (&zo)[OUT], float& d0, float& d1) {
+    const bool valid = in.valid;
+    const bool count = valid && g == 0;
+    d1 = 0.f;
+    if (ACTOR) {
+      const float z0 = zo[0], z1 = zo[OUT - 1];
+      const float mx = fmaxf(z0, z1);
+      const float lse = mx + lb_log(lb_exp(z0 - mx) + lb_exp(z1 - mx));
+      const float n0 = z0 - lse, n1 = z1 - lse;
+      const float p0 = lb_exp(n0), p1 = lb_exp(n1);
+      const float H = -(fmaxf(n0, F32_MIN) * p0) - fmaxf(n1, F32_MIN) * p1;
+      const bool a1 = in.act == 1;
+      const float logp = a1 ? n1 : n0;
+      const float A = (in.u1 - amean) / aden;
+      const float logratio = logp - in.u0;
+      const float ratio = lb_exp(logratio);
+      const float lo = 1.f - clip_range, hi = 1.f + clip_range;
+      const float cr = fminf(fmaxf(ratio, lo), hi);
+      const float s1 = ratio * A, s2 = cr * A;
+      const float gpi = -inv_n;
+      const float g1 = s1 < s2 ? gpi : (s1 > s2 ? 0.f : gpi * 0.5f);
+      const float g2 = s1 < s2 ? 0.f : (s1 > s2 ? gpi : gpi * 0.5f);
+      const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+      const float dlogp = (g1 * A + (g2 * A) * in_clip) * ratio;
+      const float dent = -ent_coef * inv_n;
+      d0 = dlogp * ((a1 ? 0.f : 1.f) - p0) + dent * (-p0 * (n0 + H));
+      d1 = dlogp * ((a1 ? 1.f : 0.f) - p1) + dent * (-p1 * (n1 + H));
+      d0 = valid ? d0 : 0.f;
+      d1 = valid ? d1 : 0.f;
+      st0 += count ? fminf(s1, s2) : 0.f;
+      st1 += count ? (ratio - 1.f) - logratio : 0.f;
+      st2 += (count && fabsf(ratio - 1.f) > clip_range) ? 1.f : 0.f;
+      st3 += count ? H : 0.f;
+    } else {
+      const float v = zo[0], R = in.u1, vo = in.u0;
+      const float gl = (vf_coef0 * halve) * inv_n;
+      auto vloss = [&](float x) -> float {
+        const float z = fabsf(x);
+        return huber ? (z < 1.f ? 0.5f * z * z : (z - 0.5f)) : x * x;
+      };
+      auto vgrad = [&](float x) -> float {
+        return huber ? (x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x)) : 2.f * x;
+      };
+      const float e = v - R;
+      const float l1 = vloss(e);
+      const float dvo = v - vo;
+      const float vcl = vo + fminf(fmaxf(dvo, -clip_range_vf), clip_range_vf);
+      const float l2 = vloss(vcl - R);
+      const float w1 = l1 > l2 ? gl : (l1 < l2 ? 0.f : gl * 0.5f);
+      const float w2 = l1 > l2 ? 0.f : (l1 < l2 ? gl : gl * 0.5f);
+      const float inside = (dvo >= -clip_range_vf && dvo <= clip_range_vf) ? 1.f : 0.f;
+      const float dv_c = w1 * vgrad(e) + (w2 * vgrad(vcl - R)) * inside;
+      const float dv = has_vclip ? dv_c : gl * vgrad(e);
+      d0 = valid ? dv : 0.f;
+      st0 += count ? (has_vclip ? fmaxf(l1, l2) : l1) : 0.f;
+      st1 += (count && has_vclip && fabsf(v - vo) > clip_range_vf) ? 1.f : 0.f;
+    }
+  };
+  // backward through the output layer for hidden block m: dZ2 = (W3^T d) * act'(H2); dW3, db2 partials
+  auto out_bwd = [&](const f4& h2m, int m, float d0, float d1, f4& dz) {
+    const f4 wa = *reinterpret_cast<const f4*>(&S.w3[0][16 * m + 4 * g]);
+    const f4 wb = *reinterpret_cast<const f4*>(&S.w3[1][16 * m + 4 * g]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float h = h2m[i];
+      const float dh = ACTOR ? fmaf(d1, wb[i], d0 * wa[i]) : d0 * wa[i];
+      aw3[0][4 * m + i] = fmaf(d0, h, aw3[0][4 * m + i]);
+      if (ACTOR) aw3[OUT - 1][4 * m + i] = fmaf(d1, h, aw3[OUT - 1][4 * m + i]);
+      dz[i] = dh * lb_act_d<RELU>(h);
+      ab2[4 * m + i] += dz[i];
+    }
+  };
+  // the forward of one tile without interleaving (the pipeline's prologue)
+  auto forward_alone = [&](const LbIn& in, float(*hs)[LB_TS], float(*tdz)[LB_TS], f4 (&dz2)[4]) {
+    f4 z1[4], h1[4], z2[4], h2[4];
+    l1_mfma(in, z1);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const f4 z = mfma4(w1a[m], in.xb, f4{0.f, 0.f, 0.f, 0.f});
-      const f4 bb = *reinterpret_cast<const f4*>(&S.b1[16 * m + 4 * g]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) h1[m][i] = lb_act<RELU>(z[i] + bb[i]);
+      act_rows(z1[m], S.b1, m, h1[m]);
+      put_t(hs, h1[m], m);
+      z2[m] = f4{0.f, 0.f, 0.f, 0.f};
     }
-    // H1 transposed for dW2's B operand
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) th[16 * m + 4 * g + i][j] = h1[m][i];
-
-    // ---- layer 2: Z2^T = W2 H1^T (B operand = the lane's own H1 registers) ---------------------
-    f4 z2[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) z2[m] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int blk = 0; blk < 4; ++blk) {
       f4 wv[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) wv[m] = *reinterpret_cast<const f4*>(&S.w2f[m][blk][lane][0]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) z2[m] = mfma4(wv[m][i], h1[blk][i], z2[m]);
+      lb_w2(S.w2f, blk, wv);
+      l2_blk(h1, blk, wv, z2);
     }
-    f4 h2[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) act_rows(z2[m], S.b2, m, h2[m]);
+    float zo[OUT], d0, d1;
+    out_layer(h2, zo);
+    loss(in, zo, d0, d1);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const f4 bb = *reinterpret_cast<const f4*>(&S.b2[16 * m + 4 * g]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) h2[m][i] = lb_act<RELU>(z2[m][i] + bb[i]);
-    }
-
-    // ---- output layer: lane partials over its 16 hidden units, summed over the lane groups -------
-    float zo[OUT];
-#pragma unroll
-    for (int o = 0; o < OUT; ++o) {
-      float p = 0.f;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const f4 wv = *reinterpret_cast<const f4*>(&S.w3[o][16 * m + 4 * g]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) p = fmaf(h2[m][i], wv[i], p);
-      }
-      zo[o] = lb_sum_groups(p) + S.b3[o];
-    }
-
-    // ---- loss per row (ppo.py:326-371; the tie rules of mlp_ppo.hip / loss.hip) -----------------
-    float d0 = 0.f, d1 = 0.f;
-    if (valid) {
-      if (ACTOR) {
-        const float z0 = zo[0], z1 = zo[OUT - 1];
-        const float mx = fmaxf(z0, z1);
-        const float se = expf(z0 - mx) + expf(z1 - mx);
-        const float lse = mx + logf(se);
-        const float n0 = z0 - lse, n1 = z1 - lse;
-        const float p0 = expf(n0), p1 = expf(n1);
-        float H = 0.f;
-        H -= fmaxf(n0, F32_MIN) * p0;
-        H -= fmaxf(n1, F32_MIN) * p1;
-        const int act = in.act == 1 ? 1 : 0;
-        const float logp = (act ? z1 : z0) - lse;
-        const float A = (in.u1 - amean) / aden;
-        const float logratio = logp - in.u0;
-        const float ratio = expf(logratio);
-        const float lo = 1.f - clip_range, hi = 1.f + clip_range;
-        const float cr = fminf(fmaxf(ratio, lo), hi);
-        const float s1 = ratio * A, s2 = cr * A;
-        const float gpi = -inv_n;
-        float g1, g2;
-        if (s1 < s2) { g1 = gpi; g2 = 0.f; }
-        else if (s1 > s2) { g1 = 0.f; g2 = gpi; }
-        else { g1 = gpi * 0.5f; g2 = gpi * 0.5f; }
-        const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-        const float dlogp = (g1 * A + (g2 * A) * in_clip) * ratio;
-        const float dent = -ent_coef * inv_n;
-        d0 = dlogp * ((act == 0 ? 1.f : 0.f) - p0) + dent * (-p0 * (n0 + H));
-        d1 = dlogp * ((act == 1 ? 1.f : 0.f) - p1) + dent * (-p1 * (n1 + H));
-        if (g == 0) {
-          st0 += (double)fminf(s1, s2);
-          st1 += (double)((ratio - 1.f) - logratio);
-          st2 += (fabsf(ratio - 1.f) > clip_range) ? 1.0 : 0.0;
-          st3 += (double)H;
-        }
-      } else {
-        const float v = zo[0], R = in.u1, vo = in.u0;
-        const float gl = (vf_coef0 * halve) * inv_n;
-        float l = v - R;
-        float dv;
-        auto vloss = [&](float x) -> float {
-          if (vf_fn == 0) return x * x;
-          const float z = fabsf(x);
-          return z < 1.f ? 0.5f * z * z : (z - 0.5f);
-        };
-        auto vgrad = [&](float x) -> float {
-          if (vf_fn == 0) return 2.f * x;
-          return x <= -1.f ? -1.f : (x >= 1.f ? 1.f : x);
-        };
-        float lv = vloss(l);
-        float vcl_cnt = 0.f;
-        if (has_vclip) {
-          const float dvo = v - vo;
-          const float vcl = vo + fminf(fmaxf(dvo, -clip_range_vf), clip_range_vf);
-          const float l2 = vloss(vcl - R);
-          float w1, w2;
-          if (lv > l2) { w1 = gl; w2 = 0.f; }
-          else if (lv < l2) { w1 = 0.f; w2 = gl; }
-          else { w1 = gl * 0.5f; w2 = gl * 0.5f; }
-          const float inside = (dvo >= -clip_range_vf && dvo <= clip_range_vf) ? 1.f : 0.f;
-          dv = w1 * vgrad(l) + (w2 * vgrad(vcl - R)) * inside;
-          vcl_cnt = (fabsf(v - vo) > clip_range_vf) ? 1.f : 0.f;
-          lv = fmaxf(lv, l2);
-        } else {
-          dv = gl * vgrad(l);
-        }
-        d0 = dv;
-        if (g == 0) {
-          st0 += (double)lv;
-          st1 += (double)vcl_cnt;
-        }
-      }
-    }
-
-    // ---- backward through the output layer: dZ2 = (W3^T d) * act'(H2); dW3, db2, db3 partials ----
-    f4 dz2[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const f4 wa = *reinterpret_cast<const f4*>(&S.w3[0][16 * m + 4 * g]);
-      const f4 wb = *reinterpret_cast<const f4*>(&S.w3[1][16 * m + 4 * g]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float h = h2[m][i];
-        const float dh = ACTOR ? fmaf(d1, wb[i], d0 * wa[i]) : d0 * wa[i];
-        aw3[0][4 * m + i] = fmaf(d0, h, aw3[0][4 * m + i]);
-        if (ACTOR) aw3[OUT - 1][4 * m + i] = fmaf(d1, h, aw3[OUT - 1][4 * m + i]);
-        const float dz = dh * lb_act_d<RELU>(h);
-        dz2[m][i] = dz;
-        ab2[4 * m + i] += dz;
-      }
+      out_bwd(h2[m], m, d0, d1, dz2[m]);
+      put_t(tdz, dz2[m], m);
     }
     ab3[0] += d0;
     if (ACTOR) ab3[OUT - 1] += d1;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) tdz[16 * m + 4 * g + i][j] = dz2[m][i];
+  };
 
-    // ---- dH1^T = W2^T dZ2^T (B operand = the lane's own dZ2 registers); dZ1 = dH1 * act'(H1) ------
-    f4 dh1[4];
+  // One pipeline step: tile k's backward (slot B) beside tile k + 1's forward (slot F), hand-scheduled
+  // as short regions (sched_barrier fences) that each pair one MFMA block with an independent VALU chunk;
+  // the compiler interleaves inside a region.  dZ2 of tile k arrives in registers; dZ2 of tile k + 1
+  // leaves in the same registers.
+  auto step = [&](const LbIn& inF, float(*tdzF)[LB_TS], float(*hsF)[LB_TS], int tB, float(*tdzB)[LB_TS],
+                  float(*hsB)[LB_TS], f4 (&dz2)[4]) {
+    float xw[4];
+    lb_load_xw(a, tB, g, j, xw);
+    f4 z1[4], h1[4], dh1[4], z2[4], h2[4], ar[4], br[4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) dh1[m] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int blk = 0; blk < 4; ++blk) {
-      f4 wv[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) wv[m] = *reinterpret_cast<const f4*>(&S.w2b[m][blk][lane][0]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) dh1[m] = mfma4(wv[m][i], dz2[blk][i], dh1[m]);
+    for (int m = 0; m < 4; ++m) {
+      dh1[m] = f4{0.f, 0.f, 0.f, 0.f};
+      z2[m] = f4{0.f, 0.f, 0.f, 0.f};
     }
-
-    // ---- dW2 += dZ2^T H1 over the tile's rows (row 4 g + s of k-step s in both operands) ---------
-    {
-      f4 ar[4], br[4];
+    f4 wa[4], wb[4];
+    lb_w2(S.w2b, 0, wa);
+    l1_mfma(inF, z1);
+    LB_FENCE();
+    dh1_blk(dz2, 0, wa, dh1);  // P1
+    lb_w2(S.w2b, 1, wb);
+    act_rows(z1[0], S.b1, 0, h1[0]);
+    act_rows(z1[1], S.b1, 1, h1[1]);
+    LB_FENCE();
+    dh1_blk(dz2, 1, wb, dh1);  // P2
+    lb_w2(S.w2b, 2, wa);
+    act_rows(z1[2], S.b1, 2, h1[2]);
+    act_rows(z1[3], S.b1, 3, h1[3]);
+    LB_FENCE();
+    dh1_blk(dz2, 2, wa, dh1);  // P3
+    lb_w2(S.w2b, 3, wb);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        ar[m] = *reinterpret_cast<const f4*>(&tdz[16 * m + j][4 * g]);
-        br[m] = *reinterpret_cast<const f4*>(&th[16 * m + j][4 * g]);
-      }
+    for (int m = 0; m < 4; ++m) put_t(hsF, h1[m], m);
+    LB_FENCE();
+    dh1_blk(dz2, 3, wb, dh1);  // P4
+    lb_w2(S.w2f, 0, wa);
+    LB_FENCE();
+    l2_blk(h1, 0, wa, z2);  // P5: layer 2 beside the dH1 transpose and the dW2 / dW1 operand reads
+    lb_w2(S.w2f, 1, wb);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+    for (int m = 0; m < 4; ++m) put_t(tdzF, dh1[m], m);  // dH1 through the forward slot's dZ2 tile
+    LB_FENCE();
+    l2_blk(h1, 1, wb, z2);
+    lb_w2(S.w2f, 2, wa);
 #pragma unroll
-        for (int mc = 0; mc < 4; ++mc)
-#pragma unroll
-          for (int mk = 0; mk < 4; ++mk) acc2[mc][mk] = mfma4(ar[mc][s], br[mk][s], acc2[mc][mk]);
+    for (int m = 0; m < 4; ++m) {
+      ar[m] = *reinterpret_cast<const f4*>(&tdzB[16 * m + j][4 * g]);
+      br[m] = *reinterpret_cast<const f4*>(&hsB[16 * m + j][4 * g]);
     }
+    LB_FENCE();
+    l2_blk(h1, 2, wa, z2);
+    lb_w2(S.w2f, 3, wb);
+    f4 az[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f4 d = *reinterpret_cast<const f4*>(&tdzF[16 * m + j][4 * g]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) az[m][s] = d[s] * lb_act_d<RELU>(br[m][s]);
+    }
+    LB_FENCE();
+    l2_blk(h1, 3, wb, z2);
+    LB_FENCE();
+    dw2_s(ar, br, 0);  // P6
+    act_rows(z2[0], S.b2, 0, h2[0]);
+    act_rows(z2[1], S.b2, 1, h2[1]);
+    LB_FENCE();
+    dw2_s(ar, br, 1);  // P7
+    act_rows(z2[2], S.b2, 2, h2[2]);
+    act_rows(z2[3], S.b2, 3, h2[3]);
+    LB_FENCE();
+    float zo[OUT], d0, d1;
+    dw2_s(ar, br, 2);  // P8
+    out_layer(h2, zo);
+    LB_FENCE();
+    dw2_s(ar, br, 3);  // P9
+    loss(inF, zo, d0, d1);
+    LB_FENCE();
+#pragma unroll
+    for (int s = 0; s < 4; ++s)  // P10: [dW1 | db1] beside the output layer's backward
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc1[m] = mfma4(az[m][s], xw[s], acc1[m]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      out_bwd(h2[m], m, d0, d1, dz2[m]);
+      put_t(tdzF, dz2[m], m);
+    }
+    ab3[0] += d0;
+    if (ACTOR) ab3[OUT - 1] += d1;
+    LB_FENCE();
+  };
 
-    // ---- [dW1 | db1] += dZ1^T [x | 1] (dZ1 transposed over H1's tile, read after it in order) -----
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) th[16 * m + 4 * g + i][j] = dh1[m][i] * lb_act_d<RELU>(h1[m][i]);
-    {
-      f4 az[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) az[m] = *reinterpret_cast<const f4*>(&th[16 * m + j][4 * g]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) acc1[m] = mfma4(az[m][s], in.xw[s], acc1[m]);
+  // ---- two-stage software pipeline over the wave's tiles; tiles past the end are all-invalid (zero
+  // gradients, never back-propagated).  Slots alternate; the loop body is unrolled over both.
+  const int n_tiles = (a.rows + 15) >> 4;
+  const int wave_id = wgn * LB_NW + w;
+  const int n_my = wave_id < n_tiles ? (n_tiles - 1 - wave_id) / LB_WAVES_PER_NET + 1 : 0;
+  float(*tdz0)[LB_TS] = S.tdz0[w];
+  float(*tdz1)[LB_TS] = S.tdz1[w];
+  float(*hs0)[LB_TS] = S.hs0[w];
+  float(*hs1)[LB_TS] = S.hs1[w];
+  if (n_my > 0) {
+    LbIn in, nx;
+    lb_load<ACTOR>(a, wave_id, g, j, in);
+    lb_load<ACTOR>(a, wave_id + LB_WAVES_PER_NET, g, j, nx);
+    f4 dz2[4];  // the forward stage's dZ2 tile, handed to the next step's dH1
+    forward_alone(in, hs0, tdz0, dz2);  // prologue: tile 0's forward
+    for (int k = 0; k < n_my; k += 2) {
+      const int t = wave_id + k * LB_WAVES_PER_NET;
+      in = nx;
+      lb_load<ACTOR>(a, t + 2 * LB_WAVES_PER_NET, g, j, nx);
+      step(in, tdz1, hs1, t, tdz0, hs0, dz2);  // forward tile k + 1 (all-invalid past the end), backward k
+      if (k + 1 >= n_my) break;
+      in = nx;
+      lb_load<ACTOR>(a, t + 3 * LB_WAVES_PER_NET, g, j, nx);
+      step(in, tdz0, hs0, t + LB_WAVES_PER_NET, tdz1, hs1, dz2);  // forward k + 2, backward k + 1
     }
   }
 
+  LB_STAMP(3);
   // ---- per-wave sums over the 16 row lanes, then the workgroup's partial in wave order -----------
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -437,7 +574,7 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
 #pragma unroll
   for (int o = 0; o < OUT; ++o) ab3[o] = lb_row_sum16(ab3[o]);
   {
-    double s[4] = {st0, st1, st2, st3};
+    double s[4] = {(double)st0, (double)st1, (double)st2, (double)st3};
 #pragma unroll
     for (int q = 0; q < 4; ++q) s[q] = wave_sum(s[q]);
     if (lane == 0) {
@@ -445,52 +582,61 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
       for (int q = 0; q < 4; ++q) S.st[w][q] = s[q];
     }
   }
-  float* accv = &S.tt[0][0][0][0];
-  __syncthreads();  // every wave is past its last tile: the transpose tiles become the accumulator
-  for (int r = 0; r < LB_NW; ++r) {
-    if (w == r) {
-      const bool first = r == 0;
-      auto put = [&](int idx, float v) { accv[idx] = first ? v : accv[idx] + v; };
+  // each wave stores its partial into a region of its own (plain stores: no read-modify-write chain),
+  // then every thread sums the regions in wave order
+  float* accv = &S.hs0[0][0][0];
+  static_assert(sizeof(float) * LB_NW * LB_PSTRIDE <= sizeof(float) * 4 * LB_NW * HID * LB_TS, "regions fit");
+  LB_STAMP(4);
+  __syncthreads();  // every wave is past its last tile: the transpose tiles become the partial regions
+  {
+    float* mine = accv + w * LB_PSTRIDE;
 #pragma unroll
-      for (int mc = 0; mc < 4; ++mc)
+    for (int mc = 0; mc < 4; ++mc)
 #pragma unroll
-        for (int mk = 0; mk < 4; ++mk)
+      for (int mk = 0; mk < 4; ++mk)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) put(oW2 + (16 * mc + 4 * g + i) * HID + 16 * mk + j, acc2[mc][mk][i]);
+        for (int i = 0; i < 4; ++i) mine[oW2 + (16 * mc + 4 * g + i) * HID + 16 * mk + j] = acc2[mc][mk][i];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 16 * m + 4 * g + i;
+        if (j < IN) mine[oW1 + c * IN + j] = acc1[m][i];
+        else if (j == 4) mine[ob1 + c] = acc1[m][i];
+      }
+    if (j == 0) {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = 16 * m + 4 * g + i;
-          if (j < IN) put(oW1 + c * IN + j, acc1[m][i]);
-          else if (j == 4) put(ob1 + c, acc1[m][i]);
+          mine[ob2 + c] = ab2[4 * m + i];
+#pragma unroll
+          for (int o = 0; o < OUT; ++o) mine[oW3 + o * HID + c] = aw3[o][4 * m + i];
         }
-      if (j == 0) {
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int c = 16 * m + 4 * g + i;
-            put(ob2 + c, ab2[4 * m + i]);
-#pragma unroll
-            for (int o = 0; o < OUT; ++o) put(oW3 + o * HID + c, aw3[o][4 * m + i]);
-          }
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int o = 0; o < OUT; ++o) put(ob3 + o, ab3[o]);
-      }
     }
-    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) mine[ob3 + o] = ab3[o];
+    }
   }
+  __syncthreads();
+  LB_STAMP(5);
   const int slot = (ACTOR ? 0 : LB_WG_PER_NET) + wgn;
   float* dst = a.part + (int64_t)slot * LB_PSTRIDE;
-  for (int e = tid; e < P_net; e += LB_NT) dst[e] = accv[e];
+  for (int e = tid; e < P_net; e += LB_NT) {
+    float v = accv[e];
+#pragma unroll
+    for (int r = 1; r < LB_NW; ++r) v += accv[r * LB_PSTRIDE + e];
+    dst[e] = v;
+  }
   if (tid < 4) {
     double s = 0.0;
     for (int r = 0; r < LB_NW; ++r) s += S.st[r][tid];
     a.statp[slot * 4 + tid] = s;
   }
+  LB_STAMP(6);
+  LB_RSTAMP(9);
 }
 
 template <int RELU>
@@ -774,6 +920,12 @@ int rai_internal::mlp_large(float* params, float* exp_avg, float* exp_avg_sq, co
   }
   return RAI_OK;
 }
+
+#ifdef RAI_STAMPS
+extern "C" int rai_mlp_large_debug_stamps(unsigned long long* host_out) {  // LB_GRID x LB_NW x 10
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_lb_stamps), sizeof(g_lb_stamps));
+}
+#endif
 
 extern "C" int rai_mlp_large_timing(int32_t capacity) {
   LbTiming& t = lb_timing();

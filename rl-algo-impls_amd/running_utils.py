@@ -60,7 +60,11 @@ def set_gemm_tuning(device: torch.device, enabled: bool) -> bool:
     RAI_TUNABLEOP_FILE or ~/.cache/rl_algo_impls_amd/tunableop_results<device>.csv, which later runs
     of the same user READ instead of re-tuning: delete it to re-tune (e.g. after a driver or library
     update).  Returns whether tuning is on."""
-    on = bool(enabled) and torch.device(device).type == "cuda" and os.environ.get("RAI_TUNABLEOP", "1") != "0"
+    if torch.device(device).type != "cuda":
+        # a CPU run (the reference's CPU path) never touches the HIP runtime: torch.cuda.tunable raises
+        # hipErrorNoDevice on a host without a GPU and would initialise HIP on one that has it
+        return False
+    on = bool(enabled) and os.environ.get("RAI_TUNABLEOP", "1") != "0"
     if on:
         path = os.environ.get("RAI_TUNABLEOP_FILE") or os.path.join(
             os.path.expanduser("~"), ".cache", "rl_algo_impls_amd", "tunableop_results%d.csv")

@@ -563,3 +563,34 @@ def test_nature_cnn_encoder_uint8_path_equals_float32_path(monkeypatch):
         assert torch.equal(a, b), name
     monkeypatch.setattr(cnn_ops, "_CONV_U8", False)
     assert enc.obs_transform(obs).kind == _lib.RAI_XFORM_U8_CHW_TO_F32_HWC
+
+
+def test_conv_dgrad_shape_gates_fall_back_instead_of_raising():
+    """A valid convolution shape the MFMA input-gradient kernels are not instantiated for (Ci < 16, Co not a
+    multiple of 16, kernel not a multiple of the stride) returns RAI_E_UNSUPPORTED (not RAI_E_SHAPE), so
+    cnn_ops falls back (MIOpen for dx, the materialised dz for the ReLU fold) instead of raising; an
+    impossible shape stays RAI_E_SHAPE."""
+    from rl_algo_impls_amd import cnn_ops
+
+    L = _lib.lib()
+    st = _lib.stream_handle(DEV)
+    p = torch.zeros(64, device=DEV).data_ptr()
+    assert L.rai_conv2d_dgrad_relu(p, p, p, 2, 20, 20, 8, 64, 4, 4, 2, p, st) == -6  # Ci < 16
+    assert L.rai_conv2d_dgrad_relu(p, p, p, 2, 20, 20, 32, 24, 4, 4, 2, p, st) == -6  # Co % 16
+    assert L.rai_conv2d_dgrad_v(p, p, 2, 20, 20, 32, 24, 4, 4, 2, p, 0, st) == -6
+    assert L.rai_conv2d_dgrad_v(p, p, 2, 20, 20, 16, 64, 4, 4, 2, p, 0, st) == -6  # Ci not 32 / 64
+    assert L.rai_conv2d_dgrad_v(p, p, 2, 3, 3, 32, 64, 4, 4, 2, p, 0, st) == -2  # kernel larger than the input
+    # the Python paths: None (fold skipped) and MIOpen's dx, equal to fp64 autograd within f32 bounds
+    B, Ci, H, Co, k, s = 3, 8, 20, 24, 4, 2
+    x, w, _ = _inputs(B, Ci, H, Co, k, seed=5)
+    OH = (H - k) // s + 1
+    dz = torch.randn(B, Co, OH, OH, generator=torch.Generator().manual_seed(9))
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
+    dzd = dz.to(DEV).contiguous(memory_format=torch.channels_last)
+    y = torch.rand_like(dzd)
+    assert cnn_ops._conv_dgrad_relu(xd, dzd, y, wd, s) is None
+    dx = cnn_ops._conv_dgrad(xd, dzd, wd, s)
+    ref = torch.ops.aten.convolution_backward(dz.double(), x.double(), w.double(), None, [s, s], [0, 0], [1, 1], False,
+                                              [0, 0], 1, [True, False, False])[0]
+    torch.testing.assert_close(dx.cpu().double(), ref, rtol=1e-4, atol=1e-4)

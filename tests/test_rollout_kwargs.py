@@ -132,3 +132,27 @@ def test_generator_from_runner_kwargs_fills_num_actions():
         np.testing.assert_array_equal(mb.num_actions.cpu().numpy(), exp)
         seen += mb.obs.shape[0]
     assert seen == 18
+
+
+@pytest.mark.gpu
+def test_num_actions_kernel_at_max_action_planes():
+    """A = RAI_GRID_MAX_A = 256 mask bytes per cell (the LDS cell tile shrinks to fit 64 KiB) and more
+    cells than one tile holds: bit-exact against the oracle, with and without the value-dependent gate."""
+    import torch
+
+    from rl_algo_impls_amd import _lib
+    from rl_algo_impls_amd.gridnet import ValueDependentMask, gridnet_num_actions
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(7)
+    nvec = np.array([64, 64, 64, 64])
+    assert nvec.sum() == _lib.RAI_GRID_MAX_A
+    B, Cc = 37, 300
+    m = torch.rand((B, Cc, int(nvec.sum())), device=dev, generator=g) < 0.004
+    a = torch.stack([torch.randint(0, int(k), (B, Cc), device=dev, generator=g) for k in nvec], -1)
+    sub = ValueDependentMask.from_reference_index_to_index_to_value({0: {1: 3, 2: 5}})
+    sub_ref, sub_val = np.array([-1, 0, 0, -1]), np.array([0, 3, 5, 0])
+    got = gridnet_num_actions(a, m, nvec, sub).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.num_actions(a.cpu().numpy(), m.cpu().numpy(), nvec, sub_ref, sub_val))
+    got = gridnet_num_actions(None, m, None, None).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.num_actions(None, m.cpu().numpy(), None, None, None))
