@@ -36,7 +36,9 @@
 #include "common.h"
 #include "internal.h"
 
-#pragma clang fp contract(off)
+// FP contraction stays ON here (mul + add -> fma): on gfx950 the f32 MFMAs and the VALU share the SIMD's f32
+// datapath, so every VALU instruction is time taken from the MFMAs, and this kernel is checked against the
+// reference at fp32 tolerance (its summation orders differ from torch's anyway), not bit for bit.
 
 namespace {
 
@@ -60,6 +62,8 @@ struct LbSmem {
   float w1[HID][4];        // W1, inputs zero-padded to 4
   float b1[HID];
   float b2[HID];
+  float b1c[HID];  // b * 2 log2(e) (lb_act_bias)
+  float b2c[HID];
   float w3[2][HID];        // W3 rows (critic: row 1 zero)
   float b3[4];
   double st[LB_NW][4];     // per-wave loss-statistic partials
@@ -90,18 +94,22 @@ struct LbArgs {
   float inv_n;           // 1 / (rows * world)
 };
 
-// tanh without the small-|x| series: 1 - 2 / (exp(2|x|) + 1), sign restored.  Absolute error ~2 ulp of 1
-// everywhere (relative error grows below |x| ~ 1e-3, where tanh(x) ~ x is consumed only through sums of
-// O(1) terms, so the absolute error is what reaches the outputs); 6 instructions, no branch.
+// tanh(z + b) = 1 - 2 / (exp(2 (z + b)) + 1) with the bias folded into the exponent's FMA:
+// exp2(z * 2 log2(e) + b * 2 log2(e)).  Absolute error ~2 ulp of 1 everywhere (no cancellation is
+// compensated: tanh(x) ~ x below |x| ~ 1e-3 is consumed only through sums of O(1) terms, so the absolute
+// error is what reaches the outputs); both tails saturate correctly (exp2 -> inf gives 1, -> 0 gives -1).
+// Five VALU instructions, no branch: on gfx950 the f32 MFMAs and the VALU share the SIMD's f32 datapath
+// (tools/mfma_valu_overlap.hip: VALU beside MFMAs is additive), so VALU instructions are the cost.
+constexpr float LB_2LOG2E = 2.885390081777927f;
 template <int RELU>
-__device__ __forceinline__ float lb_act(float z) {
-  if (RELU) return fmaxf(z, 0.f);
-  const float e = __builtin_amdgcn_exp2f(fabsf(z) * 2.885390081777927f);  // exp(2|z|)
-  return copysignf(fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f), z);
+__device__ __forceinline__ float lb_act_bias(float z, float b, float bc) {  // bc = b * 2 log2(e)
+  if (RELU) return fmaxf(z + b, 0.f);
+  const float e = __builtin_amdgcn_exp2f(fmaf(z, LB_2LOG2E, bc));
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
 template <int RELU>
 __device__ __forceinline__ float lb_act_d(float h) {  // derivative from the activation's output
-  return RELU ? (h > 0.f ? 1.f : 0.f) : 1.f - h * h;
+  return RELU ? (h > 0.f ? 1.f : 0.f) : fmaf(-h, h, 1.f);
 }
 __device__ __forceinline__ float lb_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ float lb_log(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
@@ -129,7 +137,7 @@ __device__ __forceinline__ float lb_row_sum16(float v) {
 #ifdef RAI_STAMPS
 // Diagnostic build only (never the shipped library): shader-clock stamps of every wave at the kernel's
 // phase boundaries (last launch), plus the constant-rate clock at start / end; rai_mlp_large_debug_stamps
-__device__ unsigned long long g_lb_stamps[LB_GRID][LB_NW][16];
+__device__ unsigned long long g_lb_stamps[LB_GRID][LB_NW][32];
 #define LB_STAMP(k)                                                                               \
   do {                                                                                            \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
@@ -141,6 +149,11 @@ __device__ unsigned long long g_lb_stamps[LB_GRID][LB_NW][16];
     if ((threadIdx.x & 63) == 0) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] += t_ - (t0);       \
     t0 = t_;                                                                                      \
   } while (0)
+#define LB_PH()                                                                                   \
+  do {                                                                                            \
+    LB_ACC(ph, tr);                                                                               \
+    ++ph;                                                                                         \
+  } while (0)
 #define LB_RSTAMP(k)                                                                              \
   do {                                                                                            \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                               \
@@ -150,6 +163,7 @@ __device__ unsigned long long g_lb_stamps[LB_GRID][LB_NW][16];
 #define LB_STAMP(k) do { } while (0)
 #define LB_RSTAMP(k) do { } while (0)
 #define LB_ACC(k, t0) do { } while (0)
+#define LB_PH() do { } while (0)
 #endif
 
 // Interleave an MFMA-heavy phase with a VALU-heavy one inside a scheduling region: N groups of one MFMA
@@ -230,7 +244,7 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
   LB_STAMP(0);
 #ifdef RAI_STAMPS
   if ((threadIdx.x & 63) == 0)
-    for (int k = 10; k < 16; ++k) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] = 0;
+    for (int k = 10; k < 32; ++k) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] = 0;
 #endif
   // ---- stage the weights in LDS (operand permutations for the MFMA chains) -------------------
   for (int e = tid; e < 4 * 4 * 64 * 4; e += LB_NT) {
@@ -244,8 +258,11 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
     S.w1[c][f] = f < IN ? a.params[base + oW1 + c * IN + f] : 0.f;
   }
   if (tid < HID) {
-    S.b1[tid] = a.params[base + ob1 + tid];
-    S.b2[tid] = a.params[base + ob2 + tid];
+    const float x1 = a.params[base + ob1 + tid], x2 = a.params[base + ob2 + tid];
+    S.b1[tid] = x1;
+    S.b2[tid] = x2;
+    S.b1c[tid] = x1 * LB_2LOG2E;
+    S.b2c[tid] = x2 * LB_2LOG2E;
   }
   if (tid < 2 * HID) {
     const int o = tid >> 6, c = tid & 63;
@@ -265,6 +282,8 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
 
   // constant per-lane operands: layer-1 A = W1[16 m + j][g].  The W2 permutations (layer 2 / dH1 A
   // operands) stay in LDS; each pipeline phase reads the next phase's block (lb_w2).
+  // W3 stays in LDS too: a register copy (32 VGPRs for the actor) pushed the critic path into
+  // VGPR<->AGPR shuffles and measured 2% slower.
   float w1a[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) w1a[m] = S.w1[16 * m + j][g];
@@ -302,10 +321,12 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) z1[m] = mfma4(w1a[m], in.xb, f4{0.f, 0.f, 0.f, 0.f});
   };
-  auto act_rows = [&](const f4& z, const float* bias, int m, f4& h) {  // h = act(z + b[16 m + 4 g + i])
+  // h = act(z + b[16 m + 4 g + i]); bc: the same bias times 2 log2(e)
+  auto act_rows = [&](const f4& z, const float* bias, const float* bc, int m, f4& h) {
     const f4 bb = *reinterpret_cast<const f4*>(&bias[16 * m + 4 * g]);
+    const f4 cc = *reinterpret_cast<const f4*>(&bc[16 * m + 4 * g]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) h[i] = lb_act<RELU>(z[i] + bb[i]);
+    for (int i = 0; i < 4; ++i) h[i] = lb_act_bias<RELU>(z[i], bb[i], cc[i]);
   };
   auto put_t = [&](float(*t)[LB_TS], const f4& v, int m) {  // T-layout registers -> [c][row] tile
 #pragma unroll
@@ -405,7 +426,7 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
   // backward through the output layer for hidden block m: dZ2 = (W3^T d) * act'(H2); dW3, db2 partials
   auto out_bwd = [&](const f4& h2m, int m, float d0, float d1, f4& dz) {
     const f4 wa = *reinterpret_cast<const f4*>(&S.w3[0][16 * m + 4 * g]);
-    const f4 wb = *reinterpret_cast<const f4*>(&S.w3[1][16 * m + 4 * g]);
+    const f4 wb = *reinterpret_cast<const f4*>(&S.w3[OUT - 1][16 * m + 4 * g]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float h = h2m[i];
@@ -422,7 +443,7 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
     l1_mfma(in, z1);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      act_rows(z1[m], S.b1, m, h1[m]);
+      act_rows(z1[m], S.b1, S.b1c, m, h1[m]);
       put_t(hs, h1[m], m);
       z2[m] = f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -433,7 +454,7 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
       l2_blk(h1, blk, wv, z2);
     }
 #pragma unroll
-    for (int m = 0; m < 4; ++m) act_rows(z2[m], S.b2, m, h2[m]);
+    for (int m = 0; m < 4; ++m) act_rows(z2[m], S.b2, S.b2c, m, h2[m]);
     float zo[OUT], d0, d1;
     out_layer(h2, zo);
     loss(in, zo, d0, d1);
@@ -452,6 +473,10 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
   // leaves in the same registers.
   auto step = [&](const LbIn& inF, float(*tdzF)[LB_TS], float(*hsF)[LB_TS], int tB, float(*tdzB)[LB_TS],
                   float(*hsB)[LB_TS], f4 (&dz2)[4]) {
+#ifdef RAI_STAMPS
+    unsigned long long tr = __builtin_amdgcn_s_memtime();
+    int ph = 10;
+#endif
     float xw[4];
     lb_load_xw(a, tB, g, j, xw);
     f4 z1[4], h1[4], dh1[4], z2[4], h2[4], ar[4], br[4];
@@ -464,29 +489,35 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
     lb_w2(S.w2b, 0, wa);
     l1_mfma(inF, z1);
     LB_FENCE();
+    LB_PH();
     dh1_blk(dz2, 0, wa, dh1);  // P1
     lb_w2(S.w2b, 1, wb);
-    act_rows(z1[0], S.b1, 0, h1[0]);
-    act_rows(z1[1], S.b1, 1, h1[1]);
+    act_rows(z1[0], S.b1, S.b1c, 0, h1[0]);
+    act_rows(z1[1], S.b1, S.b1c, 1, h1[1]);
     LB_FENCE();
+    LB_PH();
     dh1_blk(dz2, 1, wb, dh1);  // P2
     lb_w2(S.w2b, 2, wa);
-    act_rows(z1[2], S.b1, 2, h1[2]);
-    act_rows(z1[3], S.b1, 3, h1[3]);
+    act_rows(z1[2], S.b1, S.b1c, 2, h1[2]);
+    act_rows(z1[3], S.b1, S.b1c, 3, h1[3]);
     LB_FENCE();
+    LB_PH();
     dh1_blk(dz2, 2, wa, dh1);  // P3
     lb_w2(S.w2b, 3, wb);
 #pragma unroll
     for (int m = 0; m < 4; ++m) put_t(hsF, h1[m], m);
     LB_FENCE();
+    LB_PH();
     dh1_blk(dz2, 3, wb, dh1);  // P4
     lb_w2(S.w2f, 0, wa);
     LB_FENCE();
+    LB_PH();
     l2_blk(h1, 0, wa, z2);  // P5: layer 2 beside the dH1 transpose and the dW2 / dW1 operand reads
     lb_w2(S.w2f, 1, wb);
 #pragma unroll
     for (int m = 0; m < 4; ++m) put_t(tdzF, dh1[m], m);  // dH1 through the forward slot's dZ2 tile
     LB_FENCE();
+    LB_PH();
     l2_blk(h1, 1, wb, z2);
     lb_w2(S.w2f, 2, wa);
 #pragma unroll
@@ -495,6 +526,7 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
       br[m] = *reinterpret_cast<const f4*>(&hsB[16 * m + j][4 * g]);
     }
     LB_FENCE();
+    LB_PH();
     l2_blk(h1, 2, wa, z2);
     lb_w2(S.w2f, 3, wb);
     f4 az[4];
@@ -505,23 +537,29 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
       for (int s = 0; s < 4; ++s) az[m][s] = d[s] * lb_act_d<RELU>(br[m][s]);
     }
     LB_FENCE();
+    LB_PH();
     l2_blk(h1, 3, wb, z2);
     LB_FENCE();
+    LB_PH();
     dw2_s(ar, br, 0);  // P6
-    act_rows(z2[0], S.b2, 0, h2[0]);
-    act_rows(z2[1], S.b2, 1, h2[1]);
+    act_rows(z2[0], S.b2, S.b2c, 0, h2[0]);
+    act_rows(z2[1], S.b2, S.b2c, 1, h2[1]);
     LB_FENCE();
+    LB_PH();
     dw2_s(ar, br, 1);  // P7
-    act_rows(z2[2], S.b2, 2, h2[2]);
-    act_rows(z2[3], S.b2, 3, h2[3]);
+    act_rows(z2[2], S.b2, S.b2c, 2, h2[2]);
+    act_rows(z2[3], S.b2, S.b2c, 3, h2[3]);
     LB_FENCE();
+    LB_PH();
     float zo[OUT], d0, d1;
     dw2_s(ar, br, 2);  // P8
     out_layer(h2, zo);
     LB_FENCE();
+    LB_PH();
     dw2_s(ar, br, 3);  // P9
     loss(inF, zo, d0, d1);
     LB_FENCE();
+    LB_PH();
 #pragma unroll
     for (int s = 0; s < 4; ++s)  // P10: [dW1 | db1] beside the output layer's backward
 #pragma unroll
@@ -534,6 +572,7 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
     ab3[0] += d0;
     if (ACTOR) ab3[OUT - 1] += d1;
     LB_FENCE();
+    LB_PH();
   };
 
   // ---- two-stage software pipeline over the wave's tiles; tiles past the end are all-invalid (zero
@@ -551,19 +590,15 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
     lb_load<ACTOR>(a, wave_id + LB_WAVES_PER_NET, g, j, nx);
     f4 dz2[4];  // the forward stage's dZ2 tile, handed to the next step's dH1
     forward_alone(in, hs0, tdz0, dz2);  // prologue: tile 0's forward
-    for (int k = 0; k < n_my; k += 2) {
+    for (int k = 0; k < n_my; ++k) {
       const int t = wave_id + k * LB_WAVES_PER_NET;
+      const bool odd = (k & 1) != 0;  // tile k's slot (backward) is k & 1, tile k + 1's (forward) the other
       in = nx;
       lb_load<ACTOR>(a, t + 2 * LB_WAVES_PER_NET, g, j, nx);
-      step(in, tdz1, hs1, t, tdz0, hs0, dz2);  // forward tile k + 1 (all-invalid past the end), backward k
-      if (k + 1 >= n_my) break;
-      in = nx;
-      lb_load<ACTOR>(a, t + 3 * LB_WAVES_PER_NET, g, j, nx);
-      step(in, tdz0, hs0, t + LB_WAVES_PER_NET, tdz1, hs1, dz2);  // forward k + 2, backward k + 1
+      step(in, odd ? tdz0 : tdz1, odd ? hs0 : hs1, t, odd ? tdz1 : tdz0, odd ? hs1 : hs0, dz2);
     }
   }
 
-  LB_STAMP(3);
   // ---- per-wave sums over the 16 row lanes, then the workgroup's partial in wave order -----------
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -922,7 +957,7 @@ int rai_internal::mlp_large(float* params, float* exp_avg, float* exp_avg_sq, co
 }
 
 #ifdef RAI_STAMPS
-extern "C" int rai_mlp_large_debug_stamps(unsigned long long* host_out) {  // LB_GRID x LB_NW x 10
+extern "C" int rai_mlp_large_debug_stamps(unsigned long long* host_out) {  // LB_GRID x LB_NW x 32
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_lb_stamps), sizeof(g_lb_stamps));
 }
 #endif

@@ -20,10 +20,10 @@ large_bench.main()
 import numpy as np  # noqa: E402
 from rl_algo_impls_amd import _lib  # noqa: E402
 
-n = 256 * 4 * 16
+n = 256 * 4 * 32
 buf = (C.c_ulonglong * n)()
 assert _lib.lib().rai_mlp_large_debug_stamps(buf) == 0
-a = np.array(buf, dtype=np.float64).reshape(256, 4, 16)
+a = np.array(buf, dtype=np.float64).reshape(256, 4, 32)
 names = ["staging + sync", "register operands", "tile loop", "lane sums", "partials to LDS + sync",
          "sum + global write"]
 for k, nm in enumerate(names):
@@ -33,9 +33,17 @@ tot = a[:, :, 6] - a[:, :, 0]
 rt = (a[:, :, 9] - a[:, :, 8]) / 100e6
 print(f"{'total':>26}: median {np.median(tot):9.0f}  max {tot.max():9.0f} cycles;  "
       f"in-kernel clock {np.median(tot / rt) / 1e9:.3f} GHz; wall (100 MHz) median {np.median(rt) * 1e6:.1f} us")
-steps = np.maximum((a[:, :, 10] > 0).sum(), 1)
-for k, nm in zip((10, 11, 12), ("R1 dH1 | layer 1", "R2 layer 2 | dH1 transpose", "R3 dW2, dW1 | loss")):
-    act = a[:, :, k][a[:, :, k] > 0]
-    print(f"{nm:>30}: median {np.median(act):9.0f} cycles per wave (sum over its steps)")
+names = ["P0 layer-1 MFMAs", "P1 dH1 blk0 | act H1", "P2 dH1 blk1 | act H1", "P3 dH1 blk2 | H1 store",
+         "P4 dH1 blk3", "P5a L2 blk0 | dH1 store", "P5b L2 blk1 | dW operands", "P5c L2 blk2 | dZ1",
+         "P5d L2 blk3", "P6 dW2 s0 | act H2", "P7 dW2 s1 | act H2", "P8 dW2 s2 | output layer",
+         "P9 dW2 s3 | loss", "P10 dW1 | output backward"]
+tot_ph = 0
+for k, nm in enumerate(names):
+    v = a[:, :, 10 + k]
+    v = v[v > 0]
+    if len(v):
+        tot_ph += np.median(v)
+        print(f"{nm:>30}: median {np.median(v) / 15:8.0f} cycles per step")
+print(f"{'phases sum':>30}: {tot_ph / 15:8.0f} cycles per step (15 steps per wave at batch 131072)")
 start = a[:, :, 8] - a[:, :, 8].min()
 print(f"wave start spread (100 MHz ticks): median {np.median(start):.0f} max {start.max():.0f}")
