@@ -378,6 +378,16 @@ int rai_gather_rows(int32_t n_fields, const void* const* src, void* const* dst,
                     const int64_t* row_bytes, const int64_t* idx, int64_t n_rows, void* stream);
 
 /* --------------------------------------------------------------------------
+ * Epoch shuffle: out[i] = perm_key(i), a keyed bijection of [0, n) (6-round
+ * Feistel network over the smallest even-bit power-of-two domain >= n with
+ * cycle walking; round keys from the 64-bit key).  Stands in for
+ * torch.randperm(total_steps) of rl_algo_impls/rollout/vec_rollout.py:166-170
+ * as the epoch permutation: one independent kernel thread per index instead
+ * of a device sort.  Same key -> same permutation.
+ * ------------------------------------------------------------------------ */
+int rai_feistel_permutation(int64_t n, uint64_t key, int64_t* out, void* stream);
+
+/* --------------------------------------------------------------------------
  * Device-indexed minibatch gather for graph-replayed updates.  The source
  * fields, the epoch permutation and the minibatch counter live in a device
  * descriptor, so one captured launch sequence (gather -> forward -> loss ->

@@ -498,10 +498,10 @@ class PPO:
         opt = self.optimizer
         L = _lib.lib()
         st = _lib.stream_handle(self.device)
-        # Epoch k + 1's permutation and gather (a device randperm sort + one gather, ~0.5 ms) run on a
+        # Epoch k + 1's permutation and gather (rai_feistel_permutation + one gather) run on a
         # side stream into the other of two permuted copies while epoch k's kernel (32 CUs) runs, so
-        # the 20 launches follow each other without them.  Same permutations: the generator's
-        # offsets are taken on the host in the same order.
+        # the 20 launches follow each other without them.  Same permutations: the shuffle keys are
+        # drawn on the host in the same order.
         cur = torch.cuda.current_stream(self.device)
         two_slots = hasattr(r, "alloc_epoch_buffers")  # DeviceRollout; other rollouts: in order
         side = self._epoch_prep_stream() if two_slots else cur

@@ -110,6 +110,19 @@ class RolloutGenerator(ABC):
     def rollout(self, **kwargs) -> Rollout: ...
 
 
+def feistel_permutation(n: int, device: torch.device, key: Optional[int] = None) -> torch.Tensor:
+    """The epoch shuffle: a keyed bijection of [0, n) computed on the device (rai_feistel_permutation;
+    replaces torch.randperm(total_steps), rl_algo_impls/rollout/vec_rollout.py:166-170, whose device
+    form is a radix sort).  The 64-bit key is drawn from torch's default CPU generator, so runs under
+    torch.manual_seed repeat their shuffles."""
+    if key is None:
+        key = int(torch.randint(0, 2**63 - 1, (1,), dtype=torch.int64).item())
+    out = torch.empty(n, dtype=torch.int64, device=device)
+    rc = _lib.lib().rai_feistel_permutation(n, key & (2**64 - 1), out.data_ptr(), _lib.stream_handle(device))
+    _lib.check(rc, "rai_feistel_permutation")
+    return out
+
+
 def gather_rows(srcs: List[torch.Tensor], dsts: List[torch.Tensor], idx: torch.Tensor) -> None:
     """dst_f[i] = src_f[idx[i]] for every field, one kernel launch (rai_gather_rows)."""
     n = len(srcs)
@@ -155,6 +168,7 @@ class DeviceRollout(Rollout):
                  scale_advantage_by_values_accuracy: bool = False, gae_mode: int = EXACT,
                  perm_source: Optional[Callable[[int], torch.Tensor]] = None,
                  generator: Optional[torch.Generator] = None,
+                 perm_keys: Optional[Callable[[], int]] = None,
                  subaction_mask: Optional[Dict[int, Dict[int, int]]] = None, action_plane_space=None) -> None:
         super().__init__()
         self.device = device
@@ -173,6 +187,7 @@ class DeviceRollout(Rollout):
             self.advantages *= torch.exp(-torch.abs(self.values - self.returns) / ptp)
         self._perm_source = perm_source
         self._generator = generator
+        self._perm_keys = perm_keys
         self._flat: Optional[List[torch.Tensor]] = None
         self._perm_bufs: Dict[int, List[torch.Tensor]] = {}
 
@@ -238,7 +253,10 @@ class DeviceRollout(Rollout):
     def permutation(self) -> torch.Tensor:
         if self._perm_source is not None:
             return self._perm_source(self.total_steps).to(self.device)
-        return torch.randperm(self.total_steps, device=self.device, generator=self._generator)
+        if self._generator is not None:
+            return torch.randperm(self.total_steps, device=self.device, generator=self._generator)
+        return feistel_permutation(self.total_steps, self.device,
+                                   key=self._perm_keys() if self._perm_keys is not None else None)
 
     def alloc_epoch_buffers(self, slot: int = 0) -> None:
         """Allocate the permuted copy `slot` (on the current stream) ahead of an epoch_batch that
@@ -314,8 +332,7 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         self.seed = int(torch.initial_seed() if seed is None else seed) & 0xFFFFFFFFFFFF
         self.rng_offset = 0
         self.perm_source: Optional[Callable[[int], torch.Tensor]] = None
-        self.generator = torch.Generator(device=self.device)
-        self.generator.manual_seed(self.seed)
+        self.perm_count = 0  # epoch shuffles drawn: key (seed, count), like the samplers' (seed, offset)
 
         N = vec_env.num_envs
         T = n_steps
@@ -545,10 +562,15 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         self.policy.train()
         return next_values
 
+    def _perm_key(self) -> int:
+        k = (self.seed << 16) ^ self.perm_count
+        self.perm_count += 1
+        return k
+
     def rollout(self, gamma, gae_lambda) -> DeviceRollout:
         next_values = self._rollout(output_next_values=True)
         return DeviceRollout(
             self.device, self.next_episode_starts.clone(), next_values, self.obs, self.actions, self.rewards,
             self.episode_starts, self.values, self.logprobs if self.include_logp else None, self.action_masks, gamma,
             gae_lambda, self.scale_advantage_by_values_accuracy, self.gae_mode, self.perm_source,
-            self.generator, subaction_mask=self.subaction_mask, action_plane_space=self.action_plane_space)
+            perm_keys=self._perm_key, subaction_mask=self.subaction_mask, action_plane_space=self.action_plane_space)

@@ -10,7 +10,7 @@ import oracle
 from rl_algo_impls_amd import _lib
 from rl_algo_impls_amd.gae import EXACT, FAST, compute_advantages, compute_advantages_device
 from rl_algo_impls_amd.pg_common import DeviceBlocks, launch_loss, make_hparams
-from rl_algo_impls_amd.rollout import gather_rows
+from rl_algo_impls_amd.rollout import feistel_permutation, gather_rows
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -371,6 +371,27 @@ def test_gather_rows_multi_field():
     gather_rows(srcs, dsts, dev(idx))
     for f, d in zip(fields, dsts):
         np.testing.assert_array_equal(d.cpu().numpy(), np.ascontiguousarray(f)[idx])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 64, 1000, 4097, 524288, (1 << 20) + 7])
+def test_feistel_permutation_matches_spec_and_is_bijection(n):
+    """rai_feistel_permutation (the epoch shuffle) equals oracle.feistel_permutation bit for bit, is a
+    bijection of [0, n) (sortedness of the sorted output) and depends on the key."""
+    for key in (0, 0x1234567890ABCDEF, 2**64 - 1):
+        got = feistel_permutation(n, DEV, key=key).cpu().numpy()
+        np.testing.assert_array_equal(got, oracle.feistel_permutation(n, key))
+        np.testing.assert_array_equal(np.sort(got), np.arange(n))
+    if n >= 64:
+        a = feistel_permutation(n, DEV, key=1).cpu().numpy()
+        b = feistel_permutation(n, DEV, key=2).cpu().numpy()
+        assert (a != b).mean() > 0.9
+        assert 0.3 < np.abs(a - np.arange(n)).mean() / n < 0.37  # E|p(i) - i| = n/3 for a uniform shuffle
+
+
+def test_feistel_permutation_edge_cases():
+    assert _lib.lib().rai_feistel_permutation(0, 5, None, None) == 0
+    assert _lib.lib().rai_feistel_permutation(-1, 5, None, None) != 0
+    assert _lib.lib().rai_feistel_permutation(4, 5, None, None) != 0
 
 
 def test_categorical_sample_distribution_and_logp():

@@ -117,3 +117,13 @@ def test_learn_epoch_gae_matches(golden):
                           z["next_values"], 0.98, 0.8)
     np.testing.assert_array_equal(a2, z["advantages"])
     np.testing.assert_array_equal(r2, z["returns"])
+
+
+def test_feistel_permutation_spec_is_a_bijection():
+    """The epoch-shuffle specification (oracle.feistel_permutation, which the device kernel must match):
+    a bijection for every size including the non-power-of-two and tiny ones, key-dependent."""
+    for n in (1, 2, 3, 5, 63, 64, 65, 1000, 131072, 131073):
+        for key in (0, 7, 2**64 - 1):
+            p = oracle.feistel_permutation(n, key)
+            np.testing.assert_array_equal(np.sort(p), np.arange(n))
+    assert (oracle.feistel_permutation(1000, 1) != oracle.feistel_permutation(1000, 2)).mean() > 0.9
