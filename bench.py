@@ -224,6 +224,22 @@ def _diagnostics(tag: str) -> None:
     print(f"[bench] diag: {tag} pid {os.getpid()}", file=sys.stderr, flush=True)
 
 
+def _heartbeat(period: float = 45.0) -> None:
+    """A daemon thread printing one stderr line per `period` seconds, so a long silent stretch (the first
+    update's MIOpen find-mode tuning of every convolution shape in C3 / C5 runs minutes without output)
+    is not taken for a hang by a runner that kills commands after minutes of silence."""
+    import threading
+
+    t0 = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"[bench] alive {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def self_launch(args) -> int | None:
     """`bench.py --gpus N` (N > 1) run without a launcher: start the N ranks here, one child process
     per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (what torch.distributed.run exports), wait
@@ -269,6 +285,8 @@ def main():
     if rc is not None:
         sys.exit(rc)
     _diagnostics("start")
+    if int(os.environ.get("RANK", "0")) == 0:
+        _heartbeat()
     import numpy as np
     import torch
 

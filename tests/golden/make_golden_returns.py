@@ -40,9 +40,13 @@ CONFIGS = {
     # batch_size 256 x 20 epochs (40,960 optimizer steps per update), 4 updates with the YAML's
     # linear lr / clip decay over them.  ~3 min of CPU per update per process.
     "c2_4096x128": dict(n_envs=4096, n_steps=128, n_timesteps=4 * 4096 * 128),
+    # the same config run twice as long (8 updates, the lr / clip decay spread over 8): closer to
+    # convergence, where the return populations are tighter
+    "c2_4096x128_8u": dict(n_envs=4096, n_steps=128, n_timesteps=8 * 4096 * 128),
 }
 # seeds per config (the C2 runs are ~40x the CPU time of the 8-env ones)
-CONFIG_SEEDS = {"yaml_8x32": (1, 2, 3, 4, 5), "c1_8x128": (1, 2, 3, 4, 5), "c2_4096x128": (1, 2, 3)}
+CONFIG_SEEDS = {"yaml_8x32": (1, 2, 3, 4, 5), "c1_8x128": (1, 2, 3, 4, 5), "c2_4096x128": (1, 2, 3),
+                "c2_4096x128_8u": (1, 2, 3)}
 ALGO_KW = dict(batch_size=256, n_epochs=20, gae_lambda=0.8, gamma=0.98, ent_coef=0.0,
                learning_rate=0.001, clip_range=0.2)
 PHASES = [{"learning_rate": 0.001, "clip_range": 0.2}, {"learning_rate": 0.0, "clip_range": 0.0}]
