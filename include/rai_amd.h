@@ -627,6 +627,21 @@ int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_
                        const rai_ppo_hparams* hp, const rai_optim_hparams* ohp, rai_train_state* state,
                        float* stats, int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
                        int64_t workspace_bytes, void* stream);
+/* Data-parallel form (one process per GPU, world 2..8): rank `rank` runs its batch_size-row slices of
+ * the global minibatches (its own permuted rollout copy, n_rows rows); after each step's backward every
+ * workgroup's owned gradient is summed over the ranks in rank order through the IPC-mapped exchange
+ * regions (rai_xdp_alloc / rai_xdp_open; peers: device array of the world region pointers, rank order;
+ * step_base: optimizer steps already run through them), so every rank applies the identical clip + Adam.
+ * moments: the global minibatches' (mean, den) pairs with the normalize / standardize rule encoded
+ * (A = (adv - mean) / den), as for rai_mlp_ppo_epoch_xdp; loss means and stats rows are over
+ * batch_size x world rows (the caller sums the stats rows over the ranks). */
+int rai_mlp_wide_epoch_xdp(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq,
+                           int64_t P, const float* obs, const void* actions, const float* old_logp,
+                           const float* old_values, const float* advantages, const float* returns, int64_t n_rows,
+                           int32_t batch_size, const float* moments, int32_t world, int32_t rank, void* const* peers,
+                           int64_t step_base, const rai_ppo_hparams* hp, const rai_optim_hparams* ohp,
+                           rai_train_state* state, float* stats, int32_t max_stats, float* norms, int32_t max_norms,
+                           void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Timing hook of the large-minibatch form (bench.py's roofline): rai_mlp_large_timing(n) arms HIP
  * events around the next n gradient-kernel launches (0 disarms); rai_mlp_large_timing_read writes the

@@ -162,6 +162,8 @@ _SIGNATURES = {
     "rai_mlp_wide_epoch_workspace_bytes": (_i64, [_i32, _i32, _i64]),
     "rai_mlp_wide_epoch": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp,
                                      _vp, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
+    "rai_mlp_wide_epoch_xdp": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i32,
+                                         _i32, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
     "rai_gae_skips": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "rai_gather_minibatch": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
     "rai_minibatch_advance": (C.c_int, [_vp, _vp]),

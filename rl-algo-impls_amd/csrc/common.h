@@ -29,6 +29,14 @@ __device__ __forceinline__ void lds_barrier() {
 // time is compared signed, so a counter that steps backwards never expires a wait.
 constexpr long long RAI_SPIN_LOCAL = 200000000LL;    // 2 s: partners on the same GPU
 constexpr long long RAI_SPIN_REMOTE = 6000000000LL;  // 60 s: other ranks (they may still be launching)
+// Cross-GPU exchange regions (rai_xdp_*): [0, 2048) u64 step flags [2 nets][8 ranks][16 workgroups],
+// [2048, 4096) self-test flags, slots from 4096.  The wide whole-epoch kernel's slots
+// (mlp_wide_epoch.hip): [2 parities][world][2 nets][16 workgroups][RAI_XDP_WIDE_SLOTF floats].
+constexpr int RAI_XDP_SLOTS_OFF = 4096;
+constexpr int RAI_XDP_WIDE_SLOTF = 5376;
+__host__ __device__ constexpr long long rai_xdp_wide_bytes(int world) {
+  return RAI_XDP_SLOTS_OFF + 2LL * world * 2 * 16 * RAI_XDP_WIDE_SLOTF * 4;
+}
 __device__ __forceinline__ unsigned long long rai_clock() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ bool rai_expired(unsigned long long t0, long long limit) {
   return (long long)(rai_clock() - t0) > limit;

@@ -32,6 +32,7 @@
 #include "common.h"
 #include "internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -1738,7 +1739,10 @@ extern "C" int rai_xdp_selftest(void* const* peers, int32_t world, int32_t rank,
 }
 
 extern "C" int64_t rai_xdp_region_bytes(int32_t world) {
-  return world < 1 || world > XDP_MAXW ? 0 : xdp_region_bytes(world);
+  if (world < 1 || world > XDP_MAXW) return 0;
+  static_assert(XDP_FLAGS_BYTES == RAI_XDP_SLOTS_OFF, "one region layout");
+  // one region serves the CartPole-class epoch kernels and the wide whole-epoch kernel
+  return std::max<int64_t>(xdp_region_bytes(world), rai_xdp_wide_bytes(world));
 }
 
 // Multi-CU data-parallel step (used by rai_mlp_ppo_epoch_dp): apply the previous all-reduced

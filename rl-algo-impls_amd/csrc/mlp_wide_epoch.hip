@@ -28,7 +28,12 @@
 //      granules (agent-scope atomic store / load, no drain or counter); every workgroup sums the 2 G
 //      shares in a fixed order (clip_grad_norm_ over all parameters, bit-identical on every
 //      workgroup) and applies clip + Adam to what it owns.
-// Every spin is bounded and sets state->err.  Numerics: fp32 like the reference, exact-f32 MFMA
+// Data parallel (rai_mlp_wide_epoch_xdp, world W > 1): after the backward, each workgroup pushes the
+// gradient it owns (its W2 rows, W1 rows and small parameters, 21 KB) to slot [rank] of every rank's
+// IPC-mapped region (16-B system-scope stores, drained, one step-id flag per receiver), waits for all W
+// ranks' flags of its slice and sums the W slots in rank order, so every rank holds the bit-identical
+// global gradient before D; the loss means are over rows x W and the advantage moments are the global
+// minibatch's (computed by the caller).  Every spin is bounded and sets state->err.  Numerics: fp32 like the reference, exact-f32 MFMA
 // (v_mfma_f32_16x16x4f32), Adam with the hardware sqrt / rcp (as the CartPole epoch kernel); parity
 // to fp32 tolerance against the per-minibatch path and the reference (tests/test_gpu_trainer.py).
 #include "common.h"
@@ -55,6 +60,9 @@ constexpr int WE_OUTM = RAI_WIDE_MAX_OUT;   // 8
 constexpr int WE_SP = WE_SL + 4;            // stride of [rows][16] slices: 16-B rows, 4 rows = 16 banks
 constexpr int WE_NSMALL = 2 * WE_SL + WE_OUTM * WE_SL + 2 * WE_OUTM;  // b1 j, b2 j, W3 cols j, b3, log_std
 constexpr int WE_SC1 = 16;                  // buffer cache policy: sc1
+constexpr int WE_XDP_AUX = 17;              // sc0 | sc1: system-scope (cross-device) stores and loads
+static_assert(4096 + 1024 + WE_NSMALL <= RAI_XDP_WIDE_SLOTF && WE_NSMALL % 4 == 0, "xdp slot");
+static_assert(2 * 8 * WE_GMAX * 8 <= 2048, "xdp flags");
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
@@ -117,6 +125,12 @@ struct WeArgs {
   float* norms;
   int32_t max_norms;
   unsigned char* ws;
+  // data parallel (rai_mlp_wide_epoch_xdp): world ranks, this one xrank; every workgroup's owned
+  // gradient is summed over the ranks in rank order through the IPC-mapped regions xpeers[] each step
+  int32_t world;         // loss means over rows x world (1: single process)
+  int32_t xrank;
+  void* const* xpeers;   // device array of the world regions (rank order), nullptr when world == 1
+  int64_t xbase;         // optimizer steps already run through the regions (flags hold step ids)
 };
 
 struct WeSmem {
@@ -134,12 +148,12 @@ struct WeSmem {
   float dls[WE_B][WE_OUTM];
   float Pw[4][WE_B][WE_OUTM];  // per-wave sums of 4 slices' output partials
   alignas(16) float small[WE_NSMALL];  // b1 j | b2 j | W3[:, j] (o-major) | b3 | log_std
-  float gsm[WE_NSMALL];       // small-parameter gradients (MFMA column sums), by small index
+  alignas(16) float gsm[WE_NSMALL];  // small-parameter gradients (MFMA column sums), by small index
   double st[4][WE_B];         // per-row loss statistics, reduced off the critical path (D wait)
   float ginv[WE_OUTM], glsc[WE_OUTM], entc;  // Gaussian 1 / variance, log scale, per-row entropy
   float adamc[2];             // this step's Adam bias-correction constants (formed during the D wait)
   float coef;                 // this step's clip coefficient
-  float db1[WE_SL];           // db1 j (wave 3)
+  alignas(16) float db1[WE_SL];      // db1 j (wave 3)
   double red[4][8];
   float adv_mean, adv_den;
   int bail;
@@ -692,10 +706,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         const int srow = stat0 + mb;
         if (srow < a.max_stats) {
           float* row = a.stats + (int64_t)srow * RAI_STAT_STRIDE;
-          const double Bd = (double)rows;
+          const double Bd = (double)rows * (double)a.world;
           if (net == 0) {
             const float pi_loss = (float)(-st[0] / Bd);
-            const float ent_loss = (float)(-st[3] / (double)(HEAD == 1 ? rows * O : rows));
+            const float ent_loss = (float)(-st[3] / ((double)(HEAD == 1 ? rows * O : rows) * (double)a.world));
             row[0] = pi_loss + hp.ent_coef * ent_loss;  // the host adds vf_coef * v_loss
             row[1] = pi_loss;
             row[2] = ent_loss;
@@ -868,7 +882,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       for (int o = 0; o < WE_OUTM; ++o) dout[o] = dl[o] = 0.f;
       // statistics: [0] sum min(s1, s2) | loss, [1] sum kl | vclipped, [2] clipped, [3] entropy
       double st[4] = {0.0, 0.0, 0.0, 0.0};  // per row; summed by side_d
-      const float invB = 1.f / (float)rows;
+      const float invB = 1.f / (float)(rows * a.world);
       if (net == 0) {
 #pragma clang fp contract(off)
         const float A = c_adv;  // normalized per minibatch by we_adv_norm_kernel before the epoch
@@ -921,7 +935,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         else { g1 = g_pi * 0.5f; g2 = g_pi * 0.5f; }
         const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
         const float d_logp = valid ? (g1 * A + (g2 * A) * in_clip) * ratio : 0.f;
-        const float n_ent = (float)(HEAD == 1 ? rows * O : rows);
+        const float n_ent = (float)((HEAD == 1 ? rows * O : rows) * a.world);
         const float d_ent = valid ? -hp.ent_coef / n_ent : 0.f;
         if (HEAD == 1) {
 #pragma unroll
@@ -1131,6 +1145,90 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       }
     }
     WSTAMP(17);
+    // ============ X (data parallel): the owned gradient summed over the ranks in rank order ==========
+    if (a.world > 1) {
+      __syncthreads();  // S.gsm (waves 0-2) and S.db1 (wave 3) complete
+      const int W = a.world;
+      const unsigned long long step_id = (unsigned long long)(a.xbase + mb + 1);
+      const int rb = (int)rai_xdp_wide_bytes(W);
+      // slot floats: [0, 4096) W2 rows j as f4 (w 4 + t) 64 + lane; [4096, 5120) W1 rows j, f4 w 64 + lane;
+      // [5120, 5296) the small gradients by small index (db1 j from S.db1)
+      auto slot_off = [&](int sender) {
+        return RAI_XDP_SLOTS_OFF + ((((par * W + sender) * 2 + net) * WE_GMAX + j) * RAI_XDP_WIDE_SLOTF) * 4;
+      };
+      const bool w1_on = WE_SL * w < IN;
+      const bool sm_on = tid < WE_NSMALL / 4;
+      f4 psm = {0.f, 0.f, 0.f, 0.f};
+      if (sm_on) psm = *reinterpret_cast<const f4*>(tid < WE_SL / 4 ? &S.db1[4 * tid] : &S.gsm[4 * tid]);
+      const int my = slot_off(a.xrank);
+      for (int pr = 0; pr < W; ++pr) {
+        const __amdgpu_buffer_rsrc_t prs = we_rsrc(a.xpeers[pr], rb);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (4 * w + t < G) {
+            const f4 v = {g_r[t][0], g_r[t][1], g_r[t][2], g_r[t][3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), prs, my + ((w * 4 + t) * 64 + lane) * 16,
+                                                   0, WE_XDP_AUX);
+          }
+        if (w1_on)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, g_1), prs, my + (4096 + (w * 64 + lane) * 4) * 4,
+                                                 0, WE_XDP_AUX);
+        if (sm_on)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, psm), prs, my + (5120 + 4 * tid) * 4, 0,
+                                                 WE_XDP_AUX);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+      __syncthreads();
+      if (tid < W) {
+        unsigned long long* fl = reinterpret_cast<unsigned long long*>(a.xpeers[tid]) + (net * 8 + a.xrank) * WE_GMAX + j;
+        __hip_atomic_store(fl, step_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (w == 0) {
+        const unsigned long long* fl =
+            reinterpret_cast<const unsigned long long*>(a.xpeers[a.xrank]) + (net * 8 + (lane < W ? lane : 0)) * WE_GMAX + j;
+        const unsigned long long t0 = rai_clock();
+        for (;;) {
+          const bool ok = lane >= W || __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= step_id;
+          if (__all(ok)) break;
+          if (rai_expired(t0, RAI_SPIN_REMOTE)) {
+            if (lane == 0) {
+              __hip_atomic_store(&a.state->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              S.bail = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (S.bail) break;
+      const __amdgpu_buffer_rsrc_t lrs = we_rsrc(a.xpeers[a.xrank], rb);
+      f4 s2[4], s1 = {0.f, 0.f, 0.f, 0.f}, ssm = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) s2[t] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int pr = 0; pr < W; ++pr) {
+        const int off = slot_off(pr);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (4 * w + t < G)
+            s2[t] += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(lrs, off + ((w * 4 + t) * 64 + lane) * 16,
+                                                                                 0, WE_XDP_AUX));
+        if (w1_on)
+          s1 += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(lrs, off + (4096 + (w * 64 + lane) * 4) * 4, 0,
+                                                                            WE_XDP_AUX));
+        if (sm_on)
+          ssm += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(lrs, off + (5120 + 4 * tid) * 4, 0, WE_XDP_AUX));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (4 * w + t < G)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g_r[t][r] = s2[t][r];
+      if (w1_on) g_1 = s1;
+      if (sm_on) *reinterpret_cast<f4*>(tid < WE_SL / 4 ? &S.db1[4 * tid] : &S.gsm[4 * tid]) = ssm;
+      __syncthreads();
+      if (w == 3 && lane < WE_SL) db1_sq = S.db1[lane];
+    }
     // ============ D: this workgroup's share of |g|^2, then clip_grad_norm_ + Adam =============
     {
       double ss = 0.0;
@@ -1288,7 +1386,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
 __global__ __launch_bounds__(256) void we_pack_kernel(const float* obs, const void* actions, const float* old_logp,
                                                       const float* old_values, const float* adv, const float* ret,
                                                       int64_t n_rows, int B, int IN, int O, int head,
-                                                      const rai_ppo_hparams* hpp, float* rec) {
+                                                      const rai_ppo_hparams* hpp, const float* moments, float* rec) {
 #pragma clang fp contract(off)
   const int64_t mb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -1300,7 +1398,9 @@ __global__ __launch_bounds__(256) void we_pack_kernel(const float* obs, const vo
   const int64_t gr = r0 + (valid ? lane : 0);
   const float x = valid ? adv[gr] : 0.f;
   float A = x;
-  if (hp.normalize_advantage || hp.standardize_advantage) {
+  if (moments) {  // data parallel: the global minibatch's (mean, den), the normalize / standardize rule encoded
+    A = (x - moments[2 * mb]) / moments[2 * mb + 1];
+  } else if (hp.normalize_advantage || hp.standardize_advantage) {
     const double s1 = wave_sum_dpp(valid ? (double)x : 0.0);
     const float mean = (float)(s1 / (double)rows);
     const double dv = (double)x - (double)mean;
@@ -1346,20 +1446,20 @@ extern "C" int64_t rai_mlp_wide_epoch_workspace_bytes(int32_t hidden, int32_t in
   return (n_rows < 0 || in_dim < 1 || in_dim > WE_INMAX) ? -1 : we_ws_bytes(in_dim, n_rows);
 }
 
-extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq,
-                                  int64_t P, const float* obs, const void* actions, const float* old_logp,
-                                  const float* old_values, const float* advantages, const float* returns,
-                                  int64_t n_rows, int32_t batch_size, const rai_ppo_hparams* hp,
-                                  const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
-                                  int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
-                                  int64_t workspace_bytes, void* stream) {
+static int wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq, int64_t P,
+                      const float* obs, const void* actions, const float* old_logp, const float* old_values,
+                      const float* advantages, const float* returns, int64_t n_rows, int32_t batch_size,
+                      const float* moments, int32_t world, int32_t rank, void* const* peers, int64_t step_base,
+                      const rai_ppo_hparams* hp, const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
+                      int32_t max_stats, float* norms, int32_t max_norms, void* workspace, int64_t workspace_bytes,
+                      void* stream) {
   if (!desc || !params || !exp_avg || !exp_avg_sq || !obs || !actions || !old_logp || !old_values || !advantages ||
       !returns || !hp || !ohp || !state || !workspace)
     return RAI_E_NULLPTR;
   if (n_rows < 2 || batch_size < 2 || batch_size > WE_B) return RAI_E_SHAPE;
   if (desc->in_dim < 1 || desc->in_dim > WE_INMAX) return RAI_E_UNSUPPORTED;
   if (workspace_bytes < we_ws_bytes(desc->in_dim, n_rows)) return RAI_E_WORKSPACE;
-  if (n_rows % batch_size == 1) return RAI_E_SHAPE;  // a 1-row minibatch has no unbiased std
+  if (!moments && n_rows % batch_size == 1) return RAI_E_SHAPE;  // a 1-row minibatch has no unbiased std
   const int H = desc->hidden;
   if (H < WE_SL || H > WE_HMAX || H % WE_SL != 0) return RAI_E_UNSUPPORTED;
   if (desc->in_dim < 1 || desc->in_dim > WE_INMAX || desc->out_pi < 1 || desc->out_pi > WE_OUTM)
@@ -1389,13 +1489,17 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   a.norms = norms;
   a.max_norms = max_norms;
   a.ws = static_cast<unsigned char*>(workspace);
+  a.world = world;
+  a.xrank = rank;
+  a.xpeers = peers;
+  a.xbase = step_base;
   hipStream_t s = rai_stream(stream);
   // monotonic counters and granule tags start at 0 (tags are step + 1 >= 1)
   const hipError_t e = hipMemsetAsync(workspace, 0, WE_STATE_BYTES, s);
   if (e != hipSuccess) return (int)e;
   const int64_t nmb = (n_rows + batch_size - 1) / batch_size;
   hipLaunchKernelGGL(we_pack_kernel, dim3((unsigned)((nmb + 3) / 4)), dim3(256), 0, s, obs, actions, old_logp, old_values,
-                     advantages, returns, n_rows, (int)batch_size, desc->in_dim, desc->out_pi, desc->head, hp,
+                     advantages, returns, n_rows, (int)batch_size, desc->in_dim, desc->out_pi, desc->head, hp, moments,
                      const_cast<float*>(a.rec));
   RAI_LAUNCH_CHECK();
   const dim3 grid(8 * (H / WE_SL));
@@ -1403,4 +1507,31 @@ extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, 
   else hipLaunchKernelGGL(mlp_wide_epoch_kernel<0>, grid, dim3(WE_NT), 0, s, a);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
+}
+
+extern "C" int rai_mlp_wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq,
+                                  int64_t P, const float* obs, const void* actions, const float* old_logp,
+                                  const float* old_values, const float* advantages, const float* returns,
+                                  int64_t n_rows, int32_t batch_size, const rai_ppo_hparams* hp,
+                                  const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
+                                  int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
+                                  int64_t workspace_bytes, void* stream) {
+  return wide_epoch(desc, params, exp_avg, exp_avg_sq, P, obs, actions, old_logp, old_values, advantages, returns,
+                    n_rows, batch_size, nullptr, 1, 0, nullptr, 0, hp, ohp, state, stats, max_stats, norms, max_norms,
+                    workspace, workspace_bytes, stream);
+}
+
+extern "C" int rai_mlp_wide_epoch_xdp(const rai_mlp_wide_desc* desc, float* params, float* exp_avg, float* exp_avg_sq,
+                                      int64_t P, const float* obs, const void* actions, const float* old_logp,
+                                      const float* old_values, const float* advantages, const float* returns,
+                                      int64_t n_rows, int32_t batch_size, const float* moments, int32_t world,
+                                      int32_t rank, void* const* peers, int64_t step_base, const rai_ppo_hparams* hp,
+                                      const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
+                                      int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
+                                      int64_t workspace_bytes, void* stream) {
+  if (world < 2 || world > 8 || rank < 0 || rank >= world || step_base < 0) return RAI_E_SHAPE;
+  if (!peers || !moments) return RAI_E_NULLPTR;
+  return wide_epoch(desc, params, exp_avg, exp_avg_sq, P, obs, actions, old_logp, old_values, advantages, returns,
+                    n_rows, batch_size, moments, world, rank, peers, step_base, hp, ohp, state, stats, max_stats, norms,
+                    max_norms, workspace, workspace_bytes, stream);
 }

@@ -143,8 +143,11 @@ class PPO:
         if xdp is None:
             xdp = os.environ.get("RAI_XDP", "1") != "0"
         spec = self.fused_mlp_spec()
-        if (xdp and self.flat.flat.is_cuda and self.world > 1 and spec is not None and spec["in_dim"] <= 4
-                and spec["n_act"] <= 2 and self.world <= 8 and self.batch_size <= _lib.RAI_MLP_EPOCH_MAX_B):
+        c2_xdp = (spec is not None and spec["in_dim"] <= 4 and spec["n_act"] <= 2
+                  and self.batch_size <= _lib.RAI_MLP_EPOCH_MAX_B)
+        # the wide whole-epoch kernel (C4) keeps its one launch per epoch under data parallel too
+        wide_xdp = spec is None and self._wide_epoch_options_ok() and self._wide_step() is not None
+        if xdp and self.flat.flat.is_cuda and self.world > 1 and self.world <= 8 and (c2_xdp or wide_xdp):
             try:
                 self._xdp = self._setup_xdp(group)
             except RuntimeError as e:  # e.g. IPC unavailable: fall back to the per-step RCCL loop
@@ -561,18 +564,27 @@ class PPO:
         stats[:, 0] += float(self.vf_coef) * stats[:, 5]  # value term of the loss
         return stats, norms, 1
 
-    def _wide_epoch_step(self, r):
-        """The WideStep (descriptor) when the whole epoch can run as ONE persistent launch
-        (rai_mlp_wide_epoch): a wide-MLP policy with K = 1, Adam, minibatches of 2..64 rows, no
-        gradient accumulation / kl_cutoff / multi-reward weights / vf_weights, single process.
-        RAI_WIDE_EPOCH=0 keeps the graph-replayed per-minibatch path."""
-        if os.environ.get("RAI_WIDE_EPOCH", "1") == "0" or not hasattr(r, "epoch_batch") or self.dp_enabled:
-            return None
+    def _wide_epoch_options_ok(self) -> bool:
+        """The options rai_mlp_wide_epoch covers: K = 1, Adam, minibatches of 2..64 rows (per rank), no
+        gradient accumulation / kl_cutoff / multi-reward weights / vf_weights."""
+        if os.environ.get("RAI_WIDE_EPOCH", "1") == "0":
+            return False
         if (self.gradient_accumulation or self.kl_cutoff is not None or self.multi_reward_weights is not None
                 or self.vf_weights is not None or self.normalize_advantages_after_scaling
                 or np.ndim(self.vf_coef) > 0 or self.optimizer.kind != self.optimizer.ADAM):
+            return False
+        return 2 <= self.batch_size <= 64
+
+    def _wide_epoch_step(self, r):
+        """The WideStep (descriptor) when the whole epoch can run as ONE persistent launch
+        (rai_mlp_wide_epoch): a wide-MLP policy within _wide_epoch_options_ok, single process or data
+        parallel over the in-kernel cross-GPU exchange (rai_mlp_wide_epoch_xdp).
+        RAI_WIDE_EPOCH=0 keeps the graph-replayed per-minibatch path."""
+        if not hasattr(r, "epoch_batch") or (self.dp_enabled and self._xdp is None):
             return None
-        if not (2 <= self.batch_size <= 64) or r.total_steps < 2 or r.total_steps % self.batch_size == 1:
+        if not self._wide_epoch_options_ok():
+            return None
+        if r.total_steps < 2 or (not self.dp_enabled and r.total_steps % self.batch_size == 1):
             return None
         return self._wide_step()
 
@@ -649,6 +661,62 @@ class PPO:
         stats[:, 0] += float(self.vf_coef) * stats[:, 5]  # value term of the loss
         return stats, norms, 1
 
+    def _update_wide_epoch_xdp(self, r, wide) -> Tuple[np.ndarray, np.ndarray, int]:
+        """Data-parallel whole-epoch form (rai_mlp_wide_epoch_xdp): per epoch the permuted copy, the global
+        minibatches' advantage moments (one small all-reduce) and ONE launch whose workgroups sum their
+        owned gradients over the ranks inside the kernel; stats rows summed over the ranks after."""
+        nmb = r.num_minibatches(self.batch_size)
+        n_steps = self.n_epochs * nmb
+        blocks = self.blocks
+        blocks.ensure_tables(n_steps, n_steps)
+        blocks.upload(self._hparams(1, nmb), self.optimizer.step_count)
+        opt = self.optimizer
+        L = _lib.lib()
+        st = _lib.stream_handle(self.device)
+        ws_bytes = int(L.rai_mlp_wide_epoch_workspace_bytes(wide.spec["hidden"], wide.desc.in_dim, r.total_steps))
+        if getattr(self, "_we_ws", None) is None or self._we_ws.numel() < ws_bytes:
+            self._we_ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
+        f = self.flat
+        x = self._xdp
+        for _ in range(self.n_epochs):
+            b = r.epoch_batch(shuffle=True)
+            assert b.logprobs is not None, "PPO needs rollout logprobs (include_logp=True)"
+            moments = self._global_adv_moments(b.advantages, nmb).view(nmb, 2)
+            if not self.normalize_advantage:  # the kernel applies A = (A - mean) / den as given
+                moments[:, 0] = 0.0
+                if not self.standardize_advantage:
+                    moments[:, 1] = 1.0
+            obs = (b.obs if b.obs.dtype == torch.float32 else b.obs.float()).contiguous()
+            ev = None
+            if self.kernel_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            rc = L.rai_mlp_wide_epoch_xdp(
+                C.byref(wide.desc), f.flat.data_ptr(), opt.state1.data_ptr(), opt.state2.data_ptr(), f.P,
+                obs.data_ptr(), b.actions.contiguous().data_ptr(), b.logprobs.data_ptr(), b.values.data_ptr(),
+                b.advantages.data_ptr(), b.returns.data_ptr(), r.total_steps, self.batch_size, moments.data_ptr(),
+                self.world, x["rank"], x["peers"].data_ptr(), x["step"], blocks.hp.data_ptr(), opt.hp_dev.data_ptr(),
+                blocks.state.data_ptr(), blocks.stats.data_ptr(), int(blocks.stats.shape[0]), blocks.norms.data_ptr(),
+                int(blocks.norms.shape[0]), self._we_ws.data_ptr(), self._we_ws.numel(), st)
+            _lib.check(rc, "rai_mlp_wide_epoch_xdp")
+            if ev is not None:
+                ev[1].record()
+                self.kernel_events.append(ev)
+            x["step"] += nmb
+            opt.step_count += nmb
+        stats_t = blocks.stats[:n_steps].clone()
+        self._all_reduce(stats_t)  # every rank holds its share of the global means
+        host = torch.cat([stats_t.reshape(-1), blocks.norms[:n_steps], blocks.state.view(torch.float32)]).cpu().numpy()
+        stats = host[: n_steps * _lib.RAI_STAT_STRIDE].reshape(n_steps, _lib.RAI_STAT_STRIDE).copy()
+        norms = host[n_steps * _lib.RAI_STAT_STRIDE: n_steps * _lib.RAI_STAT_STRIDE + n_steps]
+        state = host[n_steps * _lib.RAI_STAT_STRIDE + n_steps:].view(np.int32)
+        if state[5] != 0:
+            raise RuntimeError("rai_mlp_wide_epoch_xdp: a device-side hand-off timed out (err flag set)")
+        if not self._params_agree():
+            raise RuntimeError("ranks' parameters diverged after the in-kernel cross-GPU exchange")
+        stats[:, 0] += float(self.vf_coef) * stats[:, 5]
+        return stats, norms, 1
+
     def _epoch_prep_stream(self) -> torch.cuda.Stream:
         if getattr(self, "_prep_stream", None) is None:
             self._prep_stream = torch.cuda.Stream(self.device)
@@ -706,6 +774,8 @@ class PPO:
             return self._update_fused_dp(r, spec) if self.dp_enabled else self._update_fused(r, spec)
         wide_epoch = self._wide_epoch_step(r)
         if wide_epoch is not None:
+            if self.dp_enabled:
+                return self._update_wide_epoch_xdp(r, wide_epoch)
             return self._update_wide_epoch(r, wide_epoch)
         nmb = r.num_minibatches(self.batch_size)
         n_steps = self.n_epochs * nmb

@@ -111,6 +111,64 @@ def fused_dp_worker(rank, world, port, q, backend="gloo", dp_batch="per-rank", i
     dist.destroy_process_group()
 
 
+def wide_epoch_xdp_worker(rank, world, port, q, hidden=64, rows_per_rank=32, n=512):
+    """C4-class wide MLP (Gaussian head) under data parallel with the in-kernel exchange: every rank runs
+    rai_mlp_wide_epoch_xdp on its own rows (rows_per_rank per optimizer step; global minibatch
+    rows_per_rank x world, dp_batch="global")."""
+    import torch
+
+    _init(rank, world, port, "gloo")
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.policy import ActorCritic
+    import make_golden_networks as nets
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    policy = ActorCritic(nets.halfcheetah_env(), pi_hidden_sizes=[hidden, hidden], v_hidden_sizes=[hidden, hidden],
+                         activation_fn="relu", log_std_init=-2, init_layers_orthogonal=False).to(dev)
+    algo = PPO(policy, dev, None, batch_size=rows_per_rank * world, n_epochs=2, learning_rate=3e-4, clip_range=0.2,
+               ent_coef=0.01, max_grad_norm=0.5)
+    algo.enable_data_parallel(xdp=True, dp_batch="global")
+    assert algo.batch_size == rows_per_rank
+    assert algo._xdp is not None, "in-kernel exchange not set up for the wide policy"
+    data = make_rank_data_wide(rank, dev, n)
+
+    class R:
+        total_steps = n
+
+        def num_minibatches(self, bs):
+            return -(-self.total_steps // bs)
+
+        def epoch_batch(self, shuffle=True):
+            return data
+
+    assert algo._wide_epoch_step(R()) is not None, "whole-epoch kernel not selected under data parallel"
+    stats, norms, _ = algo.update(R())
+    q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+def make_rank_data_wide(rank, dev, n=512):
+    import torch
+
+    from rl_algo_impls_amd.rollout import Batch
+
+    g = torch.Generator().manual_seed(11 + rank)
+    obs = torch.randn(n, 17, generator=g)
+    act = torch.randn(n, 6, generator=g).clamp(-1, 1)
+    logp = -4.0 + 0.3 * torch.randn(n, generator=g)
+    vals = torch.randn(n, generator=g)
+    adv = torch.randn(n, generator=g) * 2 + 0.3 * rank
+    ret = vals + adv
+    t = lambda x: x.to(dev)
+    return Batch(t(obs), t(logp), t(act), None, None, t(vals), t(adv), t(ret))
+
+
 def make_rank_data(rank, dev, n=512):
     import torch
 

@@ -316,3 +316,75 @@ def test_env_partition_split_world2_matches_single_process_c2():
     np.testing.assert_allclose(n0, norms, rtol=1e-4)
     np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("hidden,rows,n", [(64, 32, 512), (256, 32, 400)])
+def test_wide_epoch_xdp_world2_matches_single_process_global_minibatches(hidden, rows, n):
+    """The C4-class whole-epoch kernel under data parallel (rai_mlp_wide_epoch_xdp): two processes on
+    this GPU, each running its `rows`-row slices of the global minibatches in one launch per epoch, the
+    workgroups' owned gradients summed over the ranks inside the kernel.  Ranks stay bitwise equal; the
+    result equals the single-process whole-epoch update at batch 2 x rows over the interleaved rollouts
+    (fp32 tolerance: per-rank partial sums change the summation order).  n = 400: a ragged last
+    minibatch (16 rows per rank)."""
+    import queue
+    import time
+
+    import dp_worker
+    import make_golden_networks as nets
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import Batch
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.wide_epoch_xdp_worker, args=(r, 2, port, q, hidden, rows, n)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    deadline = time.time() + 240
+    while len(res) < len(procs):
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"rank exited with {dead}"
+            assert time.time() < deadline, "ranks did not report in time"
+    res.sort(key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, s0, n0), (_, p1, s1, n1) = res
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(n0, n1)
+
+    dev = torch.device("cuda", 0)
+    d0, d1 = dp_worker.make_rank_data_wide(0, dev, n), dp_worker.make_rank_data_wide(1, dev, n)
+    nmb = -(-n // rows)
+
+    def interleave(f):
+        a, b = getattr(d0, f), getattr(d1, f)
+        return torch.cat([torch.cat([a[i * rows:(i + 1) * rows], b[i * rows:(i + 1) * rows]]) for i in range(nmb)])
+
+    glob = Batch(*(interleave(f) for f in ("obs", "logprobs", "actions")), None, None,
+                 *(interleave(f) for f in ("values", "advantages", "returns")))
+    torch.manual_seed(0)
+    policy = ActorCritic(nets.halfcheetah_env(), pi_hidden_sizes=[hidden, hidden], v_hidden_sizes=[hidden, hidden],
+                         activation_fn="relu", log_std_init=-2, init_layers_orthogonal=False).to(dev)
+    algo = PPO(policy, dev, None, batch_size=2 * rows, n_epochs=2, learning_rate=3e-4, clip_range=0.2, ent_coef=0.01,
+               max_grad_norm=0.5)
+
+    class R:
+        total_steps = 2 * n
+
+        def num_minibatches(self, bs):
+            return -(-self.total_steps // bs)
+
+        def epoch_batch(self, shuffle=True):
+            return glob
+
+    assert algo._wide_epoch_step(R()) is not None
+    stats, norms, _ = algo.update(R())
+    np.testing.assert_allclose(n0, norms, rtol=2e-4)
+    np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=2e-4, atol=2e-6)

@@ -24,8 +24,8 @@ from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 LAYOUT = os.environ.get("RAI_MLP_LAYOUT", "mc8")
 NAMES = {
     "mc8": ["F1 (own columns) + barrier", "F2 + output partials + barrier", "loss + dZ2 + barrier",
-            "dH1 + dZ1 + partials + barrier", "P_B dW2 + sums", "round 1: publish + counter wait",
-            "share sum + round 2 publish + wait", "all-gather + norm + adam"],
+            "dH1 + dZ1 + partials + barrier", "P_B dW2 + sums + barrier", "round 1: publish + counter wait",
+            "share sum + round 2 publish + wait", "all-gather + norm + adam + barrier"],
     "mc4": ["F1+F2 forward", "out layer + loss + dZ2", "dH1 + partials + barrier", "P_B dW2 + sums",
            "publish + counter wait", "reduce G slots + |g|^2", "stats + norm exchange", "adam"],
     "rows": ["F1 layer1 (wave-local)", "F2 layer2 + epilogue", "out layer + loss + dZ2", "dH1 MFMA",
@@ -54,16 +54,25 @@ assert rc == 0, rc
 st = (np.array(out, dtype=np.float64) - np.array(out0, dtype=np.float64)).reshape(2, 32)
 nmb = r.total_steps // 256
 print(f"epoch {ev0.elapsed_time(ev1):.2f} ms for {nmb} minibatches -> {ev0.elapsed_time(ev1) * 1e3 / nmb:.2f} us/mb")
+# mc8: STAMP(15..19) close each compute phase's work and STAMP(1..5) the barrier wait after it; the exchange
+# phases are split by STAMP(9..14).  Every stamp is the time since the previous one, so a phase's time is
+# the sum of its work and wait stamps and the % column is over all of them (work plus waits).
+MC8_PARTS = [(15, 1), (16, 2), (17, 3), (18, 4), (19, 5), (9, 10, 6), (11, 12, 13, 7), (14, 8)]
 for net in range(2):
-    tot = st[net, 1:1 + len(NAMES)].sum()
+    if LAYOUT == "mc8":
+        ph = [sum(st[net, i] for i in parts) for parts in MC8_PARTS]
+    else:
+        ph = [st[net, i + 1] for i in range(len(NAMES))]
+    tot = sum(ph)
     print(f"--- workgroup {net} ({'actor' if net == 0 else 'critic'}): {tot / nmb:.0f} stamp-ticks/mb")
-    for i, n in enumerate(NAMES):
-        print(f"  {n:28s} {st[net, i + 1] / nmb:10.1f} ticks/mb  {100 * st[net, i + 1] / tot:5.1f}%")
-    if LAYOUT == "mc8":  # compute phases split into work and barrier wait (STAMP 15-19: work, phases 1-5: wait)
+    for n, v in zip(NAMES, ph):
+        print(f"  {n:36s} {v / nmb:10.1f} ticks/mb  {100 * v / tot:5.1f}%")
+    if LAYOUT == "mc8":  # compute phases split into work and barrier wait
         for i, n in ((15, "F1 work"), (16, "F2 work"), (17, "loss work"), (18, "dH1 work"), (19, "P_B work")):
             print(f"  {n:34s} {st[net, i] / nmb:10.1f} ticks/mb (+ barrier {st[net, i - 14] / nmb:.1f})")
-    if LAYOUT == "mc8":  # sub-phases (STAMP 9-14 split phases 6-8 above)
         for i, n in ((9, "  r1: wave-0 partial stores + drain"), (10, "  r1: barrier (other waves' drains)"),
-                     (11, "  r2: share-sum loads (+ xGMI)"), (12, "  r2: share store + norm + drain"),
-                     (13, "  r2: barrier (other waves' drains)"), (14, "  ag: gradient + norm loads, norm sum")):
+                     (6, "  r1: counter wait + stats"), (11, "  r2: share-sum loads (+ xGMI)"),
+                     (12, "  r2: share store + norm + drain"), (13, "  r2: barrier (other waves' drains)"),
+                     (7, "  r2: counter wait (both networks)"), (14, "  ag: gradient + norm loads, norm sum"),
+                     (8, "  ag: clip + adam + barrier")):
             print(f"  {n:34s} {st[net, i] / nmb:10.1f} ticks/mb")
