@@ -33,10 +33,13 @@ constexpr int M8_GMAX = 16;                          // largest CUs-per-network 
 constexpr int M8_NT = 256;                           // threads per CU (4 waves)
 constexpr int M8_NW = M8_NT / 64;
 // Geometry for G CUs per network: RC rows per CU in NTILE 16-row tiles, WPT waves per tile, each
-// wave owning CT 16-column tiles of the hidden layers; SH float4 chunks per gradient share.
-template <int G>
+// wave owning CT 16-column tiles of the hidden layers; SH float4 chunks per gradient share.  RC defaults
+// to MAXB / G (a 256-row minibatch over all G CUs); the per-rank geometry of data parallel keeps RC = 16
+// at G = 8 for minibatches of <= 128 rows (256 / world rows per rank at world 2), so no CU of the
+// network idles through the exchange.
+template <int G, int RCV = MAXB / G>
 struct M8Geo {
-  static constexpr int RC = MAXB / G;
+  static constexpr int RC = RCV;
   static constexpr int NTILE = RC / 16;
   static constexpr int WPT = M8_NW / NTILE;
   static constexpr int CT = HID / 16 / WPT;
@@ -55,9 +58,9 @@ constexpr int64_t M8_SQ_OFF = M8_S2_OFF + 2LL * 2 * WL_N * sizeof(float);   // [
 constexpr int64_t M8_SCRATCH = M8_SQ_OFF + 2LL * 2 * M8_GMAX * M8_NW * sizeof(double);
 static_assert(2 * XDP_MAXW * M8_GMAX * 8 <= XDP_TEST_OFF, "xdp share flags");
 
-template <int OUTP, int G>
+template <int OUTP, int G, int RCV>
 struct SmemM8 {
-  using Geo = M8Geo<G>;
+  using Geo = M8Geo<G, RCV>;
 #ifdef RAI_STAMPS
   unsigned long long stamps[32];
   unsigned long long t_last;
@@ -174,9 +177,9 @@ __device__ __forceinline__ bool m8_wait2(unsigned long long* sync, int i0, int i
   return true;
 }
 
-template <int OUTP, bool ACTOR, int RELU, int G>
-__device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, const int c) {
-  using Geo = M8Geo<G>;
+template <int OUTP, bool ACTOR, int RELU, int G, int RCV>
+__device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& S, const int c) {
+  using Geo = M8Geo<G, RCV>;
   constexpr int RC = Geo::RC, WPT = Geo::WPT, CT = Geo::CT, NTILE = Geo::NTILE, SH = Geo::SH;
   constexpr int net = ACTOR ? 0 : 1;
   constexpr int relu = RELU;
@@ -858,12 +861,12 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G>& S, co
   }
 }
 
-template <int RELU, int G>
+template <int RELU, int G, int RCV = MAXB / G>
 __global__ __launch_bounds__(M8_NT) void mlp_ppo_mc8_kernel(const MlpArgs a) {
-  static_assert(sizeof(SmemM8<2, G>) <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[sizeof(SmemM8<2, G>)];
+  static_assert(sizeof(SmemM8<2, G, RCV>) <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[sizeof(SmemM8<2, G, RCV>)];
   const int b = blockIdx.x, xcd = b & 7, c = b >> 3;
   if (xcd >= 2) return;  // only two XCDs' worth of blocks work (locality, not correctness)
-  if (xcd == 0) mlp_mc8<2, true, RELU, G>(a, *reinterpret_cast<SmemM8<2, G>*>(smem_raw), c);
-  else mlp_mc8<1, false, RELU, G>(a, *reinterpret_cast<SmemM8<1, G>*>(smem_raw), c);
+  if (xcd == 0) mlp_mc8<2, true, RELU, G, RCV>(a, *reinterpret_cast<SmemM8<2, G, RCV>*>(smem_raw), c);
+  else mlp_mc8<1, false, RELU, G, RCV>(a, *reinterpret_cast<SmemM8<1, G, RCV>*>(smem_raw), c);
 }

@@ -1564,6 +1564,12 @@ int mlp_cus_per_net() {
   return (e && !strcmp(e, "8")) ? 8 : 16;
 }
 
+// Per-rank geometry for minibatches of <= 128 rows (A-B: RAI_MLP_PER_RANK_GEO=0 keeps 16 CUs)
+bool mlp_per_rank_geometry() {
+  const char* e = getenv("RAI_MLP_PER_RANK_GEO");
+  return !(e && !strcmp(e, "0"));
+}
+
 int64_t num_minibatches(int64_t n_rows, int32_t batch_size) {
   return batch_size > 0 ? (n_rows + batch_size - 1) / batch_size : 0;
 }
@@ -1610,7 +1616,11 @@ int mlp_launch(MlpArgs& a, int32_t hidden, int32_t batch_size, int64_t n_rows, v
   const int layout = mlp_layout();
   if (a.in_dim <= 4 && a.n_act <= 2 && layout == 0 && !a.grad_out) {
     // multi-CU layout, G CUs per network: reduce-scatter + all-gather per minibatch
-    if (mlp_cus_per_net() == 16) {
+    if (mlp_cus_per_net() == 16 && batch_size <= 128 && mlp_per_rank_geometry()) {
+      // <= 128 rows (256 / world per rank at world 2): 8 CUs of 16 rows, not 16 CUs of which half hold no rows
+      if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_mc8_kernel<1, 8, 16>), dim3(M8Geo<8, 16>::GRID), dim3(M8_NT), 0, s, a);
+      else hipLaunchKernelGGL((mlp_ppo_mc8_kernel<0, 8, 16>), dim3(M8Geo<8, 16>::GRID), dim3(M8_NT), 0, s, a);
+    } else if (mlp_cus_per_net() == 16) {
       if (a.act_fn == 1) hipLaunchKernelGGL((mlp_ppo_mc8_kernel<1, 16>), dim3(M8Geo<16>::GRID), dim3(M8_NT), 0, s, a);
       else hipLaunchKernelGGL((mlp_ppo_mc8_kernel<0, 16>), dim3(M8Geo<16>::GRID), dim3(M8_NT), 0, s, a);
     } else {

@@ -266,13 +266,15 @@ def test_nature_cnn_bucketed_allreduce_world1_matches_single_process():
         np.testing.assert_allclose(pb, po, rtol=1e-5, atol=1e-7)
 
 
-def test_env_partition_split_world2_matches_single_process_c2():
+@pytest.mark.parametrize("world", [2, 4])
+def test_env_partition_split_world2_matches_single_process_c2(world):
     """bench.py's default multi-GPU rule (SURVEY.md 8(d) "global N fixed; per-GPU N = N/R" with
-    8(e)'s global minibatch): 2 ranks (gloo, both on cuda:0, in-kernel exchange) each own half the
-    env columns of ONE 16 x 64 CartPole-shaped rollout, compute their GAE on the device and take
-    128 of the 256 rows of each optimizer step.  Reference: the single-process update over the whole
+    8(e)'s global minibatch): `world` ranks (gloo, all on cuda:0, in-kernel exchange) each own 1/world of
+    the env columns of ONE 16 x 64 CartPole-shaped rollout, compute their GAE on the device and take
+    256 / world of the 256 rows of each optimizer step (world 2: the per-rank geometry, 8 CUs of 16 rows
+    per network; world 4: 64 rows per rank).  Reference: the single-process update over the whole
     rollout (GAE over all 64 columns) whose epoch permutation lists, for minibatch i, rank 0's rows
-    [128 i, 128 i + 128) and then rank 1's, as (t, n) of the concatenated env group."""
+    [b i, b i + b) and then rank 1's, ..., as (t, n) of the concatenated env group."""
     import queue
     import time
 
@@ -283,12 +285,12 @@ def test_env_partition_split_world2_matches_single_process_c2():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=dp_worker.split_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=dp_worker.split_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = []
     deadline = time.time() + 240
-    while len(res) < 2:
+    while len(res) < world:
         try:
             res.append(q.get(timeout=2))
         except queue.Empty:
@@ -299,15 +301,17 @@ def test_env_partition_split_world2_matches_single_process_c2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, p0, s0, n0, x0), (_, p1, s1, n1, x1) = res
-    assert x0 and x1, "the in-kernel exchange was not used"
-    np.testing.assert_array_equal(p0, p1)
+    assert all(x[4] for x in res), "the in-kernel exchange was not used"
+    p0, s0, n0 = res[0][1], res[0][2], res[0][3]
+    for x in res[1:]:
+        np.testing.assert_array_equal(p0, x[1])
 
-    T, N, half, b = dp_worker.SPLIT_T, dp_worker.SPLIT_N, dp_worker.SPLIT_N // 2, 128
-    local = torch.arange(T * half)  # rank-local flat row -> (t, n) of the whole env group
-    to_global = [(local // half) * N + (local % half) + r * half for r in range(2)]
-    perm = torch.cat([torch.cat([to_global[0][i * b:(i + 1) * b], to_global[1][i * b:(i + 1) * b]])
-                      for i in range(T * half // b)])
+    T, N = dp_worker.SPLIT_T, dp_worker.SPLIT_N
+    part, b = N // world, 256 // world
+    local = torch.arange(T * part)  # rank-local flat row -> (t, n) of the whole env group
+    to_global = [(local // part) * N + (local % part) + r * part for r in range(world)]
+    perm = torch.cat([torch.cat([to_global[r][i * b:(i + 1) * b] for r in range(world)])
+                      for i in range(T * part // b)])
     dev = torch.device("cuda", 0)
     r = dp_worker.split_device_rollout(dp_worker.split_rollout_tensors(), torch.arange(N), dev, perm)
     torch.manual_seed(0)
