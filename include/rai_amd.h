@@ -378,6 +378,15 @@ int rai_gather_rows(int32_t n_fields, const void* const* src, void* const* dst,
                     const int64_t* row_bytes, const int64_t* idx, int64_t n_rows, void* stream);
 
 /* --------------------------------------------------------------------------
+ * Rollout staging (the env-step loop of rl_algo_impls/rollout/sync_step_rollout.py:193-207):
+ * rai_copy_d2h_sync copies device -> host (pinned) on the stream and waits for the stream (the
+ * step's actions for the host env); rai_copy_h2d_multi issues n (<= RAI_MAX_FIELDS) asynchronous
+ * host (pinned) -> device copies on the stream (rewards, terminations, next observations).
+ * ------------------------------------------------------------------------ */
+int rai_copy_d2h_sync(const void* src, void* dst, int64_t bytes, void* stream);
+int rai_copy_h2d_multi(int32_t n, void* const* dst, const void* const* src, const int64_t* bytes, void* stream);
+
+/* --------------------------------------------------------------------------
  * Epoch shuffle: out[i] = perm_key(i), a keyed bijection of [0, n) (6-round
  * Feistel network over the smallest even-bit power-of-two domain >= n with
  * cycle walking; round keys from the 64-bit key).  Stands in for

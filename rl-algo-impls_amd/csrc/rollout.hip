@@ -307,6 +307,37 @@ __global__ __launch_bounds__(256) void gaussian_sample_kernel(
 
 }  // namespace
 
+// Rollout host <-> device staging in one native call each (the env-step loop of
+// rl_algo_impls/rollout/sync_step_rollout.py:193-207: actions to the host env, then its rewards,
+// terminations and next observations back).  Issued here rather than as separate torch copies, whose
+// per-call dispatch costs ~10 us each on the 128-step C2 loop.
+extern "C" int rai_copy_d2h_sync(const void* src, void* dst, int64_t bytes, void* stream) {
+  if (bytes < 0) return RAI_E_SHAPE;
+  if (bytes == 0) return RAI_OK;
+  if (!src || !dst) return RAI_E_NULLPTR;
+  hipStream_t s = rai_stream(stream);
+  hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return (int)e;
+  e = hipStreamSynchronize(s);
+  return e == hipSuccess ? RAI_OK : (int)e;
+}
+
+extern "C" int rai_copy_h2d_multi(int32_t n, void* const* dst, const void* const* src, const int64_t* bytes,
+                                  void* stream) {
+  if (n < 0 || n > RAI_MAX_FIELDS) return RAI_E_SHAPE;
+  if (n == 0) return RAI_OK;
+  if (!dst || !src || !bytes) return RAI_E_NULLPTR;
+  hipStream_t s = rai_stream(stream);
+  for (int i = 0; i < n; ++i) {
+    if (bytes[i] < 0) return RAI_E_SHAPE;
+    if (bytes[i] == 0) continue;
+    if (!dst[i] || !src[i]) return RAI_E_NULLPTR;
+    const hipError_t e = hipMemcpyAsync(dst[i], src[i], (size_t)bytes[i], hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  return RAI_OK;
+}
+
 extern "C" int rai_gather_rows(int32_t n_fields, const void* const* src, void* const* dst,
                                const int64_t* row_bytes, const int64_t* idx, int64_t n_rows,
                                void* stream) {

@@ -520,6 +520,9 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         # starts go host -> device straight into slot s + 1 (two device copies per step fewer); the other
         # policies' graph-replayed forwards read the fixed next_obs_dev buffer, so they keep the slot copy
         direct = self.fused_step is not None and os.environ.get("RAI_ROLLOUT_DIRECT", "1") != "0"
+        if direct and self.action_masks is None and os.environ.get("RAI_ROLLOUT_NATIVE", "1") != "0":
+            self._fused_step_loop()
+            return self._finish_rollout(output_next_values)
         for s in range(self.n_steps):
             if not direct or s == 0:
                 self.obs[s].copy_(self.next_obs_dev)
@@ -551,6 +554,62 @@ class SyncStepRolloutGenerator(RolloutGenerator):
                                                                                            non_blocking=True)
             self._stage_obs(obs, self.obs[s + 1] if into_slot else None)
             self._stage_masks()
+        return self._finish_rollout(output_next_values)
+
+    def _fused_step_loop(self) -> None:
+        """The CartPole-class env-step loop with one native call per host <-> device hand-off: the fused
+        policy step (forward, sample, slot writes) into slot s, the actions copied to the pinned host
+        buffer and waited for (rai_copy_d2h_sync), the host env step, then the rewards, terminations and
+        next observations copied straight into their slots (rai_copy_h2d_multi).  Same kernels, same
+        sampler stream and the same slot contents as the generic loop above (RAI_ROLLOUT_NATIVE=0); the
+        per-step torch copy / event dispatches it replaces cost ~45 us of the ~95 us step at C2."""
+        L = _lib.lib()
+        sp = self.fused_step
+        pi, v = self._layer_ptrs()
+        st = _lib.stream_handle(self.device)
+        N, T = self.num_envs, self.n_steps
+        self.obs[0].copy_(self.next_obs_dev)
+        self.episode_starts[0].copy_(self.next_episode_starts)
+        slot = lambda t: (t.data_ptr(), t[0].numel() * t.element_size())  # base, bytes per step slot
+        (ob, obs_b), (ab, act_b), (lb, lp_b), (vb, v_b), (rb, rew_b), (eb, es_b) = (
+            slot(self.obs), slot(self.actions), slot(self.logprobs), slot(self.values), slot(self.rewards),
+            slot(self.episode_starts))
+        h_act, h_rew, h_done, h_obs = self.h_act, self.h_rew, self.h_done, self.h_obs
+        assert h_act.numel() * h_act.element_size() == act_b and h_obs.numel() * h_obs.element_size() == obs_b
+        h_act_np, h_rew_np, h_done_np, h_obs_np = h_act.numpy(), h_rew.numpy(), h_done.numpy(), h_obs.numpy()
+        dst = (C.c_void_p * 3)()
+        src = (C.c_void_p * 3)(h_rew.data_ptr(), h_done.data_ptr(), h_obs.data_ptr())
+        nbytes = (C.c_int64 * 3)(rew_b, es_b, obs_b)
+        last = (self.next_episode_starts.data_ptr(), self.next_obs_dev.data_ptr())
+        in_dim, n_act, act_fn = sp["in_dim"], sp["n_act"], sp["activation"]
+        for s in range(T):
+            rc = L.rai_mlp_policy_step(pi, v, ob + s * obs_b, N, in_dim, 64, n_act, act_fn, self.seed, self.rng_offset,
+                                       ab + s * act_b, lb + s * lp_b, vb + s * v_b, st)
+            if rc:
+                _lib.check(rc, "rai_mlp_policy_step")
+            self.rng_offset += 1
+            rc = L.rai_copy_d2h_sync(ab + s * act_b, h_act_np.ctypes.data, act_b, st)
+            if rc:
+                _lib.check(rc, "rai_copy_d2h_sync")
+            obs, rew, term, trunc, info = self.vec_env.step(h_act_np)
+            if info and "episode" in info:
+                done_mask = np.asarray(info.get("_episode", np.ones(self.num_envs, dtype=bool)))
+                self.episode_returns.extend(np.asarray(info["episode"]["r"])[done_mask].tolist())
+                self.episode_lengths.extend(np.asarray(info["episode"]["l"])[done_mask].tolist())
+            np.copyto(h_rew_np, rew, casting="same_kind")
+            np.logical_or(term, trunc, out=h_done_np)
+            np.copyto(h_obs_np, obs, casting="same_kind")
+            dst[0] = rb + s * rew_b
+            if s + 1 < T:
+                dst[1], dst[2] = eb + (s + 1) * es_b, ob + (s + 1) * obs_b
+            else:
+                dst[1], dst[2] = last
+            rc = L.rai_copy_h2d_multi(3, dst, src, nbytes, st)
+            if rc:
+                _lib.check(rc, "rai_copy_h2d_multi")
+
+    def _finish_rollout(self, output_next_values: bool) -> Optional[torch.Tensor]:
+        net = self.policy.network
         next_values = None
         if output_next_values:
             if self.fused_step is not None:

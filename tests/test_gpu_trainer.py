@@ -655,8 +655,9 @@ def test_fused_rollout_direct_slot_staging_is_identical(monkeypatch):
     from rl_algo_impls_amd.policy import ActorCritic
 
     out = []
-    for direct in ("1", "0"):
+    for direct, native in (("1", "1"), ("1", "0"), ("0", "0")):
         monkeypatch.setenv("RAI_ROLLOUT_DIRECT", direct)
+        monkeypatch.setenv("RAI_ROLLOUT_NATIVE", native)  # the native staging loop (default) vs torch copies
         torch.manual_seed(3)
         env = SyntheticVecEnv(96, "cartpole", seed=5)
         policy = ActorCritic(env).to(DEV)
@@ -670,6 +671,7 @@ def test_fused_rollout_direct_slot_staging_is_identical(monkeypatch):
                                                                    gen.values, gen.logprobs, r.next_values,
                                                                    r.next_episode_starts, r.advantages)])
         out.append(res)
-    for a, b in zip(out[0], out[1]):
-        for x, y in zip(a, b):
-            np.testing.assert_array_equal(x, y)
+    for other in out[1:]:
+        for a, b in zip(out[0], other):
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
