@@ -192,6 +192,16 @@ int rai_bias_relu_bwd_nchw(const float* dy, const float* y, int64_t B, int32_t H
 int rai_conv2d_bias_relu_fwd(const float* x, const float* w, const float* b, int64_t B, int32_t H, int32_t W,
                              int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, int32_t out_nchw,
                              float* y, void* stream);
+/* Split-K form (round 5): where the default tiling leaves CUs idle (NatureCNN conv2 / conv3 at the update
+ * minibatch B = 256), the reduction is cut in two halves run as separate workgroups (two per CU, half the
+ * LDS-resident weights each) whose raw sums go to `part` (rai_conv2d_fwd_splitk_bytes(...) bytes, 0 when
+ * the shape takes no split: the call is then rai_conv2d_bias_relu_fwd), and a second pass adds them in
+ * order with the bias and the ReLU. Same results as the one-pass form up to fp32 summation order. */
+int64_t rai_conv2d_fwd_splitk_bytes(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW,
+                                    int32_t stride, int32_t out_nchw);
+int rai_conv2d_bias_relu_fwd_splitk(const float* x, const float* w, const float* b, int64_t B, int32_t H, int32_t W,
+                                    int32_t Ci, int32_t Co, int32_t KH, int32_t KW, int32_t stride, int32_t out_nchw,
+                                    float* y, float* part, int64_t part_bytes, void* stream);
 /* The same with a fixed workgroup blocking (variant 0 = chosen by shape, as above; 1-15 = the blockings, prefetch depths and LDS-resident-weight forms
  * in csrc/conv.hip, for same-box A/B timing in tools/conv_bench.py). */
 int rai_conv2d_bias_relu_fwd_v(const float* x, const float* w, const float* b, int64_t B, int32_t H, int32_t W,

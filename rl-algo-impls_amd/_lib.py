@@ -182,6 +182,9 @@ _SIGNATURES = {
     "rai_bias_relu_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "rai_bias_relu_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "rai_bias_relu_fwd_nchw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "rai_conv2d_fwd_splitk_bytes": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32]),
+    "rai_conv2d_bias_relu_fwd_splitk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                                  _vp, _vp, _i64, _vp]),
     "rai_conv2d_bias_relu_fwd": (C.c_int, [_vp, _vp, _vp, _i64] + [_i32] * 8 + [_vp, _vp]),
     "rai_conv2d_bias_relu_fwd_v": (C.c_int, [_vp, _vp, _vp, _i64] + [_i32] * 8 + [_vp, _i32, _vp]),
     "rai_conv2d_wgrad_workspace_bytes": (_i64, [_i64] + [_i32] * 7),

@@ -297,6 +297,13 @@ def _conv_fwd_mfma(x, w, b, stride, flatten, x_div=None) -> torch.Tensor:
                                                  Co, KH, KW, s, 1 if flatten else 0, y.data_ptr(),
                                                  _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd_u8")
         return y
+    nb = int(L.rai_conv2d_fwd_splitk_bytes(B, H, W, Ci, Co, KH, KW, s, 1 if flatten else 0))
+    if nb > 0:  # split-K where the tiling leaves CUs idle (conv2 / conv3 at B = 256): partials + ordered sum
+        part = torch.empty(nb // 4, dtype=torch.float32, device=x.device)
+        _lib.check(L.rai_conv2d_bias_relu_fwd_splitk(x.data_ptr(), w.data_ptr(), b.data_ptr(), B, H, W, Ci, Co, KH, KW,
+                                                     s, 1 if flatten else 0, y.data_ptr(), part.data_ptr(), nb,
+                                                     _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd_splitk")
+        return y
     _lib.check(L.rai_conv2d_bias_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), B, H, W, Ci, Co, KH,
                                           KW, s, 1 if flatten else 0, y.data_ptr(),
                                           _lib.stream_handle(x.device)), "rai_conv2d_bias_relu_fwd")

@@ -25,6 +25,8 @@
 // float4 and issues 4 * TCO * TPX MFMAs.  Operands are read straight from global memory (L1/L2:
 // the weights are shared by every workgroup, overlapping receptive fields re-read the same lines),
 // two quads in flight per wave.
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <unordered_map>
 #include <unordered_set>
@@ -48,6 +50,11 @@ struct ConvFwdArgs {
   float* y;
   int64_t M;  // B * OH * OW output pixels
   int H, W, Ci, Co, KW, S, OH, OW, K;
+  // split-K (conv_fwd_lds_kernel only): blockIdx.z takes quads [nq z / ksplit, nq (z + 1) / ksplit) of the
+  // reduction and, with ksplit > 1, stores its raw partial sums to part[z][p][co] (no bias / ReLU);
+  // conv_fwd_splitk_reduce_kernel then adds the splits in order, the bias and the ReLU
+  int ksplit = 1;
+  float* part = nullptr;
 };
 
 // The uint8 forms' x = u / d for the four bytes of a dword.  U8 == 1: a 256-entry LDS table of the IEEE
@@ -225,16 +232,20 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   __shared__ float lut[U8 == 1 ? 256 : 1];  // U8 == 1: lut[u] = u / xdiv (IEEE division, as the gather's prescale)
   if (U8 == 1)
     for (int i = threadIdx.x; i < 256; i += 512) lut[i] = (float)i / a.xdiv;
-  const int K = a.K, KP = K + 4;
-  const int nch = K >> 2;
+  const int K = a.K;
+  // this split's chunk range [c0, c0 + nch) of the K / 4 chunks, in whole quads
+  const int zs = blockIdx.z, nq_all = K >> 4;
+  const int q0 = (int)((int64_t)nq_all * zs / a.ksplit), q1 = (int)((int64_t)nq_all * (zs + 1) / a.ksplit);
+  const int c0 = 4 * q0, nch = 4 * (q1 - q0), KP = 4 * nch + 4;
   const int co_wg = blockIdx.y * COT;
   for (int q = threadIdx.x; q < nch; q += 512) {
-    const int k = 4 * q, kpos = k / a.Ci, ci0 = k - kpos * a.Ci, kh = kpos / a.KW, kw = kpos - kh * a.KW;
+    const int k = 4 * (c0 + q), kpos = k / a.Ci, ci0 = k - kpos * a.Ci, kh = kpos / a.KW, kw = kpos - kh * a.KW;
     xoff[q] = (kh * a.W + kw) * a.Ci + ci0;
   }
   for (int e = threadIdx.x; e < COT * nch; e += 512) {
     const int r = e / nch, q = e - r * nch;
-    *reinterpret_cast<f4*>(wl + r * KP + 4 * q) = *reinterpret_cast<const f4*>(a.w + (int64_t)(co_wg + r) * K + 4 * q);
+    *reinterpret_cast<f4*>(wl + r * KP + 4 * q) =
+        *reinterpret_cast<const f4*>(a.w + (int64_t)(co_wg + r) * K + 4 * (c0 + q));
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -336,6 +347,18 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
         }
       }
     }
+    if (a.ksplit > 1) {  // raw partial sums of this split, [z][p][co]
+#pragma unroll
+      for (int tc = 0; tc < TCO; ++tc) {
+        const int co = co_wg + 16 * (TCO * wco + tc) + 4 * g;
+#pragma unroll
+        for (int tp = 0; tp < TPX; ++tp) {
+          const int64_t p = px0 + 16 * tp + li;
+          if (p < a.M) *reinterpret_cast<f4*>(a.part + ((int64_t)zs * a.M + p) * a.Co + co) = acc[tc][tp];
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int tc = 0; tc < TCO; ++tc) {
       const int co = co_wg + 16 * (TCO * wco + tc) + 4 * g;
@@ -368,14 +391,24 @@ int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   constexpr int PXT = 16 * TPX * WPX, COT = 16 * TCO * WCO;
   if (a.Co % COT) return RAI_E_SHAPE;
   if (BUF && (a.M / ((int64_t)a.OH * a.OW)) * a.H * a.W * a.Ci * (U8 ? 1 : 4) >= (1LL << 31)) return RAI_E_SHAPE;
-  const size_t lds = (size_t)COT * (a.K + 4) * sizeof(float);
+  const int nq_all = a.K >> 4, ks = a.ksplit < 1 ? 1 : a.ksplit;
+  if (ks > 1 && (!a.part || ks > nq_all)) return RAI_E_SHAPE;
+  const int ksplit_k = 16 * ((nq_all + ks - 1) / ks);  // the largest split's K
+  const size_t lds = (size_t)COT * (ksplit_k + 4) * sizeof(float);
   if (lds + CV_MAXCHUNK * 4 > 160 * 1024) return RAI_E_SHAPE;
   const int64_t ntiles = (a.M + PXT - 1) / PXT;
   const int64_t cot = a.Co / COT;
-  int64_t gx = num_cus() / cot;  // one persistent workgroup per CU
+  // persistent workgroups: two per CU for the small-K layer (conv1: 33 KB of weight rows; every
+  // instantiation stays under 128 VGPRs), so its 400 tiles at B = 256 run as one round of co-resident
+  // workgroups instead of two rounds of one: conv1 23.8 vs 25.5 us (u8 26.9 vs 27.9) at B = 256, 68.1 vs
+  // 76.8 us at 1,024.  Not for the 66-75 KB layers: conv2 at B = 1,024 took 73.0 vs 59.8 us with two
+  // (profiles/r5l_conv_bench_*.txt).  RAI_CONV_FWD_WPC=1 / 2 forces one / two.
+  const char* we = getenv("RAI_CONV_FWD_WPC");
+  const int wpc = (we && !strcmp(we, "1")) ? 1 : (we && !strcmp(we, "2")) ? 2 : (lds <= 40 * 1024 ? 2 : 1);
+  int64_t gx = (int64_t)wpc * num_cus() / cot;  // per split
   if (gx > ntiles) gx = ntiles;
   if (gx < 1) gx = 1;
-  const dim3 grid((unsigned)gx, (unsigned)cot);
+  const dim3 grid((unsigned)gx, (unsigned)cot, (unsigned)ks);
   if (nchw) {
     auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF, BUF, U8>;
     const int e = allow_lds(reinterpret_cast<const void*>(k));
@@ -404,6 +437,51 @@ int launch_fwd(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
     hipLaunchKernelGGL((conv_fwd_kernel<TCO, TPX, WCO, WPX, false, PF>), grid, dim3(CV_THREADS), 0, st, a);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
+}
+
+// Split-K forward's second pass: y = ReLU(sum over the splits in order of part[z] + b).  NHWC output: one
+// float4 of 4 channels per thread (the partials' own layout).  NCHW output (the layer nn.Flatten follows):
+// one workgroup per image, the image's OH*OW x Co tile summed into LDS, then written in the flattened
+// (co, oh, ow) order, coalesced both ways.
+constexpr int CV_RED_NCHW_MAX = 8192;  // floats of one image's output tile in LDS
+__global__ __launch_bounds__(256) void conv_fwd_splitk_reduce_kernel(const float* __restrict__ part, int S, int64_t M,
+                                                                     int Co, const float* __restrict__ b, float* y,
+                                                                     int nchw, int OHW) {
+  if (!nchw) {
+    const int64_t n4 = M * Co / 4;
+    const f4* p4 = reinterpret_cast<const f4*>(part);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+      f4 v = p4[i];
+      for (int z = 1; z < S; ++z) v += p4[z * n4 + i];
+      const f4 bv = *reinterpret_cast<const f4*>(b + (int)((4 * i) % Co));
+      f4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t = v[r] + bv[r];
+        o[r] = t < 0.f ? 0.f : t;
+      }
+      reinterpret_cast<f4*>(y)[i] = o;
+    }
+    return;
+  }
+  __shared__ float t[CV_RED_NCHW_MAX];
+  const int64_t n = blockIdx.x;
+  const int e4 = OHW * Co / 4;
+  const f4* p4 = reinterpret_cast<const f4*>(part + n * OHW * Co);
+  const int64_t zs4 = M * Co / 4;
+  for (int i = threadIdx.x; i < e4; i += 256) {  // [r][co] order, 4 channels per thread
+    f4 v = p4[i];
+    for (int z = 1; z < S; ++z) v += p4[z * zs4 + i];
+    const int r = (4 * i) / Co, co = (4 * i) - r * Co;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float tt = v[q] + b[co + q];
+      t[(co + q) * OHW + r] = tt < 0.f ? 0.f : tt;
+    }
+  }
+  __syncthreads();
+  float* yn = y + n * OHW * Co;
+  for (int i = threadIdx.x; i < OHW * Co; i += 256) yn[i] = t[i];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1618,6 +1696,95 @@ extern "C" int rai_conv2d_bias_relu_fwd_u8(const uint8_t* x, float x_divisor, co
   if (Co % 64 == 0 && lds64 + CV_MAXCHUNK * 4 <= 160 * 1024)
     return valu ? launch_fwd_lds<2, 1, 2, 4, 4, true, 2>(a, nchw, st) : launch_fwd_lds<2, 1, 2, 4, 4, true, 1>(a, nchw, st);
   return RAI_E_UNSUPPORTED;
+}
+
+// Split-K factor the forward takes for a shape (1: none): 2 where the default LDS-weight variant's tiles
+// leave CUs idle (fewer tile workgroups than CUs) and each half keeps >= 8 quads of the reduction, so the
+// two halves run as twice the workgroups, two per CU (half the LDS each); then a second pass adds them.
+// Opt-in (RAI_CONV_FWD_SPLITK=1): measured SLOWER than the one-pass forward at the C3 update's B = 256
+// (conv2 27.8 vs 23.1 us, conv3 24.7 vs 17.8 us, profiles/r5l_conv_bench_*.txt): the partials' extra
+// 2 x 3-6 MB and the second launch cost more than the idle CUs the split fills.
+static int fwd_splitk_factor(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW,
+                             int32_t stride, int32_t out_nchw) {
+  const char* e = getenv("RAI_CONV_FWD_SPLITK");
+  if (!(e && !strcmp(e, "1"))) return 1;
+  if (B < 1 || Ci % 4 || Co % 64 || stride < 1 || KH > H || KW > W) return 1;
+  const int64_t K = (int64_t)KH * KW * Ci;
+  if (K % 32 || K / 4 > CV_MAXCHUNK || K / 16 < 16) return 1;
+  const int64_t OH = (H - KH) / stride + 1, OW = (W - KW) / stride + 1, M = B * OH * OW;
+  if (out_nchw && OH * OW * Co > CV_RED_NCHW_MAX) return 1;
+  // the default variant's workgroup tiles (16: 32 co x 256 px, 17: 64 co x 64 px; see rai_conv2d_bias_relu_fwd_v)
+  const int ncu = num_cus();
+  const size_t lds32 = (size_t)32 * (K + 4) * 4;
+  const int64_t wg32 = ncu / (Co / 32), wg64 = ncu / (Co / 64);
+  const int64_t rounds32 = ((M + 255) / 256 + wg32 - 1) / wg32, rounds64 = ((M + 63) / 64 + wg64 - 1) / wg64;
+  const bool v32 = lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && 2 * rounds32 <= rounds64;
+  const int64_t tiles = v32 ? (M + 255) / 256 * (Co / 32) : (M + 63) / 64 * (Co / 64);
+  return tiles < ncu ? 2 : 1;
+}
+
+extern "C" int64_t rai_conv2d_fwd_splitk_bytes(int64_t B, int32_t H, int32_t W, int32_t Ci, int32_t Co, int32_t KH,
+                                               int32_t KW, int32_t stride, int32_t out_nchw) {
+  const int S = fwd_splitk_factor(B, H, W, Ci, Co, KH, KW, stride, out_nchw);
+  if (S < 2) return 0;
+  const int64_t OH = (H - KH) / stride + 1, OW = (W - KW) / stride + 1;
+  return (int64_t)S * B * OH * OW * Co * (int64_t)sizeof(float);
+}
+
+extern "C" int rai_conv2d_bias_relu_fwd_splitk(const float* x, const float* w, const float* b, int64_t B, int32_t H,
+                                               int32_t W, int32_t Ci, int32_t Co, int32_t KH, int32_t KW,
+                                               int32_t stride, int32_t out_nchw, float* y, float* part,
+                                               int64_t part_bytes, void* stream) {
+  const int S = fwd_splitk_factor(B, H, W, Ci, Co, KH, KW, stride, out_nchw);
+  if (S < 2) return rai_conv2d_bias_relu_fwd_v(x, w, b, B, H, W, Ci, Co, KH, KW, stride, out_nchw, y, 0, stream);
+  if (!x || !w || !b || !y || !part) return RAI_E_NULLPTR;
+  if (part_bytes < rai_conv2d_fwd_splitk_bytes(B, H, W, Ci, Co, KH, KW, stride, out_nchw)) return RAI_E_WORKSPACE;
+  if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y | (uintptr_t)part) & 15) return RAI_E_SHAPE;
+  if ((int64_t)H * W * Ci * B > (1LL << 40)) return RAI_E_SHAPE;
+  ConvFwdArgs a;
+  a.x = x;
+  a.xu8 = nullptr;
+  a.xdiv = 1.f;
+  a.xinv = 1.f;
+  a.w = w;
+  a.b = b;
+  a.y = y;
+  a.H = H;
+  a.W = W;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.KW = KW;
+  a.S = stride;
+  a.OH = (H - KH) / stride + 1;
+  a.OW = (W - KW) / stride + 1;
+  a.K = KH * KW * Ci;
+  a.M = B * a.OH * a.OW;
+  a.ksplit = S;
+  a.part = part;
+  hipStream_t st = rai_stream(stream);
+  const bool buf = B * H * W * (int64_t)Ci * 4 < (1LL << 31);
+  const size_t lds32 = (size_t)32 * (a.K + 4) * 4;
+  const int ncu = num_cus();
+  const int64_t wg32 = ncu / (Co / 32), wg64 = ncu / (Co / 64);
+  const int64_t rounds32 = ((a.M + 255) / 256 + wg32 - 1) / wg32, rounds64 = ((a.M + 63) / 64 + wg64 - 1) / wg64;
+  int e;
+  if (lds32 + CV_MAXCHUNK * 4 <= 160 * 1024 && 2 * rounds32 <= rounds64)
+    e = buf ? launch_fwd_lds<2, 2, 1, 8, 3, true>(a, false, st) : launch_fwd_lds<2, 2, 1, 8, 3>(a, false, st);
+  else
+    e = buf ? launch_fwd_lds<2, 1, 2, 4, 4, true>(a, false, st) : launch_fwd_lds<2, 1, 2, 4, 4>(a, false, st);
+  if (e != RAI_OK) return e;
+  const int OHW = a.OH * a.OW;
+  if (out_nchw) {
+    hipLaunchKernelGGL(conv_fwd_splitk_reduce_kernel, dim3((unsigned)B), dim3(256), 0, st, part, S, a.M, Co, b, y, 1,
+                       OHW);
+  } else {
+    int64_t blocks = (a.M * Co / 4 + 255) / 256;
+    if (blocks > 4 * ncu) blocks = 4 * ncu;
+    hipLaunchKernelGGL(conv_fwd_splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, S, a.M, Co, b, y,
+                       0, OHW);
+  }
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
 }
 
 extern "C" int rai_conv2d_bias_relu_fwd(const float* x, const float* w, const float* b, int64_t B, int32_t H,

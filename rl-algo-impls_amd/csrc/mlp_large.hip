@@ -247,11 +247,21 @@ __device__ __forceinline__ void lb_net(const LbArgs& a, LbSmem& S, int wgn) {
     for (int k = 10; k < 32; ++k) g_lb_stamps[blockIdx.x][threadIdx.x >> 6][k] = 0;
 #endif
   // ---- stage the weights in LDS (operand permutations for the MFMA chains) -------------------
-  for (int e = tid; e < 4 * 4 * 64 * 4; e += LB_NT) {
-    const int i = e & 3, l = (e >> 2) & 63, blk = (e >> 8) & 3, m = e >> 10;
-    const int lg = l >> 4, lj = l & 15;
-    S.w2f[m][blk][l][i] = a.params[base + oW2 + (16 * m + lj) * HID + 16 * blk + 4 * lg + i];
-    S.w2b[m][blk][l][i] = a.params[base + oW2 + (16 * blk + 4 * lg + i) * HID + 16 * m + lj];
+  {
+    // W2 read once, coalesced (element e = tid + LB_NT u, row-major), every load in flight before the
+    // first LDS store; each element then lands in both operand permutations:
+    //   w2f[m][blk][16 lg + lj][i] = W2[16 m + lj][16 blk + 4 lg + i]
+    //   w2b[m][blk][16 lg + lj][i] = W2[16 blk + 4 lg + i][16 m + lj]
+    constexpr int PER = HID * HID / LB_NT;
+    float wv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) wv[u] = a.params[base + oW2 + tid + LB_NT * u];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + LB_NT * u, r = e >> 6, c = e & 63;
+      S.w2f[r >> 4][c >> 4][16 * ((c & 15) >> 2) + (r & 15)][c & 3] = wv[u];
+      S.w2b[c >> 4][r >> 4][16 * ((r & 15) >> 2) + (c & 15)][r & 3] = wv[u];
+    }
   }
   for (int e = tid; e < HID * 4; e += LB_NT) {
     const int c = e >> 2, f = e & 3;

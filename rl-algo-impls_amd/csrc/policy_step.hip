@@ -5,9 +5,12 @@
 // rl_algo_impls/rollout/sync_step_rollout.py:193-201 — the per-step sequence that otherwise is
 // ~10 small PyTorch launches (3 linears + 2 activations per network) plus the sampling kernel.
 //
-// One wave per 16 env rows: layer 1 (one v_mfma_f32_16x16x4f32 per 16-column tile, K = in_dim
-// padded to 4/8), layer 2 (4 column tiles x 16 k-steps), the output layer as DPP row sums; the
-// weights of both networks are staged once per workgroup in LDS.  Sampling is the one of
+// A workgroup owns 32 env rows: waves 0-1 run the critic on its two 16-row tiles while waves 2-3 run
+// the actor on the same tiles (the two networks side by side instead of one after the other in every
+// wave: half the dependent chain per wave, twice the workgroups).  Per network and tile: layer 1 (one
+// v_mfma_f32_16x16x4f32 per 16-column tile, K = in_dim padded to 4/8), layer 2 (4 column tiles x 16
+// k-steps), the output layer as DPP row sums; the weights of both networks are staged once per
+// workgroup in LDS.  Sampling is the one of
 // rai_categorical_sample (Philox4x32-10 keyed by seed, counter (offset, row); inverse CDF on the
 // unnormalised mass), so the two paths draw from the same stream.
 #include "common.h"
@@ -21,8 +24,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr int HID = 64;
 constexpr int LD = 66;
-constexpr int NT = 256;        // 4 waves x 16 rows
-constexpr int ROWS = 64;
+constexpr int NT = 256;        // 4 waves: (critic, actor) x two 16-row tiles
+constexpr int ROWS = 32;
 
 struct NetPtrs {
   const float* W1;  // [64][in]
@@ -58,7 +61,7 @@ struct StepSmem {
   float b3a[8];
   float b3v;
   float X[ROWS][INP];
-  float H1[ROWS][LD];
+  float H1[2][ROWS][LD];  // per network
 };
 
 __device__ __forceinline__ int kmap(int g, int kk) { return (g & 1) * 32 + (g >> 1) * 16 + kk; }
@@ -215,27 +218,30 @@ __global__ __launch_bounds__(NT) void mlp_policy_step_kernel(const StepArgs a) {
   }
   __syncthreads();
 
-  const int R = w * 16;
+  const int R = (w & 1) * 16;  // this wave's 16-row tile; waves 0-1 the critic, 2-3 the actor
   const int q = li & 3;
   const int64_t my_row = row0 + R + g * 4 + q;  // the row whose outputs this lane writes (li < 4)
   float h2[4][4];
-  // ---- critic: value of every row ----
-  mlp_hidden<INP, RELU>(S.n[1], S.H1, S.X, R, g, li, h2);
-  float val = 0.f;
+  if (w < 2) {
+    // ---- critic: value of every row ----
+    mlp_hidden<INP, RELU>(S.n[1], S.H1[1], S.X, R, g, li, h2);
+    float val = 0.f;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float p = h2[0][r] * S.W3v[li];
-    p = fmaf(h2[1][r], S.W3v[16 + li], p);
-    p = fmaf(h2[2][r], S.W3v[32 + li], p);
-    p = fmaf(h2[3][r], S.W3v[48 + li], p);
-    const float s = row_sum16(p);
-    val = q == r ? s : val;
+    for (int r = 0; r < 4; ++r) {
+      float p = h2[0][r] * S.W3v[li];
+      p = fmaf(h2[1][r], S.W3v[16 + li], p);
+      p = fmaf(h2[2][r], S.W3v[32 + li], p);
+      p = fmaf(h2[3][r], S.W3v[48 + li], p);
+      const float s = row_sum16(p);
+      val = q == r ? s : val;
+    }
+    val += S.b3v;
+    if (li < 4 && my_row < a.N) a.values[my_row] = val;
+    return;
   }
-  val += S.b3v;
-  if (li < 4 && my_row < a.N) a.values[my_row] = val;
   if (!sample) return;
   // ---- actor: logits, categorical sample, log-prob ----
-  mlp_hidden<INP, RELU>(S.n[0], S.H1, S.X, R, g, li, h2);
+  mlp_hidden<INP, RELU>(S.n[0], S.H1[0], S.X, R, g, li, h2);
   float z[OUTP];
 #pragma unroll
   for (int o = 0; o < OUTP; ++o) {

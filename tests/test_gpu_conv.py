@@ -72,6 +72,42 @@ def test_conv_bias_relu_fwd_matches_fp64(case, B):
     assert (err <= tol).all(), float((err / tol).max())
 
 
+@pytest.mark.parametrize("case,B", [((32, 20, 64, 4, 2, False), 256), ((64, 9, 64, 3, 1, True), 256),
+                                    ((64, 9, 64, 3, 1, False), 200), ((64, 9, 64, 3, 1, True), 37)])
+def test_conv_fwd_splitk_matches_fp64_and_one_pass(case, B, monkeypatch):
+    """The split-K forward (rai_conv2d_bias_relu_fwd_splitk, opt-in: conv2 / conv3 of NatureCNN at the
+    update's B = 256, where the one-pass tiling leaves CUs idle): two halves of the reduction as separate
+    workgroups, raw partial sums, an ordered second pass with the bias and the ReLU (NHWC and the
+    flattened NCHW order).  Within the worst-case f32 summation bound of the fp64 convolution, close to
+    the one-pass kernel, and deterministic."""
+    Ci, H, Co, k, s, flat = case
+    monkeypatch.setenv("RAI_CONV_FWD_SPLITK", "1")  # opt-in (measured slower than the one-pass form)
+    L = _lib.lib()
+    nb = int(L.rai_conv2d_fwd_splitk_bytes(B, H, H, Ci, Co, k, k, s, 1 if flat else 0))
+    assert nb > 0, "the shape takes the split"
+    x, w, b = _inputs(B, Ci, H, Co, k, seed=B + 3)
+    OH = (H - k) // s + 1
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
+    bd = b.to(DEV)
+    outs = []
+    for _ in range(2):
+        y = torch.full((B, Co * OH * OH), float("nan"), device=DEV)
+        part = torch.full((nb // 4,), float("nan"), device=DEV)
+        _lib.check(L.rai_conv2d_bias_relu_fwd_splitk(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), B, H, H, Ci, Co, k, k,
+                                                     s, 1 if flat else 0, y.data_ptr(), part.data_ptr(), nb,
+                                                     _lib.stream_handle(DEV)), "rai_conv2d_bias_relu_fwd_splitk")
+        torch.cuda.synchronize()
+        outs.append(y.cpu())
+    assert torch.equal(outs[0], outs[1])
+    ref, bound = _reference(x, w, b, s, flat)
+    err = (outs[0].double() - ref).abs()
+    tol = (Ci * k * k + 2) * 2.0 ** -24 * bound + 1e-30
+    assert (err <= tol).all(), float((err / tol).max())
+    one = _run(x, w, b, s, flat)
+    torch.testing.assert_close(outs[0], one, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("variant", list(range(1, 21)))
 def test_conv_every_blocking_variant(variant):
     Ci, H, Co, k, s, flat = 32, 20, 64, 4, 2, False

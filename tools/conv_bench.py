@@ -88,6 +88,22 @@ def main():
                 err = (y[:8].double().cpu() - yd).abs().max().item() / max(yd.abs().max().item(), 1e-30)
                 t = timeit(mine, args.reps)
                 row[f"v{v}"] = {"us": round(t, 2), "tflops": round(row["flops"] / t / 1e6, 1), "relerr": err}
+            nbs = int(L.rai_conv2d_fwd_splitk_bytes(B, H, H, Ci, Co, k, k, s, 1 if flat else 0))
+            if nbs > 0:  # the split-K form the product takes for this shape (cnn_ops._conv_fwd_mfma)
+                part = torch.empty(nbs // 4, dtype=torch.float32, device=dev)
+
+                def mine_split():
+                    return L.rai_conv2d_bias_relu_fwd_splitk(x.data_ptr(), w.data_ptr(), b.data_ptr(), B, H, H, Ci,
+                                                             Co, k, k, s, 1 if flat else 0, y.data_ptr(),
+                                                             part.data_ptr(), nbs, st)
+                rc = mine_split()
+                if rc == 0:
+                    torch.cuda.synchronize()
+                    err = (y[:8].double().cpu() - yd).abs().max().item() / max(yd.abs().max().item(), 1e-30)
+                    t = timeit(mine_split, args.reps)
+                    row["splitk"] = {"us": round(t, 2), "tflops": round(row["flops"] / t / 1e6, 1), "relerr": err}
+                else:
+                    row["splitk"] = f"rc={rc}"
             if Ci == 4:  # conv1 on the uint8 frames (the product's C3 path): the same forward with the /255 in-kernel
                 xu = torch.randint(0, 256, (B, Ci, H, H), generator=g, dtype=torch.uint8).to(dev)
                 xu = xu.contiguous(memory_format=torch.channels_last)
