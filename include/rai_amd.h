@@ -525,6 +525,21 @@ int rai_mlp_policy_step(const float* const* pi_params, const float* const* v_par
                         int64_t N, int32_t in_dim, int32_t hidden, int32_t n_actions,
                         int32_t activation, uint64_t seed, uint64_t offset, int64_t* actions_out,
                         float* logp_out, float* values_out, void* stream);
+/* The same step with the env hand-off folded in (sync_step_rollout.py:193-207): obs_host / rew_host /
+ * done_host are DEVICE addresses of host-mapped pinned buffers (rai_host_alloc) holding the env's next
+ * observations (N x in_dim f32), rewards (N f32) and terminations (N u8); the kernel reads the
+ * observations from there and writes them into obs_slot, copies rewards / terminations into rew_dst /
+ * done_dst (either pair may be NULL), and writes the sampled actions to actions_out AND actions_host.
+ * One launch + rai_stream_sync per env step instead of the copies. */
+int rai_mlp_policy_step_mapped(const float* const* pi_params, const float* const* v_params, const float* obs_host,
+                               float* obs_slot, int64_t N, int32_t in_dim, int32_t hidden, int32_t n_actions,
+                               int32_t activation, uint64_t seed, uint64_t offset, int64_t* actions_out,
+                               float* logp_out, float* values_out, int64_t* actions_host, const float* rew_host,
+                               float* rew_dst, const uint8_t* done_host, uint8_t* done_dst, void* stream);
+/* Host-mapped (coherent) pinned memory: host_out for the CPU, dev_out for kernels. */
+int rai_host_alloc(int64_t bytes, void** host_out, void** dev_out);
+int rai_host_free(void* host);
+int rai_stream_sync(void* stream);
 
 /* --------------------------------------------------------------------------
  * Fused PPO epoch for MLP actor-critics (Flatten encoder, separate

@@ -144,6 +144,11 @@ _SIGNATURES = {
     "rai_gather_rows": (C.c_int, [_i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "rai_feistel_permutation": (C.c_int, [_i64, C.c_uint64, _vp, _vp]),
     "rai_copy_d2h_sync": (C.c_int, [_vp, _vp, _i64, _vp]),
+    "rai_mlp_policy_step_mapped": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _u64, _u64, _vp, _vp,
+                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rai_host_alloc": (C.c_int, [_i64, _vp, _vp]),
+    "rai_host_free": (C.c_int, [_vp]),
+    "rai_stream_sync": (C.c_int, [_vp]),
     "rai_copy_h2d_multi": (C.c_int, [_i32, _vp, _vp, _vp, _vp]),
     "rai_gae_trajectories": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _f64p, _f64p, _i32, _i32, _vp, _vp, _vp]),
     "rai_gridnet_logp_entropy": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -44,6 +44,15 @@ struct StepArgs {
   int64_t* actions;  // nullable (value-only call)
   float* logp;       // nullable
   float* values;     // [N]
+  // host-mapped staging (rai_mlp_policy_step_mapped; all nullable): obs_host replaces obs as the input and
+  // is copied into obs (the rollout slot); rew_host / done_host are copied into rew_dst / done_dst; the
+  // sampled actions are also written to act_host
+  const float* obs_host;
+  const float* rew_host;
+  float* rew_dst;
+  const uint8_t* done_host;
+  uint8_t* done_dst;
+  int64_t* act_host;
 };
 
 template <int INP>
@@ -195,11 +204,24 @@ __global__ __launch_bounds__(NT) void mlp_policy_step_kernel(const StepArgs a) {
   const float w3v = tid < HID ? a.v.W3[tid] : 0.f;
   const float b3a = (sample && tid < NA && tid < 8) ? a.pi.b3[tid] : 0.f;
   const float b3v = tid == 0 ? a.v.b3[0] : 0.f;
+  const float* xsrc = a.obs_host ? a.obs_host : a.obs;
 #pragma unroll
   for (int u = 0; u < XPT; ++u) {
     const int e = tid + u * NT, r = e / INP, k = e % INP;
     const int64_t row = row0 + r;
-    xv[u] = (e < ROWS * INP && row < a.N && k < IN) ? a.obs[row * IN + k] : 0.f;
+    xv[u] = (e < ROWS * INP && row < a.N && k < IN) ? xsrc[row * IN + k] : 0.f;
+  }
+  if (a.obs_host) {  // the observations into the rollout slot (vector stores)
+#pragma unroll
+    for (int u = 0; u < XPT; ++u) {
+      const int e = tid + u * NT, r = e / INP, k = e % INP;
+      const int64_t row = row0 + r;
+      if (e < ROWS * INP && row < a.N && k < IN) const_cast<float*>(a.obs)[row * IN + k] = xv[u];
+    }
+  }
+  if (tid < ROWS && row0 + tid < a.N) {
+    if (a.rew_host) a.rew_dst[row0 + tid] = a.rew_host[row0 + tid];
+    if (a.done_host) a.done_dst[row0 + tid] = a.done_host[row0 + tid];
   }
   store_net<INP>(rv, S.n[1], tid);
   if (sample) store_net<INP>(rp, S.n[0], tid);
@@ -283,6 +305,7 @@ __global__ __launch_bounds__(NT) void mlp_policy_step_kernel(const StepArgs a) {
     for (int o = 1; o < OUTP; ++o)
       if (o == act) zact = z[o];
     a.actions[my_row] = act;
+    if (a.act_host) a.act_host[my_row] = act;
     a.logp[my_row] = zact - lse;
   }
 }
@@ -324,4 +347,79 @@ extern "C" int rai_mlp_policy_step(const float* const* pi_params, const float* c
   else launch_step<8, 8>(a, activation, s);
   RAI_LAUNCH_CHECK();
   return RAI_OK;
+}
+
+// The same step with the host hand-off folded in (the CartPole-class rollout loop,
+// rl_algo_impls/rollout/sync_step_rollout.py:193-207): the env's next observations, rewards and
+// terminations are read by the kernel straight from host-mapped pinned memory (rai_host_alloc) and
+// written into their rollout slots, and the actions are written to host-mapped memory as well, so one
+// launch and one stream wait replace three H2D copies, the D2H copy and their API calls per env step.
+extern "C" int rai_mlp_policy_step_mapped(const float* const* pi_params, const float* const* v_params,
+                                          const float* obs_host, float* obs_slot, int64_t N, int32_t in_dim,
+                                          int32_t hidden, int32_t n_actions, int32_t activation, uint64_t seed,
+                                          uint64_t offset, int64_t* actions_out, float* logp_out,
+                                          float* values_out, int64_t* actions_host, const float* rew_host,
+                                          float* rew_dst, const uint8_t* done_host, uint8_t* done_dst,
+                                          void* stream) {
+  if (!v_params || !obs_slot || !values_out || !pi_params || !actions_out || !logp_out) return RAI_E_NULLPTR;
+  if ((rew_host == nullptr) != (rew_dst == nullptr) || (done_host == nullptr) != (done_dst == nullptr))
+    return RAI_E_NULLPTR;
+  if (hidden != HID || in_dim < 1 || in_dim > 8 || n_actions < 1 || n_actions > 8 || N < 1 ||
+      (activation != 0 && activation != 1))
+    return RAI_E_SHAPE;
+  for (int i = 0; i < 6; ++i)
+    if (!v_params[i] || !pi_params[i]) return RAI_E_NULLPTR;
+  StepArgs a = {};
+  a.pi = {pi_params[0], pi_params[1], pi_params[2], pi_params[3], pi_params[4], pi_params[5]};
+  a.v = {v_params[0], v_params[1], v_params[2], v_params[3], v_params[4], v_params[5]};
+  a.obs = obs_slot;
+  a.N = N;
+  a.in_dim = in_dim;
+  a.n_act = n_actions;
+  a.seed = seed;
+  a.offset = offset;
+  a.actions = actions_out;
+  a.logp = logp_out;
+  a.values = values_out;
+  a.obs_host = obs_host;
+  a.rew_host = rew_host;
+  a.rew_dst = rew_dst;
+  a.done_host = done_host;
+  a.done_dst = done_dst;
+  a.act_host = actions_host;
+  hipStream_t s = rai_stream(stream);
+  if (in_dim <= 4 && n_actions <= 2) launch_step<4, 2>(a, activation, s);
+  else launch_step<8, 8>(a, activation, s);
+  RAI_LAUNCH_CHECK();
+  return RAI_OK;
+}
+
+// Host-mapped pinned memory for the kernels above: coherent (fine-grained) host memory the GPU reads and
+// writes over the bus, with its device-side address.
+extern "C" int rai_host_alloc(int64_t bytes, void** host_out, void** dev_out) {
+  if (bytes < 1) return RAI_E_SHAPE;
+  if (!host_out || !dev_out) return RAI_E_NULLPTR;
+  void* h = nullptr;
+  hipError_t e = hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return (int)e;
+  }
+  *host_out = h;
+  *dev_out = d;
+  return RAI_OK;
+}
+
+extern "C" int rai_host_free(void* host) {
+  if (!host) return RAI_OK;
+  const hipError_t e = hipHostFree(host);
+  return e == hipSuccess ? RAI_OK : (int)e;
+}
+
+extern "C" int rai_stream_sync(void* stream) {
+  const hipError_t e = hipStreamSynchronize(rai_stream(stream));
+  return e == hipSuccess ? RAI_OK : (int)e;
 }

@@ -30,6 +30,7 @@ from typing import Callable, Deque, Dict, Iterator, List, Optional
 
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -108,6 +109,11 @@ class RolloutGenerator(ABC):
 
     @abstractmethod
     def rollout(self, **kwargs) -> Rollout: ...
+
+
+def _free_host_buffers(hosts: List[int]) -> None:
+    for h in hosts:
+        _lib.lib().rai_host_free(C.c_void_p(h))
 
 
 def feistel_permutation(n: int, device: torch.device, key: Optional[int] = None) -> torch.Tensor:
@@ -521,7 +527,10 @@ class SyncStepRolloutGenerator(RolloutGenerator):
         # policies' graph-replayed forwards read the fixed next_obs_dev buffer, so they keep the slot copy
         direct = self.fused_step is not None and os.environ.get("RAI_ROLLOUT_DIRECT", "1") != "0"
         if direct and self.action_masks is None and os.environ.get("RAI_ROLLOUT_NATIVE", "1") != "0":
-            self._fused_step_loop()
+            if os.environ.get("RAI_ROLLOUT_MAPPED", "1") != "0" and self.obs_dtype == torch.float32:
+                self._fused_step_loop_mapped()
+            else:
+                self._fused_step_loop()
             return self._finish_rollout(output_next_values)
         for s in range(self.n_steps):
             if not direct or s == 0:
@@ -607,6 +616,82 @@ class SyncStepRolloutGenerator(RolloutGenerator):
             rc = L.rai_copy_h2d_multi(3, dst, src, nbytes, st)
             if rc:
                 _lib.check(rc, "rai_copy_h2d_multi")
+
+    def _mapped_buffers(self) -> Dict[str, tuple]:
+        """Host-mapped pinned staging buffers (rai_host_alloc: coherent host memory the policy-step kernel
+        reads and writes directly) for the env hand-off: name -> (host address, device address, numpy view)."""
+        if getattr(self, "_mapped", None) is None:
+            L = _lib.lib()
+            N = self.num_envs
+            in_dim = int(np.prod(self.obs.shape[2:]))
+            bufs: Dict[str, tuple] = {}
+            for name, n, dt in (("obs", N * in_dim, np.float32), ("rew", N, np.float32), ("done", N, np.uint8),
+                                ("act", N, np.int64)):
+                nbytes = n * np.dtype(dt).itemsize
+                h, d = C.c_void_p(), C.c_void_p()
+                rc = L.rai_host_alloc(nbytes, C.byref(h), C.byref(d))
+                if rc:
+                    for hh, _, _ in bufs.values():
+                        L.rai_host_free(C.c_void_p(hh))
+                    _lib.check(rc, "rai_host_alloc")
+                arr = np.frombuffer((C.c_char * nbytes).from_address(h.value), dtype=dt)
+                bufs[name] = (h.value, d.value, arr)
+            bufs["obs"] = bufs["obs"][:2] + (bufs["obs"][2].reshape(N, in_dim),)
+            weakref.finalize(self, _free_host_buffers, [b[0] for b in bufs.values()])
+            self._mapped = bufs
+        return self._mapped
+
+    def _fused_step_loop_mapped(self) -> None:
+        """The CartPole-class env-step loop with ONE launch and one stream wait per env step: the policy
+        step kernel reads the env's next observations, rewards and terminations straight from host-mapped
+        pinned memory into their slots and writes the sampled actions to host-mapped memory too
+        (rai_mlp_policy_step_mapped), so no per-step copy is issued.  Same kernel arithmetic and sampler
+        stream as _fused_step_loop (RAI_ROLLOUT_MAPPED=0), bit-identical buffers."""
+        L = _lib.lib()
+        sp = self.fused_step
+        pi, v = self._layer_ptrs()
+        st = _lib.stream_handle(self.device)
+        N, T = self.num_envs, self.n_steps
+        m = self._mapped_buffers()
+        (obs_h, obs_d, obs_np), (rew_h, rew_d, rew_np), (done_h, done_d, done_np), (act_h, act_d, act_np) = (
+            m["obs"], m["rew"], m["done"], m["act"])
+        self.obs[0].copy_(self.next_obs_dev)
+        self.episode_starts[0].copy_(self.next_episode_starts)
+        slot = lambda t: (t.data_ptr(), t[0].numel() * t.element_size())
+        (ob, obs_b), (ab, act_b), (lb, lp_b), (vb, v_b), (rb, rew_b), (eb, es_b) = (
+            slot(self.obs), slot(self.actions), slot(self.logprobs), slot(self.values), slot(self.rewards),
+            slot(self.episode_starts))
+        assert obs_np.nbytes == obs_b and act_np.nbytes == act_b and rew_np.nbytes == rew_b and done_np.nbytes == es_b
+        in_dim, n_act, act_fn = sp["in_dim"], sp["n_act"], sp["activation"]
+        for s in range(T):
+            if s == 0:  # slot 0 already holds next_obs_dev / next_episode_starts (device copies above)
+                rc = L.rai_mlp_policy_step_mapped(pi, v, None, ob, N, in_dim, 64, n_act, act_fn, self.seed,
+                                                  self.rng_offset, ab, lb, vb, act_d, None, None, None, None, st)
+            else:  # step s - 1's env results: observations -> obs slot s, rewards -> slot s - 1, starts -> slot s
+                rc = L.rai_mlp_policy_step_mapped(pi, v, obs_d, ob + s * obs_b, N, in_dim, 64, n_act, act_fn,
+                                                  self.seed, self.rng_offset, ab + s * act_b, lb + s * lp_b,
+                                                  vb + s * v_b, act_d, rew_d, rb + (s - 1) * rew_b, done_d,
+                                                  eb + s * es_b, st)
+            if rc:
+                _lib.check(rc, "rai_mlp_policy_step_mapped")
+            self.rng_offset += 1
+            rc = L.rai_stream_sync(st)
+            if rc:
+                _lib.check(rc, "rai_stream_sync")
+            obs, rew, term, trunc, info = self.vec_env.step(act_np)
+            if info and "episode" in info:
+                done_mask = np.asarray(info.get("_episode", np.ones(self.num_envs, dtype=bool)))
+                self.episode_returns.extend(np.asarray(info["episode"]["r"])[done_mask].tolist())
+                self.episode_lengths.extend(np.asarray(info["episode"]["l"])[done_mask].tolist())
+            np.copyto(rew_np, rew, casting="same_kind")
+            np.logical_or(term, trunc, out=done_np)
+            np.copyto(obs_np, obs.reshape(obs_np.shape), casting="same_kind")
+        # the last step's results: rewards -> slot T - 1, starts / observations -> next_* (async copies from
+        # the mapped buffers; the next rollout writes them only after its first stream wait)
+        dst = (C.c_void_p * 3)(rb + (T - 1) * rew_b, self.next_episode_starts.data_ptr(), self.next_obs_dev.data_ptr())
+        src = (C.c_void_p * 3)(rew_h, done_h, obs_h)
+        nbytes = (C.c_int64 * 3)(rew_b, es_b, obs_b)
+        _lib.check(L.rai_copy_h2d_multi(3, dst, src, nbytes, st), "rai_copy_h2d_multi")
 
     def _finish_rollout(self, output_next_values: bool) -> Optional[torch.Tensor]:
         net = self.policy.network

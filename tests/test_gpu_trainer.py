@@ -655,9 +655,10 @@ def test_fused_rollout_direct_slot_staging_is_identical(monkeypatch):
     from rl_algo_impls_amd.policy import ActorCritic
 
     out = []
-    for direct, native in (("1", "1"), ("1", "0"), ("0", "0")):
+    for direct, native, mapped in (("1", "1", "1"), ("1", "1", "0"), ("1", "0", "0"), ("0", "0", "0")):
         monkeypatch.setenv("RAI_ROLLOUT_DIRECT", direct)
         monkeypatch.setenv("RAI_ROLLOUT_NATIVE", native)  # the native staging loop (default) vs torch copies
+        monkeypatch.setenv("RAI_ROLLOUT_MAPPED", mapped)  # host-mapped hand-off in the policy-step kernel
         torch.manual_seed(3)
         env = SyntheticVecEnv(96, "cartpole", seed=5)
         policy = ActorCritic(env).to(DEV)
