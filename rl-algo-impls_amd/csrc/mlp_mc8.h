@@ -96,30 +96,16 @@ __device__ __forceinline__ void ppo_row_loss(const float (&z)[OUTP], const RowLo
     for (int o = 0; o < OUTP; ++o)
       if (o < NA) m = fmaxf(m, z[o]);
     float se = 0.f;
-#ifdef RAI_M8_FAST_LOSS  // A-B builds: the probabilities as exp(z - m) / se, reusing the softmax terms
-    float ez[OUTP];
-#pragma unroll
-    for (int o = 0; o < OUTP; ++o) {
-      ez[o] = o < NA ? expf(z[o] - m) : 0.f;
-      se += ez[o];
-    }
-    const float inv_se = 1.f / se;
-#else
 #pragma unroll
     for (int o = 0; o < OUTP; ++o)
       if (o < NA) se += expf(z[o] - m);
-#endif
     const float lse = m + logf(se);
     float H = 0.f;
 #pragma unroll
     for (int o = 0; o < OUTP; ++o)
       if (o < NA) {
         const float n = z[o] - lse;
-#ifdef RAI_M8_FAST_LOSS
-        H -= fmaxf(n, F32_MIN) * (ez[o] * inv_se);
-#else
         H -= fmaxf(n, F32_MIN) * expf(n);
-#endif
       }
     const int act = min(max(c_act, 0), NA - 1);
     float zact = z[0];
@@ -145,11 +131,7 @@ __device__ __forceinline__ void ppo_row_loss(const float (&z)[OUTP], const RowLo
     for (int o = 0; o < OUTP; ++o)
       if (o < NA) {
         const float n = z[o] - lse;
-#ifdef RAI_M8_FAST_LOSS
-        const float p = ez[o] * inv_se;
-#else
         const float p = expf(n);
-#endif
         dq[o] = dlogp * ((o == act ? 1.f : 0.f) - p) + dent * (-p * (n + H));
       }
     st[0] = fminf(s1, s2);
