@@ -557,7 +557,10 @@ def main():
         # mlp_launch): G = 16 CUs per network unless RAI_MLP_CUS=8
         act = int(cfg["policy"].get("activation_fn", "tanh") == "relu")
         G = 8 if os.environ.get("RAI_MLP_CUS") == "8" else 16
-        kname = "mlp_ppo_mc8_kernel<%d, %d>" % (act, G)
+        RC = 256 // G  # rows per CU (M8Geo<G, RC>)
+        if G == 16 and algo.batch_size <= 128 and os.environ.get("RAI_MLP_PER_RANK_GEO") != "0":
+            G, RC = 8, 16  # the per-rank geometry for <= 128-row minibatches (data parallel)
+        kname = "mlp_ppo_mc8_kernel<%d, %d, %d>" % (act, G, RC)
         roofline = {"kernel": kname + f" (rai_mlp_ppo_epoch, {G} CUs per network)", "bound": "mfma",
                     "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
                     "traffic": traffic(kname), "traffic_source": traffic_source(kname), "avg_ms": round(ms, 3),

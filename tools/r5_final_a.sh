@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-T=${TAG:-r5z}
+T=${TAG:-r5y}
 OUT=gpurun_out/prof_$T
 TAG=$T CONFIGS="cartpole halfcheetah" bash tools/profile_bench.sh || exit 1
 mv "$OUT/stats_cartpole" "$OUT/stats_cartpole_yaml"

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-T=${TAG:-r5z}
+T=${TAG:-r5y}
 TAG=$T bash tools/c3_pmc_groups.sh || exit 1
 python3 tools/c3_traffic.py "gpurun_out/c3grp_$T/FETCH_SIZE.json" "gpurun_out/c3grp_$T/WRITE_SIZE.json" \
   "profiles/${T}_pong_traffic.json" || exit 1
