@@ -169,6 +169,42 @@ def make_rank_data_wide(rank, dev, n=512):
     return Batch(t(obs), t(logp), t(act), None, None, t(vals), t(adv), t(ret))
 
 
+def large_dp_worker(rank, world, port, q, rows_per_rank=512, n=2048):
+    """SURVEY 8(d) batch policy (b) under data parallel: the CartPole-class policy at minibatches of
+    rows_per_rank x world rows (> 256, the large-minibatch kernels), dp_batch="global" over gloo."""
+    import torch
+
+    _init(rank, world, port, "gloo")
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.ppo import PPO
+    import make_golden_networks as nets
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    algo = PPO(nets.build("cartpole").to(dev), dev, None, batch_size=rows_per_rank * world, n_epochs=2,
+               learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
+    algo.enable_data_parallel(dp_batch="global")
+    assert algo.batch_size == rows_per_rank and algo._xdp is None and algo.fused_mlp_spec() is not None
+    data = make_rank_data(rank, dev, n)
+
+    class R:
+        total_steps = n
+
+        def num_minibatches(self, bs):
+            return -(-self.total_steps // bs)
+
+        def epoch_batch(self, shuffle=True):
+            return data
+
+    stats, norms, _ = algo.update(R())
+    q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
 def make_rank_data(rank, dev, n=512):
     import torch
 

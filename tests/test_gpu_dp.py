@@ -392,3 +392,68 @@ def test_wide_epoch_xdp_world2_matches_single_process_global_minibatches(hidden,
     np.testing.assert_allclose(n0, norms, rtol=2e-4)
     np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=2e-4, atol=1e-6)
     np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=2e-4, atol=2e-6)
+
+
+def test_scaled_batch_policy_dp_world2_matches_single_process():
+    """SURVEY 8(d)'s batch policy (b) under data parallel: two ranks (gloo, one GPU) run 512-row slices of
+    1,024-row global minibatches through the large-minibatch kernels (grads mode) with a per-step gradient
+    all-reduce; ranks bitwise equal, and equal to the single process at batch 1,024 over the interleaved
+    rollouts (fp32 tolerance: per-rank partial sums)."""
+    import queue
+    import time
+
+    import dp_worker
+    import make_golden_networks as nets
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import Batch
+
+    rows, n = 512, 2048
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.large_dp_worker, args=(r, 2, port, q, rows, n)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    deadline = time.time() + 240
+    while len(res) < 2:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"rank exited with {dead}"
+            assert time.time() < deadline, "ranks did not report in time"
+    res.sort(key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, s0, n0), (_, p1, s1, n1) = res
+    np.testing.assert_array_equal(p0, p1)
+
+    dev = torch.device("cuda", 0)
+    d0, d1 = dp_worker.make_rank_data(0, dev, n), dp_worker.make_rank_data(1, dev, n)
+    nmb = n // rows
+
+    def interleave(f):
+        a, b = getattr(d0, f), getattr(d1, f)
+        return torch.cat([torch.cat([a[i * rows:(i + 1) * rows], b[i * rows:(i + 1) * rows]]) for i in range(nmb)])
+
+    glob = Batch(*(interleave(f) for f in ("obs", "logprobs", "actions")), None, None,
+                 *(interleave(f) for f in ("values", "advantages", "returns")))
+    torch.manual_seed(0)
+    algo = PPO(nets.build("cartpole").to(dev), dev, None, batch_size=2 * rows, n_epochs=2, learning_rate=3e-3,
+               clip_range=0.2, ent_coef=0.01)
+
+    class R:
+        total_steps = 2 * n
+
+        def num_minibatches(self, bs):
+            return -(-self.total_steps // bs)
+
+        def epoch_batch(self, shuffle=True):
+            return glob
+
+    stats, norms, _ = algo.update(R())
+    np.testing.assert_allclose(n0, norms, rtol=2e-4)
+    np.testing.assert_allclose(s0[:, :6], stats[:, :6], rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=2e-4, atol=2e-6)
