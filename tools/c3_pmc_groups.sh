@@ -11,14 +11,18 @@ export TMPDIR=/tmp
 TAG=${TAG:-r4}
 OUT=gpurun_out/c3grp_$TAG
 mkdir -p "$OUT"
-OURS='conv_|rai_|gather|bias_relu|heads|pg_loss|loss_|clip_optim|grad_sumsq|gae|sample|policy|minibatch|wrw'
+# round 5: "ours" split into the convolutions and the rest of this repo's kernels (the round-5 run of the
+# combined group aborted inside rocprofiler-sdk at a conv_wrw_kernel launch: profiles/r5y_c3_ours_fetch_crash.txt)
+CONV='conv_'
+OURS='rai_|gather|bias_relu|heads|pg_loss|loss_|clip_optim|grad_sumsq|gae|sample|policy|minibatch'
 GEMM='Cijk|gemm|Gemm|GEMM'
 sha256sum rl-algo-impls_amd/lib/librai_amd.so > "$OUT/lib_sha256.txt"
-for grp in ours gemm rest; do
+for grp in ${GROUPS_:-conv ours gemm rest}; do
   case $grp in
+    conv) sel=(--kernel-include-regex "$CONV") ;;
     ours) sel=(--kernel-include-regex "$OURS") ;;
     gemm) sel=(--kernel-include-regex "$GEMM") ;;
-    rest) sel=(--kernel-exclude-regex "$OURS|$GEMM") ;;
+    rest) sel=(--kernel-exclude-regex "$CONV|$OURS|$GEMM") ;;
   esac
   for C in FETCH_SIZE WRITE_SIZE; do
     echo "== $grp $C" | tee -a "$OUT/steps.log"
@@ -37,7 +41,7 @@ import json, sys
 out = sys.argv[1]
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     merged = {"kernels": {}}
-    for g in ("ours", "gemm", "rest"):
+    for g in ("conv", "ours", "gemm", "rest"):
         merged["kernels"].update(json.load(open(f"{out}/{g}_{c}.json"))["kernels"])
     json.dump(merged, open(f"{out}/{c}.json", "w"), indent=1)
 PY

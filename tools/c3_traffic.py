@@ -8,8 +8,9 @@ correction for wide streaming reads, exact for 16-B-per-lane loads and uncalibra
 ones; Infinity-Cache hits count as fetches).  Kernels dispatched at least once per optimizer step
 (>= 2,048 dispatches) form the minibatch step; the rest of the update's kernels (rollout forward,
 GAE, per-epoch gathers) are added once.  The bench's own extra measurements in the same process (the
-bandwidth-regime GAE, gae_stream_kernel) and MIOpen find-mode trial kernels (present in the FETCH
-pass only: the WRITE pass reuses the find database) are excluded.
+bandwidth-regime GAE, gae_stream_kernel), MIOpen find-mode trial kernels (present in the FETCH
+pass only: the WRITE pass reuses the find database) and TunableOp's GEMM tuning trials (hipBLASLt kernels
+dispatched fewer times than there are optimizer steps) are excluded.
 """
 import hashlib
 import json
@@ -23,8 +24,14 @@ def main():
     f = json.load(open(sys.argv[1]))["kernels"]
     w = json.load(open(sys.argv[2]))["kernels"]
     kernels, step_b, upd_b = {}, 0.0, 0.0
+    dropped = 0.0
     for k, we in w.items():
         if "gae_stream_kernel" in k:
+            continue
+        if k.startswith("Cijk") and we["dispatches"] < STEPS:
+            # hipBLASLt solutions TunableOp times while tuning, inside the profiled (first) update: 1,200+
+            # GEMM kernels, ~2.6 TB.  The rollout's fc-forward GEMMs (129 per update) go with them.
+            dropped += 2.0 * f.get(k, {}).get("FETCH_SIZE", 0.0) * 1024 + we.get("WRITE_SIZE", 0.0) * 1024
             continue
         fe = f.get(k, {})
         n = we["dispatches"]
@@ -46,6 +53,7 @@ def main():
            "bytes_per_optimizer_step": round(step_b),
            "bytes_per_update": round(step_b * STEPS + upd_b),
            "bytes_per_update_outside_steps": round(upd_b),
+           "bytes_excluded_gemm_tuning_trials": round(dropped),
            "kernels": dict(top)}
     json.dump(doc, open(sys.argv[3], "w"), indent=1)
     print(f"per optimizer step {step_b / 1e6:.1f} MB, per update {(step_b * STEPS + upd_b) / 1e9:.2f} GB")
