@@ -24,8 +24,13 @@
 //            gradient of its network (19 KB) and the 16 share norms of both networks (fixed
 //            order: every CU on every rank forms the bit-identical clip_grad_norm_ total), and
 //            applies the identical clip + Adam to its own LDS copy of the weights.
-// The norm needs no separate exchange.  Slots are double-buffered by minibatch parity; the
-// reuse argument is the 4-CU one per round (a CU cannot pass round r of step k + 1 before every
+// The norm needs no separate exchange.  Publish form: write-through (sc1) by default; when the step-0
+// arrival shows every CU of the network on ONE XCC (HW_REG_XCC_ID, registered by each CU before it
+// arrives), the partial and summed-share slots go out as plain stores drained into that XCC's L2 (the
+// lines stay there; write-through drops them and the readers then fetch past the L2).  The readers'
+// loads stay sc1 (past their own L1 only) and the share norms, read by the other network's XCC, stay
+// write-through.  Placement decides only the store form, never correctness.  Slots are
+// double-buffered by minibatch parity; the reuse argument is the 4-CU one per round (a CU cannot pass round r of step k + 1 before every
 // CU that reads its round-r slot of step k has published round r + 1 of step k, or round 1 of
 // step k + 1).  Every spin is bounded by elapsed clock and sets state.err.
 
@@ -48,9 +53,14 @@ struct M8Geo {
   static_assert(RC % 16 == 0 && NTILE * WPT == M8_NW && CT * WPT * 16 == HID, "geometry");
   static_assert(SH <= M8_NT, "one share chunk per thread");
 };
-// sync words (u64, zeroed per launch): round-1 and round-2 arrival counters per network
+// sync words (u64, zeroed per launch): round-1 and round-2 arrival counters per network; per network
+// the set of XCCs its CUs run on (one bit per HW_REG_XCC_ID)
 constexpr int M8_CNT1 = 0;
 constexpr int M8_CNT2 = 2;
+constexpr int M8_XCC = 6;
+// Adam's bias corrections are tabulated in LDS for the first M8_BC_MAX steps of a launch (C2: 2,048
+// minibatches per epoch launch); later steps form them in the loop
+constexpr int M8_BC_MAX = 2048;
 // scratch (workspace) layout, bytes (sized for M8_GMAX; smaller G use a prefix of each region)
 constexpr int64_t M8_S1_BYTES = 2LL * 2 * M8_GMAX * WL_N * sizeof(float);  // [net][par][c][WL_N] partials
 constexpr int64_t M8_S2_OFF = M8_S1_BYTES;                                  // [net][par][WL_N] summed gradient
@@ -69,6 +79,8 @@ struct SmemM8 {
   double st[4][4];   // round 2: share |g|^2
   float strow[Geo::RC][4];  // per-row loss statistics, reduced off the critical path (round-1 wait)
   int bail;
+  int xl;            // every CU of this network on one XCC: gradient slots published with plain stores
+  float bc[M8_BC_MAX][2];  // per step of the launch: Adam's 1 / sqrt(1 - beta2^t) and -lr / (1 - beta1^t)
   float db3p[Geo::NTILE][OUTP];
   float Wt[WL_N];    // weights
   float Gb[WL_N];    // this CU's partial gradient
@@ -87,8 +99,7 @@ struct RowLossHp {
 };
 template <int OUTP, bool ACTOR>
 __device__ __forceinline__ void ppo_row_loss(const float (&z)[OUTP], const RowLossHp& h, int c_act, float c_a,
-                                             float c_b, float amean, float aden, float (&dq)[OUTP],
-                                             float (&st)[4]) {
+                                             float c_b, float A, float (&dq)[OUTP], float (&st)[4]) {
   if (ACTOR) {
     const int NA = h.NA;
     float m = F32_MIN;
@@ -113,7 +124,6 @@ __device__ __forceinline__ void ppo_row_loss(const float (&z)[OUTP], const RowLo
     for (int o = 1; o < OUTP; ++o)
       if (o == act) zact = z[o];
     const float logp = zact - lse;
-    const float A = (c_b - amean) / aden;
     const float logratio = logp - c_a;
     const float ratio = expf(logratio);
     const float lo = 1.f - h.clip_range, hi = 1.f + h.clip_range;
@@ -280,13 +290,35 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
     }
   };
   if (nmb > 0) prefetch(0);
-  // bias-correction powers beta^t, carried per thread (no LDS round trip per step)
-  double pw1 = ipow(beta1_d, step0), pw2 = ipow(beta2_d, step0);
-  if (tid == 0) S.bail = 0;
+  // Adam's bias corrections of every step of the launch, t = step0 + mb + 1, as the per-minibatch
+  // optimizer forms them (ipow, fp64): tabulated here, so no fp64 divide sits in the step loop
+  auto bias_corr = [&](int mb, float& inv_bc2_sqrt, float& neg_step) {
+    const long long t = step0 + mb + 1;
+    inv_bc2_sqrt = 1.f / (float)sqrt(1.0 - ipow(beta2_d, t));
+    neg_step = (float)(-((double)lr / (1.0 - ipow(beta1_d, t))));
+  };
+  for (int k = tid; k < min(nmb, M8_BC_MAX); k += M8_NT) bias_corr(k, S.bc[k][0], S.bc[k][1]);
+  if (tid == 0) {
+    S.bail = 0;
+    S.xl = 0;
+    // register this CU's XCC (completed before its first round-1 arrival: the vmcnt wait below)
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    __hip_atomic_fetch_or(&sync[M8_XCC + net], 1ull << (xcc & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 #ifdef RAI_STAMPS
   if (tid == 0) S.t_last = __builtin_amdgcn_s_memtime();
 #endif
+
+  // the loss's divides off the step's critical path: 1 / (rows x world) of a full and of the last
+  // minibatch, and each row's normalized advantage (adv - mean) / (std + eps) -- step 0's here, every
+  // later step's in the previous step's round-1 wait, once its prefetched row has landed
+  const float invB_full = 1.f / (float)(B * a.world);
+  const float invB_last = nmb > 0 ? 1.f / (float)((int)(n_rows - (int64_t)(nmb - 1) * B) * a.world) : 0.f;
+  float r_A = 0.f;
+  if (ACTOR && nmb > 0) r_A = (r_b - r_c) / r_d;
 
   constexpr long long MC_WAIT_LOCAL = RAI_SPIN_LOCAL, MC_WAIT_REMOTE = RAI_SPIN_REMOTE;
   for (int mb = 0; mb < nmb; ++mb) {
@@ -294,9 +326,9 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
     const int64_t row0 = (int64_t)mb * B;
     const int rows = (int)min((int64_t)B, n_rows - row0);
     const int c_act = r_act;
-    const float c_a = r_a, c_b = r_b, amean = r_c, aden = r_d, c_x = r_x;
+    const float c_a = r_a, c_b = r_b, c_A = r_A, c_x = r_x;
     if (mb + 1 < nmb) prefetch(mb + 1);
-    lh.invB = 1.f / (float)(rows * a.world);
+    lh.invB = mb + 1 < nmb ? invB_full : invB_last;
     const int R = T * 16;              // first local row of this wave's tile
     const int RG = c * RC + R;         // ... and its row within the minibatch
 
@@ -388,7 +420,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         dq[o] = 0.f;
       }
       float sr[4] = {0.f, 0.f, 0.f, 0.f};
-      if (RG + g * 4 + q < rows) ppo_row_loss<OUTP, ACTOR>(z, lh, c_act, c_a, c_b, amean, aden, dq, sr);
+      if (RG + g * 4 + q < rows) ppo_row_loss<OUTP, ACTOR>(z, lh, c_act, c_a, c_b, c_A, dq, sr);
       if (li < 4 && hf_ == 0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) S.strow[lr_][i] = sr[i];
@@ -591,12 +623,24 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
       f4 pv[MC_CPT];
 #pragma unroll
       for (int i = 0; i < MC_CPT; ++i) pv[i] = *reinterpret_cast<const f4*>(&S.Gb[4 * min(tid + M8_NT * i, WL_CH - 1)]);
+      if (__builtin_amdgcn_readfirstlane(S.xl)) {  // one XCC: plain stores, the lines stay in its L2
 #pragma unroll
-      for (int i = 0; i < MC_CPT; ++i) {
-        const int ch = tid + M8_NT * i;
-        if (ch < WL_CH) __builtin_amdgcn_raw_buffer_store_b128(as_u4(pv[i]), srs, sbase + 16 * ch, 0, 16);
+        for (int i = 0; i < MC_CPT; ++i) {
+          const int ch = tid + M8_NT * i;
+          if (ch < WL_CH) __builtin_amdgcn_raw_buffer_store_b128(as_u4(pv[i]), srs, sbase + 16 * ch, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MC_CPT; ++i) {
+          const int ch = tid + M8_NT * i;
+          if (ch < WL_CH) __builtin_amdgcn_raw_buffer_store_b128(as_u4(pv[i]), srs, sbase + 16 * ch, 0, 16);
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
+      if (ACTOR) {  // the next step's advantages (its prefetch has landed with the drain)
+        r_A = (r_b - r_c) / r_d;
+        asm volatile("" : "+v"(r_A));
+      }
     }
     STAMP(9);
     __syncthreads();
@@ -607,6 +651,16 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         atomicExch(a.err, 1);
         S.bail = 1;
       }
+#ifndef RAI_M8_NO_XCC_LOCAL
+      if (mb == 0) {
+        // every CU of the network registered its XCC before its step-0 arrival: from step 1 on, when they
+        // all share one XCC (one L2), the gradient slots go out as plain stores (drained into that L2)
+        // instead of write-through; the readers' sc1 loads bypass only their L1, so they read that L2
+        const unsigned long long m =
+            __hip_atomic_fetch_or(&sync[M8_XCC + net], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S.xl = m != 0 && (m & (m - 1)) == 0;
+      }
+#endif
     } else if (w == 1) {
       // while wave 0 waits for the other CUs: this CU's loss statistics (fp64 sums over its rows in
       // row order of the lanes); CU 0 turns them into rows at the end.  Off the gradient's path.
@@ -626,12 +680,14 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
     __syncthreads();
     if (S.bail) break;
     STAMP(6);
-    // this step's Adam bias corrections (fp64 sqrt / divide) off the gradient's critical path: formed
-    // while the shares are summed and exchanged, used after the round-2 wait
-    pw1 *= beta1_d;
-    pw2 *= beta2_d;
-    const float inv_bc2_sqrt = 1.f / (float)sqrt(1.0 - pw2);
-    const float neg_step = (float)(-((double)lr / (1.0 - pw1)));
+    // this step's Adam bias corrections: the launch's table (an LDS read), or formed here past its end
+    float inv_bc2_sqrt, neg_step;
+    if (mb < M8_BC_MAX) {
+      inv_bc2_sqrt = S.bc[mb][0];
+      neg_step = S.bc[mb][1];
+    } else {
+      bias_corr(mb, inv_bc2_sqrt, neg_step);
+    }
     const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
     {
       RELANE();
@@ -704,7 +760,11 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
       STAMP(11);
       // ---- round 2: publish the summed share and its squared norm ----
       const int s2 = (int)M8_S2_OFF + ((net * 2 + par) * WL_N + 4 * chl) * (int)sizeof(float);
-      if (own) __builtin_amdgcn_raw_buffer_store_b128(as_u4(s), srs, s2, 0, 16);
+      if (__builtin_amdgcn_readfirstlane(S.xl)) {
+        if (own) __builtin_amdgcn_raw_buffer_store_b128(as_u4(s), srs, s2, 0, 0);
+      } else {
+        if (own) __builtin_amdgcn_raw_buffer_store_b128(as_u4(s), srs, s2, 0, 16);
+      }
       double ss = 0.0;
       if (own) {
 #pragma unroll
@@ -759,11 +819,13 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
       STAMP(14);
       float coef = 1.f;
       if (max_grad_norm > 0.f) coef = fminf(max_grad_norm / (total_norm + 1e-6f), 1.f);
+      // branch-free over the chunks (one basic block: the transcendentals of all chunks interleave); a lane
+      // past the last chunk updates a clamped copy and stores nothing (its moments are never written back)
 #pragma unroll
       for (int i = 0; i < MC_CPT; ++i) {
         const int ch = tid + M8_NT * i;
-        if (ch < WL_CH) {
-          f4 p = *reinterpret_cast<const f4*>(&S.Wt[4 * ch]);
+        {
+          f4 p = *reinterpret_cast<const f4*>(&S.Wt[4 * min(ch, WL_CH - 1)]);
 #ifdef RAI_M8_SCALAR_ADAM  // A/B builds only: one element per VALU op
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -789,7 +851,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
             vreg[i][2 * h + 1] = vv.y;
           }
 #endif
-          *reinterpret_cast<f4*>(&S.Wt[4 * ch]) = p;
+          if (ch < WL_CH) *reinterpret_cast<f4*>(&S.Wt[4 * ch]) = p;
         }
       }
       if (ACTOR && c == 0 && tid == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;

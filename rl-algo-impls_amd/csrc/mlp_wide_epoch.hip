@@ -97,7 +97,8 @@ inline int64_t we_ws_bytes(int in_dim, int64_t n_rows) {
   return WE_REC_OFF + ((n_rows * we_rec_floats(in_dim) * 4 + 255) & ~(int64_t)255);
 }
 constexpr int WE_RU = (WE_B * (WE_LIN + WE_INMAX) / 4 + 255) / 256;  // 16-B record loads per thread
-enum { WE_CA = 0, WE_CB = 2, WE_CC = 4 };  // counters (A: H1, B: head partials, C: dH1 tiles); D: granules
+enum { WE_CA = 0, WE_CB = 2, WE_CC = 4, WE_CXCC = 6 };  // counters (A: H1, B: head partials, C: dH1 tiles;
+                                                      // line 6: per network the set of XCCs); D: granules
 static_assert(WE_STATE_BYTES % 16 == 0, "memset block");
 
 typedef __attribute__((address_space(1))) unsigned long long we_gu64;
@@ -157,6 +158,7 @@ struct WeSmem {
   double red[4][8];
   float adv_mean, adv_den;
   int bail;
+  int xl;  // every workgroup of this network on one XCC: hand-off slots published with plain stores
 };
 
 #ifdef RAI_STAMPS
@@ -408,11 +410,19 @@ __device__ __forceinline__ f4 we_dh1_tile(const float* act_row, const float* w2t
   return (acc0 + acc1) + (acc2 + acc3);
 }
 
+// A within-network hand-off store: write-through (sc1), or plain when every workgroup of the network runs
+// on one XCC (xl: the data then stays in that XCC's L2, where the readers' sc1 loads -- past their own L1
+// only -- find it; write-through drops the line and the readers fetch past the L2).  xl is wave-uniform.
+__device__ __forceinline__ void we_st16(u4v v, __amdgpu_buffer_rsrc_t rs, int off, bool xl) {
+  if (xl) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, WE_SC1);
+}
+
 // Publish W2 rows j for the column owners as transposed 16 x 16 tiles (16-B sc1 stores; no drain
 // here: the next H1 publish's drain covers them, before the A arrival their readers wait on).  Wave
 // w writes tiles ct = w + 4 m; lane (u = lane >> 2, kk4 = lane & 3) one 16-B row piece of each.
 __device__ __forceinline__ void we_publish_w2(const float (*W2r)[WE_HP], __amdgpu_buffer_rsrc_t wrs, int64_t base,
-                                              int G, int w, int lane) {
+                                              int G, int w, int lane, bool xl) {
   const int u = lane >> 2, kk4 = lane & 3;
 #pragma unroll
   for (int m = 0; m < WE_GMAX / 4; ++m) {
@@ -420,8 +430,7 @@ __device__ __forceinline__ void we_publish_w2(const float (*W2r)[WE_HP], __amdgp
     if (ct < G) {
       const f4 v = {W2r[4 * kk4][WE_SL * ct + u], W2r[4 * kk4 + 1][WE_SL * ct + u], W2r[4 * kk4 + 2][WE_SL * ct + u],
                     W2r[4 * kk4 + 3][WE_SL * ct + u]};
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), wrs,
-                                             (int)(base + (int64_t)ct * 1024 + (u * WE_SL + 4 * kk4) * 4), 0, WE_SC1);
+      we_st16(__builtin_bit_cast(u4v, v), wrs, (int)(base + (int64_t)ct * 1024 + (u * WE_SL + 4 * kk4) * 4), xl);
     }
   }
 }
@@ -605,10 +614,20 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   const double beta1_d = ohp.beta1_d, beta2_d = ohp.beta2_d;
   const float c1 = (float)(1.0 - beta1_d), c2 = (float)(1.0 - beta2_d);
   double pw1 = ipow(beta1_d, step0), pw2 = ipow(beta2_d, step0);
-  if (tid == 0) S.bail = 0;
+  if (tid == 0) {
+    S.bail = 0;
+    S.xl = 0;
+    // register this workgroup's XCC (completed long before its step-0 A arrival: the drains between)
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    __hip_atomic_fetch_or(&ctr[WE_CXCC * (WE_CTR_STRIDE / 8) + net], 1ull << (xcc & 15), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
+  bool xl = false;  // the store form of the B / C / W2 hand-offs from step 0 on and of A from step 1 on
   const int64_t w2t_mine = WE_W2T_OFF + net * WE_W2T_NET + (int64_t)j * WE_GMAX * 1024;  // my published tiles
-  we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane);  // the initial W2, for step 0's column owners
+  we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane, false);  // the initial W2, for step 0's column owners
 
   // the next minibatch's records are loaded into registers one step ahead: one contiguous block of
   // rws x R floats (R = 12 + IN4), WE_RU 16-B loads per thread (those past the block not issued:
@@ -735,7 +754,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       const int r = tid >> 2, q = tid & 3;
       const f4 v = {S.H1j[r][4 * q], S.H1j[r][4 * q + 1], S.H1j[r][4 * q + 2], S.H1j[r][4 * q + 3]};
       const int64_t off = WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT + ((int64_t)r * H + WE_SL * j + 4 * q) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), wrs, (int)off, 0, WE_SC1);
+      we_st16(__builtin_bit_cast(u4v, v), wrs, (int)off, xl);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     WSTAMP(0);
@@ -746,13 +765,24 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     if (w == 1) side_a();
     if (WE_DEFER_W2 && mb > 0) adam_w2();
     if (!we_wait(ctr, WE_CA + net, want, a.state, S.bail)) break;
+#ifndef RAI_WE_NO_XCC_LOCAL
+    if (mb == 0) {  // every workgroup of the network registered its XCC before its step-0 A arrival
+      if (tid == 0) {
+        const unsigned long long m = __hip_atomic_fetch_or(&ctr[WE_CXCC * (WE_CTR_STRIDE / 8) + net], 0ull,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S.xl = m != 0 && (m & (m - 1)) == 0;
+      }
+      __syncthreads();
+      xl = __builtin_amdgcn_readfirstlane(S.xl) != 0;
+    }
+#endif
     WSTAMP(1);
     we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // H1 -> Act
     // W2 rows j (as updated by the last Adam step) for this step's column owners: issued after the
     // gather's drain, so they drain in the background during fwd2 -- by the B publish's drain, before
     // this workgroup's B arrival, after which the column owners load them (step 0: the tiles published
     // before the loop)
-    if (mb > 0) we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane);
+    if (mb > 0) we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane, xl);
     lds_barrier();
     WSTAMP(2);
     // ============ fwd2: H2[:, j] = act(H1 W2[j]^T + b2[j]); wave w: row tile w =============
@@ -786,7 +816,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
           p[q] = s;
         }
         const int64_t off = WE_P_OFF + (int64_t)(net * 2 + par) * WE_P_SLOT + (((int64_t)j * WE_B + r) * WE_OUTM + o0) * 4;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, p), wrs, (int)off, 0, WE_SC1);
+        we_st16(__builtin_bit_cast(u4v, p), wrs, (int)off, xl);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1031,7 +1061,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       for (int u = 0; u < 4; ++u) z[u] = dh[u] * we_actd(act, h2[u]);
       *reinterpret_cast<f4*>(&S.Z2j[r][4 * q]) = z;
       const int64_t off = WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT + ((int64_t)r * H + WE_SL * j + 4 * q) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, z), wrs, (int)off, 0, WE_SC1);
+      we_st16(__builtin_bit_cast(u4v, z), wrs, (int)off, xl);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
