@@ -84,7 +84,12 @@ struct SmemM8 {
   float db3p[Geo::NTILE][OUTP];
   float Wt[WL_N];    // weights
   float Gb[WL_N];    // this CU's partial gradient
-  float X[Geo::RC][4];
+  // this step's rows (staged by wave 3 in the previous step's waits): observations zero-padded to 4
+  // columns (the F1 operand and dW1's X), actions, old log-prob / value, advantage / return, and the
+  // normalized advantage
+  alignas(16) float px[Geo::RC][4];
+  int pact[Geo::RC];
+  float pa[Geo::RC], pb[Geo::RC], pA[Geo::RC];
   float H1[Geo::RC][LD];
   float Z2[Geo::RC][LD];
   float Zp[Geo::WPT][Geo::RC][OUTP];  // output-layer partial sums of the column parts
@@ -263,33 +268,57 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
   const int norm0 = a.state->norm_index;
   lh.pi_coef = a.state->pi_coef_zero ? 0.f : 1.f;
 
-  int r_act = 0;
-  float r_a = 0.f, r_b = 0.f, r_c = 0.f, r_d = 1.f, r_x = 0.f;
-  auto prefetch = [&](int mb) {
-    const int64_t row0 = (int64_t)mb * B;
-    const int rows = (int)min((int64_t)B, n_rows - row0);
-    int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    asm volatile("" : "+v"(ln));
-    const int xr = c * RC + T * 16 + (ln & 15), xg = ln >> 4;
-    r_x = (xr < rows && xg < IN) ? a.obs[(row0 + xr) * IN + xg] : 0.f;
-    const int rr = c * RC + T * 16 + (ln >> 4) * 4 + (ln & 3);
-    if (rr < rows) {
-      const int64_t r = row0 + rr;
+  // The step's rows are staged by wave 3 off the critical path: its loads issue in the previous step's
+  // round-1 wait and land in LDS in its round-2 wait (step 0's before the loop), so the step itself only
+  // reads LDS -- no global address arithmetic or load issue ahead of F1.
+  constexpr int PXN = (RC * 4 + 63) / 64;  // observation floats per lane of wave 3
+  float q_x[PXN], q_a = 0.f, q_b = 0.f, q_c = 0.f, q_d = 1.f;
+  int q_act = 0;
+  auto pf_issue = [&](int m) {
+    const int64_t r0 = (int64_t)m * B;
+    const int rws = (int)min((int64_t)B, n_rows - r0);
+    const int ln = tid & 63;
+#pragma unroll
+    for (int k = 0; k < PXN; ++k) {
+      const int e = ln + 64 * k, row = c * RC + (e >> 2), col = e & 3;
+      q_x[k] = (e < RC * 4 && row < rws && col < IN) ? a.obs[(r0 + row) * IN + col] : 0.f;
+    }
+    q_act = 0;
+    q_a = q_b = 0.f;
+    if (ln < RC && c * RC + ln < rws) {
+      const int64_t r = r0 + c * RC + ln;
       if (ACTOR) {
-        r_act = (int)a.actions[r];
-        r_a = a.old_logp[r];
-        r_b = a.adv[r];
+        q_act = (int)a.actions[r];
+        q_a = a.old_logp[r];
+        q_b = a.adv[r];
       } else {
-        r_a = a.old_values[r];
-        r_b = a.ret[r];
+        q_a = a.old_values[r];
+        q_b = a.ret[r];
       }
     }
     if (ACTOR) {
-      r_c = a.moments[2 * mb];
-      r_d = a.moments[2 * mb + 1];
+      q_c = a.moments[2 * m];
+      q_d = a.moments[2 * m + 1];
     }
   };
-  if (nmb > 0) prefetch(0);
+  auto pf_store = [&]() {
+    const int ln = tid & 63;
+#pragma unroll
+    for (int k = 0; k < PXN; ++k) {
+      const int e = ln + 64 * k;
+      if (e < RC * 4) S.px[e >> 2][e & 3] = q_x[k];
+    }
+    if (ln < RC) {
+      S.pact[ln] = q_act;
+      S.pa[ln] = q_a;
+      S.pb[ln] = q_b;
+      if (ACTOR) S.pA[ln] = (q_b - q_c) / q_d;  // (adv - mean) / (std + eps): the loss's divide, staged
+    }
+  };
+  if (w == 3 && nmb > 0) {
+    pf_issue(0);
+    pf_store();
+  }
   // Adam's bias corrections of every step of the launch, t = step0 + mb + 1, as the per-minibatch
   // optimizer forms them (ipow, fp64): tabulated here, so no fp64 divide sits in the step loop
   auto bias_corr = [&](int mb, float& inv_bc2_sqrt, float& neg_step) {
@@ -312,22 +341,21 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
   if (tid == 0) S.t_last = __builtin_amdgcn_s_memtime();
 #endif
 
-  // the loss's divides off the step's critical path: 1 / (rows x world) of a full and of the last
-  // minibatch, and each row's normalized advantage (adv - mean) / (std + eps) -- step 0's here, every
-  // later step's in the previous step's round-1 wait, once its prefetched row has landed
+  // the loss's 1 / (rows x world) off the step's critical path, for a full and for the last minibatch
   const float invB_full = 1.f / (float)(B * a.world);
   const float invB_last = nmb > 0 ? 1.f / (float)((int)(n_rows - (int64_t)(nmb - 1) * B) * a.world) : 0.f;
-  float r_A = 0.f;
-  if (ACTOR && nmb > 0) r_A = (r_b - r_c) / r_d;
 
   constexpr long long MC_WAIT_LOCAL = RAI_SPIN_LOCAL, MC_WAIT_REMOTE = RAI_SPIN_REMOTE;
   for (int mb = 0; mb < nmb; ++mb) {
     const int par = mb & 1;
     const int64_t row0 = (int64_t)mb * B;
     const int rows = (int)min((int64_t)B, n_rows - row0);
-    const int c_act = r_act;
-    const float c_a = r_a, c_b = r_b, c_A = r_A, c_x = r_x;
-    if (mb + 1 < nmb) prefetch(mb + 1);
+    int ln0 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(ln0));
+    const float c_x = S.px[T * 16 + (ln0 & 15)][ln0 >> 4];
+    const int lrow = T * 16 + (ln0 >> 4) * 4 + (ln0 & 3);  // the loss's row of this lane
+    const int c_act = S.pact[lrow];
+    const float c_a = S.pa[lrow], c_b = S.pb[lrow], c_A = ACTOR ? S.pA[lrow] : 0.f;
     lh.invB = mb + 1 < nmb ? invB_full : invB_last;
     const int R = T * 16;              // first local row of this wave's tile
     const int RG = c * RC + R;         // ... and its row within the minibatch
@@ -343,7 +371,6 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         z[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(c_x, S.Wt[WL_W1 + (16 * (CT * hf_ + tt) + li) * 4 + g], zero,
                                                      0, 0, 0);
       }
-      if (hf_ == 0) S.X[16 * T_ + li][g] = c_x;
 #pragma unroll
       for (int tt = 0; tt < CT; ++tt) {
         const int t = CT * hf_ + tt;
@@ -495,7 +522,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const f4 xr = *reinterpret_cast<const f4*>(&S.X[16 * T_ + g * 4 + r][0]);
+        const f4 xr = *reinterpret_cast<const f4*>(&S.px[16 * T_ + g * 4 + r][0]);
 #pragma unroll
         for (int tt = 0; tt < CT; ++tt) {
           const int t = CT * hf_ + tt;
@@ -637,10 +664,6 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
-      if (ACTOR) {  // the next step's advantages (its prefetch has landed with the drain)
-        r_A = (r_b - r_c) / r_d;
-        asm volatile("" : "+v"(r_A));
-      }
     }
     STAMP(9);
     __syncthreads();
@@ -676,6 +699,8 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         __builtin_amdgcn_raw_buffer_store_b128(p1, str, so + 16, 0, 16);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (w == 3 && mb + 1 < nmb) {
+      pf_issue(mb + 1);  // the next step's rows: loads in flight through round 2
     }
     __syncthreads();
     if (S.bail) break;
@@ -790,6 +815,8 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         atomicExch(a.err, 1);
         S.bail = 1;
       }
+    } else if (w == 3 && mb + 1 < nmb) {
+      pf_store();  // the next step's rows -> LDS (this step's px / p* reads all preceded round 1)
     }
     __syncthreads();
     if (S.bail) break;
