@@ -64,7 +64,7 @@ constexpr int M8_BC_MAX = 2048;
 // scratch (workspace) layout, bytes (sized for M8_GMAX; smaller G use a prefix of each region)
 constexpr int64_t M8_S1_BYTES = 2LL * 2 * M8_GMAX * WL_N * sizeof(float);  // [net][par][c][WL_N] partials
 constexpr int64_t M8_S2_OFF = M8_S1_BYTES;                                  // [net][par][WL_N] summed gradient
-constexpr int64_t M8_SQ_OFF = M8_S2_OFF + 2LL * 2 * WL_N * sizeof(float);   // [par][net][c][wave] share |g|^2 (f64)
+constexpr int64_t M8_SQ_OFF = M8_S2_OFF + 2LL * 2 * WL_N * sizeof(float);   // [par][net][c][hi, lo] share |g|^2 granules
 constexpr int64_t M8_SCRATCH = M8_SQ_OFF + 2LL * 2 * M8_GMAX * M8_NW * sizeof(double);
 static_assert(2 * XDP_MAXW * M8_GMAX * 8 <= XDP_TEST_OFF, "xdp share flags");
 
@@ -75,8 +75,7 @@ struct SmemM8 {
   unsigned long long stamps[32];
   unsigned long long t_last;
 #endif
-  double pw[2];
-  double st[4][4];   // round 2: share |g|^2
+  double sq[M8_NW];  // round 2: the wave parts of this CU's share |g|^2
   float strow[Geo::RC][4];  // per-row loss statistics, reduced off the critical path (round-1 wait)
   int bail;
   int xl;            // every CU of this network on one XCC: gradient slots published with plain stores
@@ -223,6 +222,9 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
   const float max_grad_norm = a.ohp->max_grad_norm;
   unsigned long long* const sync = a.xchg;
   const __amdgpu_buffer_rsrc_t srs = mc_rsrc(a.scratch, (int)M8_SCRATCH);
+  // [par][net][c][hi, lo] share-norm granules (within the share-norm region)
+  unsigned long long* const sq_gran =
+      reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(a.scratch) + M8_SQ_OFF);
   const int nmb_all = (int)((a.n_rows + a.batch - 1) / a.batch);
   const __amdgpu_buffer_rsrc_t str = mc_rsrc(a.statp, 2 * nmb_all * G * 32);
 
@@ -796,20 +798,21 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         for (int q = 0; q < 4; ++q) ss = __builtin_fma((double)s[q], (double)s[q], ss);
       }
       ss = wave_sum_v(ss);
-      // each wave publishes its part of the share norm with the share itself, in the same drain (the
-      // readers add the four parts in wave order: the CU's norm is ((w0 + w1) + w2) + w3 as before,
-      // but without a second store -> drain round trip after a workgroup barrier)
-      if (lane == 0) {
-        const int so = (int)M8_SQ_OFF + (((par * 2 + net) * G + c) * M8_NW + w) * (int)sizeof(double);
-        const u4v pk = __builtin_bit_cast(u4v, (double __attribute__((ext_vector_type(2)))){ss, 0.0});
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_shufflevector(pk, pk, 0, 1), srs, so, 0, 16);
-      }
+      if (lane == 0) S.sq[w] = ss;  // the CU's share norm: its four wave parts, summed below in wave order
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     STAMP(12);
     __syncthreads();
     STAMP(13);
     if (tid == 0) {
+      // the share norm goes out as two tagged 8-B granules (hi / lo words of the double; agent-scope
+      // atomic stores, the data is the flag: no drain), read by every CU of both networks after the
+      // round-2 wait; the tag is the global optimizer step (unique across launches)
+      const double cu = ((S.sq[0] + S.sq[1]) + S.sq[2]) + S.sq[3];
+      const unsigned long long u = __double_as_longlong(cu), tg = (unsigned long long)(unsigned)(step0 + mb + 1) << 32;
+      unsigned long long* gq = sq_gran + ((par * 2 + net) * G + c) * 2;
+      __hip_atomic_store(gq, tg | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gq + 1, tg | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(&sync[M8_CNT2 + net], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!m8_wait2(sync, M8_CNT2, M8_CNT2 + 1, (unsigned long long)G * (mb + 1), MC_WAIT_LOCAL)) {
         atomicExch(a.err, 1);
@@ -831,16 +834,28 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         const int chl = min(tid + M8_NT * i, WL_CH - 1);
         gr[i] = as_f4(__builtin_amdgcn_raw_buffer_load_b128(srs, gbase + 16 * chl, 0, 16));
       }
-      // the 2G share norms (net-major, CU order), lane l holding number l (its four wave parts added in
-      // wave order); fixed-order wave sum
+      // the 2G share norms (net-major, CU order), lane l polling the granules of number l until both
+      // carry this step's tag (they were stored before their CU's round-2 arrival); fixed-order wave sum
       static_assert(M8_NW == 4, "four wave parts per share norm");
-      const int lq = min(lane, 2 * G - 1);
-      const int sqo = (int)M8_SQ_OFF + (par * 2 * G + lq) * M8_NW * (int)sizeof(double);
-      const auto d2a = __builtin_bit_cast(double __attribute__((ext_vector_type(2))),
-                                          __builtin_amdgcn_raw_buffer_load_b128(srs, sqo, 0, 16));
-      const auto d2b = __builtin_bit_cast(double __attribute__((ext_vector_type(2))),
-                                          __builtin_amdgcn_raw_buffer_load_b128(srs, sqo + 16, 0, 16));
-      const double sq = ((d2a[0] + d2a[1]) + d2b[0]) + d2b[1];
+      const unsigned long long* gq = sq_gran + (par * 2 * G + min(lane, 2 * G - 1)) * 2;
+      const unsigned tag = (unsigned)(step0 + mb + 1);
+      unsigned long long qh, ql;
+      {
+        const unsigned long long t0 = rai_clock();
+        for (;;) {
+          qh = __hip_atomic_load(gq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ql = __hip_atomic_load(gq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__all((unsigned)(qh >> 32) == tag && (unsigned)(ql >> 32) == tag)) break;
+          if (rai_expired(t0, MC_WAIT_LOCAL)) {
+            if (lane == 0) {
+              atomicExch(a.err, 1);
+              S.bail = 1;
+            }
+            break;
+          }
+        }
+      }
+      const double sq = __longlong_as_double((long long)((qh << 32) | (ql & 0xffffffffull)));
       const double tot = wave_sum_v(lane < 2 * G ? sq : 0.0);
       const float total_norm = (float)sqrt(tot);
       STAMP(14);

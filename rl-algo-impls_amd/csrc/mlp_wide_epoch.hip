@@ -655,6 +655,12 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
   };
   if (nmb > 0) prefetch(0);
+  // the loss's divides by the minibatch size (rows x world) and the entropy count, for a full and for the
+  // last minibatch: off the step's critical path
+  const int rows_last = nmb > 0 ? (int)(n_rows - (int64_t)(nmb - 1) * B) : 0;
+  const float invB_full = 1.f / (float)(B * a.world), invB_last = 1.f / (float)(rows_last * a.world);
+  const float dent_full = -hp.ent_coef / (float)((HEAD == 1 ? B * O : B) * a.world);
+  const float dent_last = -hp.ent_coef / (float)((HEAD == 1 ? rows_last * O : rows_last) * a.world);
 #ifdef RAI_STAMPS
   unsigned long long st_acc[24] = {0}, t_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -912,7 +918,8 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       for (int o = 0; o < WE_OUTM; ++o) dout[o] = dl[o] = 0.f;
       // statistics: [0] sum min(s1, s2) | loss, [1] sum kl | vclipped, [2] clipped, [3] entropy
       double st[4] = {0.0, 0.0, 0.0, 0.0};  // per row; summed by side_d
-      const float invB = 1.f / (float)(rows * a.world);
+      const bool full = mb + 1 < nmb;  // the loss's per-step divides, formed before the loop
+      const float invB = full ? invB_full : invB_last;
       if (net == 0) {
 #pragma clang fp contract(off)
         const float A = c_adv;  // normalized per minibatch by we_adv_norm_kernel before the epoch
@@ -965,8 +972,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
         else { g1 = g_pi * 0.5f; g2 = g_pi * 0.5f; }
         const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
         const float d_logp = valid ? (g1 * A + (g2 * A) * in_clip) * ratio : 0.f;
-        const float n_ent = (float)((HEAD == 1 ? rows * O : rows) * a.world);
-        const float d_ent = valid ? -hp.ent_coef / n_ent : 0.f;
+        const float d_ent = valid ? (full ? dent_full : dent_last) : 0.f;
         if (HEAD == 1) {
 #pragma unroll
           for (int o = 0; o < WE_OUTM; ++o) {
@@ -1326,7 +1332,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       if (lane == 0) S.coef = coef;
       if (net == 0 && j == 0 && lane == 0 && a.norms && norm0 + mb < a.max_norms) a.norms[norm0 + mb] = total_norm;
     } else if (w == 1) {
+#ifndef RAI_WE_SKIP_SIDE_D  // timing experiments only: stale Adam constants and no stats rows
       side_d();
+#endif
     }
     __syncthreads();
     if (S.bail) break;
