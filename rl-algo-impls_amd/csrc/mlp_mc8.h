@@ -217,9 +217,11 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
   lh.vf_fn = a.hp->vf_loss_fn;
   lh.halve = a.hp->ppo2_vf_coef_halving ? 0.5f : 1.f;
   lh.NA = NA;
-  const float beta2 = a.ohp->beta2, adam_eps = a.ohp->eps, lr = a.ohp->lr;
+  float beta2 = a.ohp->beta2, adam_eps = a.ohp->eps;
+  const float lr = a.ohp->lr;
   const double beta1_d = a.ohp->beta1_d, beta2_d = a.ohp->beta2_d;
-  const float max_grad_norm = a.ohp->max_grad_norm;
+  float max_grad_norm = a.ohp->max_grad_norm;
+  float w1c = (float)(1.0 - beta1_d), w2c = (float)(1.0 - beta2_d);  // Adam's lerp / addcmul weights
   unsigned long long* const sync = a.xchg;
   const __amdgpu_buffer_rsrc_t srs = mc_rsrc(a.scratch, (int)M8_SCRATCH);
   // [par][net][c][hi, lo] share-norm granules (within the share-norm region)
@@ -344,8 +346,14 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
 #endif
 
   // the loss's 1 / (rows x world) off the step's critical path, for a full and for the last minibatch
-  const float invB_full = 1.f / (float)(B * a.world);
-  const float invB_last = nmb > 0 ? 1.f / (float)((int)(n_rows - (int64_t)(nmb - 1) * B) * a.world) : 0.f;
+  float invB_full = 1.f / (float)(B * a.world);
+  float invB_last = nmb > 0 ? 1.f / (float)((int)(n_rows - (int64_t)(nmb - 1) * B) * a.world) : 0.f;
+  // loop-invariant floats held in VGPRs: uniform, but the kernel runs at the SGPR limit, and kept in SGPRs
+  // they are spilled to VGPR lanes and restored with v_readlane inside the step
+  asm volatile("" : "+v"(beta2), "+v"(adam_eps), "+v"(max_grad_norm), "+v"(w1c), "+v"(w2c), "+v"(invB_full),
+               "+v"(invB_last));
+  asm volatile("" : "+v"(lh.clip_range), "+v"(lh.ent_coef), "+v"(lh.vf_coef0), "+v"(lh.halve), "+v"(lh.clip_range_vf),
+               "+v"(lh.pi_coef));
 
   constexpr long long MC_WAIT_LOCAL = RAI_SPIN_LOCAL, MC_WAIT_REMOTE = RAI_SPIN_REMOTE;
   for (int mb = 0; mb < nmb; ++mb) {
@@ -715,7 +723,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
     } else {
       bias_corr(mb, inv_bc2_sqrt, neg_step);
     }
-    const float w1 = (float)(1.0 - beta1_d), w2 = (float)(1.0 - beta2_d);
+    const float w1 = w1c, w2 = w2c;
     {
       RELANE();
       const int ch = c * SH + tid;

@@ -11,7 +11,7 @@ bash tools/gpu_pytest.sh ${T}_dptests 400 tests/test_gpu_dp.py -k "fused_dp or e
 timeout -k 10 200 python tools/mlp_stamps.py > gpurun_out/${T}_stamps.txt 2>&1 &&
 for i in 1 2; do
   for cfg in c2 c4; do
-    for v in new base alt2; do
+    for v in new base; do
       [ $cfg = c2 ] && [ $v = alt2 ] && continue
       case $v in new) lib=$L/librai_amd.so;; base) lib=$L/librai_amd_alt.so;; alt2) lib=$L/librai_amd_alt2.so;; esac
       if [ $cfg = c2 ]; then args="--steps 2"; else args="--config halfcheetah --steps 1 --warmup 1"; fi
