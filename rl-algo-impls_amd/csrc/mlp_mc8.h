@@ -964,6 +964,8 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
     }
   }
 #ifdef RAI_STAMPS
+  if (c == 0 && tid == 0) S.stamps[31] = (unsigned long long)S.xl;  // launches with the one-XCC store form
+  __syncthreads();
   if (c == 0 && tid < 32) atomicAdd(&g_stamps[net][tid], S.stamps[tid]);  // summed over launches
 #endif
   if (ACTOR && c == 0 && tid == 0) {

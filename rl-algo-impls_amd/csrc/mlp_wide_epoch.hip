@@ -1368,7 +1368,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   }
 #ifdef RAI_STAMPS
   if (j == 0 && tid == 0)
-    for (int i = 0; i < 24; ++i) atomicAdd(&g_we_stamps[net][i], st_acc[i]);
+    for (int i = 0; i < 24; ++i) atomicAdd(&g_we_stamps[net][i], i == 23 ? (unsigned long long)xl : st_acc[i]);
 #endif
 
   // ---- write back what this workgroup owns: parameters and Adam moments ----------------------

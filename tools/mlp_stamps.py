@@ -58,6 +58,8 @@ print(f"epoch {ev0.elapsed_time(ev1):.2f} ms for {nmb} minibatches -> {ev0.elaps
 # phases are split by STAMP(9..14).  Every stamp is the time since the previous one, so a phase's time is
 # the sum of its work and wait stamps and the % column is over all of them (work plus waits).
 MC8_PARTS = [(15, 1), (16, 2), (17, 3), (18, 4), (19, 5), (9, 10, 6), (11, 12, 13, 7), (14, 8)]
+if LAYOUT == "mc8":  # slot 31: launches whose network ran on one XCC (plain-store hand-offs)
+    print(f"one-XCC store form: actor {st[0, 31]:.0f}, critic {st[1, 31]:.0f} of 1 launch")
 for net in range(2):
     if LAYOUT == "mc8":
         ph = [sum(st[net, i] for i in parts) for parts in MC8_PARTS]

@@ -55,6 +55,8 @@ st = (np.array(out, dtype=np.float64) - np.array(out0, dtype=np.float64)).reshap
 nmb = (r.total_steps + 63) // 64
 assert algo._we_ws is not None, "whole-epoch kernel not used"
 print(f"epoch {ev0.elapsed_time(ev1):.2f} ms for {nmb} minibatches -> {ev0.elapsed_time(ev1) * 1e3 / nmb:.2f} us/mb")
+# slot 23: launches whose network ran on one XCC (plain-store hand-offs)
+print(f"one-XCC store form: actor {st[0, 23]:.0f}, critic {st[1, 23]:.0f} of 1 launch")
 for net in range(2):
     tot = st[net, :len(NAMES)].sum()
     print(f"--- workgroup 0 of the {'actor' if net == 0 else 'critic'}: {tot / nmb:.0f} ticks/mb")
