@@ -351,6 +351,20 @@ __device__ __forceinline__ void adam_fast(float& p, float& m, float& v, float g,
   p = p + c4 * (m * __builtin_amdgcn_rcpf(denom));
 }
 
+typedef float f2a __attribute__((ext_vector_type(2)));
+// adam_fast on an element pair (packed f32 VALU; the same operations per element)
+__device__ __forceinline__ void adam_fast2(f2a& p, f2a& m, f2a& v, f2a g, float c1, float c2, float beta2, float inv_c3,
+                                           float c4, float eps) {
+  const f2a C1 = {c1, c1}, Cb = {c2, c2}, B2 = {beta2, beta2}, IC = {inv_c3, inv_c3}, EP = {eps, eps}, C4 = {c4, c4};
+  m = m + C1 * (g - m);
+  v = v * B2;
+  v = v + (Cb * g) * g;
+  const f2a sq = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+  const f2a denom = sq * IC + EP;
+  const f2a rc = {__builtin_amdgcn_rcpf(denom.x), __builtin_amdgcn_rcpf(denom.y)};
+  p = p + C4 * (m * rc);
+}
+
 // arrive on counter `ci` after every wave's stores drained (caller: s_waitcnt vmcnt(0) in every
 // storing wave, then this); lane 0 polls until ctr[ci] >= want.
 // dH1 tile of wave w: D[i][u] = sum_k dZ2[16 w + i][k] W2[k][16 j + u] over k in [0, H): lane group g
@@ -473,14 +487,14 @@ __device__ __forceinline__ f4 we_fwd1(const float* xa, const float* wa, int nk) 
 // at the row's start), sc1 like every load of handed-off bytes; wave w takes rows w, w + 4, ...  The
 // data lands without VGPRs or ds_write instructions; the caller's barrier follows the vmcnt(0) here.
 __device__ __forceinline__ void we_gather_lds(const unsigned char* ws, int64_t base, int H, float (*Act)[WE_HP], int w,
-                                              int lane) {
+                                              int lane, bool drain = true) {
   if (lane < (H >> 2)) {
     const float* src = reinterpret_cast<const float*>(ws + base) + 4 * lane;
 #pragma unroll
     for (int r = w; r < WE_B; r += 4)
       __builtin_amdgcn_global_load_lds(src + (int64_t)r * H, &Act[r][0], 16, 0, WE_SC1);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Wave 1 runs `side` (work off the critical path: LDS in, LDS / plain global out) while lane 0 polls.
@@ -671,22 +685,39 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) g_r[t][r] = 0.f;
-  auto adam_w2 = [&]() {
+  // (element pairs in packed f32 math; branch-free over the column tiles: a tile past H has zero moments
+  // and gradient, so its update leaves those padding columns of W2r -- never read -- as they are.  All the
+  // LDS reads first, then the arithmetic, then the stores, so the pairs' latencies overlap.)
+  auto adam_w2 = [&](int t0, int t1) {  // the column tiles t in [t0, t1) of each wave
     const float coef = S.coef;
     const float inv_c3 = S.adamc[0], c4 = S.adamc[1];
+    const f2a C2 = {coef, coef};
+    f2a pp[4][2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int ct = 4 * w + t;
-      if (ct < G) {
+    for (int t = t0; t < t1; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float& p = S.W2r[4 * g + r][WE_SL * ct + li];
-          float pv = p;
-          adam_fast(pv, m_r[t][r], v_r[t][r], g_r[t][r] * coef, c1, c2, beta2, inv_c3, c4, eps);
-          p = pv;
-        }
+      for (int h = 0; h < 2; ++h)
+        pp[t][h] = f2a{S.W2r[4 * g + 2 * h][WE_SL * (4 * w + t) + li], S.W2r[4 * g + 2 * h + 1][WE_SL * (4 * w + t) + li]};
+#pragma unroll
+    for (int t = t0; t < t1; ++t) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f2a mm = {m_r[t][2 * h], m_r[t][2 * h + 1]}, vv = {v_r[t][2 * h], v_r[t][2 * h + 1]};
+        const f2a gg = f2a{g_r[t][2 * h], g_r[t][2 * h + 1]} * C2;
+        adam_fast2(pp[t][h], mm, vv, gg, c1, c2, beta2, inv_c3, c4, eps);
+        m_r[t][2 * h] = mm.x;
+        m_r[t][2 * h + 1] = mm.y;
+        v_r[t][2 * h] = vv.x;
+        v_r[t][2 * h + 1] = vv.y;
       }
     }
+#pragma unroll
+    for (int t = t0; t < t1; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        S.W2r[4 * g + 2 * h][WE_SL * (4 * w + t) + li] = pp[t][h].x;
+        S.W2r[4 * g + 2 * h + 1][WE_SL * (4 * w + t) + li] = pp[t][h].y;
+      }
   };
 
   for (int mb = 0; mb < nmb; ++mb) {
@@ -769,7 +800,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     // wait.  Same values as applying it at the end of the previous step.
     we_arrive(ctr, WE_CA + net);
     if (w == 1) side_a();
-    if (WE_DEFER_W2 && mb > 0) adam_w2();
+    // (half of it: the other half runs under the H1 gather's LDS-DMA below)
+    if (WE_DEFER_W2 && mb > 0) adam_w2(0, 2);
+    WSTAMP(22);  // (stamps: the A wait split into the deferred Adam and the rest of the wait)
     if (!we_wait(ctr, WE_CA + net, want, a.state, S.bail)) break;
 #ifndef RAI_WE_NO_XCC_LOCAL
     if (mb == 0) {  // every workgroup of the network registered its XCC before its step-0 A arrival
@@ -783,13 +816,17 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
 #endif
     WSTAMP(1);
-    we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // H1 -> Act
-    // W2 rows j (as updated by the last Adam step) for this step's column owners: issued after the
-    // gather's drain, so they drain in the background during fwd2 -- by the B publish's drain, before
-    // this workgroup's B arrival, after which the column owners load them (step 0: the tiles published
-    // before the loop)
-    if (mb > 0) we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane, xl);
+    // H1 -> Act by LDS-DMA, and while it lands the deferred W2 Adam's other half (LDS rows W2r, disjoint
+    // from Act); then the drain and the barrier
+    we_gather_lds(a.ws, WE_H1_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane, false);
+    if (WE_DEFER_W2 && mb > 0) adam_w2(2, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
+    // W2 rows j (as updated by the last Adam step, every wave's tiles: after the barrier) for this step's
+    // column owners: drained in the background during fwd2 -- by the B publish's drain, before this
+    // workgroup's B arrival, after which the column owners load them (step 0: the tiles published before
+    // the loop)
+    if (mb > 0) we_publish_w2(S.W2r, wrs, w2t_mine, G, w, lane, xl);
     WSTAMP(2);
     // ============ fwd2: H2[:, j] = act(H1 W2[j]^T + b2[j]); wave w: row tile w =============
     {
@@ -1343,7 +1380,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       const float coef = S.coef;
       const float inv_c3 = S.adamc[0], c4 = S.adamc[1];
       // (the W2 row slice: deferred to the next step's A wait, adam_w2)
-      if (!WE_DEFER_W2) adam_w2();
+      if (!WE_DEFER_W2) adam_w2(0, 4);
       if (WE_SL * w + li < IN) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1363,7 +1400,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     WSTAMP(21);
   }
   if (WE_DEFER_W2 && !S.bail && nmb > 0) {  // the last step's deferred W2 Adam
-    adam_w2();
+    adam_w2(0, 4);
     lds_barrier();
   }
 #ifdef RAI_STAMPS

@@ -22,10 +22,11 @@ from rl_algo_impls_amd.policy import ActorCritic  # noqa: E402
 from rl_algo_impls_amd.ppo import PPO  # noqa: E402
 from rl_algo_impls_amd.rollout import SyncStepRolloutGenerator  # noqa: E402
 
-NAMES = ["X + fwd1 + publish H1", "A wait (wave 1: Gaussian constants)", "gather H1", "fwd2 tile",
+NAMES = ["X + fwd1 + publish H1", "A wait (after the deferred Adam)", "gather H1", "fwd2 tile",
          "partials + publish P", "B wait", "load partials", "loss compute (wave 0)", "loss LDS out + barrier",
          "bwd2 dZ2 + publish", "small grads", "dW2 rows", "C wait", "gather dZ2", "dH1 + dZ1", "-", "dW1",
-         "db1 (wave 3)", "norm share + drain", "prefetch issue", "D wait (wave 1: stats)", "clip + Adam"]
+         "db1 (wave 3)", "norm share + drain", "prefetch issue", "D wait (wave 1: stats)", "clip + Adam",
+         "A: arrival + deferred W2 Adam"]
 lib = _lib.lib()
 fn = getattr(lib, "rai_wide_epoch_debug_stamps")
 fn.restype = C.c_int
