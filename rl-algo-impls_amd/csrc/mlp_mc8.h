@@ -807,7 +807,9 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
       }
       ss = wave_sum_v(ss);
       if (lane == 0) S.sq[w] = ss;  // the CU's share norm: its four wave parts, summed below in wave order
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the waves that stored share chunks drain them (the others -- wave 3 with the next step's row loads in
+      // flight -- have nothing to drain)
+      if (64 * w < SH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     STAMP(12);
     __syncthreads();

@@ -926,6 +926,84 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     }
     lds_barrier();
     WSTAMP(6);
+#ifndef RAI_WE_LOSS_ONE_WAVE
+    if (HEAD == 1 && net == 0) {
+      // Gaussian actor: every wave, 16 rows each, four lanes per row (lane & 3 = dimension pair dp: dims
+      // 2 dp, 2 dp + 1).  The log-prob's eight per-dimension terms are gathered across the quad and summed
+      // in dimension order (the one-wave form's order), so every lane of the quad forms the identical row
+      // values; each lane then writes the loss gradient of its two dimensions.
+#pragma clang fp contract(off)
+      const int rq = lane >> 2, dp = lane & 3;
+      const int r = 16 * w + rq;
+      const bool valid = r < rows;
+      const float* lr_ = &S.Xl[WE_B * WE_INMAX + r * WE_LIN];
+      const float c_adv = lr_[0], c_lpold = lr_[1];
+      const int o0 = 2 * dp;
+      const float2 ca = *reinterpret_cast<const float2*>(&lr_[4 + o0]);  // the action's dims o0, o0 + 1
+      float outv[2], term[2], ginv2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int o = o0 + e;
+        outv[e] = (((S.Pw[0][r][o] + S.Pw[1][r][o]) + S.Pw[2][r][o]) + S.Pw[3][r][o]) +
+                  S.small[2 * WE_SL + WE_OUTM * WE_SL + o];
+        ginv2[e] = S.ginv[o];
+        const float xo = (e ? ca.y : ca.x) - outv[e];
+        const float tm = -(xo * xo) * (0.5f * ginv2[e]) - S.glsc[o] - 0.91893853320467274f;
+        term[e] = o < O ? tm : 0.f;
+      }
+      // the eight terms in every lane of the quad (quad_perm broadcasts), summed in dimension order
+      auto qb = [](float v, int k) {
+        const int x = __float_as_int(v);
+        int y;
+        switch (k) {
+          case 0: y = __builtin_amdgcn_mov_dpp(x, 0x00, 0xF, 0xF, false); break;
+          case 1: y = __builtin_amdgcn_mov_dpp(x, 0x55, 0xF, 0xF, false); break;
+          case 2: y = __builtin_amdgcn_mov_dpp(x, 0xAA, 0xF, 0xF, false); break;
+          default: y = __builtin_amdgcn_mov_dpp(x, 0xFF, 0xF, 0xF, false); break;
+        }
+        return __int_as_float(y);
+      };
+      float lp = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lp += qb(term[0], k);
+        lp += qb(term[1], k);
+      }
+      const float A = c_adv;  // normalized per minibatch by we_pack_kernel before the epoch
+      const float ent = S.entc;
+      const float invB = mb + 1 < nmb ? invB_full : invB_last;
+      const float logratio = lp - c_lpold;
+      const float ratio = expf(logratio);
+      const float lo = 1.f - hp.clip_range, hi = 1.f + hp.clip_range;
+      const float cr = fminf(fmaxf(ratio, lo), hi);
+      const float s1 = ratio * A, s2 = cr * A;
+      const float g_pi = -invB;
+      float g1, g2;
+      if (s1 < s2) { g1 = g_pi; g2 = 0.f; }
+      else if (s1 > s2) { g1 = 0.f; g2 = g_pi; }
+      else { g1 = g_pi * 0.5f; g2 = g_pi * 0.5f; }
+      const float in_clip = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+      const float d_logp = valid ? (g1 * A + (g2 * A) * in_clip) * ratio : 0.f;
+      const float d_ent = valid ? (mb + 1 < nmb ? dent_full : dent_last) : 0.f;
+      float dd[2], dlv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool on = o0 + e < O;
+        const float xo = (e ? ca.y : ca.x) - outv[e];
+        dd[e] = on ? d_logp * (xo * ginv2[e]) : 0.f;
+        dlv[e] = on ? d_logp * ((xo * xo) * ginv2[e] - 1.f) + d_ent : 0.f;
+      }
+      *reinterpret_cast<float2*>(&S.dOut[r][o0]) = float2{dd[0], dd[1]};
+      *reinterpret_cast<float2*>(&S.dls[r][o0]) = float2{dlv[0], dlv[1]};
+      if (dp == 0) {
+        S.st[0][r] = valid ? (double)fminf(s1, s2) : 0.0;
+        S.st[1][r] = valid ? (double)((ratio - 1.f) - logratio) : 0.0;
+        S.st[2][r] = valid ? ((fabsf(ratio - 1.f) > hp.clip_range) ? 1.0 : 0.0) : 0.0;
+        S.st[3][r] = valid ? (double)ent : 0.0;
+      }
+      WSTAMP(7);
+    } else
+#endif
     if (w == 0) {
       const int r = lane;
       const bool valid = r < rows;

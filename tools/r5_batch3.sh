@@ -8,7 +8,7 @@ L=$PWD/rl-algo-impls_amd/lib
 mkdir -p gpurun_out
 bash tools/gpu_pytest.sh ${T}_tests 600 tests/test_gpu_trainer.py -k "fused or c2_horizon or learns or reference_steps or wide" &&
 bash tools/gpu_pytest.sh ${T}_dptests 400 tests/test_gpu_dp.py -k "fused_dp or env_partition or wide_epoch_xdp" &&
-timeout -k 10 200 python tools/mlp_stamps.py > gpurun_out/${T}_stamps.txt 2>&1 &&
+timeout -k 10 200 python tools/mlp_stamps.py > gpurun_out/${T}_stamps.txt 2>&1 && timeout -k 10 200 python tools/wide_stamps.py > gpurun_out/${T}_wide_stamps.txt 2>&1 &&
 for i in 1 2; do
   for cfg in c2 c4; do
     for v in new base; do
