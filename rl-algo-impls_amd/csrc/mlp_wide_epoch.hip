@@ -487,12 +487,18 @@ __device__ __forceinline__ f4 we_fwd1(const float* xa, const float* wa, int nk) 
 // at the row's start), sc1 like every load of handed-off bytes; wave w takes rows w, w + 4, ...  The
 // data lands without VGPRs or ds_write instructions; the caller's barrier follows the vmcnt(0) here.
 __device__ __forceinline__ void we_gather_lds(const unsigned char* ws, int64_t base, int H, float (*Act)[WE_HP], int w,
-                                              int lane, bool drain = true) {
+                                              int lane, bool drain = true, bool own_tile = false) {
   if (lane < (H >> 2)) {
     const float* src = reinterpret_cast<const float*>(ws + base) + 4 * lane;
+    if (own_tile) {  // rows [16 w, 16 w + 16): this wave's row tile
 #pragma unroll
-    for (int r = w; r < WE_B; r += 4)
-      __builtin_amdgcn_global_load_lds(src + (int64_t)r * H, &Act[r][0], 16, 0, WE_SC1);
+      for (int r = 16 * w; r < 16 * w + 16; ++r)
+        __builtin_amdgcn_global_load_lds(src + (int64_t)r * H, &Act[r][0], 16, 0, WE_SC1);
+    } else {
+#pragma unroll
+      for (int r = w; r < WE_B; r += 4)
+        __builtin_amdgcn_global_load_lds(src + (int64_t)r * H, &Act[r][0], 16, 0, WE_SC1);
+    }
   }
   if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -656,16 +662,19 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     const int row = e4 / R4, c4 = e4 - row * R4;
     dst[u] = row >= WE_B ? -1 : (c4 < WE_LIN / 4 ? WE_B * WE_INMAX + row * WE_LIN + 4 * c4 : row * IN4 + 4 * (c4 - WE_LIN / 4));
   }
+  // buffer loads: the minibatch's block offset is one scalar, each thread's 16-B offset in it is fixed, and
+  // a record past the rollout's last row reads 0 (the buffer's bound: the last, partial minibatch)
+  const __amdgpu_buffer_rsrc_t rrs = we_rsrc(a.rec, n_rows * R * 4);
   auto prefetch = [&](int m) {
     const int64_t r0 = (int64_t)m * B;
     const int rws = (int)min((int64_t)B, n_rows - r0);
     const int n4 = rws * R4;
-    const f4* src = reinterpret_cast<const f4*>(a.rec + r0 * R);
+    const int boff = (int)(r0 * R * 4);
 #pragma unroll
     for (int u = 0; u < WE_RU; ++u) {
-      const int e4 = tid + WE_NT * u;
       xr[u] = f4{0.f, 0.f, 0.f, 0.f};
-      if (WE_NT * u + 64 * w < n4 && e4 < n4) xr[u] = src[e4];
+      if (WE_NT * u + 64 * w < n4)  // wave-uniform skip of the 16-B pieces past the block
+        xr[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rrs, 16 * (tid + WE_NT * u), boff, 0));
     }
   };
   if (nmb > 0) prefetch(0);
@@ -1236,8 +1245,10 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     __syncthreads();
     if (S.bail) break;
     WSTAMP(12);
-    we_gather_lds(a.ws, WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane);  // dZ2 -> Act
-    lds_barrier();
+    // dZ2 -> Act: wave w gathers the 16 rows of its own dH1 row tile (the only rows it reads below), so its
+    // own drain suffices -- no workgroup barrier (the W2 column tiles it also reads were drained before the
+    // C arrival's barrier)
+    we_gather_lds(a.ws, WE_Z2_OFF + (int64_t)(net * 2 + par) * WE_ACT_SLOT, H, S.Act, w, lane, true, true);
     WSTAMP(13);
     // ============ bwd1: dH1[:, j] = dZ2 W2[:, slice j] -> dZ1, dW1 rows j, db1 j ==================
     {
@@ -1620,6 +1631,8 @@ static int wide_epoch(const rai_mlp_wide_desc* desc, float* params, float* exp_a
   if (desc->head != 0 && desc->head != 1) return RAI_E_MODE;
   if (desc->head == 1 && !desc->log_std) return RAI_E_NULLPTR;
   if (desc->accumulate) return RAI_E_UNSUPPORTED;
+  // the per-row records are read through one buffer resource (32-bit byte bound)
+  if (n_rows * we_rec_floats(desc->in_dim) * 4 >= (1LL << 31)) return RAI_E_UNSUPPORTED;
   for (int n = 0; n < 2; ++n)
     for (int i = 0; i < 6; ++i) {
       if (!desc->w[n][i]) return RAI_E_NULLPTR;
