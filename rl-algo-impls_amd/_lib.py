@@ -26,6 +26,14 @@ RAI_WIDE_MAX_IN = 64
 RAI_WIDE_MAX_OUT = 8
 RAI_STAT_STRIDE = 5 + 2 * RAI_MAX_K
 ABI_VERSION = 1
+# the RAI_E_* return codes of include/rai_amd.h (tests/test_boundary.py checks them against the header)
+RAI_E_NULLPTR = -1
+RAI_E_SHAPE = -2
+RAI_E_MODE = -3
+RAI_E_TOO_MANY_COLUMNS = -4
+RAI_E_WORKSPACE = -5
+RAI_E_UNSUPPORTED = -6
+RAI_E_DP_BASE = -1000
 
 
 class PPOHparams(C.Structure):

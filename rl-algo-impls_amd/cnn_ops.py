@@ -320,7 +320,7 @@ def _conv_dgrad(x, dz, w, stride) -> torch.Tensor:
         dx = torch.empty((B, Ci, H, W), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
         rc = _lib.lib().rai_conv2d_dgrad(dz.data_ptr(), w.data_ptr(), B, H, W, Ci, Co, KH, KW, s, dx.data_ptr(),
                                          _lib.stream_handle(x.device))
-        if rc != -6:  # RAI_E_UNSUPPORTED: no instantiation for the shape, MIOpen below
+        if rc != _lib.RAI_E_UNSUPPORTED:  # no instantiation for the shape: MIOpen below
             _lib.check(rc, "rai_conv2d_dgrad")
             return dx
     return torch.ops.aten.convolution_backward(dz, x, w, None, _pair(stride), [0, 0], [1, 1], False, [0, 0], 1,
@@ -338,7 +338,7 @@ def _conv_dgrad_relu(x, dy, y, w, stride):
     dx = torch.empty((B, Ci, H, W), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
     rc = _lib.lib().rai_conv2d_dgrad_relu(dy.data_ptr(), y.data_ptr(), w.data_ptr(), B, H, W, Ci, Co, KH, KW, s,
                                           dx.data_ptr(), _lib.stream_handle(x.device))
-    if rc == -6:  # RAI_E_UNSUPPORTED
+    if rc == _lib.RAI_E_UNSUPPORTED:
         return None
     _lib.check(rc, "rai_conv2d_dgrad_relu")
     return dx

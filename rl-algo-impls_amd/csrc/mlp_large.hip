@@ -21,7 +21,7 @@
 //       dW2 += dZ2^T H1 and [dW1 | db1] += dZ1^T [x | 1] on MFMA with the rows as the reduction axis
 //       (dZ2, H1, dZ1 transposed through a per-wave LDS tile; the x operand is loaded transposed);
 //       dW3, db2, db3 as per-lane partial sums.
-//     Accumulators persist over the wave's tiles; the 8 waves add their partials in LDS in wave order
+//     Accumulators persist over the wave's tiles; the LB_NW (= 4) waves add their partials in LDS in wave order
 //     and the workgroup writes ONE partial gradient (its network's parameter block) + loss-statistic
 //     partials.  Tiles are dealt to waves statically: the summation order is fixed (deterministic).
 //  2. lb_reduce_kernel: every parameter's 128 workgroup partials summed in workgroup order -> the flat

@@ -755,7 +755,8 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
         // and sums the world slots in rank order (identical bits on every rank). ------------------
         const int W = a.xworld;
         const unsigned long long step_id = (unsigned long long)(a.xbase + kk_mb + 1);
-        const int slot_off = XDP_FLAGS_BYTES + ((par * W + a.xrank) * 2 + net) * WL_N * (int)sizeof(float);
+        const int xpar = (int)((a.xbase + kk_mb) & 1);  // global-step parity: mb restarts at 0 every launch
+        const int slot_off = XDP_FLAGS_BYTES + ((xpar * W + a.xrank) * 2 + net) * WL_N * (int)sizeof(float);
         for (int pr = 0; pr < W; ++pr) {
           const __amdgpu_buffer_rsrc_t prs = mc_rsrc(a.xpeers[pr], (int)xdp_region_bytes(W));
 #pragma unroll
@@ -795,7 +796,7 @@ __device__ __forceinline__ void mlp_mc(const MlpArgs& a, SmemM<OUTP>& S, const i
           const int chl = min(tid + MC_NT * i, WL_CH - 1);
           f4 sum = f4{0.f, 0.f, 0.f, 0.f};
           for (int pr = 0; pr < W; ++pr) {
-            const int off = XDP_FLAGS_BYTES + ((par * W + pr) * 2 + net) * WL_N * (int)sizeof(float);
+            const int off = XDP_FLAGS_BYTES + ((xpar * W + pr) * 2 + net) * WL_N * (int)sizeof(float);
             sum += as_f4(__builtin_amdgcn_raw_buffer_load_b128(lrs, off + 16 * chl, 0, XDP_AUX));
           }
           if (tid + MC_NT * i < WL_CH) gr[i] = sum;

@@ -756,7 +756,8 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         // in rank order (identical bits on every rank) ---------------------------------------
         const int W = a.xworld;
         const unsigned long long step_id = (unsigned long long)(a.xbase + mb + 1);
-        const int slot_off = XDP_FLAGS_BYTES + ((par * W + a.xrank) * 2 + net) * WL_N * (int)sizeof(float);
+        const int xpar = (int)((a.xbase + mb) & 1);  // global-step parity: mb restarts at 0 every launch
+        const int slot_off = XDP_FLAGS_BYTES + ((xpar * W + a.xrank) * 2 + net) * WL_N * (int)sizeof(float);
         for (int pr = 0; pr < W; ++pr) {
           const __amdgpu_buffer_rsrc_t prs = mc_rsrc(a.xpeers[pr], (int)xdp_region_bytes(W));
           if (own) __builtin_amdgcn_raw_buffer_store_b128(as_u4(s), prs, slot_off + 16 * ch, 0, XDP_AUX);
@@ -787,7 +788,7 @@ __device__ __forceinline__ void mlp_mc8(const MlpArgs& a, SmemM8<OUTP, G, RCV>& 
         const __amdgpu_buffer_rsrc_t lrs = mc_rsrc(a.xpeers[a.xrank], (int)xdp_region_bytes(W));
         f4 sum = f4{0.f, 0.f, 0.f, 0.f};
         for (int pr = 0; pr < W; ++pr) {
-          const int off = XDP_FLAGS_BYTES + ((par * W + pr) * 2 + net) * WL_N * (int)sizeof(float);
+          const int off = XDP_FLAGS_BYTES + ((xpar * W + pr) * 2 + net) * WL_N * (int)sizeof(float);
           sum += as_f4(__builtin_amdgcn_raw_buffer_load_b128(lrs, off + 16 * chl, 0, XDP_AUX));
         }
         s = sum;

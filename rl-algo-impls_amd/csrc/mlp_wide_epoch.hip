@@ -662,8 +662,9 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     const int row = e4 / R4, c4 = e4 - row * R4;
     dst[u] = row >= WE_B ? -1 : (c4 < WE_LIN / 4 ? WE_B * WE_INMAX + row * WE_LIN + 4 * c4 : row * IN4 + 4 * (c4 - WE_LIN / 4));
   }
-  // buffer loads: the minibatch's block offset is one scalar, each thread's 16-B offset in it is fixed, and
-  // a record past the rollout's last row reads 0 (the buffer's bound: the last, partial minibatch)
+  // buffer loads: the minibatch's block offset joins each thread's fixed 16-B offset in the VECTOR offset,
+  // so a record past the rollout's last row reads 0 (the buffer's bound applies to voffset only -- soffset
+  // is excluded from the range check -- which covers the rows [rws, B) of the last, partial minibatch)
   const __amdgpu_buffer_rsrc_t rrs = we_rsrc(a.rec, n_rows * R * 4);
   auto prefetch = [&](int m) {
     const int64_t r0 = (int64_t)m * B;
@@ -674,7 +675,7 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
     for (int u = 0; u < WE_RU; ++u) {
       xr[u] = f4{0.f, 0.f, 0.f, 0.f};
       if (WE_NT * u + 64 * w < n4)  // wave-uniform skip of the 16-B pieces past the block
-        xr[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rrs, 16 * (tid + WE_NT * u), boff, 0));
+        xr[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rrs, boff + 16 * (tid + WE_NT * u), 0, 0));
     }
   };
   if (nmb > 0) prefetch(0);
@@ -1312,11 +1313,15 @@ __device__ void we_epoch(const WeArgs& a, WeSmem& S, const int net, const int j)
       __syncthreads();  // S.gsm (waves 0-2) and S.db1 (wave 3) complete
       const int W = a.world;
       const unsigned long long step_id = (unsigned long long)(a.xbase + mb + 1);
+      // the cross-rank slots alternate with the GLOBAL step (not mb, which restarts every launch): with an
+      // odd minibatch count a rank entering the next launch early would otherwise reuse the parity a slow
+      // peer is still summing
+      const int xpar = (int)((a.xbase + mb) & 1);
       const int rb = (int)rai_xdp_wide_bytes(W);
       // slot floats: [0, 4096) W2 rows j as f4 (w 4 + t) 64 + lane; [4096, 5120) W1 rows j, f4 w 64 + lane;
       // [5120, 5296) the small gradients by small index (db1 j from S.db1)
       auto slot_off = [&](int sender) {
-        return RAI_XDP_SLOTS_OFF + ((((par * W + sender) * 2 + net) * WE_GMAX + j) * RAI_XDP_WIDE_SLOTF) * 4;
+        return RAI_XDP_SLOTS_OFF + ((((xpar * W + sender) * 2 + net) * WE_GMAX + j) * RAI_XDP_WIDE_SLOTF) * 4;
       };
       const bool w1_on = WE_SL * w < IN;
       const bool sm_on = tid < WE_NSMALL / 4;

@@ -122,3 +122,13 @@ def test_ctypes_signatures_match_header_arity():
         params = decls[name].strip()
         n = 0 if params in ("", "void") else params.count(",") + 1
         assert len(args) == n, (name, len(args), n)
+
+
+def test_error_code_constants_match_header():
+    """_lib's RAI_E_* constants are the header's enum values (cnn_ops' MIOpen fallback keys on
+    RAI_E_UNSUPPORTED: a renumbered enum must fail here, not turn the fallback into a hard error)."""
+    hdr = (ROOT / "include" / "rai_amd.h").read_text()
+    codes = {m.group(1): int(m.group(2)) for m in re.finditer(r"\b(RAI_E_[A-Z_]+)\s*=\s*(-?\d+)", hdr)}
+    assert codes and "RAI_E_UNSUPPORTED" in codes
+    for name, v in codes.items():
+        assert getattr(_lib, name) == v, name
