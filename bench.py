@@ -86,6 +86,12 @@ def parse():
                    help="split (default) = SURVEY 8(d): the config's num_envs is global, each rank owns "
                         "num_envs / world of them (total work fixed: strong scaling); per-rank = every rank "
                         "owns num_envs envs (per-GPU work fixed: weak scaling)")
+    p.add_argument("--dp-update", default="auto", choices=["auto", "exchange", "replicated"],
+                   help="data-parallel update (PPO.enable_data_parallel update_mode): exchange = the ranks' "
+                        "gradients summed every optimizer step; replicated = one all-gather of the rollout per "
+                        "update, the identical single-process update on every rank (global minibatch only); "
+                        "auto (default) = replicated for the dependent-chain epoch kernels (C2 at the YAML "
+                        "batch, C4), exchange otherwise")
     p.add_argument("--deterministic", type=int, default=0, choices=[0, 1],
                    help="1: torch.use_deterministic_algorithms + MIOpen deterministic solvers (the reference's "
                         "set_device_optimizations default, rl_algo_impls/runner/running_utils.py:161-166); off by "
@@ -375,7 +381,8 @@ def main():
     gen = SyncStepRolloutGenerator(policy, env, n_steps=T, seed=1234 + rank, **rollout_kw)
     algo = PPO(policy, dev, None, **algo_kw)
     if world > 1 or args.dp_rehearsal:  # minibatch rule: one for every config, named in the JSON line
-        algo.enable_data_parallel(dp_batch=args.dp_batch)
+        algo.enable_data_parallel(dp_batch=args.dp_batch,
+                                  update_mode=None if args.dp_update == "auto" else args.dp_update)
 
     def barrier():
         if world > 1:
@@ -638,7 +645,12 @@ def main():
             "lib_sha256": lib_sha,
         }
         if args.dp_rehearsal or world > 1:
-            if algo._xdp is not None:
+            line["config"]["dp_update"] = algo.dp_update_mode
+            if algo.dp_update_mode == "replicated":
+                line["dp_path"] = ("replicated update: each rank steps its env share, one all-gather of the rollout "
+                                   "per update (" + backend + "), the identical single-process update on every "
+                                   "rank (strong scaling of the rollout only; the update is a dependent chain)")
+            elif algo._xdp is not None:
                 line["dp_path"] = "in-kernel cross-GPU exchange (IPC-mapped xGMI regions), one launch per epoch"
             elif algo._dp_comm is not None and getattr(algo, "_buckets", None) is not None:
                 line["dp_path"] = ("bucketed RCCL all-reduce per optimizer step on a side stream, overlapped with "

@@ -94,13 +94,14 @@ class PPO:
         self._dp_comm = None
         self.dp_enabled = False  # enable_data_parallel() called (any world size, incl. 1-rank rehearsal)
         self.dp_batch = "per-rank"
+        self.dp_update_mode = "exchange"  # or "replicated" (enable_data_parallel)
         self.global_batch_size = batch_size
         self._yaml_batch_size = batch_size  # enable_data_parallel derives the per-rank size from it
         self._buckets = None
 
     # -- data parallel (one process per GPU) ------------------------------------------------
     def enable_data_parallel(self, group=None, native_dp: bool = True, xdp: Optional[bool] = None,
-                             dp_batch: str = "global") -> None:
+                             dp_batch: str = "global", update_mode: Optional[str] = None) -> None:
         """Data parallelism: every rank owns its own env group and HBM rollout; a global
         minibatch is the union of the ranks' minibatch slices, gradients are summed over ranks
         with one all-reduce per optimizer step (RCCL over xGMI via torch.distributed, or the
@@ -115,7 +116,18 @@ class PPO:
         minibatch batch_size x world); "global" — SURVEY.md 8(e)'s rule: batch_size / world rows
         per rank, so the global minibatch is batch_size (rl_algo_impls/ppo/ppo.py:314,
         rollout/vec_rollout.py:108-111) and the update equals the single-process one over the
-        ranks' interleaved rollouts."""
+        ranks' interleaved rollouts.
+
+        update_mode: "exchange" — every optimizer step sums the ranks' gradients (in-kernel over the
+        IPC-mapped regions, native RCCL loop, bucketed all-reduce or the Python loop, in that order of
+        preference); "replicated" (dp_batch "global" only) — each rank steps its own env group, ONE
+        all-gather per update assembles the rollout of the whole env group (GAE is per env column, so
+        the local advantages / returns concatenate), and every rank runs the identical single-process
+        update over it: bitwise the single-process update, with no cross-rank traffic inside the
+        dependent optimizer-step chain; "auto" (default; RAI_DP_UPDATE overrides) — replicated where
+        the update is a dependent chain of one-launch-per-epoch steps (the fused CartPole-class epoch
+        kernel at <= 256 rows, the wide whole-epoch kernel), whose per-step cross-GPU hop costs more
+        than the rows it spreads, exchange otherwise."""
         import torch.distributed as dist
 
         self.dp_group = group
@@ -140,6 +152,24 @@ class PPO:
         # graphs over the buckets: both are rebuilt against the new communicator
         self._buckets = None
         self._graphed = None
+        if update_mode is None:
+            update_mode = os.environ.get("RAI_DP_UPDATE", "auto")
+        if update_mode not in ("auto", "exchange", "replicated"):
+            raise ValueError(f"update_mode must be 'auto', 'exchange' or 'replicated', not {update_mode!r}")
+        if update_mode == "replicated" and dp_batch != "global":
+            raise ValueError("update_mode='replicated' runs the single-process update over the whole env "
+                             "group: it needs dp_batch='global'")
+        self.dp_update_mode = "exchange"
+        if update_mode != "exchange" and dp_batch == "global":
+            self.batch_size = yaml_bs  # the single-process minibatch, for the path check below
+            if update_mode == "replicated" or (self.world > 1 and self.flat.flat.is_cuda
+                                               and self._dependent_chain_update()):
+                self.dp_update_mode = "replicated"
+            else:
+                self.batch_size = yaml_bs // self.world
+        if self.dp_update_mode == "replicated":
+            self._broadcast_params(group)
+            return
         if xdp is None:
             xdp = os.environ.get("RAI_XDP", "1") != "0"
         spec = self.fused_mlp_spec()
@@ -155,7 +185,13 @@ class PPO:
                 self._xdp = None
         if self._xdp is None and self.flat.flat.is_cuda and dist.get_backend(group) == "nccl" and native_dp:
             self._dp_comm = self._native_comm(group)
-        with torch.no_grad():  # identical starting weights everywhere
+        self._broadcast_params(group)
+
+    def _broadcast_params(self, group) -> None:
+        """Identical starting weights on every rank (rank 0's)."""
+        import torch.distributed as dist
+
+        with torch.no_grad():
             src = dist.get_global_rank(group, 0) if group is not None else 0
             if self.flat.flat.is_cuda and dist.get_backend(group) == "gloo":
                 h = self.flat.flat.cpu()
@@ -163,6 +199,58 @@ class PPO:
                 self.flat.flat.copy_(h)
             else:
                 dist.broadcast(self.flat.flat, src=src, group=group)
+
+    def _dependent_chain_update(self) -> bool:
+        """True when this trainer's single-process update is a chain of one-launch-per-epoch dependent
+        optimizer steps (rai_mlp_ppo_epoch's fused kernel at <= 256 rows, rai_mlp_wide_epoch): there a
+        per-step cross-GPU exchange adds its hop to every step and shrinks nothing the step waits on."""
+        spec = self.fused_mlp_spec()
+        if spec is not None:
+            return self.batch_size <= _lib.RAI_MLP_EPOCH_MAX_B
+        return self._wide_epoch_options_ok() and self._wide_step() is not None
+
+    def _replicated_rollout(self, r):
+        """The rollout of the whole env group from every rank's own (T, N/R, ...) rollout: one all-gather
+        per field (RCCL over xGMI; gloo through host memory), rank r's envs as columns [r N/R, (r+1) N/R).
+        The epoch permutations must agree on every rank: a perm_source the caller injected is used as
+        is, otherwise the shuffle keys derive from rank 0's next key (one 8-byte broadcast)."""
+        import torch.distributed as dist
+
+        from .rollout import DeviceRollout
+
+        g, W = self.dp_group, self.world
+        gloo = dist.get_backend(g) == "gloo"
+
+        def gather(t):
+            if t is None:
+                return None
+            src = t.contiguous()
+            if gloo:
+                h = src.cpu()
+                parts = [torch.empty_like(h) for _ in range(W)]
+                dist.all_gather(parts, h, group=g)
+                out = torch.stack(parts).to(src.device)
+            else:
+                out = torch.empty((W,) + tuple(src.shape), dtype=src.dtype, device=src.device)
+                dist.all_gather_into_tensor(out, src, group=g)
+            return out.transpose(0, 1).reshape((src.shape[0], W * src.shape[1]) + tuple(src.shape[2:]))
+
+        keys = None
+        if r._perm_source is None:
+            k = torch.tensor([r._perm_keys() if r._perm_keys is not None else 0], dtype=torch.int64)
+            if not gloo:
+                k = k.to(self.device)
+            dist.broadcast(k, src=dist.get_global_rank(g, 0) if g is not None else 0, group=g)
+            k0, count = int(k.item()), [0]
+
+            def keys():
+                count[0] += 1
+                return (k0 * 0x9E3779B97F4A7C15 + count[0]) & (2**63 - 1)
+
+        return DeviceRollout.from_fields(
+            self.device, gather(r.obs), gather(r.actions), gather(r.values), gather(r.advantages),
+            gather(r.returns), gather(r.logprobs), gather(r.action_masks), gather(r.num_actions),
+            perm_keys=keys, perm_source=r._perm_source)
 
     def _setup_xdp(self, group) -> dict:
         """Exchange regions for the in-kernel cross-GPU all-reduce (rai_mlp_ppo_epoch_xdp): one
@@ -446,8 +534,9 @@ class PPO:
         self.last_rollout_seconds = perf_counter() - start_time  # host env + policy steps (synced per step)
         timesteps_elapsed += r.total_steps
         stats, norms, K = self.update(r)
-        explained_var = r.explained_variance()
-        train_stats = self._train_stats(stats, norms, K, r.num_minibatches(self.batch_size), explained_var)
+        ru = getattr(self, "last_update_rollout", None) or r  # the whole env group's under replicated DP
+        explained_var = ru.explained_variance()
+        train_stats = self._train_stats(stats, norms, K, ru.num_minibatches(self.batch_size), explained_var)
         train_stats.write_to_tensorboard(self.tb_writer)
         end_time = perf_counter()
         self.last_update_seconds = end_time - start_time
@@ -769,6 +858,21 @@ class PPO:
     def update(self, r) -> Tuple[np.ndarray, np.ndarray, int]:
         """All epochs x minibatches of one update, enqueued without host syncs;
         returns the per-minibatch stats rows and grad norms (one D2H copy)."""
+        self.last_update_rollout = r
+        if self.dp_enabled and self.dp_update_mode == "replicated":
+            # data parallel by replication: the whole env group's rollout on every rank, then the
+            # single-process update (no exchange inside it); the ranks' weights are checked equal after
+            g = self._replicated_rollout(r)
+            self.last_update_rollout = g
+            self.dp_enabled = False
+            try:
+                out = self.update(g)
+            finally:
+                self.dp_enabled = True
+                self.last_update_rollout = g
+            if self.world > 1 and not self._params_agree():
+                raise RuntimeError("ranks' parameters diverged under the replicated data-parallel update")
+            return out
         spec = self.fused_mlp_spec() if hasattr(r, "epoch_batch") else None
         if spec is not None:
             return self._update_fused_dp(r, spec) if self.dp_enabled else self._update_fused(r, spec)

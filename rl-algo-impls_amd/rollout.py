@@ -197,6 +197,27 @@ class DeviceRollout(Rollout):
         self._flat: Optional[List[torch.Tensor]] = None
         self._perm_bufs: Dict[int, List[torch.Tensor]] = {}
 
+    @classmethod
+    def from_fields(cls, device: torch.device, obs: torch.Tensor, actions: torch.Tensor, values: torch.Tensor,
+                    advantages: torch.Tensor, returns: torch.Tensor, logprobs: Optional[torch.Tensor],
+                    action_masks: Optional[torch.Tensor] = None, num_actions: Optional[torch.Tensor] = None,
+                    perm_keys: Optional[Callable[[], int]] = None,
+                    perm_source: Optional[Callable[[int], torch.Tensor]] = None) -> "DeviceRollout":
+        """A rollout over (T, N, ...) fields whose advantages / returns are already computed (GAE is
+        independent per env column, so the column groups of several ranks' rollouts concatenate into the
+        rollout of the whole env group: PPO's replicated data-parallel update, ppo.py).  Only what the
+        update reads is set: the Batch fields, the epoch permutation source, the explained variance."""
+        self = cls.__new__(cls)
+        Rollout.__init__(self)
+        self.device = device
+        self.obs, self.actions, self.values, self.logprobs = obs, actions, values, logprobs
+        self.advantages, self.returns = advantages, returns
+        self.action_masks, self.num_actions = action_masks, num_actions
+        self.rewards = self.episode_starts = self.next_episode_starts = self.next_values = None
+        self._perm_source, self._generator, self._perm_keys = perm_source, None, perm_keys
+        self._flat, self._perm_bufs = None, {}
+        return self
+
     # -- Rollout API ---------------------------------------------------------------------
     @property
     def y_true(self) -> np.ndarray:
@@ -208,7 +229,7 @@ class DeviceRollout(Rollout):
 
     @property
     def total_steps(self) -> int:
-        return int(self.rewards.shape[0] * self.rewards.shape[1])
+        return int(self.values.shape[0] * self.values.shape[1])
 
     def num_minibatches(self, batch_size: int) -> int:
         return self.total_steps // batch_size + (1 if self.total_steps % batch_size else 0)

@@ -88,7 +88,8 @@ def fused_dp_worker(rank, world, port, q, backend="gloo", dp_batch="per-rank", i
     policy = nets.build("cartpole").to(dev)
     bs = 128 * (world if dp_batch == "global" else 1)
     algo = PPO(policy, dev, None, batch_size=bs, n_epochs=2, learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
-    algo.enable_data_parallel(xdp=os.environ.get("RAI_XDP", "1") != "0", dp_batch=dp_batch)
+    algo.enable_data_parallel(xdp=os.environ.get("RAI_XDP", "1") != "0", dp_batch=dp_batch,
+                              update_mode=os.environ.get("RAI_DP_UPDATE", "exchange"))
     assert algo.batch_size == 128 and algo.global_batch_size == 128 * world
     expect_xdp = world > 1 and os.environ.get("RAI_XDP", "1") != "0" and inject_fail_rank is None
     assert (algo._dp_comm is not None) == (backend == "nccl" and not expect_xdp)
@@ -131,7 +132,7 @@ def wide_epoch_xdp_worker(rank, world, port, q, hidden=64, rows_per_rank=32, n=5
                          activation_fn="relu", log_std_init=-2, init_layers_orthogonal=False).to(dev)
     algo = PPO(policy, dev, None, batch_size=rows_per_rank * world, n_epochs=2, learning_rate=3e-4, clip_range=0.2,
                ent_coef=0.01, max_grad_norm=0.5)
-    algo.enable_data_parallel(xdp=True, dp_batch="global")
+    algo.enable_data_parallel(xdp=True, dp_batch="global", update_mode="exchange")
     assert algo.batch_size == rows_per_rank
     assert algo._xdp is not None, "in-kernel exchange not set up for the wide policy"
     data = make_rank_data_wide(rank, dev, n)
@@ -185,7 +186,7 @@ def large_dp_worker(rank, world, port, q, rows_per_rank=512, n=2048):
     torch.manual_seed(0)
     algo = PPO(nets.build("cartpole").to(dev), dev, None, batch_size=rows_per_rank * world, n_epochs=2,
                learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
-    algo.enable_data_parallel(dp_batch="global")
+    algo.enable_data_parallel(dp_batch="global", update_mode="exchange")
     assert algo.batch_size == rows_per_rank and algo._xdp is None and algo.fused_mlp_spec() is not None
     data = make_rank_data(rank, dev, n)
 
@@ -295,7 +296,7 @@ def wide_dp_worker(rank, world, port, q, dp_batch="per-rank"):
     policy, r = wide_policy_and_rollout(make_wide_rank_data(rank, dev), dev)
     algo = PPO(policy, dev, None, batch_size=64 * (world if dp_batch == "global" else 1), n_epochs=2,
                learning_rate=3e-4, ent_coef=0.01)
-    algo.enable_data_parallel(dp_batch=dp_batch)
+    algo.enable_data_parallel(dp_batch=dp_batch, update_mode="exchange")
     assert algo.batch_size == 64
     stats, norms, _ = algo.update(r)
     assert algo._wide not in (None, False), "wide path not taken"
@@ -528,13 +529,139 @@ def split_worker(rank, world, port, q):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     algo = PPO(nets.build("cartpole").to(dev), dev, None, **SPLIT_KW)
-    algo.enable_data_parallel(dp_batch="global")
+    algo.enable_data_parallel(dp_batch="global", update_mode="exchange")
     assert algo.batch_size == SPLIT_KW["batch_size"] // world and algo.fused_mlp_spec() is not None
     n = SPLIT_N // world
     cols = torch.arange(rank * n, (rank + 1) * n)
     r = split_device_rollout(split_rollout_tensors(), cols, dev, torch.arange(SPLIT_T * n))
     stats, norms, _ = algo.update(r)
     q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms, algo._xdp is not None))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+def replicated_worker(rank, world, port, q):
+    """PPO's replicated data-parallel update on CPU (gloo): the batch rule (every rank keeps the YAML
+    minibatch), the rollout assembly (rank r's (T, N/R, ...) fields become env columns
+    [r N/R, (r+1) N/R) of the whole group's rollout) and the shuffle keys agreed from rank 0's."""
+    import torch
+
+    _init(rank, world, port)
+    import _pkgload
+
+    _pkgload.load()
+    from rl_algo_impls_amd.ppo import PPO
+    from rl_algo_impls_amd.rollout import DeviceRollout
+    import make_golden_networks as nets
+
+    out = {}
+    torch.manual_seed(rank)
+    algo = PPO(nets.build("cartpole"), torch.device("cpu"), None, batch_size=256)
+    algo.enable_data_parallel(dp_batch="global", update_mode="replicated")
+    out["sizes"] = (algo.batch_size, algo.global_batch_size, algo.dp_update_mode)
+    out["params"] = float(algo.flat.flat.double().sum())
+    try:
+        algo.enable_data_parallel(dp_batch="per-rank", update_mode="replicated")
+        out["per_rank"] = "accepted"
+    except ValueError as e:
+        out["per_rank"] = str(e)
+    algo.enable_data_parallel(dp_batch="global")  # auto on a CPU trainer: the exchange rule
+    out["auto_cpu"] = (algo.batch_size, algo.dp_update_mode)
+    T, n = 5, 3
+    g = torch.Generator().manual_seed(100 + rank)
+    f = lambda *s: torch.randn((T, n) + s, generator=g)
+    local = dict(obs=f(4), actions=torch.randint(0, 2, (T, n), generator=g), values=f(), advantages=f(),
+                 returns=f(), logprobs=f())
+    keys = iter(range(1000 * (rank + 1), 1000 * (rank + 2)))
+    r = DeviceRollout.from_fields(torch.device("cpu"), local["obs"], local["actions"], local["values"],
+                                  local["advantages"], local["returns"], local["logprobs"],
+                                  perm_keys=lambda: next(keys))
+    algo.world = world
+    gr = algo._replicated_rollout(r)
+    out["local"] = {k: v.numpy() for k, v in local.items()}
+    out["gathered"] = {k: getattr(gr, k).numpy() for k in local}
+    out["total_steps"] = gr.total_steps
+    out["keys"] = [gr._perm_keys() for _ in range(3)]
+    q.put((rank, out))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+REPL_T, REPL_N = 16, 64
+
+
+def replicated_rollout_tensors(kind, seed=31):
+    """One (T, N) rollout of the CartPole-class (C2 fused epoch kernel) or HalfCheetah-class (C4 wide
+    whole-epoch kernel) shape, identical wherever it is built."""
+    import torch
+
+    g = torch.Generator().manual_seed(seed)
+    T, N = REPL_T, REPL_N
+    if kind == "cartpole":
+        obs, act = torch.randn(T, N, 4, generator=g), torch.randint(0, 2, (T, N), generator=g)
+        logp = -0.69 + 0.05 * torch.randn(T, N, generator=g)
+    else:
+        obs, act = torch.randn(T, N, 17, generator=g), torch.randn(T, N, 6, generator=g).clamp(-1, 1)
+        logp = -1.0 + 0.1 * torch.randn(T, N, generator=g)
+    return dict(obs=obs, act=act, rew=torch.randn(T, N, generator=g),
+                starts=(torch.rand(T, N, generator=g) < 0.05).to(torch.uint8), vals=torch.randn(T, N, generator=g),
+                logp=logp, nstarts=(torch.rand(N, generator=g) < 0.05).to(torch.uint8), nvals=torch.randn(N, generator=g),
+                perm=torch.randperm(T * N, generator=g))
+
+
+def replicated_trainer(kind, dev):
+    """(PPO trainer seeded identically everywhere, whole-epoch path of `kind`)."""
+    import torch
+
+    from rl_algo_impls_amd.policy import ActorCritic
+    from rl_algo_impls_amd.ppo import PPO
+    import make_golden_networks as nets
+
+    torch.manual_seed(0)
+    if kind == "cartpole":
+        return PPO(nets.build("cartpole").to(dev), dev, None, **SPLIT_KW)
+    policy = ActorCritic(nets.halfcheetah_env(), pi_hidden_sizes=[256, 256], v_hidden_sizes=[256, 256],
+                         activation_fn="relu", log_std_init=-1.0, init_layers_orthogonal=False).to(dev)
+    return PPO(policy, dev, None, batch_size=64, n_epochs=2, learning_rate=3e-4, clip_range=0.2, ent_coef=0.01,
+               max_grad_norm=0.5, gamma=0.99, gae_lambda=0.95)
+
+
+def replicated_device_rollout(d, cols, dev, gamma, lam):
+    """DeviceRollout (GAE on the device) over env columns `cols`; the epoch permutation is the fixed
+    permutation of the WHOLE env group's T x N rows (the replicated update draws it over the gathered
+    rollout)."""
+    from rl_algo_impls_amd.rollout import DeviceRollout
+
+    t = lambda x: x[:, cols].contiguous().to(dev)
+    perm = d["perm"]
+    return DeviceRollout(dev, d["nstarts"][cols].contiguous().to(dev), d["nvals"][cols].contiguous().to(dev),
+                         t(d["obs"]), t(d["act"]), t(d["rew"]), t(d["starts"]), t(d["vals"]), t(d["logp"]), None,
+                         gamma, lam, perm_source=lambda n: perm.clone())
+
+
+def replicated_gpu_worker(rank, world, port, q, kind):
+    """bench.py's default multi-GPU rules (env split, global minibatch) with PPO's automatic update mode on
+    a dependent-chain path: rank r owns env columns [r N/R, (r+1) N/R) and computes their GAE; the update
+    is replicated (one all-gather of the rollout, the single-process update on every rank)."""
+    import torch
+
+    _init(rank, world, port)
+    import _pkgload
+
+    _pkgload.load()
+    dev = torch.device("cuda", 0)
+    algo = replicated_trainer(kind, dev)
+    algo.enable_data_parallel(dp_batch="global")
+    assert algo.dp_update_mode == "replicated" and algo._xdp is None and algo._dp_comm is None
+    n = REPL_N // world
+    r = replicated_device_rollout(replicated_rollout_tensors(kind), torch.arange(rank * n, (rank + 1) * n), dev,
+                                  algo.gamma, algo.gae_lambda)
+    stats, norms, _ = algo.update(r)
+    assert algo.last_update_rollout.total_steps == REPL_T * REPL_N
+    we = getattr(algo, "_we_ws", None) is not None
+    q.put((rank, algo.flat.flat.cpu().numpy(), stats, norms, we))
     import torch.distributed as dist
 
     dist.destroy_process_group()

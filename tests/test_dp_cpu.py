@@ -54,3 +54,33 @@ def test_dp_batch_rules_world2():
         assert "not divisible" in out[("global", 255)]
         assert out["repeat"] == [(128, 256), (128, 256), (256, 512), (128, 256)]
     assert res[0][("global", 256)][2] == res[1][("global", 256)][2]  # identical weights after the broadcast
+
+
+def test_replicated_update_rollout_assembly_world2():
+    """update_mode='replicated': every rank keeps the YAML minibatch (the single-process update runs on
+    each), 'per-rank' batches are rejected, a CPU trainer's 'auto' keeps the exchange rule; the whole
+    env group's rollout is rank 0's envs then rank 1's (bitwise), identical on both ranks, and both
+    ranks draw the same shuffle keys (derived from rank 0's)."""
+    import dp_worker
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.replicated_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        out = res[rank]
+        assert out["sizes"] == (256, 256, "replicated")
+        assert "dp_batch='global'" in out["per_rank"]
+        assert out["auto_cpu"] == (128, "exchange")
+        assert out["total_steps"] == 5 * 6
+        for k, v in out["gathered"].items():
+            want = np.concatenate([res[0]["local"][k], res[1]["local"][k]], axis=1)
+            np.testing.assert_array_equal(v, want, err_msg=k)
+    assert res[0]["params"] == res[1]["params"]
+    assert res[0]["keys"] == res[1]["keys"] and len(set(res[0]["keys"])) == 3

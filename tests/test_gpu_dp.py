@@ -322,6 +322,53 @@ def test_env_partition_split_world2_matches_single_process_c2(world):
     np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("kind,world", [("cartpole", 2), ("cartpole", 4), ("halfcheetah", 2)])
+def test_replicated_update_matches_single_process_bitwise(kind, world):
+    """PPO.enable_data_parallel's automatic update mode on a dependent-chain path (the C2 fused epoch
+    kernel at 256 rows; the C4 wide whole-epoch kernel at 64 rows) under bench.py's default rules (env
+    split, global minibatch): `world` ranks (gloo, all on cuda:0) each own 1/world of the env columns of
+    ONE rollout and compute their GAE; one all-gather assembles the whole env group's rollout and every
+    rank runs the single-process update over it.  Result: BITWISE the single-process update over the
+    whole rollout (same kernels, same inputs, same permutation), identical on every rank."""
+    import queue
+    import time
+
+    import dp_worker
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=dp_worker.replicated_gpu_worker, args=(r, world, port, q, kind))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    deadline = time.time() + 240
+    while len(res) < world:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"rank exited with {dead}"
+            assert time.time() < deadline, "ranks did not report in time"
+    res.sort(key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dev = torch.device("cuda", 0)
+    algo = dp_worker.replicated_trainer(kind, dev)
+    r = dp_worker.replicated_device_rollout(dp_worker.replicated_rollout_tensors(kind), torch.arange(dp_worker.REPL_N),
+                                            dev, algo.gamma, algo.gae_lambda)
+    stats, norms, _ = algo.update(r)
+    assert (getattr(algo, "_we_ws", None) is not None) == (kind == "halfcheetah")
+    p1 = algo.flat.flat.cpu().numpy()
+    for _, p, s, n, we in res:
+        assert we == (kind == "halfcheetah"), "the whole-epoch kernel path on every rank"
+        np.testing.assert_array_equal(p, p1)
+        np.testing.assert_array_equal(n, norms)
+        np.testing.assert_array_equal(s, stats)
+
+
 @pytest.mark.parametrize("hidden,rows,n", [(64, 32, 512), (256, 32, 400)])
 def test_wide_epoch_xdp_world2_matches_single_process_global_minibatches(hidden, rows, n):
     """The C4-class whole-epoch kernel under data parallel (rai_mlp_wide_epoch_xdp): two processes on
