@@ -120,21 +120,29 @@ def latency_roofline(G: int, avg_ms: float, steps_per_launch: int, kname: str) -
         latency, constants table), layer 1 one more, and dW2 16 independent-accumulator MFMAs at
         the 32-cycle issue rate: (1 + 16 + 16) x 40 + 16 x 32 = 1,832 cycles at 2.4 GHz (G = 8:
         two tiles of 32 columns per wave, 3,136 cycles);
-      * two cross-CU all-to-all edges among the network's G CUs (reduce-scatter, then all-gather of
-        the summed gradient and the share norms), each at least the price list's 'allgather' row
-        at its cheapest (8 KB published by 32 CUs, parked: 2.4 us).
+      * two cross-CU all-to-all edges among the network's G CUs (reduce-scatter of the partial
+        gradients, then all-gather of the summed shares and their norms).  Priced (round 6) for the
+        exchange the kernel runs: G = 16 readers, one network's CUs inside one XCD.  Each edge moves one
+        network's gradient, 4,610 floats = 18 KB of payload, i.e. a 32 KB sweep in the price list's
+        granule bytes (an edge size counts 2x the payload); the 'allgather' row prices a 32 KB sweep at
+        2.9 us parked (the waiting CUs run no HBM stream) for 256 readers, and the same row's reader
+        correction takes 1.9 us off for <= 32 readers ("256 -> 32 readers -1.9 on a 16 KB sweep, 32 -> 8
+        no further gain"): 1.0 us per edge.  No same-XCD credit is taken (the price list's cross-XCD
+        delta, +0.1-0.3 us, is the 'handoff-1to1' row's).  Rounds 1-5 priced each edge at the row's
+        256-reader 8 KB figure (2.4 us), a floor of 5.56 us that overstated the frac by ~2x.
     frac = floor / measured us per step: the share of the step the hardware's latencies account for."""
     RC = 256 // G  # rows per CU; CT 16-column tiles per wave (csrc/mlp_mc8.h M8Geo)
     CT = 64 // 16 // (4 // (RC // 16))
     chain = lambda n_dep, n_issue: max(n_dep * 40, n_issue * 32)  # dependent latency vs issue rate
     mfma_cycles = chain(1, CT) + 2 * chain(16, 16 * CT) + chain(RC // 4, RC)
     t_mfma = mfma_cycles / 2.4e3  # us at 2.4 GHz
-    t_edge = 2.4
+    t_edge = 2.9 - 1.9  # 'allgather' 32 KB parked, <= 32 readers (MI355X_MICROARCH.md price list)
     floor_us = t_mfma + 2 * t_edge
     step_us = avg_ms * 1e3 / max(steps_per_launch, 1)
     return {"kernel": kname, "bound": "latency", "achieved": round(step_us, 3), "peak": round(floor_us, 3),
             "unit": "us per dependent optimizer step", "frac": round(floor_us / step_us, 4),
-            "floor_terms_us": {"mfma_chain": round(t_mfma, 3), "allgather_edges": 2 * t_edge},
+            "floor_terms_us": {"mfma_chain": round(t_mfma, 3), "allgather_edges": round(2 * t_edge, 3)},
+            "edge_pricing": "allgather row, 32 KB sweep (18 KB payload) parked 2.9 us, -1.9 us for <= 32 readers",
             "steps_per_launch": steps_per_launch}
 
 
@@ -400,6 +408,7 @@ def main():
     large = (args.config == "cartpole" and algo.fused_mlp_spec() is not None
              and algo.batch_size > _lib.RAI_MLP_EPOCH_MAX_B)
     nmb = (T * N + algo.batch_size - 1) // algo.batch_size
+    large_steps = large
     _diagnostics("setup")
     for i in range(args.warmup):
         tw = time.perf_counter()
@@ -521,11 +530,14 @@ def main():
                 "peak": 8000.0, "unit": "GB/s", "frac": round(gae_bytes / (gae_us * 1e-6) / 1e9 / 8000.0, 4),
                 "traffic": traffic(gae_name), "traffic_source": traffic_source(gae_name), "avg_us": round(gae_us, 3),
                 "bytes_per_launch": gae_bytes}
+    # rows one update's epoch launches cover: the whole env group's under the replicated data-parallel update
+    # (every rank runs the single-process update over the gathered rollout), this rank's otherwise
+    TN = T * N * (world if getattr(algo, "dp_update_mode", "exchange") == "replicated" and world > 1 else 1)
     if epoch_ms and args.config == "halfcheetah":
         # dominant kernel: the persistent wide-MLP epoch (rai_mlp_wide_epoch, csrc/mlp_wide_epoch.hip):
         # one launch = every minibatch step of one epoch = T*N samples of forward+backward at SURVEY.md
         # 8(d)'s 0.832 MFLOP/sample (HalfCheetah MLP, torch.utils.flop_counter), f32 MFMA peak
-        flops = 0.832e6 * T * N
+        flops = 0.832e6 * TN
         ms = float(np.mean(epoch_ms))
         tf = flops / (ms * 1e-3) / 1e12
         head = 1  # Gaussian
@@ -534,7 +546,7 @@ def main():
                     "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
                     "traffic": traffic(kname), "traffic_source": traffic_source(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
-        steps_per_launch = (T * N + algo.batch_size - 1) // algo.batch_size
+        steps_per_launch = (TN + algo.batch_size - 1) // algo.batch_size
         roof_lat = latency_roofline_wide(ms, steps_per_launch, kname)
     elif large_ms:
         # dominant kernel: the large-minibatch gradient kernel (csrc/mlp_large.hip, lb_grads_kernel), one launch
@@ -557,7 +569,7 @@ def main():
     elif epoch_ms:
         # dominant kernel: one fused PPO epoch per launch = T*N samples of forward+backward at
         # SURVEY.md 8(d)'s 52,352 FLOP/sample (CartPole MLP, torch.utils.flop_counter), f32 MFMA peak
-        flops = 52352.0 * T * N
+        flops = 52352.0 * TN
         ms = float(np.mean(epoch_ms))
         tf = flops / (ms * 1e-3) / 1e12
         # the kernel rai_mlp_ppo_epoch dispatches for in_dim <= 4, n_actions <= 2 (csrc/mlp_ppo.hip
@@ -572,7 +584,7 @@ def main():
                     "achieved": round(tf, 4), "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 6),
                     "traffic": traffic(kname), "traffic_source": traffic_source(kname), "avg_ms": round(ms, 3),
                     "flops_per_launch": flops, "launches_timed": len(epoch_ms)}
-        roof_lat = latency_roofline(G, ms, (T * N + algo.batch_size - 1) // algo.batch_size, kname)
+        roof_lat = latency_roofline(G, ms, (TN + algo.batch_size - 1) // algo.batch_size, kname)
     elif args.config in UPDATE_FLOPS:
         # no fused epoch kernel: the update's convolutions / GEMMs on MFMA (MIOpen, hipBLASLt) against
         # the f32 MFMA peak, from SURVEY.md 8(d)'s algorithmic FLOPs per env step (rollout forward +
@@ -650,6 +662,9 @@ def main():
                 line["dp_path"] = ("replicated update: each rank steps its env share, one all-gather of the rollout "
                                    "per update (" + backend + "), the identical single-process update on every "
                                    "rank (strong scaling of the rollout only; the update is a dependent chain)")
+            elif algo._xdp is not None and large_steps:
+                line["dp_path"] = ("in-kernel cross-GPU exchange (IPC-mapped xGMI regions) inside each optimizer "
+                                   "step's reduce launch; no host sync or RCCL call per step")
             elif algo._xdp is not None:
                 line["dp_path"] = "in-kernel cross-GPU exchange (IPC-mapped xGMI regions), one launch per epoch"
             elif algo._dp_comm is not None and getattr(algo, "_buckets", None) is not None:

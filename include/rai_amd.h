@@ -729,6 +729,12 @@ int rai_mlp_ppo_epoch_dp(float* params, float* grads, float* exp_avg, float* exp
  * regions (the flags hold monotonic step ids and are zeroed only at allocation).
  * world <= 8.  Replaces the per-step RCCL all-reduce of rai_mlp_ppo_epoch_dp for
  * this policy class (same semantics, no per-step launches).
+ * batch_size > 256 (SURVEY 8(d) batch policy (b), in_dim <= 4, two actions): the large-minibatch
+ * steps (rai_mlp_ppo_epoch's all-CU form, three launches per optimizer step, no host sync); the
+ * exchange sits in each step's reduce launch: every 64-parameter block of this rank's reduced
+ * gradient goes into every rank's region, each block waits for the world's flags of that block
+ * and sums the slots in rank order, then clip + Adam run on the identical global gradient.
+ * Replaces rai_mlp_ppo_grads -> host RCCL all-reduce -> rai_clip_optim_step per step.
  * ------------------------------------------------------------------------ */
 int64_t rai_xdp_region_bytes(int32_t world);
 int rai_xdp_handle_bytes(void);

@@ -43,6 +43,7 @@
 namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u4v_lb __attribute__((ext_vector_type(4)));
 
 constexpr int HID = 64;
 constexpr int LB_NT = 256;            // 4 waves: one per SIMD (each pipelines two tiles)
@@ -693,6 +694,25 @@ __global__ __launch_bounds__(LB_NT, 1) void lb_grads_kernel(LbArgs a) {
   else lb_net<RELU, false>(a, S, wgn);
 }
 
+// Cross-GPU exchange layout of the large-minibatch reduce (data parallel, rai_mlp_ppo_epoch_xdp at batch
+// > 256), inside each rank's IPC-mapped region past the words the setup canary writes (common.h; the
+// canary's payload floats sit at [RAI_XDP_SLOTS_OFF, +2 KB): flag words there would read as huge step
+// ids and never wait -- the flags are never re-zeroed, so they must live where only step ids are stored):
+//   [LB_XF_OFF, +16 KB)  u64 flags[reduce block][sender rank]: step id of the last block pushed
+//   [LB_XS_OFF, ...)     f32 slots[2 parities][world][LB_XSLOT]: each rank's reduced gradient of the step,
+//                        64 parameters per reduce block
+constexpr int LB_XMAXW = 8;
+constexpr int LB_MAX_P = 2 * LB_PSTRIDE;
+constexpr int LB_RED_MAX_BLOCKS = (LB_MAX_P + 63) / 64;
+constexpr int64_t LB_XF_OFF = RAI_XDP_SLOTS_OFF + 4096;
+constexpr int64_t LB_XS_OFF = LB_XF_OFF + 16384;
+constexpr int LB_XSLOT = LB_RED_MAX_BLOCKS * 64;
+constexpr int LB_XAUX = 17;  // sc0 | sc1: system-scope (cross-device) stores and loads
+static_assert(LB_RED_MAX_BLOCKS * LB_XMAXW * 8 <= 16384, "flag words fit");
+__host__ __device__ constexpr int64_t lb_xdp_bytes(int world) {
+  return LB_XS_OFF + 2LL * world * LB_XSLOT * (int64_t)sizeof(float);
+}
+
 struct LbRed {
   const float* part;
   const double* statp;
@@ -706,7 +726,62 @@ struct LbRed {
   int32_t max_stats;
   int32_t bump_step;     // epoch mode: advance state->opt_step (read by the optimizer launch)
   double n_total;        // rows * world
+  // data parallel over the exchange regions (xworld > 1): this step's id and slot parity
+  void* const* xpeers;
+  int32_t xrank;
+  int32_t xworld;
+  unsigned long long xstep;
 };
+
+// The exchange of one reduce block (wave 0 of it): this rank's 64 summed values (tot) go into slot
+// [parity][xrank] of EVERY rank's region (16-B system-scope stores: 16 lanes x 16 B), the wave drains,
+// one flag word per receiver; then the W flags of this block in the own region are polled and the W
+// slots summed in rank order (the same bits on every rank).  Slot reuse: a rank writes parity p again
+// two steps later, only after its own step in between passed this wait, i.e. after every peer pushed
+// that step -- which each peer does only after it finished summing the parity-p slots.
+__device__ void lb_exchange_block(const LbRed& r, float* tot) {
+  const int lane = threadIdx.x & 63;
+  const int W = r.xworld;
+  const int par = (int)((r.xstep - 1) & 1);
+  const int64_t rb = lb_xdp_bytes(W);
+  const int64_t slot0 = LB_XS_OFF + ((int64_t)par * W * LB_XSLOT + (int64_t)blockIdx.x * 64) * 4;
+  f4 mine = {0.f, 0.f, 0.f, 0.f};
+  if (lane < 16) mine = reinterpret_cast<const f4*>(tot)[lane];
+  for (int pr = 0; pr < W; ++pr) {
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(r.xpeers[pr], (short)0, (int)rb, 0x00020000);
+    if (lane < 16)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v_lb, mine), prs,
+                                             (int)(slot0 + (int64_t)r.xrank * LB_XSLOT * 4) + 16 * lane, 0, LB_XAUX);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot stores landed before any flag
+  if (lane < W) {
+    unsigned long long* fl = reinterpret_cast<unsigned long long*>(static_cast<char*>(r.xpeers[lane]) + LB_XF_OFF) +
+                             blockIdx.x * LB_XMAXW + r.xrank;
+    __hip_atomic_store(fl, r.xstep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const unsigned long long* own =
+      reinterpret_cast<const unsigned long long*>(static_cast<const char*>(r.xpeers[r.xrank]) + LB_XF_OFF) +
+      blockIdx.x * LB_XMAXW;
+  const unsigned long long t0 = rai_clock();
+  for (;;) {
+    const bool ok = lane >= W || __hip_atomic_load(own + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= r.xstep;
+    if (__all(ok)) break;
+    if (rai_expired(t0, RAI_SPIN_REMOTE)) {
+      if (lane == 0) atomicExch(&r.state->err, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(r.xpeers[r.xrank], (short)0, (int)rb, 0x00020000);
+  f4 sum = {0.f, 0.f, 0.f, 0.f};
+  if (lane < 16) {
+    sum = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(lrs, (int)slot0 + 16 * lane, 0, LB_XAUX));
+    for (int pr = 1; pr < W; ++pr)
+      sum += __builtin_bit_cast(
+          f4, __builtin_amdgcn_raw_buffer_load_b128(lrs, (int)(slot0 + (int64_t)pr * LB_XSLOT * 4) + 16 * lane, 0, LB_XAUX));
+    reinterpret_cast<f4*>(tot)[lane] = sum;
+  }
+}
 
 // Every parameter's LB_WG_PER_NET workgroup partials in a fixed order: a block owns 64 parameters and
 // its four waves each sum one quarter of the partials (32 independent loads in flight per lane; one
@@ -733,9 +808,18 @@ __global__ __launch_bounds__(LB_RED_NT) void lb_reduce_kernel(LbRed r) {
   }
   __syncthreads();
   double sq = 0.0;
+  if (r.xworld > 1) {  // data parallel: the block's 64 sums over every rank, in rank order
+    __shared__ __align__(16) float tot[64];
+    if (q4 == 0) tot[c] = p < r.P ? (quarter[0][c] + quarter[1][c]) + (quarter[2][c] + quarter[3][c]) : 0.f;
+    __syncthreads();
+    if (q4 == 0) lb_exchange_block(r, tot);
+    __syncthreads();
+    if (q4 == 0) quarter[0][c] = tot[c], quarter[1][c] = quarter[2][c] = quarter[3][c] = 0.f;
+    __syncthreads();
+  }
   if (q4 == 0) {
     if (p < r.P) {
-      const float v = (quarter[0][c] + quarter[1][c]) + (quarter[2][c] + quarter[3][c]);
+      const float v = r.xworld > 1 ? quarter[0][c] : (quarter[0][c] + quarter[1][c]) + (quarter[2][c] + quarter[3][c]);
       r.grad[p] = v;
       sq = (double)v * (double)v;
     }
@@ -831,8 +915,6 @@ struct LbWs {
   float* grad;
   float* part;
 };
-constexpr int LB_MAX_P = 2 * LB_PSTRIDE;
-constexpr int LB_RED_MAX_BLOCKS = (LB_MAX_P + 63) / 64;
 LbWs lb_carve(void* ws, int64_t nmb) {
   unsigned char* p = static_cast<unsigned char*>(ws);
   LbWs w;
@@ -876,6 +958,8 @@ LbTiming& lb_timing() {
 
 }  // namespace
 
+int64_t rai_internal::mlp_large_xdp_bytes(int32_t world) { return lb_xdp_bytes(world); }
+
 bool rai_internal::mlp_large_supported(int32_t in_dim, int32_t n_act, int32_t hidden) {
   return hidden == HID && in_dim >= 1 && in_dim <= 4 && n_act == 2;
 }
@@ -892,8 +976,11 @@ int rai_internal::mlp_large(float* params, float* exp_avg, float* exp_avg_sq, co
                             int32_t act_fn, int32_t mb_begin, int32_t mb_count, const float* moments, int32_t world,
                             const rai_ppo_hparams* hp, const rai_optim_hparams* ohp, rai_train_state* state,
                             float* stats, int32_t max_stats, float* norms, int32_t max_norms, float* grad_out,
-                            void* workspace, int64_t workspace_bytes, hipStream_t s) {
+                            void* workspace, int64_t workspace_bytes, hipStream_t s, const LargeXdp* xdp) {
   if (!mlp_large_supported(in_dim, n_act, HID)) return RAI_E_UNSUPPORTED;
+  if (xdp && (grad_out || !moments || !xdp->peers || xdp->world < 2 || xdp->world > LB_XMAXW || xdp->rank < 0 ||
+              xdp->rank >= xdp->world || xdp->world != world || xdp->step_base < 0))
+    return RAI_E_SHAPE;
   if (batch < 2 || n_rows < 1 || world < 1 || (act_fn != 0 && act_fn != 1)) return RAI_E_SHAPE;
   if (!params || !obs || !actions || !old_logp || !old_values || !adv || !ret || !hp || !state || !workspace)
     return RAI_E_NULLPTR;
@@ -966,6 +1053,10 @@ int rai_internal::mlp_large(float* params, float* exp_avg, float* exp_avg_sq, co
     r.max_stats = max_stats;
     r.bump_step = grads_mode ? 0 : 1;
     r.n_total = (double)a.rows * (double)world;
+    r.xpeers = xdp ? xdp->peers : nullptr;
+    r.xrank = xdp ? xdp->rank : 0;
+    r.xworld = xdp ? xdp->world : 1;
+    r.xstep = xdp ? (unsigned long long)(xdp->step_base + (mb - (grads_mode ? mb_begin : 0)) + 1) : 0ull;
     hipLaunchKernelGGL(lb_reduce_kernel, dim3(red_blocks), dim3(LB_RED_NT), 0, s, r);
     RAI_LAUNCH_CHECK();
     if (!grads_mode) {

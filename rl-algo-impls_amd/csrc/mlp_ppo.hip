@@ -1687,10 +1687,17 @@ extern "C" int rai_mlp_ppo_epoch_xdp(float* params, float* exp_avg, float* exp_a
                                      const rai_optim_hparams* ohp, rai_train_state* state, float* stats,
                                      int32_t max_stats, float* norms, int32_t max_norms, void* workspace,
                                      int64_t workspace_bytes, void* stream) {
-  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3)) || batch_size > MAXB)
-    return RAI_E_UNSUPPORTED;
   if (!moments || !peers) return RAI_E_NULLPTR;
   if (world < 2 || world > XDP_MAXW || rank < 0 || rank >= world || step_base < 0) return RAI_E_SHAPE;
+  if (batch_size > MAXB) {  // large minibatches (mlp_large.hip): the exchange inside each step's reduce launch
+    if (!rai_internal::mlp_large_supported(in_dim, n_actions, hidden)) return RAI_E_UNSUPPORTED;
+    const rai_internal::LargeXdp x = {peers, rank, world, step_base};
+    return rai_internal::mlp_large(params, exp_avg, exp_avg_sq, obs, actions, old_logp, old_values, advantages,
+                                   returns, n_rows, batch_size, in_dim, n_actions, activation, 0, 1 << 30, moments,
+                                   world, hp, ohp, state, stats, max_stats, norms, max_norms, nullptr, workspace,
+                                   workspace_bytes, rai_stream(stream), &x);
+  }
+  if (!(in_dim <= 4 && n_actions <= 2 && (mlp_layout() == 0 || mlp_layout() == 3))) return RAI_E_UNSUPPORTED;
   MlpArgs a = {};
   a.params = params; a.exp_avg = exp_avg; a.exp_avg_sq = exp_avg_sq;
   a.obs = obs; a.actions = actions; a.old_logp = old_logp; a.old_values = old_values;
@@ -1751,8 +1758,10 @@ extern "C" int rai_xdp_selftest(void* const* peers, int32_t world, int32_t rank,
 extern "C" int64_t rai_xdp_region_bytes(int32_t world) {
   if (world < 1 || world > XDP_MAXW) return 0;
   static_assert(XDP_FLAGS_BYTES == RAI_XDP_SLOTS_OFF, "one region layout");
-  // one region serves the CartPole-class epoch kernels and the wide whole-epoch kernel
-  return std::max<int64_t>(xdp_region_bytes(world), rai_xdp_wide_bytes(world));
+  // one region serves the CartPole-class epoch kernels (<= 256 rows and the large-minibatch steps) and the
+  // wide whole-epoch kernel
+  return std::max<int64_t>(std::max<int64_t>(xdp_region_bytes(world), rai_xdp_wide_bytes(world)),
+                           rai_internal::mlp_large_xdp_bytes(world));
 }
 
 // Multi-CU data-parallel step (used by rai_mlp_ppo_epoch_dp): apply the previous all-reduced

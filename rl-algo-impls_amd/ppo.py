@@ -173,8 +173,10 @@ class PPO:
         if xdp is None:
             xdp = os.environ.get("RAI_XDP", "1") != "0"
         spec = self.fused_mlp_spec()
-        c2_xdp = (spec is not None and spec["in_dim"] <= 4 and spec["n_act"] <= 2
-                  and self.batch_size <= _lib.RAI_MLP_EPOCH_MAX_B)
+        # the CartPole-class fused epoch kernel (<= 256 rows per rank) and the large-minibatch steps (batch
+        # policy (b): the exchange inside each step's reduce launch, mlp_large.hip)
+        c2_xdp = (spec is not None and spec["in_dim"] <= 4
+                  and (spec["n_act"] <= 2 if self.batch_size <= _lib.RAI_MLP_EPOCH_MAX_B else spec["n_act"] == 2))
         # the wide whole-epoch kernel (C4) keeps its one launch per epoch under data parallel too
         wide_xdp = spec is None and self._wide_epoch_options_ok() and self._wide_step() is not None
         if xdp and self.flat.flat.is_cuda and self.world > 1 and self.world <= 8 and (c2_xdp or wide_xdp):

@@ -170,9 +170,11 @@ def make_rank_data_wide(rank, dev, n=512):
     return Batch(t(obs), t(logp), t(act), None, None, t(vals), t(adv), t(ret))
 
 
-def large_dp_worker(rank, world, port, q, rows_per_rank=512, n=2048):
+def large_dp_worker(rank, world, port, q, rows_per_rank=512, n=2048, xdp=False):
     """SURVEY 8(d) batch policy (b) under data parallel: the CartPole-class policy at minibatches of
-    rows_per_rank x world rows (> 256, the large-minibatch kernels), dp_batch="global" over gloo."""
+    rows_per_rank x world rows (> 256, the large-minibatch kernels), dp_batch="global" over gloo; xdp: the
+    gradient summed over the ranks inside each step's reduce launch (IPC-mapped regions) instead of the
+    per-step host all-reduce."""
     import torch
 
     _init(rank, world, port, "gloo")
@@ -186,8 +188,8 @@ def large_dp_worker(rank, world, port, q, rows_per_rank=512, n=2048):
     torch.manual_seed(0)
     algo = PPO(nets.build("cartpole").to(dev), dev, None, batch_size=rows_per_rank * world, n_epochs=2,
                learning_rate=3e-3, clip_range=0.2, ent_coef=0.01)
-    algo.enable_data_parallel(dp_batch="global", update_mode="exchange")
-    assert algo.batch_size == rows_per_rank and algo._xdp is None and algo.fused_mlp_spec() is not None
+    algo.enable_data_parallel(xdp=xdp, dp_batch="global", update_mode="exchange")
+    assert algo.batch_size == rows_per_rank and (algo._xdp is not None) == xdp and algo.fused_mlp_spec() is not None
     data = make_rank_data(rank, dev, n)
 
     class R:

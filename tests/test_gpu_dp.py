@@ -441,10 +441,14 @@ def test_wide_epoch_xdp_world2_matches_single_process_global_minibatches(hidden,
     np.testing.assert_allclose(p0, algo.flat.flat.cpu().numpy(), rtol=2e-4, atol=2e-6)
 
 
-def test_scaled_batch_policy_dp_world2_matches_single_process():
-    """SURVEY 8(d)'s batch policy (b) under data parallel: two ranks (gloo, one GPU) run 512-row slices of
-    1,024-row global minibatches through the large-minibatch kernels (grads mode) with a per-step gradient
-    all-reduce; ranks bitwise equal, and equal to the single process at batch 1,024 over the interleaved
+@pytest.mark.parametrize("xdp,world", [(False, 2), (True, 2), (True, 4)],
+                         ids=["host_allreduce_w2", "in_kernel_w2", "in_kernel_w4"])
+def test_scaled_batch_policy_dp_world2_matches_single_process(xdp, world):
+    """SURVEY 8(d)'s batch policy (b) under data parallel: `world` ranks (gloo, one GPU) run 512-row slices
+    of 512 x world-row global minibatches through the large-minibatch kernels, the gradient summed over
+    the ranks either by a per-step host all-reduce (grads mode) or inside each step's reduce launch
+    through the IPC-mapped exchange regions (rai_mlp_ppo_epoch_xdp: no host sync, no RCCL call per
+    step); ranks bitwise equal, and equal to the single process at batch 512 x world over the interleaved
     rollouts (fp32 tolerance: per-rank partial sums)."""
     import queue
     import time
@@ -454,16 +458,17 @@ def test_scaled_batch_policy_dp_world2_matches_single_process():
     from rl_algo_impls_amd.ppo import PPO
     from rl_algo_impls_amd.rollout import Batch
 
-    rows, n = 512, 2048
+    rows, n = 512, 2048  # > 256 rows per rank: the large-minibatch kernels at every world size
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=dp_worker.large_dp_worker, args=(r, 2, port, q, rows, n)) for r in range(2)]
+    procs = [ctx.Process(target=dp_worker.large_dp_worker, args=(r, world, port, q, rows, n, xdp))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = []
     deadline = time.time() + 240
-    while len(res) < 2:
+    while len(res) < world:
         try:
             res.append(q.get(timeout=2))
         except queue.Empty:
@@ -474,25 +479,26 @@ def test_scaled_batch_policy_dp_world2_matches_single_process():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, p0, s0, n0), (_, p1, s1, n1) = res
-    np.testing.assert_array_equal(p0, p1)
+    _, p0, s0, n0 = res[0]
+    for x in res[1:]:
+        np.testing.assert_array_equal(p0, x[1])
+        np.testing.assert_array_equal(n0, x[3])
 
     dev = torch.device("cuda", 0)
-    d0, d1 = dp_worker.make_rank_data(0, dev, n), dp_worker.make_rank_data(1, dev, n)
+    ds = [dp_worker.make_rank_data(r, dev, n) for r in range(world)]
     nmb = n // rows
 
     def interleave(f):
-        a, b = getattr(d0, f), getattr(d1, f)
-        return torch.cat([torch.cat([a[i * rows:(i + 1) * rows], b[i * rows:(i + 1) * rows]]) for i in range(nmb)])
+        return torch.cat([torch.cat([getattr(d, f)[i * rows:(i + 1) * rows] for d in ds]) for i in range(nmb)])
 
     glob = Batch(*(interleave(f) for f in ("obs", "logprobs", "actions")), None, None,
                  *(interleave(f) for f in ("values", "advantages", "returns")))
     torch.manual_seed(0)
-    algo = PPO(nets.build("cartpole").to(dev), dev, None, batch_size=2 * rows, n_epochs=2, learning_rate=3e-3,
+    algo = PPO(nets.build("cartpole").to(dev), dev, None, batch_size=world * rows, n_epochs=2, learning_rate=3e-3,
                clip_range=0.2, ent_coef=0.01)
 
     class R:
-        total_steps = 2 * n
+        total_steps = world * n
 
         def num_minibatches(self, bs):
             return -(-self.total_steps // bs)
