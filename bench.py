@@ -98,7 +98,7 @@ def parse():
                         "default: ~100x slower C3 convolutions on MI355X (rl-algo-impls_amd/running_utils.py)")
     p.add_argument("--cudnn-benchmark", type=int, default=None, choices=[0, 1],
                    help="MIOpen find mode (torch.backends.cudnn.benchmark) for the convolutions; default on for "
-                        "the CNN configs (pong, microrts)")
+                        "pong; microrts runs immediate mode over the shipped find database (same solver picks)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--roofline-reps", type=int, default=200)
@@ -341,6 +341,10 @@ def main():
     os.environ.setdefault("RAI_TUNABLEOP_FILE", os.path.join(os.environ.get("TMPDIR", "/tmp"),
                                                              f"rai_bench_{os.getpid()}_tunableop%d.csv"))
 
+    # the shipped MIOpen find database (running_utils.seed_miopen_find_db) is seeded into this run's TMPDIR,
+    # not the user's cache: every bench run starts from the shipped records only
+    os.environ.setdefault("RAI_MIOPEN_DB_DIR", os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                                            f"rai_bench_{os.getpid()}_miopen"))
     set_device_optimizations(dev, use_deterministic_algorithms=bool(args.deterministic))
     tunableop = torch.cuda.tunable.is_enabled()
     # RAI_AUTOGRAD_MT=0 (profiling runs): autograd runs the backward on the calling thread instead of its
@@ -351,7 +355,12 @@ def main():
     # MIOpen find mode for the CNN convolutions (C3 / C5): every candidate solver timed at the first call
     # of each problem, the fastest kept.  Measured C3: 1.10 s per update against 1.26 s with the default
     # immediate-mode choice (profiles/r2o_pong_find_mode_bench_line.json vs r2l)
-    cudnn_benchmark = args.cudnn_benchmark if args.cudnn_benchmark is not None else args.config in ("pong", "microrts")
+    # C5 (microrts): immediate mode reads the solver choices from the shipped find database (running_utils.
+    # seed_miopen_find_db), which are find mode's own picks: same update time (13.75k vs 13.76k env-steps/s,
+    # profiles/r6d_c5_bench_immediate.json vs r6c_c5_bench.json) without the first update's search (30.5 s
+    # warm-up instead of 193 s with the database and 543 s without: torch passes benchmark as MIOpen's
+    # exhaustiveSearch, which re-times every solver of every problem even when the database holds it)
+    cudnn_benchmark = args.cudnn_benchmark if args.cudnn_benchmark is not None else args.config == "pong"
     if os.environ.get("RAI_CUDNN_BENCHMARK") is not None:
         cudnn_benchmark = os.environ["RAI_CUDNN_BENCHMARK"] == "1"
     torch.backends.cudnn.benchmark = bool(cudnn_benchmark) and not args.deterministic
@@ -647,6 +656,7 @@ def main():
                        "n_epochs": algo_kw["n_epochs"], "batch_policy": args.batch_policy, "seq_len": T,
                        "deterministic": bool(args.deterministic),
                        "miopen_find_mode": bool(torch.backends.cudnn.benchmark),
+                       "miopen_user_db": os.environ.get("MIOPEN_USER_DB_PATH"),
                        "gemm_tunableop": bool(tunableop),
                        "parallelism": f"dp{world}"},
             "roofline": roofline,

@@ -37,16 +37,52 @@ import torch
 
 def set_device_optimizations(device: torch.device, set_float32_matmul_precision: Optional[str] = None,
                              use_deterministic_algorithms: bool = True) -> None:
-    """running_utils.py:161-172, plus GEMM tuning when determinism is off (set_gemm_tuning)."""
+    """running_utils.py:161-172, plus GEMM tuning when determinism is off (set_gemm_tuning) and the
+    shipped MIOpen find database (seed_miopen_find_db)."""
     set_gemm_tuning(device, not use_deterministic_algorithms)
     torch.use_deterministic_algorithms(use_deterministic_algorithms)
     torch.backends.cudnn.deterministic = bool(use_deterministic_algorithms)
     if use_deterministic_algorithms and "MIOPEN_USER_DB_PATH" not in os.environ:
         os.environ["MIOPEN_USER_DB_PATH"] = os.path.join(os.path.expanduser("~"), ".cache", "rl_algo_impls_amd",
                                                          "miopen-deterministic")
+    elif not use_deterministic_algorithms and torch.device(device).type == "cuda":
+        seed_miopen_find_db()
     if torch.device(device).type == "cuda" and set_float32_matmul_precision:
         logging.info(f"Setting torch.set_float32_matmul_precision to {set_float32_matmul_precision}")
         torch.set_float32_matmul_precision(set_float32_matmul_precision)
+
+
+MIOPEN_DB_SHIPPED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
+
+
+def seed_miopen_find_db(dst: Optional[str] = None) -> Optional[str]:
+    """Point MIOpen's user database at a directory seeded with the find / perf records this package ships
+    (miopen_db/: MIOpen's find-mode solver timings for the squeeze-U-Net (C5) and NatureCNN (C3) problem
+    shapes on gfx950 with 256 CUs, recorded by a bench run on MI355X).  Without them the first C5 update
+    times every candidate solver of ~130 convolution problems: 534 s on a fresh box (profiles/
+    r5d_c5_bench_stderr.txt), 543 s again in round 6 (r6c_c5_bench_stderr.txt); with them MIOpen reads
+    the recorded choice and only compiles the chosen kernels.  MIOpen keys the files by architecture,
+    CU count and its own version, so a different GPU or MIOpen build ignores them and searches as
+    before.  Shipped files are copied (never overwriting) into dst = RAI_MIOPEN_DB_DIR or
+    ~/.cache/rl_algo_impls_amd/miopen, since MIOpen appends to the user database.  Only when the caller
+    has not set MIOPEN_USER_DB_PATH; like every MIOpen setting it must precede the first convolution of
+    the process.  Returns the directory used (None: caller's own setting kept)."""
+    if "MIOPEN_USER_DB_PATH" in os.environ:
+        return None
+    dst = dst or os.environ.get("RAI_MIOPEN_DB_DIR") or os.path.join(
+        os.path.expanduser("~"), ".cache", "rl_algo_impls_amd", "miopen")
+    try:
+        os.makedirs(dst, exist_ok=True)
+        import shutil
+
+        for name in sorted(os.listdir(MIOPEN_DB_SHIPPED)) if os.path.isdir(MIOPEN_DB_SHIPPED) else []:
+            if name.endswith(".txt") and not os.path.exists(os.path.join(dst, name)):
+                shutil.copyfile(os.path.join(MIOPEN_DB_SHIPPED, name), os.path.join(dst, name))
+    except OSError as e:  # an unwritable home: MIOpen's default database, a search on first use
+        logging.warning(f"MIOpen find database not seeded ({e})")
+        return None
+    os.environ["MIOPEN_USER_DB_PATH"] = dst
+    return dst
 
 
 def set_gemm_tuning(device: torch.device, enabled: bool) -> bool:

@@ -9,6 +9,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r4}
+CONFIG=${CONFIG:-pong}  # round 6: any bench config (microrts for C5); GROUPS_=all: one unrestricted pass per counter
 OUT=gpurun_out/c3grp_$TAG
 mkdir -p "$OUT"
 # round 5: "ours" split into the convolutions and the rest of this repo's kernels (the round-5 run of the
@@ -23,12 +24,13 @@ for grp in ${GROUPS_:-conv ours gemm rest}; do
     ours) sel=(--kernel-include-regex "$OURS") ;;
     gemm) sel=(--kernel-include-regex "$GEMM") ;;
     rest) sel=(--kernel-exclude-regex "$CONV|$OURS|$GEMM") ;;
+    all) sel=() ;;
   esac
   for C in FETCH_SIZE WRITE_SIZE; do
     echo "== $grp $C" | tee -a "$OUT/steps.log"
     RAI_GRAPHS=1 RAI_GRAPH_EAGER=1 timeout -s KILL 400 rocprofv3 --pmc $C "${sel[@]}" --output-format csv \
-      -d "$OUT/${grp}_$C" -o run -- python3 bench.py --config pong --no-cpu-baseline --roofline-reps 1 --steps 1 \
-      --warmup 0 > "$OUT/${grp}_$C.log" 2>&1
+      -d "$OUT/${grp}_$C" -o run -- python3 bench.py --config "$CONFIG" --no-cpu-baseline --roofline-reps 1 --steps 1 \
+      --warmup 0 ${BENCH_EXTRA:-} > "$OUT/${grp}_$C.log" 2>&1
     rc=$?
     echo "== $grp $C rc=$rc" | tee -a "$OUT/steps.log"
     [ $rc -eq 0 ] || { grep -v amdgpu.ids "$OUT/${grp}_$C.log" | tail -20; exit $rc; }
@@ -36,12 +38,12 @@ for grp in ${GROUPS_:-conv ours gemm rest}; do
     python3 tools/pmc_kernels.py "$f" "$OUT/${grp}_$C.json" --delete || exit 1
   done
 done
-python3 - "$OUT" <<'PY'
+python3 - "$OUT" ${GROUPS_:-conv ours gemm rest} <<'PY'
 import json, sys
 out = sys.argv[1]
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     merged = {"kernels": {}}
-    for g in ("conv", "ours", "gemm", "rest"):
+    for g in sys.argv[2:]:
         merged["kernels"].update(json.load(open(f"{out}/{g}_{c}.json"))["kernels"])
     json.dump(merged, open(f"{out}/{c}.json", "w"), indent=1)
 PY

@@ -17,7 +17,7 @@ import json
 import os
 import sys
 
-STEPS = 2048
+STEPS = int(os.environ.get("TRAFFIC_STEPS", "2048"))  # minibatch steps per update (C3 2,048; C5 86)
 
 
 def main():
