@@ -509,7 +509,24 @@ struct ConvWrwArgs {
   int64_t M;    // pixels
   int64_t per;  // pixels per split
   int H, W, Ci, Co, KW, S_, OH, OW, K;
+  int xcd_map;  // 1: the k tiles of one pixel split run back to back on ONE XCD (see wrw_tile)
 };
+
+// The (pixel split, k tile) a workgroup works on.  Dispatch deals consecutive workgroups round-robin over the
+// 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch: blocks b and b + 8 share one; speed only, never
+// correctness).  With the grid's natural order the KT k tiles of split s are dispatched S workgroups apart,
+// so each reads the split's dz / y rows (and its input rows) from beyond its XCD's L2 again.  xcd_map
+// renumbers: workgroup lin -> XCD slot lin % 8 keeps split s = 8 (slot / KT) + lin % 8, k tile slot % KT, so
+// a split's k tiles are dispatched consecutively on the same XCD and the later ones read its rows from L2.
+struct WrwTile {
+  int s, kt;
+};
+__device__ __forceinline__ WrwTile wrw_tile(int xcd_map) {
+  if (!xcd_map) return WrwTile{(int)blockIdx.x, (int)blockIdx.y};
+  const int lin = (int)(blockIdx.x + blockIdx.y * gridDim.x);
+  const int slot = lin >> 3, KT = (int)gridDim.y;
+  return WrwTile{8 * (slot / KT) + (lin & 7), slot % KT};
+}
 
 template <int VC, int PF, bool RB, bool BUF = false, int U8 = 0>
 __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs a) {
@@ -525,13 +542,14 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
   f4* const red = reinterpret_cast<f4*>(lds);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int li = lane & 15, g = lane >> 4;
-  const int k0 = blockIdx.y * 64 + 4 * li;  // this lane's 4 k (one chunk: Ci % 4 == 0)
+  const WrwTile tile = wrw_tile(a.xcd_map);
+  const int k0 = tile.kt * 64 + 4 * li;  // this lane's 4 k (one chunk: Ci % 4 == 0)
   int xo;
   {
     const int kpos = k0 / a.Ci, ci0 = k0 - kpos * a.Ci, kh = kpos / a.KW, kw = kpos - kh * a.KW;
     xo = (kh * a.W + kw) * a.Ci + ci0;
   }
-  const int64_t pbeg = (int64_t)blockIdx.x * a.per;
+  const int64_t pbeg = (int64_t)tile.s * a.per;
   const int n_p = (int)max((int64_t)0, min(a.per, a.M - pbeg));
   const int OHW = a.OH * a.OW;
   const int64_t n0 = pbeg / OHW;  // offsets are relative to the split's first sample
@@ -671,8 +689,8 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
   }
   __syncthreads();
   if (wv > 0) return;
-  if (RB && blockIdx.y == 0 && g == 0) {  // this split's bias-gradient partial (one k tile writes it)
-    float* dp = a.part + (int64_t)gridDim.x * a.Co * a.K + (int64_t)blockIdx.x * a.Co;
+  if (RB && tile.kt == 0 && g == 0) {  // this split's bias-gradient partial (one k tile writes it)
+    float* dp = a.part + (int64_t)gridDim.x * a.Co * a.K + (int64_t)tile.s * a.Co;
 #pragma unroll
     for (int j = 0; j < VC; ++j) {
       float v = dbl[li * VC + j];
@@ -688,7 +706,7 @@ __global__ __launch_bounds__(CV_THREADS) void conv_wrw_kernel(const ConvWrwArgs 
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) acc[j][jj] += red[(q * NB + j * 4 + jj) * 64 + lane];
   // partial tile: lane (i, g) holds co = VC*(4g + r) + j, k = k0 .. k0 + 3 (one float4 per (j, r))
-  float* pp = a.part + (int64_t)blockIdx.x * a.Co * a.K;
+  float* pp = a.part + (int64_t)tile.s * a.Co * a.K;
 #pragma unroll
   for (int j = 0; j < VC; ++j)
 #pragma unroll
@@ -1399,6 +1417,11 @@ static int wgrad_partials(const float* x, const float* dz, const float* y, int64
   if (target_wgs < 0 || target_wgs > 1024) return RAI_E_SHAPE;
   const WrwPlan p = wrw_plan(a.M, Co, a.K, target_wgs);
   a.per = p.per;
+  static const int env_xcd = [] {  // A/B: RAI_WRW_XCD=0 keeps the grid's natural order (read once)
+    const char* e = getenv("RAI_WRW_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  a.xcd_map = (env_xcd != 0 && p.S % 8 == 0) ? 1 : 0;
   // a split's offsets from its first sample fit int32
   if ((int64_t)(WR_MAXPX / (a.OH * a.OW) + 2) * H * W * Ci > 0x7fffffffLL) return RAI_E_SHAPE;
   const dim3 grid((unsigned)p.S, (unsigned)p.KT);
