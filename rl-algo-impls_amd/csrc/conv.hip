@@ -55,6 +55,7 @@ struct ConvFwdArgs {
   // conv_fwd_splitk_reduce_kernel then adds the splits in order, the bias and the ReLU
   int ksplit = 1;
   float* part = nullptr;
+  int xcd_map = 0;  // conv_fwd_lds_kernel: the co tiles of one pixel-tile stream on ONE XCD (fwd_tile)
 };
 
 // The uint8 forms' x = u / d for the four bytes of a dword.  U8 == 1: a 256-entry LDS table of the IEEE
@@ -237,7 +238,19 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   const int zs = blockIdx.z, nq_all = K >> 4;
   const int q0 = (int)((int64_t)nq_all * zs / a.ksplit), q1 = (int)((int64_t)nq_all * (zs + 1) / a.ksplit);
   const int c0 = 4 * q0, nch = 4 * (q1 - q0), KP = 4 * nch + 4;
-  const int co_wg = blockIdx.y * COT;
+  // (pixel-tile stream, co tile) of this workgroup.  The workgroups of one stream read the same input
+  // pixels; dispatch deals consecutive workgroups round-robin over the 8 XCDs (speed only, never
+  // correctness), so with the natural order and a stream count that is not a multiple of 8 (conv2 at
+  // B = 256: 81) the co tiles of a stream sit on different XCDs and each fetches the pixels past its L2.
+  // xcd_map (host: gridDim.x a multiple of 8): workgroup lin keeps XCD slot lin % 8, and the gridDim.y co
+  // tiles of stream 8 (lin / 8 / cot) + lin % 8 are consecutive slots of that XCD.
+  int sx = (int)blockIdx.x, sy = (int)blockIdx.y;
+  if (a.xcd_map) {
+    const int lin = (int)(blockIdx.x + blockIdx.y * gridDim.x), slot = lin >> 3, cot = (int)gridDim.y;
+    sx = 8 * (slot / cot) + (lin & 7);
+    sy = slot % cot;
+  }
+  const int co_wg = sy * COT;
   for (int q = threadIdx.x; q < nch; q += 512) {
     const int k = 4 * (c0 + q), kpos = k / a.Ci, ci0 = k - kpos * a.Ci, kh = kpos / a.KW, kw = kpos - kh * a.KW;
     xoff[q] = (kh * a.W + kw) * a.Ci + ci0;
@@ -260,7 +273,7 @@ __global__ __launch_bounds__(512) void conv_fwd_lds_kernel(const ConvFwdArgs a) 
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       U8 ? (void*)const_cast<uint8_t*>(a.xu8) : (void*)const_cast<float*>(a.x), 0,
       BUF ? (int)((a.M / (a.OH * a.OW)) * a.H * a.W * a.Ci * (U8 ? 1 : 4)) : 0, 0x00020000);
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int64_t tile = sx; tile < ntiles; tile += gridDim.x) {
     const int64_t px0 = tile * PXT + 16 * TPX * wpx;
     const float* xb[TPX];
     int xbo[TPX];  // BUF: the same base as an element offset into x (host: x < 2 GB)
@@ -408,17 +421,28 @@ int launch_fwd_lds(const ConvFwdArgs& a, bool nchw, hipStream_t st) {
   int64_t gx = (int64_t)wpc * num_cus() / cot;  // per split
   if (gx > ntiles) gx = ntiles;
   if (gx < 1) gx = 1;
+  // XCD-aware stream order (conv_fwd_lds_kernel): gx rounded up to a multiple of 8 (a stream past the
+  // tiles runs no iteration).  RAI_CONV_FWD_XCD=0 keeps the natural order (A/B)
+  static const int env_xcd = [] {
+    const char* e = getenv("RAI_CONV_FWD_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  ConvFwdArgs ax = a;
+  if (env_xcd != 0 && cot > 1) {
+    gx = (gx + 7) / 8 * 8;
+    ax.xcd_map = 1;
+  }
   const dim3 grid((unsigned)gx, (unsigned)cot, (unsigned)ks);
   if (nchw) {
     auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, true, PF, BUF, U8>;
     const int e = allow_lds(reinterpret_cast<const void*>(k));
     if (e != RAI_OK) return e;
-    hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
+    hipLaunchKernelGGL(k, grid, dim3(512), lds, st, ax);
   } else {
     auto k = conv_fwd_lds_kernel<TCO, TPX, WCO, WPX, false, PF, BUF, U8>;
     const int e = allow_lds(reinterpret_cast<const void*>(k));
     if (e != RAI_OK) return e;
-    hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
+    hipLaunchKernelGGL(k, grid, dim3(512), lds, st, ax);
   }
   RAI_LAUNCH_CHECK();
   return RAI_OK;

@@ -18,6 +18,8 @@ policy on a fresh CartPoleVecEnv(8, seed + 1000).  Only outputs are stored.
 
     python tests/golden/make_golden_returns.py                 # all configs and seeds
     python tests/golden/make_golden_returns.py c2_4096x128     # one config; other configs' runs kept
+    python tests/golden/make_golden_returns.py c2_4096x128_8u --add-seeds 4 5 6 7 8
+                                                               # more seeds, the config's runs kept
 """
 from __future__ import annotations
 
@@ -46,7 +48,7 @@ CONFIGS = {
 }
 # seeds per config (the C2 runs are ~40x the CPU time of the 8-env ones)
 CONFIG_SEEDS = {"yaml_8x32": (1, 2, 3, 4, 5), "c1_8x128": (1, 2, 3, 4, 5), "c2_4096x128": (1, 2, 3),
-                "c2_4096x128_8u": (1, 2, 3)}
+                "c2_4096x128_8u": (1, 2, 3, 4, 5, 6, 7, 8)}  # 4-8 added in round 6 (--add-seeds)
 ALGO_KW = dict(batch_size=256, n_epochs=20, gae_lambda=0.8, gamma=0.98, ent_coef=0.0,
                learning_rate=0.001, clip_range=0.2)
 PHASES = [{"learning_rate": 0.001, "clip_range": 0.2}, {"learning_rate": 0.0, "clip_range": 0.0}]
@@ -134,16 +136,23 @@ def run_one(args):
 
 
 def main():
-    names = sys.argv[1:] or list(CONFIGS)
-    jobs = [(c, s) for c in names for s in CONFIG_SEEDS[c]]
-    with mp.get_context("spawn").Pool(min(4, len(jobs))) as pool:
+    argv = sys.argv[1:]
+    add = None
+    if "--add-seeds" in argv:
+        i = argv.index("--add-seeds")
+        add = [int(x) for x in argv[i + 1:]]
+        argv = argv[:i]
+    names = argv or list(CONFIGS)
+    jobs = [(c, s) for c in names for s in (add if add is not None else CONFIG_SEEDS[c])]
+    with mp.get_context("spawn").Pool(min(int(__import__("os").environ.get("RETURNS_PROCS", "4")), len(jobs))) as pool:
         res = pool.map(run_one, jobs)
     path = HERE / "returns_cartpole.json"
     out = json.loads(path.read_text()) if path.exists() else dict(runs={})
     out.update(configs={k: CONFIGS[k] for k in set(out["runs"]) | set(names)}, algo_kw=ALGO_KW, phases=PHASES,
                durations=DURATIONS, eval_episodes=EVAL_EPISODES)
     for c in names:
-        out["runs"][c] = {}
+        if add is None:
+            out["runs"][c] = {}
     for cfg, seed, r in res:
         out["runs"].setdefault(cfg, {})[str(seed)] = r
         print(cfg, seed, "final rolling", round(r["final_rolling_mean"], 1), "eval", r["eval_mean"])
