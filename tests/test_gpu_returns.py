@@ -50,11 +50,11 @@ def test_reference_return_fixture_is_consistent():
             for r in REF["runs"][cfg].values():
                 assert np.all(np.diff([p[1] for p in r["curve"]]) > 0), r["curve"]
             assert len(REF["runs"][cfg]) == 3 and 80 < finals.mean() < 200
-        elif cfg == "c2_4096x128_8u":  # 8 updates: near convergence (eval 487-500), the curve flattens at the end
+        elif cfg == "c2_4096x128_8u":  # 8 updates: near convergence (eval 459-500), the curve flattens at the end
             for r in REF["runs"][cfg].values():
                 pts = [p[1] for p in r["curve"]]
                 assert np.all(np.diff(pts[:6]) > 0) and pts[-1] > 250, r["curve"]
-            assert len(REF["runs"][cfg]) == 3 and evals.min() > 480
+            assert len(REF["runs"][cfg]) == 8 and evals.min() > 450
         else:
             assert (finals >= 475).sum() >= 3, finals
             assert 200 < aucs.mean() < 450
@@ -217,16 +217,21 @@ def test_episode_return_matches_reference_at_c2():
 @pytest.mark.gpu
 def test_episode_return_matches_reference_at_c2_8_updates():
     """C2 (4096 envs x 128 steps, batch 256 x 20 epochs) trained twice as long -- 8 updates with the lr /
-    clip decay spread over 8 (make_golden_returns.py c2_4096x128_8u, the reference's PPO.learn, seeds
-    1-3) -- where both populations approach CartPole's 500 ceiling and the bands can be tight.  The
-    reference: final rolling means 284-416, deterministic 10-episode evals 487.1 / 499.8 / 497.7.
-    Bands derived from the reference's own seed spread (sd = its sample standard deviation over seeds):
-      * the mean deterministic evaluation within max(25, 4 sd of the reference's evals) of the
-        reference's mean (25 at these seeds: 470-520, where round 4's 4-update test allowed +-200);
-      * every update's mean rolling mean within 2 sd of the reference's per-update seed spread + 10 %;
-      * the mean area under the curve within 15 %."""
+    clip decay spread over 8 (make_golden_returns.py c2_4096x128_8u, the reference's PPO.learn) -- where
+    both populations approach CartPole's 500 ceiling.  EIGHT seeds on each side (round 6 added reference
+    seeds 4-8: three could not tell a 15 % gap at updates 5-7 from noise).  The reference: final rolling
+    means 284-459, deterministic 10-episode evals 459-500.  Two-sample checks between the seed
+    populations (the device samples actions from its own RNG, so runs are not comparable seed by seed):
+      * Welch's t-test on the per-seed area under the rolling-mean curve (learning speed) and on the final
+        rolling mean: no difference at the 1 % level (p > 0.01), and the AUC means within 15 %;
+      * every update's mean rolling mean within 3 standard errors of the difference of the two means
+        (sqrt(var_ref / n + var_dev / n)) + 5 % of the reference's mean;
+      * the mean deterministic evaluation within max(15, 3 standard errors of the difference)."""
+    from scipy import stats
+
     cfg = "c2_4096x128_8u"
     seeds = _seeds(cfg)
+    assert len(seeds) == 8
     ref_curves = np.array([[p[1] for p in REF["runs"][cfg][str(s)]["curve"]] for s in seeds])
     r_fin, r_auc, r_eval = _ref(cfg)
     dev_curves, evals = [], []
@@ -236,15 +241,22 @@ def test_episode_return_matches_reference_at_c2_8_updates():
         dev_curves.append([p[1] for p in curve])
         evals.append(ev)
     dev_curves, evals = np.array(dev_curves), np.array(evals)
-    eval_band = max(25.0, 4 * float(r_eval.std(ddof=1)))
-    curve_band = 2 * ref_curves.std(0, ddof=1) + 0.1 * ref_curves.mean(0)
+    n = len(seeds)
+    se = lambda a, b: np.sqrt(a.var(0, ddof=1) / n + b.var(0, ddof=1) / n)
+    d_auc, d_fin = dev_curves.mean(1), dev_curves[:, -1]
+    p_auc = float(stats.ttest_ind(d_auc, r_auc, equal_var=False).pvalue)
+    p_fin = float(stats.ttest_ind(d_fin, r_fin, equal_var=False).pvalue)
+    curve_band = 3 * se(ref_curves, dev_curves) + 0.05 * ref_curves.mean(0)
+    eval_band = max(15.0, 3 * float(se(r_eval, evals)))
     msg = (f"device curves {dev_curves.round(1).tolist()} eval {evals.round(1).tolist()}; reference curves "
-           f"{ref_curves.round(1).tolist()} eval {r_eval.round(1).tolist()}; eval band {eval_band:.1f}, "
-           f"curve band {curve_band.round(1).tolist()}")
+           f"{ref_curves.round(1).tolist()} eval {r_eval.round(1).tolist()}; Welch p AUC {p_auc:.3f} final "
+           f"{p_fin:.3f}; mean curves device {dev_curves.mean(0).round(1).tolist()} reference "
+           f"{ref_curves.mean(0).round(1).tolist()} band {curve_band.round(1).tolist()}; eval band {eval_band:.1f}")
     print(msg)
     _write_report(f"returns_{cfg}.json", device_curves=dev_curves.tolist(), device_eval=evals.tolist(),
                   reference_curves=ref_curves.tolist(), reference_eval=r_eval.tolist(), seeds=seeds,
-                  eval_band=eval_band, curve_band=curve_band.tolist())
-    assert abs(evals.mean() - r_eval.mean()) <= eval_band, msg
+                  welch_p_auc=p_auc, welch_p_final=p_fin, eval_band=eval_band, curve_band=curve_band.tolist())
+    assert p_auc > 0.01 and p_fin > 0.01, msg
+    assert abs(d_auc.mean() / r_auc.mean() - 1) <= 0.15, msg
     assert (np.abs(dev_curves.mean(0) - ref_curves.mean(0)) <= curve_band).all(), msg
-    assert abs(dev_curves.mean() / ref_curves.mean() - 1) <= 0.15, msg
+    assert abs(evals.mean() - r_eval.mean()) <= eval_band, msg
