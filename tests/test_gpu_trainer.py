@@ -323,6 +323,72 @@ def test_long_horizon_matches_reference_learn_epoch(golden, generic):
         (ld, z["losses"], lu)
 
 
+def _long_wide_update(z, ulp=False):
+    """learn_epoch_long_wide.npz's rollout and permutations through PPO.learn_epoch on the device: the C4
+    policy ([256, 256] ReLU, Gaussian head), whose epochs run as ONE rai_mlp_wide_epoch launch each."""
+    from rl_algo_impls_amd.policy import ActorCritic
+
+    kw = json.loads(str(z["kw"]))
+    policy = ActorCritic(nets.halfcheetah_env(), **json.loads(str(z["policy"])))
+    init = torch.from_numpy(z["init"])
+    if ulp:
+        init = torch.nextafter(init, torch.full_like(init, float("inf")))
+    nets.load_flat(policy, init.numpy())
+    policy = policy.to(DEV)
+    rec = Recorder()
+    algo = PPO(policy, DEV, rec, **kw)
+    perms = [p.astype(np.int64) for p in z["perms"]]
+    t = lambda k: torch.from_numpy(z[k]).to(DEV)
+    r = DeviceRollout(DEV, t("next_episode_starts"), t("next_values"), t("obs"), t("actions"), t("rewards"),
+                      t("episode_starts"), t("values"), t("logprobs"), None, kw["gamma"], kw["gae_lambda"],
+                      perm_source=lambda n: torch.from_numpy(perms.pop(0)))
+    np.testing.assert_array_equal(r.advantages.cpu().numpy(), z["advantages"])
+    captured = []
+    real_update = algo.update
+
+    def update(rr):
+        out = real_update(rr)
+        captured.append(np.asarray(out[1], np.float64))
+        return out
+
+    algo.update = update
+
+    class Gen:
+        def rollout(self, gamma, gae_lambda):
+            return r
+
+    algo.learn_epoch(0, r.total_steps, Gen(), None)
+    torch.cuda.synchronize()
+    assert getattr(algo, "_we_ws", None) is not None, "the whole-epoch kernel path"
+    assert not perms and algo.optimizer.step_count == len(z["grad_norms"]) == 2048
+    return algo.flat.flat.detach().cpu().double().numpy(), captured[0]
+
+
+def test_long_horizon_wide_epoch_matches_reference_learn_epoch(golden):
+    """2,048 DEPENDENT optimizer steps of the C4-class whole-epoch kernel (rai_mlp_wide_epoch, C4's policy and
+    hyperparameters) pinned to the reference itself (learn_epoch_long_wide.npz, tests/golden/make_golden_long.py:
+    64 envs x 32 steps, batch 64, 64 epochs, the reference's rollout and permutations injected).  This
+    trajectory is far more sensitive than C2's: at lr 2e-5 Adam moves every weight by ~lr per step
+    whatever its gradient's size, so weights whose gradients are noise flip direction under a one-ulp
+    change of the start (the reference's own ulp floor is 7.6e-2 of the update).  So: the first 64 steps'
+    gradient norms to 1e-4 (before divergence compounds), and the final update (params - init) within
+    4x the larger ulp floor (reference's, device's) of the reference's update."""
+    z = golden("learn_epoch_long_wide.npz")
+    init = z["init"].astype(np.float64)
+    pd, nd = _long_wide_update(z)
+    pu, nu = _long_wide_update(z, ulp=True)
+    pr, pr_u = z["params"].astype(np.float64), z["params_ulp"].astype(np.float64)
+    nr = z["grad_norms"]
+    upd = lambda p: p - init
+    rel = lambda a, b: float(np.linalg.norm(a - b) / np.linalg.norm(upd(b)))
+    drift, floor_ref, floor_dev = rel(pd, pr), rel(pr_u, pr), rel(pu, pd)
+    print(f"long horizon (wide epoch): |p_dev - p_ref| / |update| = {drift:.3e}, ulp floors ref {floor_ref:.3e} "
+          f"dev {floor_dev:.3e}; first-64 grad-norm rel diff max {np.max(np.abs(nd[:64] - nr[:64]) / nr[:64]):.3e}")
+    assert np.isfinite(pd).all()
+    np.testing.assert_allclose(nd[:64], nr[:64], rtol=1e-4)
+    assert drift <= 4 * max(floor_ref, floor_dev), (drift, floor_ref, floor_dev)
+
+
 def test_a2c_step_matches_reference(golden):
     z = golden("a2c_step.npz")
     policy = nets.build("cartpole")
