@@ -41,6 +41,34 @@ def test_cpu_trainer_learn_epoch_matches_reference(golden):
     np.testing.assert_allclose(got, z["losses"], rtol=2e-4, atol=1e-7)
 
 
+def test_cpu_trainer_long_horizon_matches_reference(golden):
+    """The oracle's CPU restatement over 2,048 DEPENDENT optimizer steps (learn_epoch_long.npz, the reference's
+    own learn_epoch: 256 envs x 128 steps, batch 256 x 16 epochs): its GAE bit-exact, its first 64 gradient
+    norms to 1e-5 and its final weights within 4x the reference's own one-ulp drift floor (the fixture's
+    params_ulp) -- the same rule the device path meets in tests/test_gpu_trainer.py."""
+    z = golden("learn_epoch_long.npz")
+    kw = json.loads(str(z["kw"]))
+    adv = oracle.compute_advantages(z["rewards"], z["values"], z["episode_starts"], z["next_episode_starts"],
+                                    z["next_values"], kw["gamma"], kw["gae_lambda"])
+    np.testing.assert_array_equal(adv, z["advantages"])
+    torch.manual_seed(0)
+    pol = cpu_trainer.MLPActorCritic()
+    cpu_trainer.load_flat(pol, z["init"])
+    ppo = cpu_trainer.CpuPPO(pol, lr=kw["learning_rate"], batch_size=kw["batch_size"], n_epochs=kw["n_epochs"],
+                             clip_range=kw["clip_range"], ent_coef=kw["ent_coef"])
+    fl = lambda a: torch.as_tensor(np.asarray(a).reshape((-1,) + np.asarray(a).shape[2:]))
+    b = dict(obs=fl(z["obs"]), logprobs=fl(z["logprobs"]), actions=fl(z["actions"]), values=fl(z["values"]),
+             advantages=fl(adv), returns=fl(adv + z["values"]))
+    rows, _ = ppo.update(b, perms=[p.astype(np.int64) for p in z["perms"]])
+    assert len(rows) == len(z["grad_norms"]) == 2048
+    np.testing.assert_allclose(rows[:64, 6], z["grad_norms"][:64], rtol=1e-5)
+    pr, pu = z["params"].astype(np.float64), z["params_ulp"].astype(np.float64)
+    got = cpu_trainer.flat_params(pol).astype(np.float64)
+    rel = lambda a, b: float(np.linalg.norm(a - b) / np.linalg.norm(b))
+    drift, floor = rel(got, pr), rel(pu, pr)
+    assert drift <= max(4 * floor, 1e-6), (drift, floor)
+
+
 def test_cpu_trainer_pong_steps_match_reference(golden):
     z = golden("pong_steps.npz")
     meta = json.loads(str(z["index"]))
