@@ -46,12 +46,15 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
   }
 }
 
-// Keyed permutation of [0, n) (the epoch shuffle).  A 6-round balanced Feistel network over the
-// smallest even-bit domain 2^(2h) >= n, whose round function is the lowbias32 integer hash of
-// (right half ^ round key) masked to h bits, with cycle walking back into [0, n): a bijection for every
-// key, computed independently per index (no sort).  Replaces the device torch.randperm (a radix sort
+// Keyed permutation of [0, n) (the epoch shuffle).  A 6-round unbalanced Feistel network over the
+// smallest domain 2^b >= n (b >= 2), split into a high part of h1 = b/2 bits and a low part of
+// h2 = b - h1 bits whose widths swap every round; the round function is the lowbias32 integer hash of
+// (low part ^ round key) masked to the high part's width, with cycle walking back into [0, n): a
+// bijection for every key, computed independently per index (no sort).  Replaces the device torch.randperm (a radix sort
 // of n random keys plus merge passes, ~0.27 ms per epoch at n = 524,288 on the scaled batch policy,
 // where the epoch kernels fill every CU and the side-stream overlap of the 32-CU epoch kernel is gone).
+// (The first version used a balanced network over the even-bit domain 2^(2h), up to 4n: at n = 2^19
+// that is 2n, and a wave waits for its longest cycle walk: 31.2 us per epoch against 6.8 us now.)
 // The reference draws torch.randperm on the host CPU generator (vec_rollout.py:166-175); the shuffle is
 // a different random stream either way, and parity tests inject the reference's permutations.
 __device__ __forceinline__ uint32_t perm_mix32(uint32_t x) {
@@ -65,24 +68,27 @@ __device__ __forceinline__ uint32_t perm_mix32(uint32_t x) {
 constexpr int PERM_ROUNDS = 6;
 struct PermArgs {
   uint32_t k[PERM_ROUNDS];
-  int32_t half;  // h
+  int32_t h1, h2;  // high / low part widths, h1 + h2 = b
   int64_t n;
   int64_t* out;
 };
 __global__ __launch_bounds__(256) void feistel_perm_kernel(const PermArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
-  const uint32_t mask = a.half >= 32 ? 0xffffffffu : ((1u << a.half) - 1u);
+  const uint32_t m1 = (1u << a.h1) - 1u, m2 = (1u << a.h2) - 1u;
   uint64_t x = (uint64_t)i;
-  do {  // walks at most a few times: the domain is < 4n
-    uint32_t L = (uint32_t)(x >> a.half), R = (uint32_t)x & mask;
+  do {  // the domain 2^b is < 2n: walks twice on average, never when n is a power of two
+    uint32_t hi = (uint32_t)(x >> a.h2), lo = (uint32_t)x & m2;  // h1 and h2 bits
 #pragma unroll
-    for (int r = 0; r < PERM_ROUNDS; ++r) {
-      const uint32_t t = L ^ (perm_mix32(R ^ a.k[r]) & mask);
-      L = R;
-      R = t;
+    for (int r = 0; r < PERM_ROUNDS; r += 2) {
+      const uint32_t t = hi ^ (perm_mix32(lo ^ a.k[r]) & m1);  // (h1, h2) -> (h2, h1)
+      hi = lo;
+      lo = t;
+      const uint32_t u = hi ^ (perm_mix32(lo ^ a.k[r + 1]) & m2);  // (h2, h1) -> (h1, h2)
+      hi = lo;
+      lo = u;
     }
-    x = ((uint64_t)L << a.half) | R;
+    x = ((uint64_t)hi << a.h2) | lo;
   } while (x >= (uint64_t)a.n);
   a.out[i] = (int64_t)x;
 }
@@ -386,7 +392,9 @@ extern "C" int rai_feistel_permutation(int64_t n, uint64_t key, int64_t* out, vo
   PermArgs a;
   int bits = 0;
   while (bits < 62 && ((int64_t)1 << bits) < n) ++bits;
-  a.half = bits < 2 ? 1 : (bits + 1) / 2;
+  if (bits < 2) bits = 2;
+  a.h1 = bits / 2;
+  a.h2 = bits - a.h1;
   const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
   for (int r = 0; r < PERM_ROUNDS; ++r) a.k[r] = perm_mix32_host(lo ^ perm_mix32_host(hi + 0x9e3779b9u * (uint32_t)(r + 1)));
   a.n = n;

@@ -10,6 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r4}
 CONFIG=${CONFIG:-pong}  # round 6: any bench config (microrts for C5); GROUPS_=all: one unrestricted pass per counter
+# (COUNTERS restricts the passes to a subset of FETCH_SIZE WRITE_SIZE)
 OUT=gpurun_out/c3grp_$TAG
 mkdir -p "$OUT"
 # round 5: "ours" split into the convolutions and the rest of this repo's kernels (the round-5 run of the
@@ -24,9 +25,13 @@ for grp in ${GROUPS_:-conv ours gemm rest}; do
     ours) sel=(--kernel-include-regex "$OURS") ;;
     gemm) sel=(--kernel-include-regex "$GEMM") ;;
     rest) sel=(--kernel-exclude-regex "$CONV|$OURS|$GEMM") ;;
+    # "rest" split in two (round 6: a C5 rest WRITE_SIZE pass ended in a SIGSEGV inside the profiler's
+    # dispatch path at a torch reduction launch, profiles/r6z_c5_rest_write_crash.txt)
+    restat) sel=(--kernel-include-regex "at::native") ;;
+    restx) sel=(--kernel-exclude-regex "$CONV|$OURS|$GEMM|at::native") ;;
     all) sel=() ;;
   esac
-  for C in FETCH_SIZE WRITE_SIZE; do
+  for C in ${COUNTERS:-FETCH_SIZE WRITE_SIZE}; do
     echo "== $grp $C" | tee -a "$OUT/steps.log"
     RAI_GRAPHS=1 RAI_GRAPH_EAGER=1 timeout -s KILL 400 rocprofv3 --pmc $C "${sel[@]}" --output-format csv \
       -d "$OUT/${grp}_$C" -o run -- python3 bench.py --config "$CONFIG" --no-cpu-baseline --roofline-reps 1 --steps 1 \
@@ -41,10 +46,12 @@ done
 python3 - "$OUT" ${GROUPS_:-conv ours gemm rest} <<'PY'
 import json, sys
 out = sys.argv[1]
+import os
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     merged = {"kernels": {}}
     for g in sys.argv[2:]:
-        merged["kernels"].update(json.load(open(f"{out}/{g}_{c}.json"))["kernels"])
+        if os.path.exists(f"{out}/{g}_{c}.json"):  # COUNTERS may restrict a run to one counter
+            merged["kernels"].update(json.load(open(f"{out}/{g}_{c}.json"))["kernels"])
     json.dump(merged, open(f"{out}/{c}.json", "w"), indent=1)
 PY
 exit 0
